@@ -1,0 +1,165 @@
+/*
+ * ref_harness.c -- TEST INFRASTRUCTURE.  Drives the *reference* encoder
+ * (allweax/hartallo, compiled by oracle/Makefile into oracle/_ref/libhl.a)
+ * through its public API exactly like source/test_encoder.c:135-146 does
+ * (threads_count=1, SAD distortion, rc off, max_ref_frame=1) and dumps, per
+ * frame:
+ *   <prefix>.264      Annex-B stream (hdr bytes + 00 00 01 + slice bytes,
+ *                     as test_encoder.c:220-236 writes it)
+ *   <prefix>.rec.yuv  the reconstructed (deblocked) reference picture
+ *   <prefix>.mbs      one mbrec.h record per macroblock
+ * The dumps are read back through the reference's own structures
+ * (hl_codec_264_t / hl_codec_264_layer_t / hl_codec_264_mb_t).
+ *
+ * usage: ref_enc W H N qp me_range deblock gop early_term in.yuv out_prefix [quiet]
+ */
+#include <hartallo/hl_api.h>
+#include <hartallo/hl_frame.h>
+#include <hartallo/hl_codec.h>
+#include <hartallo/hl_object.h>
+#include <hartallo/hl_debug.h>
+#include <hartallo/hl_cpu.h>
+#include <hartallo/h264/hl_codec_264.h>
+#include <hartallo/h264/hl_codec_264_layer.h>
+#include <hartallo/h264/hl_codec_264_mb.h>
+#include <hartallo/h264/hl_codec_264_dpb.h>
+#include <hartallo/h264/hl_codec_264_pict.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include "mbrec.h"
+
+static void dump_mb(const hl_codec_264_mb_t* m, int32_t* r)
+{
+    int i, j, c;
+    memset(r, 0, sizeof(int32_t) * MBR_STRIDE);
+    r[MBR_FLAGS] = ((m->flags_type & HL_CODEC_264_MB_TYPE_FLAGS_INTRA) ? 1 : 0)
+                 | ((m->flags_type & HL_CODEC_264_MB_TYPE_FLAGS_INTER) ? 2 : 0)
+                 | ((m->flags_type & HL_CODEC_264_MB_TYPE_FLAGS_SKIP) ? 4 : 0)
+                 | ((m->MbPartPredMode[0] == HL_CODEC_264_MB_MODE_INTRA_16X16) ? 8 : 0)
+                 | ((m->MbPartPredMode[0] == HL_CODEC_264_MB_MODE_INTRA_4X4) ? 16 : 0);
+    r[MBR_MB_TYPE] = (int32_t)m->mb_type;
+    for (i = 0; i < 4; ++i) r[MBR_SUB_MB_TYPE + i] = (int32_t)m->sub_mb_type[i];
+    r[MBR_NUM_MB_PART] = m->NumMbPart;
+    for (i = 0; i < 4; ++i) for (j = 0; j < 4; ++j) {
+        r[MBR_MVL0 + (i * 4 + j) * 2 + 0] = m->mvL0[i][j].x;
+        r[MBR_MVL0 + (i * 4 + j) * 2 + 1] = m->mvL0[i][j].y;
+        r[MBR_MVD + (i * 4 + j) * 2 + 0] = m->mvd_l0[i][j].x;
+        r[MBR_MVD + (i * 4 + j) * 2 + 1] = m->mvd_l0[i][j].y;
+        r[MBR_MVL0_CAP + (i * 4 + j) * 2 + 0] = m->MvL0[i][j].x;
+        r[MBR_MVL0_CAP + (i * 4 + j) * 2 + 1] = m->MvL0[i][j].y;
+    }
+    r[MBR_CBP_L4x4] = (int32_t)m->CodedBlockPatternLuma4x4;
+    r[MBR_CBP] = (int32_t)m->coded_block_pattern;
+    r[MBR_CBP_L] = (int32_t)m->CodedBlockPatternLuma;
+    r[MBR_CBP_C] = (int32_t)m->CodedBlockPatternChroma;
+    for (c = 0; c < 2; ++c) {
+        r[MBR_CBP_CAC + c] = (int32_t)m->CodedBlockPatternChromaAC4x4[c];
+        r[MBR_CBP_CDC + c] = (int32_t)m->CodedBlockPatternChromaDC4x4[c];
+    }
+    r[MBR_I16_MODE] = m->Intra16x16PredMode;
+    for (i = 0; i < 16; ++i) {
+        r[MBR_I4_MODE + i] = m->Intra4x4PredMode[i];
+        r[MBR_PREV_FLAG + i] = m->prev_intra4x4_pred_mode_flag[i];
+        r[MBR_REM_MODE + i] = m->rem_intra4x4_pred_mode[i];
+        r[MBR_TC_LUMA + i] = m->TotalCoeffsLuma[i];
+        r[MBR_I16_DC + i] = m->Intra16x16DCLevel[i];
+        for (j = 0; j < 16; ++j) {
+            r[MBR_LUMA_LEVEL + i * 16 + j] = m->LumaLevel[i][j];
+            r[MBR_I16_AC + i * 16 + j] = m->Intra16x16ACLevel[i][j];
+        }
+    }
+    r[MBR_CHROMA_MODE] = m->intra_chroma_pred_mode;
+    r[MBR_QPY] = m->QPy;
+    for (c = 0; c < 2; ++c) for (i = 0; i < 4; ++i) {
+        r[MBR_TC_CAC + c * 4 + i] = m->TotalCoeffsChromaACCbCr[c][i];
+        r[MBR_CHROMA_DC + c * 4 + i] = m->ChromaDCLevel[c][i];
+        for (j = 0; j < 16; ++j) r[MBR_CHROMA_AC + (c * 4 + i) * 16 + j] = m->ChromaACLevel[c][i][j];
+    }
+    r[MBR_ETYPE] = m->e_type;
+}
+
+int main(int argc, char** argv)
+{
+    if (argc < 11) {
+        fprintf(stderr, "usage: %s W H N qp me_range deblock gop early_term in.yuv out_prefix [quiet]\n", argv[0]);
+        return 1;
+    }
+    int W = atoi(argv[1]), H = atoi(argv[2]), N = atoi(argv[3]), qp = atoi(argv[4]);
+    int mer = atoi(argv[5]), db = atoi(argv[6]), gop = atoi(argv[7]), et = atoi(argv[8]);
+    const char* in = argv[9];
+    const char* pre = argv[10];
+    int quiet = argc > 11;
+    char path[1024];
+
+    hl_debug_set_level(HL_DEBUG_LEVEL_ERROR);
+    hl_engine_set_cpu_flags(kCpuFlagAll);
+    if (hl_engine_init()) return 2;
+
+    const struct hl_codec_plugin_def_s* pl = 0;
+    struct hl_codec_s* c = 0;
+    struct hl_codec_result_s* r = 0;
+    hl_frame_video_t* f = 0;
+    hl_codec_plugin_find(HL_CODEC_TYPE_H264, &pl);
+    hl_codec_create(pl, &c);
+    hl_codec_result_create(&r);
+    hl_frame_video_create(&f);
+    c->gop_size = gop; c->me_range = mer; c->qp = qp; c->fps.num = 1; c->fps.den = 15;
+    c->rc_bitrate = -1; c->deblock_flag = db; c->threads_count = 1; c->max_ref_frame = 1;
+    c->distortion_mesure_type = HL_VIDEO_DISTORTION_MESURE_TYPE_SAD;
+    c->me_type = (HL_VIDEO_ME_TYPE_INTEGER | HL_VIDEO_ME_TYPE_HALF | HL_VIDEO_ME_TYPE_QUATER);
+    c->me_part_types = HL_VIDEO_ME_PART_TYPE_ALL;
+    c->me_subpart_types = HL_VIDEO_ME_SUBPART_TYPE_ALL;
+    c->me_early_term_flag = et;
+
+    size_t fs = (size_t)W * H * 3 / 2;
+    uint8_t* buf = (uint8_t*)malloc(fs);
+    FILE* fi = fopen(in, "rb");
+    if (!fi) { fprintf(stderr, "cannot open %s\n", in); return 3; }
+    snprintf(path, sizeof(path), "%s.264", pre);
+    FILE* fo = fopen(path, "wb");
+    FILE* frec = 0;
+    FILE* fmb = 0;
+    if (!quiet) {
+        snprintf(path, sizeof(path), "%s.rec.yuv", pre);
+        frec = fopen(path, "wb");
+        snprintf(path, sizeof(path), "%s.mbs", pre);
+        fmb = fopen(path, "wb");
+    }
+    static const uint8_t scp[3] = { 0, 0, 1 };
+    int32_t rec[MBR_STRIDE];
+    int n = 0;
+    double tot = 0;
+    while (n < N && fread(buf, 1, fs, fi) == fs) {
+        struct timespec t0, t1;
+        hl_frame_video_fill(f, HL_VIDEO_CHROMA_YUV420, W, H, buf, fs);
+        f->encoding = HL_VIDEO_ENCODING_TYPE_AUTO;
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+        int e = hl_codec_encode(c, (hl_frame_t*)f, r);
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        if (e) { fprintf(stderr, "encode err %d at frame %d\n", e, n); return 4; }
+        tot += (t1.tv_sec - t0.tv_sec) + (t1.tv_nsec - t0.tv_nsec) * 1e-9;
+        if (r->type & HL_CODEC_RESULT_TYPE_HDR) fwrite(c->hdr_bytes, 1, c->hdr_bytes_count, fo);
+        if (r->type & HL_CODEC_RESULT_TYPE_DATA) { fwrite(scp, 1, 3, fo); fwrite(r->data_ptr, 1, r->data_size, fo); }
+        if (!quiet) {
+            hl_codec_264_t* p264 = (hl_codec_264_t*)c;
+            hl_codec_264_layer_t* L = p264->layers.pc_active;
+            const hl_codec_264_pict_t* pict = L->pc_fs_curr->p_pict;
+            fwrite(pict->pc_data_y, 1, (size_t)W * H, frec);
+            fwrite(pict->pc_data_u, 1, (size_t)W * H / 4, frec);
+            fwrite(pict->pc_data_v, 1, (size_t)W * H / 4, frec);
+            for (size_t a = 0; a < L->u_list_macroblocks_count; ++a) {
+                dump_mb(L->pp_list_macroblocks[a], rec);
+                fwrite(rec, sizeof(int32_t), MBR_STRIDE, fmb);
+            }
+        }
+        n++;
+    }
+    fclose(fo);
+    if (frec) fclose(frec);
+    if (fmb) fclose(fmb);
+    printf("{\"frames\": %d, \"seconds\": %.6f, \"fps\": %.4f, \"mb_per_s\": %.1f}\n",
+           n, tot, n / tot, (double)n * (W / 16) * (H / 16) / tot);
+    return 0;
+}
