@@ -1,0 +1,29 @@
+# Builds (for gfx950):
+#   hartallo_amd/libhartallo_amd.so  the product: HIP kernels + host writer + C ABI
+#   tests/emu/libhl_emu.so           test-only host build of the kernel logic
+#   oracle/...                       test-only CPU oracle and reference build (oracle/Makefile)
+HIPCC   ?= /opt/rocm/bin/hipcc
+ARCH    ?= gfx950
+CSRC    := hartallo_amd/csrc
+HDRS    := $(wildcard $(CSRC)/*.h) include/hartallo_amd.h
+# -ffp-contract=off: the RDO costs are IEEE double and must round exactly like the reference
+CXXFLAGS := -std=c++17 -O3 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-variable
+
+.PHONY: all product emu oracle clean
+all: product emu oracle
+
+product: hartallo_amd/libhartallo_amd.so
+emu: tests/emu/libhl_emu.so
+
+hartallo_amd/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp $(HDRS)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -shared -o $@ $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp
+
+tests/emu/libhl_emu.so: tests/emu/hl_emu.hip $(CSRC)/hl_writer.cpp $(HDRS)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -O2 -shared -o $@ tests/emu/hl_emu.hip $(CSRC)/hl_writer.cpp
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -f hartallo_amd/libhartallo_amd.so tests/emu/libhl_emu.so
+	$(MAKE) -C oracle clean

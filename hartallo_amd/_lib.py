@@ -1,0 +1,188 @@
+"""ctypes binding of libhartallo_amd.so (include/hartallo_amd.h).
+
+The library is the HIP build for gfx950; there is no CPU fallback.  Loading
+fails loudly when the library is missing, and encoding fails loudly when no
+GPU is present.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhartallo_amd.so")
+
+# include/hartallo_amd.h
+HL_AMD_SUCCESS = 0
+HL_AMD_ERROR_INVALID_PARAMETER = 1
+HL_AMD_ERROR_INVALID_STATE = 3
+HL_AMD_ERROR_INVALID_FORMAT = 4
+HL_AMD_ERROR_NOT_IMPLEMENTED = 7
+HL_AMD_ERROR_OUTOFMEMMORY = 8
+HL_AMD_ERROR_SYSTEM = 13
+HL_AMD_ERROR_TOOSHORT = 15
+HL_AMD_RESULT_TYPE_DATA = 1
+HL_AMD_RESULT_TYPE_HDR = 2
+
+# every symbol include/hartallo_amd.h declares
+EXPORTED_SYMBOLS = (
+    "hl_amd_encoder_create",
+    "hl_amd_encoder_destroy",
+    "hl_amd_encode",
+    "hl_amd_encode_device",
+    "hl_amd_get_recon",
+    "hl_amd_set_timing",
+    "hl_amd_get_timing",
+    "hl_amd_last_reruns",
+    "hl_amd_version",
+)
+
+
+class HlAmdError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what} failed with HL_ERROR {code}")
+        self.code = code
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("width", "height", "qp", "me_range", "deblock", "gop_size", "me_early_term", "device")]
+
+
+class _Result(ctypes.Structure):
+    _fields_ = [
+        ("type", ctypes.c_int32),
+        ("hdr", ctypes.c_void_p),
+        ("hdr_size", ctypes.c_size_t),
+        ("data", ctypes.c_void_p),
+        ("data_size", ctypes.c_size_t),
+    ]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Loads the HIP library.  torch (if installed) is imported first so the
+    process ends up with one HIP runtime (torch ships its own
+    libamdhip64.so.7, which then also satisfies this library)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} is missing: build it with `make product` (hipcc --offload-arch=gfx950)")
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = ctypes.CDLL(path)
+    vp, i32 = ctypes.c_void_p, ctypes.c_int32
+    lib.hl_amd_encoder_create.argtypes = [ctypes.POINTER(_Params), ctypes.POINTER(vp)]
+    lib.hl_amd_encoder_create.restype = i32
+    lib.hl_amd_encoder_destroy.argtypes = [vp]
+    lib.hl_amd_encoder_destroy.restype = None
+    for f in (lib.hl_amd_encode, lib.hl_amd_encode_device):
+        f.argtypes = [vp, vp, vp, vp, ctypes.POINTER(_Result)]
+        f.restype = i32
+    lib.hl_amd_get_recon.argtypes = [vp, vp, vp, vp]
+    lib.hl_amd_get_recon.restype = i32
+    lib.hl_amd_set_timing.argtypes = [vp, i32]
+    lib.hl_amd_set_timing.restype = i32
+    lib.hl_amd_get_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+    lib.hl_amd_get_timing.restype = i32
+    lib.hl_amd_last_reruns.argtypes = [vp]
+    lib.hl_amd_last_reruns.restype = i32
+    lib.hl_amd_version.argtypes = []
+    lib.hl_amd_version.restype = ctypes.c_char_p
+    _lib = lib
+    return lib
+
+
+@dataclass
+class EncodeResult:
+    """hl_codec_result_t of one encode() call (hl_codec.h:152-168)."""
+
+    type: int
+    data: bytes
+    hdr: bytes
+
+    def annexb(self) -> bytes:
+        """Bytes the reference's test harness writes for this frame
+        (test_encoder.c:220-236): headers when signalled, then a start code
+        and the slice NAL."""
+        out = self.hdr if self.type & HL_AMD_RESULT_TYPE_HDR else b""
+        return out + b"\x00\x00\x01" + self.data
+
+
+class Encoder:
+    """One H.264 encode stream on one GPU (one hl_codec_t, not reentrant)."""
+
+    def __init__(self, width: int, height: int, qp: int = 28, me_range: int = 16, deblock: int = 1, gop_size: int = 30,
+                 me_early_term: int = 0, device: int = 0):
+        self.lib = load_library()
+        self.width, self.height = width, height
+        p = _Params(width, height, qp, me_range, deblock, gop_size, me_early_term, device)
+        h = ctypes.c_void_p()
+        rc = self.lib.hl_amd_encoder_create(ctypes.byref(p), ctypes.byref(h))
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_encoder_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.hl_amd_encoder_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _result(self, r: _Result) -> EncodeResult:
+        data = ctypes.string_at(r.data, r.data_size) if r.type & HL_AMD_RESULT_TYPE_DATA else b""
+        hdr = ctypes.string_at(r.hdr, r.hdr_size) if r.type & HL_AMD_RESULT_TYPE_HDR else b""
+        return EncodeResult(r.type, data, hdr)
+
+    def encode(self, y, u, v) -> EncodeResult:
+        """Encodes planar YUV420 from host memory (numpy uint8 arrays)."""
+        import numpy as np
+
+        ys = [np.ascontiguousarray(p, dtype=np.uint8) for p in (y, u, v)]
+        if ys[0].size != self.width * self.height or ys[1].size != self.width * self.height // 4 or ys[2].size != ys[1].size:
+            raise HlAmdError(HL_AMD_ERROR_INVALID_FORMAT, "encode (plane sizes)")
+        r = _Result()
+        rc = self.lib.hl_amd_encode(self._h, ys[0].ctypes.data, ys[1].ctypes.data, ys[2].ctypes.data, ctypes.byref(r))
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_encode")
+        return self._result(r)
+
+    def encode_device(self, y_ptr: int, u_ptr: int, v_ptr: int, collect: bool = True):
+        """Encodes planes already resident in device memory (raw pointers)."""
+        r = _Result()
+        rc = self.lib.hl_amd_encode_device(self._h, ctypes.c_void_p(y_ptr), ctypes.c_void_p(u_ptr), ctypes.c_void_p(v_ptr), ctypes.byref(r))
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_encode_device")
+        return self._result(r) if collect else r.data_size
+
+    def recon(self):
+        import numpy as np
+
+        y = np.empty(self.width * self.height, np.uint8)
+        u = np.empty(self.width * self.height // 4, np.uint8)
+        v = np.empty_like(u)
+        rc = self.lib.hl_amd_get_recon(self._h, y.ctypes.data, u.ctypes.data, v.ctypes.data)
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_get_recon")
+        return y, u, v
+
+    def set_timing(self, on: bool):
+        self.lib.hl_amd_set_timing(self._h, 1 if on else 0)
+
+    def timing_ms(self):
+        a = (ctypes.c_float * 4)()
+        self.lib.hl_amd_get_timing(self._h, a)
+        return list(a)
+
+    def last_reruns(self) -> int:
+        return self.lib.hl_amd_last_reruns(self._h)

@@ -1,0 +1,377 @@
+// hl_encoder.hip -- the gfx950 encode path behind include/hartallo_amd.h.
+//
+// Per frame (hl_codec_264_encode_frame, encode.c:144-527, restated):
+//   1. k_planes      quarter-pel planes of the reference picture (HBM-bound)
+//   2. k_mb_diag     macroblock decisions on an anti-diagonal wavefront:
+//                    MB (x, y) runs after (x-1, y) and (x+1, y-1), i.e. in
+//                    launch d = x + 2y; one 256-lane workgroup per MB
+//   3. row-start validation of the rdo.Single_ctr speculation (host), with a
+//      re-run of the wavefront from the first mispredicted row
+//   4. k_deblock_diag the in-place Baseline deblocking, same wavefront order
+//   5. host CAVLC serialisation of the MB records (hl_writer.cpp)
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/hartallo_amd.h"
+#include "hl_filters.h"
+#include "hl_writer.h"
+
+using namespace hl;
+
+#define HL_HIP_CHECK(x)                                                                  \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) {                                                          \
+            fprintf(stderr, "hartallo_amd: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            return HL_AMD_ERROR_SYSTEM;                                                  \
+        }                                                                                \
+    } while (0)
+
+constexpr int kMbThreads = 256;
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+// Quarter-pel planes: one lane per padded sample, all four planes.
+__global__ __launch_bounds__(256) void k_planes(const uint8_t* __restrict__ ref, int W, int H, uint8_t* pf, uint8_t* pb,
+                                                uint8_t* ph, uint8_t* pj, int pstride)
+{
+    const int PW = W + 2 * kPad, PH = H + 2 * kPad;
+    const int px = blockIdx.x * 64 + (threadIdx.x & 63), py = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (px >= PW || py >= PH) return;
+    const int x = px - kPad, y = py - kPad;
+    const size_t o = (size_t)py * pstride + px;
+    pf[o] = qpel_plane_sample(ref, W, H, 0, x, y);
+    pb[o] = qpel_plane_sample(ref, W, H, 1, x, y);
+    ph[o] = qpel_plane_sample(ref, W, H, 2, x, y);
+    pj[o] = qpel_plane_sample(ref, W, H, 3, x, y);
+}
+
+// macroblocks (x, y) with x + 2 * (y - row0) == diag
+__device__ __forceinline__ void diag_mb(int mbw, int mbh, int row0, int diag, int k, int& x, int& y)
+{
+    const int ylo = std::max(0, (diag - mbw + 2) / 2);
+    const int yy = ylo + k;
+    y = row0 + yy;
+    x = diag - 2 * yy;
+}
+
+__global__ __launch_bounds__(kMbThreads) void k_mb_diag(FrameArgs F, int diag, int row0)
+{
+    __shared__ Shared S;
+    int x, y;
+    diag_mb(F.mbw, F.mbh, row0, diag, blockIdx.x, x, y);
+    const int addr = y * F.mbw + x;
+    const int s_in = x == 0 ? F.spec[y] : F.chain[addr - 1].s_out;
+    encode_mb(F, S, addr, threadIdx.x, kMbThreads, s_in);
+}
+
+__global__ __launch_bounds__(64) void k_deblock_diag(DeblockArgs D, int mbh, int diag)
+{
+    int x, y;
+    diag_mb(D.mbw, mbh, 0, diag, blockIdx.x, x, y);
+    const int addr = y * D.mbw + x;
+    for (int step = 0; step < 8; ++step) {
+        if (threadIdx.x < 32) deblock_mb_step(D, addr, step, threadIdx.x);
+        __syncthreads();
+    }
+}
+
+static int diag_count(int mbw, int rows, int diag)
+{
+    const int ylo = std::max(0, (diag - mbw + 2) / 2);
+    const int yhi = std::min(rows - 1, diag / 2);
+    return yhi >= ylo ? yhi - ylo + 1 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// encoder context
+// ---------------------------------------------------------------------------
+struct hl_amd_encoder_s {
+    hl_amd_params_t p;
+    int W, H, Wc, Hc, mbw, mbh, nmb, qpc, pstride;
+    hipStream_t stream;
+    uint8_t* d_in[3];
+    uint8_t* d_pic[2][3];  // [cur/ref swap][plane]
+    int cur;
+    uint8_t* d_pl[4];
+    MbState *d_st, *d_snap;
+    MbRecord* d_rec;
+    MbChain* d_chain;
+    int32_t* d_spec;
+    MbRecord* h_rec;
+    MbChain* h_chain;
+    int32_t* h_spec;
+    std::vector<uint8_t> hdr, out, scratch;
+    int32_t frame_index, gop_left, pict_count, idr_pic_id, chain_end, reruns;
+    bool timing;
+    hipEvent_t ev[4];
+    float ms[4];
+};
+
+static void free_all(hl_amd_encoder_t* e)
+{
+    for (int c = 0; c < 3; ++c) {
+        (void)hipFree(e->d_in[c]);
+        (void)hipFree(e->d_pic[0][c]);
+        (void)hipFree(e->d_pic[1][c]);
+    }
+    for (int i = 0; i < 4; ++i) (void)hipFree(e->d_pl[i]);
+    (void)hipFree(e->d_st);
+    (void)hipFree(e->d_snap);
+    (void)hipFree(e->d_rec);
+    (void)hipFree(e->d_chain);
+    (void)hipFree(e->d_spec);
+    (void)hipHostFree(e->h_rec);
+    (void)hipHostFree(e->h_chain);
+    (void)hipHostFree(e->h_spec);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    for (int i = 0; i < 4; ++i)
+        if (e->ev[i]) (void)hipEventDestroy(e->ev[i]);
+}
+
+extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encoder_t** out)
+{
+    if (!p || !out) return HL_AMD_ERROR_INVALID_PARAMETER;
+    *out = nullptr;
+    if (p->width <= 0 || p->height <= 0 || (p->width & 15) || (p->height & 15)) return HL_AMD_ERROR_INVALID_FORMAT;
+    if (p->qp < 0 || p->qp > 51) return HL_AMD_ERROR_INVALID_PARAMETER;
+    if (p->me_early_term) return HL_AMD_ERROR_NOT_IMPLEMENTED;
+    HL_HIP_CHECK(hipSetDevice(p->device));
+    hl_amd_encoder_t* e = new hl_amd_encoder_s();
+    e->p = *p;
+    e->W = p->width;
+    e->H = p->height;
+    e->Wc = e->W / 2;
+    e->Hc = e->H / 2;
+    e->mbw = e->W / 16;
+    e->mbh = e->H / 16;
+    e->nmb = e->mbw * e->mbh;
+    e->qpc = kQpToQpc[p->qp];
+    e->pstride = (e->W + 2 * kPad + 63) & ~63;
+    const size_t pls = (size_t)e->pstride * (e->H + 2 * kPad);
+    bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess;
+    for (int c = 0; c < 3 && ok; ++c) {
+        const size_t sz = c ? (size_t)e->Wc * e->Hc : (size_t)e->W * e->H;
+        ok = hipMalloc(&e->d_in[c], sz) == hipSuccess && hipMalloc(&e->d_pic[0][c], sz) == hipSuccess &&
+             hipMalloc(&e->d_pic[1][c], sz) == hipSuccess && hipMemset(e->d_pic[0][c], 0, sz) == hipSuccess &&
+             hipMemset(e->d_pic[1][c], 0, sz) == hipSuccess;
+    }
+    for (int i = 0; i < 4 && ok; ++i) ok = hipMalloc(&e->d_pl[i], pls) == hipSuccess;
+    ok = ok && hipMalloc(&e->d_st, sizeof(MbState) * e->nmb) == hipSuccess && hipMalloc(&e->d_snap, sizeof(MbState) * e->nmb) == hipSuccess &&
+         hipMalloc(&e->d_rec, sizeof(MbRecord) * e->nmb) == hipSuccess && hipMalloc(&e->d_chain, sizeof(MbChain) * e->nmb) == hipSuccess &&
+         hipMalloc(&e->d_spec, sizeof(int32_t) * e->mbh) == hipSuccess &&
+         hipHostMalloc(&e->h_rec, sizeof(MbRecord) * e->nmb, hipHostMallocDefault) == hipSuccess &&
+         hipHostMalloc(&e->h_chain, sizeof(MbChain) * e->nmb, hipHostMallocDefault) == hipSuccess &&
+         hipHostMalloc(&e->h_spec, sizeof(int32_t) * e->mbh, hipHostMallocDefault) == hipSuccess;
+    ok = ok && hipMemset(e->d_st, 0, sizeof(MbState) * e->nmb) == hipSuccess;
+    for (int i = 0; i < 4 && ok; ++i) ok = hipEventCreate(&e->ev[i]) == hipSuccess;
+    if (!ok) {
+        free_all(e);
+        delete e;
+        return HL_AMD_ERROR_OUTOFMEMMORY;
+    }
+    const StreamParams sp{e->W, e->H, p->qp, p->deblock};
+    e->scratch.resize(slice_scratch_bytes(sp));
+    e->out.resize(slice_scratch_bytes(sp) + 64);
+    e->hdr.resize(256);
+    e->hdr.resize(write_stream_headers(sp, e->hdr.data(), e->hdr.size()));
+    *out = e;
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" void hl_amd_encoder_destroy(hl_amd_encoder_t* e)
+{
+    if (!e) return;
+    (void)hipStreamSynchronize(e->stream);
+    free_all(e);
+    delete e;
+}
+
+// Launches the MB wavefront for rows [row0, mbh).
+static hipError_t run_wavefront(hl_amd_encoder_t* e, const FrameArgs& F, int row0)
+{
+    const int rows = e->mbh - row0;
+    const int ndiag = (e->mbw - 1) + 2 * (rows - 1) + 1;
+    for (int d = 0; d < ndiag; ++d) {
+        const int n = diag_count(e->mbw, rows, d);
+        if (!n) continue;
+        k_mb_diag<<<n, kMbThreads, 0, e->stream>>>(F, d, row0);
+    }
+    return hipGetLastError();
+}
+
+// Checks the row-start speculation of rdo.Single_ctr; returns the first row
+// to re-run (and fixes its speculated value) or -1 when the frame is exact.
+static int validate_chain(hl_amd_encoder_t* e, int row0, int& chain_end)
+{
+    int carry = e->h_spec[row0];
+    for (int y = row0; y < e->mbh; ++y) {
+        const MbChain* row = e->h_chain + (size_t)y * e->mbw;
+        if (y > row0 && e->h_spec[y] != carry) {
+            for (int x = 0; x < e->mbw; ++x) {
+                if (row[x].dep) {
+                    e->h_spec[y] = carry;
+                    return y;
+                }
+                if (row[x].fresh) break;
+            }
+        }
+        bool any_fresh = false;
+        for (int x = 0; x < e->mbw && !any_fresh; ++x) any_fresh = row[x].fresh != 0;
+        if (any_fresh) carry = row[e->mbw - 1].s_out;
+    }
+    chain_end = carry;
+    return -1;
+}
+
+static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t* u, const uint8_t* v, hl_amd_result_t* r)
+{
+    const bool intra = e->gop_left <= 0;
+    if (intra) e->gop_left = e->p.gop_size;
+    uint8_t** cur = e->d_pic[e->cur];
+    uint8_t** ref = e->d_pic[e->cur ^ 1];
+    FrameArgs F;
+    F.W = e->W;
+    F.H = e->H;
+    F.Wc = e->Wc;
+    F.Hc = e->Hc;
+    F.mbw = e->mbw;
+    F.mbh = e->mbh;
+    F.qp = e->p.qp;
+    F.qpc = e->qpc;
+    F.is_intra = intra;
+    F.me_range = std::min(64, std::max(1, e->p.me_range));
+    F.lambda = 0.852 * (double)(1 << ((e->p.qp - 12) / 3));
+    F.src[0] = y;
+    F.src[1] = u;
+    F.src[2] = v;
+    for (int c = 0; c < 3; ++c) {
+        F.cur[c] = cur[c];
+        F.ref[c] = ref[c];
+    }
+    for (int i = 0; i < 4; ++i) F.pl[i] = e->d_pl[i];
+    F.pstride = e->pstride;
+    F.st = e->d_st;
+    F.rec = e->d_rec;
+    F.chain = e->d_chain;
+    F.spec = e->d_spec;
+
+    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[0], e->stream));
+    if (!intra) {
+        dim3 grid((e->W + 2 * kPad + 63) / 64, (e->H + 2 * kPad + 3) / 4);
+        k_planes<<<grid, 256, 0, e->stream>>>(ref[0], e->W, e->H, e->d_pl[0], e->d_pl[1], e->d_pl[2], e->d_pl[3], e->pstride);
+        HL_HIP_CHECK(hipGetLastError());
+    }
+    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[1], e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(e->d_snap, e->d_st, sizeof(MbState) * e->nmb, hipMemcpyDeviceToDevice, e->stream));
+    e->h_spec[0] = e->chain_end;
+    for (int yy = 1; yy < e->mbh; ++yy) e->h_spec[yy] = 9;
+    int row0 = 0, chain_end = 0;
+    e->reruns = 0;
+    for (;;) {
+        HL_HIP_CHECK(hipMemcpyAsync(e->d_spec, e->h_spec, sizeof(int32_t) * e->mbh, hipMemcpyHostToDevice, e->stream));
+        HL_HIP_CHECK(run_wavefront(e, F, row0));
+        HL_HIP_CHECK(hipMemcpyAsync(e->h_chain, e->d_chain, sizeof(MbChain) * e->nmb, hipMemcpyDeviceToHost, e->stream));
+        HL_HIP_CHECK(hipStreamSynchronize(e->stream));
+        const int bad = validate_chain(e, row0, chain_end);
+        if (bad < 0) break;
+        ++e->reruns;
+        const size_t off = (size_t)bad * e->mbw;
+        HL_HIP_CHECK(hipMemcpyAsync(e->d_st + off, e->d_snap + off, sizeof(MbState) * (e->nmb - off), hipMemcpyDeviceToDevice, e->stream));
+        row0 = bad;
+    }
+    e->chain_end = chain_end;
+    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[2], e->stream));
+    if (e->p.deblock) {
+        DeblockArgs D;
+        D.W = e->W;
+        D.H = e->H;
+        D.Wc = e->Wc;
+        D.mbw = e->mbw;
+        D.qp = e->p.qp;
+        D.qpc = e->qpc;
+        for (int c = 0; c < 3; ++c) D.pic[c] = cur[c];
+        D.st = e->d_st;
+        const int ndiag = (e->mbw - 1) + 2 * (e->mbh - 1) + 1;
+        for (int d = 0; d < ndiag; ++d) {
+            const int n = diag_count(e->mbw, e->mbh, d);
+            if (n) k_deblock_diag<<<n, 64, 0, e->stream>>>(D, e->mbh, d);
+        }
+        HL_HIP_CHECK(hipGetLastError());
+    }
+    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[3], e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(e->h_rec, e->d_rec, sizeof(MbRecord) * e->nmb, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipStreamSynchronize(e->stream));
+    if (e->timing) {
+        (void)hipEventElapsedTime(&e->ms[0], e->ev[0], e->ev[1]);
+        (void)hipEventElapsedTime(&e->ms[1], e->ev[1], e->ev[2]);
+        (void)hipEventElapsedTime(&e->ms[2], e->ev[2], e->ev[3]);
+        (void)hipEventElapsedTime(&e->ms[3], e->ev[0], e->ev[3]);
+    }
+    const StreamParams sp{e->W, e->H, e->p.qp, e->p.deblock};
+    const SliceState ss{intra ? 1 : 0, e->pict_count, e->idr_pic_id};
+    const size_t n = write_slice(sp, ss, e->h_rec, e->scratch.data(), e->out.data(), e->out.size());
+    if (!n) return HL_AMD_ERROR_TOOSHORT;
+    r->type = HL_AMD_RESULT_TYPE_DATA;
+    r->data = e->out.data() + 3;
+    r->data_size = n - 3;
+    r->hdr = e->hdr.data();
+    r->hdr_size = e->hdr.size();
+    if (e->frame_index == 0) r->type |= HL_AMD_RESULT_TYPE_HDR;
+    // the reconstructed picture becomes RefPicList0[0]
+    e->cur ^= 1;
+    ++e->pict_count;
+    if (intra) ++e->idr_pic_id;
+    --e->gop_left;
+    ++e->frame_index;
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_encode_device(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t* u, const uint8_t* v, hl_amd_result_t* r)
+{
+    if (!e || !y || !u || !v || !r) return HL_AMD_ERROR_INVALID_PARAMETER;
+    return encode_frame(e, y, u, v, r);
+}
+
+extern "C" int32_t hl_amd_encode(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t* u, const uint8_t* v, hl_amd_result_t* r)
+{
+    if (!e || !y || !u || !v || !r) return HL_AMD_ERROR_INVALID_PARAMETER;
+    HL_HIP_CHECK(hipMemcpyAsync(e->d_in[0], y, (size_t)e->W * e->H, hipMemcpyHostToDevice, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(e->d_in[1], u, (size_t)e->Wc * e->Hc, hipMemcpyHostToDevice, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(e->d_in[2], v, (size_t)e->Wc * e->Hc, hipMemcpyHostToDevice, e->stream));
+    return encode_frame(e, e->d_in[0], e->d_in[1], e->d_in[2], r);
+}
+
+extern "C" int32_t hl_amd_get_recon(hl_amd_encoder_t* e, uint8_t* y, uint8_t* u, uint8_t* v)
+{
+    if (!e || !y || !u || !v) return HL_AMD_ERROR_INVALID_PARAMETER;
+    uint8_t** ref = e->d_pic[e->cur ^ 1];
+    HL_HIP_CHECK(hipMemcpyAsync(y, ref[0], (size_t)e->W * e->H, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(u, ref[1], (size_t)e->Wc * e->Hc, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(v, ref[2], (size_t)e->Wc * e->Hc, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipStreamSynchronize(e->stream));
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_set_timing(hl_amd_encoder_t* e, int32_t enable)
+{
+    if (!e) return HL_AMD_ERROR_INVALID_PARAMETER;
+    e->timing = enable != 0;
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_get_timing(hl_amd_encoder_t* e, float* ms4)
+{
+    if (!e || !ms4) return HL_AMD_ERROR_INVALID_PARAMETER;
+    memcpy(ms4, e->ms, sizeof(e->ms));
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_last_reruns(hl_amd_encoder_t* e) { return e ? e->reruns : -1; }
+
+extern "C" const char* hl_amd_version(void) { return "hartallo_amd 0.1 (gfx950)"; }

@@ -1,0 +1,137 @@
+// hl_filters.h -- picture-level filters of the encode path for gfx950:
+//  * the quarter-pel reference planes (full, b, h, j) of 8.4.2.2.1, padded so
+//    every motion-search fetch is a plain 2D load (pred_inter.c:339-885 and
+//    the clamped index table of interpol.c:74-225 give the edge semantics:
+//    every tap coordinate is clamped to the picture independently);
+//  * the Baseline deblocking filter of one macroblock (8.7, deblock.c:192-3553),
+//    luma and chroma lines in parallel lanes, edges in the reference's order.
+#pragma once
+#include "hl_mbcore.h"
+
+namespace hl {
+
+HD int tap6(int a, int b, int c, int d, int e, int f) { return a - 5 * (b + e) + 20 * (c + d) + f; }
+
+// One sample of the padded plane `plane` at picture coordinates (x, y).
+HD uint8_t qpel_plane_sample(const uint8_t* ref, int W, int H, int plane, int x, int y)
+{
+    auto S = [&](int xx, int yy) -> int { return ref[clip3(0, H - 1, yy) * W + clip3(0, W - 1, xx)]; };
+    auto h1 = [&](int xx) -> int { return tap6(S(xx, y - 2), S(xx, y - 1), S(xx, y), S(xx, y + 1), S(xx, y + 2), S(xx, y + 3)); };
+    switch (plane) {
+    case 0: return (uint8_t)S(x, y);
+    case 1: return (uint8_t)clip255((tap6(S(x - 2, y), S(x - 1, y), S(x, y), S(x + 1, y), S(x + 2, y), S(x + 3, y)) + 16) >> 5);
+    case 2: return (uint8_t)clip255((h1(x) + 16) >> 5);
+    default: return (uint8_t)clip255((tap6(h1(x - 2), h1(x - 1), h1(x), h1(x + 1), h1(x + 2), h1(x + 3)) + 512) >> 10);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Deblocking
+// ---------------------------------------------------------------------------
+// bS of the 4-sample segment between p (in MB P at (px,py)) and q (in MB Q at
+// (qx,qy)), deblock.c:1784-1834.  ref_idx_l0 is never written by the encoder
+// (always 0) and predFlagL0 is 1 for every partition of an inter MB.
+HD int deblock_bs(const MbState& P, const MbState& Q, int px, int py, int qx, int qy, bool mb_edge)
+{
+    if ((P.flags & FL_INTRA) || (Q.flags & FL_INTRA)) return mb_edge ? 4 : 3;
+    if ((P.cbp_l4x4 & (1 << blk_idx(px, py))) || (Q.cbp_l4x4 & (1 << blk_idx(qx, qy)))) return 2;
+    auto part = [](const MbState& m, int x, int y, int& pi, int& spi) {
+        pi = (16 / m.part_w) * (y / m.part_h) + (x / m.part_w);
+        spi = (m.e_type == ET_P8x8 || m.e_type == ET_P8x8REF0) ? (8 / m.sub_w[pi]) * ((y % 8) / m.sub_h[pi]) + ((x % 8) / m.sub_w[pi]) : 0;
+    };
+    int pp, ps, qp, qs;
+    part(P, px, py, pp, ps);
+    part(Q, qx, qy, qp, qs);
+    if (iabs(P.mv[pp][ps][0] - Q.mv[qp][qs][0]) >= 4) return 1;
+    return iabs(P.mv[pp][ps][1] - Q.mv[qp][qs][1]) >= 4 ? 1 : 0;
+}
+
+// Filters one line across an edge; s points at q0, step reaches q1.
+HD void deblock_line(uint8_t* s, int step, int bS, bool chroma, int indexA, int alpha, int beta)
+{
+    const int p0 = s[-step], p1 = s[-2 * step], q0 = s[0], q1 = s[step];
+    const int p2 = chroma ? 0 : s[-3 * step], q2 = chroma ? 0 : s[2 * step];
+    if (!(iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta)) return;
+    const int ap = iabs(p2 - p0), aq = iabs(q2 - q0);
+    if (bS < 4) {
+        const int tc0 = tc0_of(indexA, bS);
+        const int tc = chroma ? tc0 + 1 : tc0 + (ap < beta) + (aq < beta);
+        const int delta = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+        s[-step] = (uint8_t)clip255(p0 + delta);
+        s[0] = (uint8_t)clip255(q0 - delta);
+        if (!chroma && ap < beta) s[-2 * step] = (uint8_t)(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
+        if (!chroma && aq < beta) s[step] = (uint8_t)(q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));
+    }
+    else {
+        const int p3 = chroma ? 0 : s[-4 * step], q3 = chroma ? 0 : s[3 * step];
+        const bool strong = iabs(p0 - q0) < ((alpha >> 2) + 2);
+        if (!chroma && ap < beta && strong) {
+            s[-step] = (uint8_t)((p2 + (p1 << 1) + (p0 << 1) + (q0 << 1) + q1 + 4) >> 3);
+            s[-2 * step] = (uint8_t)((p2 + p1 + p0 + q0 + 2) >> 2);
+            s[-3 * step] = (uint8_t)(((p3 << 1) + (p2 << 1) + p2 + p1 + p0 + q0 + 4) >> 3);
+        }
+        else {
+            s[-step] = (uint8_t)(((p1 << 1) + p0 + q1 + 2) >> 2);
+        }
+        if (!chroma && aq < beta && strong) {
+            s[0] = (uint8_t)((p1 + (p0 << 1) + (q0 << 1) + (q1 << 1) + q2 + 4) >> 3);
+            s[step] = (uint8_t)((p0 + q0 + q1 + q2 + 2) >> 2);
+            s[2 * step] = (uint8_t)(((q3 << 1) + (q2 << 1) + q2 + q1 + q0 + p0 + 4) >> 3);
+        }
+        else {
+            s[0] = (uint8_t)(((q1 << 1) + q0 + p1 + 2) >> 2);
+        }
+    }
+}
+
+struct DeblockArgs {
+    int32_t W, H, Wc, mbw, qp, qpc;
+    uint8_t* pic[3];
+    const MbState* st;
+};
+
+// Step `step` (0..7) of the deblocking of macroblock `addr` for lane `lane`
+// (0..31): lanes 0-15 filter the luma lines of luma edge `step`
+// (vertical 0,4,8,12 then horizontal 0,4,8,12), lanes 16-31 the chroma
+// lines of chroma edge `step` (vertical 0,4 then horizontal 0,4; steps 0-3).
+HD void deblock_mb_step(const DeblockArgs& D, int addr, int step, int lane)
+{
+    const int mbx = addr % D.mbw, mby = addr / D.mbw;
+    const MbState& Q = D.st[addr];
+    const bool internal = !((Q.e_type == ET_P16x16 || (Q.flags & FL_SKIP)) && !Q.cbp_l);
+    const bool chroma = lane >= 16;
+    int vert, edge;
+    if (!chroma) {
+        vert = step < 4;
+        edge = (step & 3) * 4;
+    }
+    else {
+        if (step >= 4) return;
+        vert = step < 2;
+        edge = (step & 1) * 4;
+    }
+    const bool mb_edge = edge == 0;
+    if (mb_edge && (vert ? mbx == 0 : mby == 0)) return;
+    if (!mb_edge && !internal) return;
+    const MbState& P = mb_edge ? (vert ? D.st[addr - 1] : D.st[addr - D.mbw]) : Q;
+    if (!chroma) {
+        const int i = lane, k = i >> 2;
+        const int bS = vert ? deblock_bs(P, Q, mb_edge ? 12 : edge - 4, k * 4, edge, k * 4, mb_edge)
+                            : deblock_bs(P, Q, k * 4, mb_edge ? 12 : edge - 4, k * 4, edge, mb_edge);
+        if (!bS) return;
+        const int indexA = clip3(0, 51, D.qp);
+        uint8_t* s = vert ? D.pic[0] + (mby * 16 + i) * D.W + mbx * 16 + edge : D.pic[0] + (mby * 16 + edge) * D.W + mbx * 16 + i;
+        deblock_line(s, vert ? 1 : D.W, bS, false, indexA, kAlpha[indexA], kBeta[indexA]);
+    }
+    else {
+        const int comp = (lane - 16) >> 3, i = (lane - 16) & 7, k = i >> 1, ledge = edge * 2;
+        const int bS = vert ? deblock_bs(P, Q, mb_edge ? 12 : ledge - 4, k * 4, ledge, k * 4, mb_edge)
+                            : deblock_bs(P, Q, k * 4, mb_edge ? 12 : ledge - 4, k * 4, ledge, mb_edge);
+        if (!bS) return;
+        const int indexA = clip3(0, 51, D.qpc);
+        uint8_t* s = vert ? D.pic[1 + comp] + (mby * 8 + i) * D.Wc + mbx * 8 + edge : D.pic[1 + comp] + (mby * 8 + edge) * D.Wc + mbx * 8 + i;
+        deblock_line(s, vert ? 1 : D.Wc, bS, true, indexA, kAlpha[indexA], kBeta[indexA]);
+    }
+}
+
+}  // namespace hl

@@ -1,0 +1,1912 @@
+// hl_mbcore.h -- one macroblock of the reference's RDO encode loop, written
+// for one gfx950 workgroup per macroblock.
+//
+// Scope (reference paths relative to source/h264/):
+//   P-MB decision      hl_codec_264_rdo.c:678-1271   guess_inter()
+//   diamond search     hl_codec_264_me_ds.c:104-477  search_partition()
+//   candidate cost     hl_codec_264_me_ds.c:527-688  eval_candidates()
+//   intra decision     hl_codec_264_rdo.c:99-299, 1526-2136 guess_intra()
+//   reconstruction     hl_codec_264_rdo.c:2140-2782
+//   MV prediction      hl_codec_264_utils.c:709-963, hl_codec_264_mb.c:426-541
+//
+// Execution model.  Control flow is uniform: every lane runs the same loop
+// nest (partitions, diamond steps, intra modes) and computes the same scalar
+// decisions from LDS, so they live in SGPRs.  Data-parallel phases are
+// strided loops over (candidate x 4x4 block), (mode x block) or pixels,
+// separated by HL_SYNC().  Built for the host with nthr = 1 the same code
+// runs serially; that build is only used by tests/ to diff the kernel logic
+// against the oracle without a GPU.
+//
+// Order-dependent reference state is reproduced exactly:
+//  * TotalCoeffsLuma of the live MB is rewritten by every trial CAVLC call
+//    (residual.c:796-806); the nC a candidate sees depends on all candidates
+//    evaluated before it.  eval_candidates() resolves this with a
+//    last-writer lookup over the candidates of the step.
+//  * CodedBlockPatternLuma of the live MB is stale (previous frame) during
+//    the search (utils.h:9-20).
+//  * pc_esd->rdo.Single_ctr is one encoder-global counter read stale by the
+//    I16x16 RDO; it is carried in Ctx::chain and recorded in MbChain so the
+//    host can validate row-start speculation.
+#pragma once
+#include "hl_prims.h"
+#include "hl_types.h"
+
+namespace hl {
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define HL_SYNC() __syncthreads()
+#else
+#define HL_SYNC() ((void)0)
+#endif
+
+constexpr int kPad = 40;  // padding of the luma reference planes (origin clip is +-17, block 16, tap 3)
+constexpr int kNA = -1;   // not-available sample marker
+
+struct FrameArgs {
+    int32_t W, H, Wc, Hc, mbw, mbh;
+    int32_t qp, qpc, is_intra, me_range;
+    double lambda;
+    const uint8_t* src[3];
+    uint8_t* cur[3];
+    const uint8_t* ref[3];  // ref[0] unused (luma goes through pl[])
+    const uint8_t* pl[4];   // padded luma reference: full, half-h (b), half-v (h), centre (j)
+    int32_t pstride;
+    MbState* st;
+    MbRecord* rec;
+    MbChain* chain;
+    const int32_t* spec;  // speculated Single_ctr at each row start
+};
+
+struct NbInfo {
+    int32_t avail, intra, e_type, part_w, part_h;
+    int32_t sub_w[4], sub_h[4];
+    int16_t mv[4][4][2];
+};
+
+struct PartDef {
+    int8_t num_part, num_sub, sub_w, sub_h, part_w, part_h, hdr_bits, sub_type;
+};
+// Partition families searched by guess_inter (rdo.c:731-760), in order.
+static constexpr PartDef kParts[7] = {
+    {1, 1, 16, 16, 16, 16, 3, -1}, {2, 1, 16, 8, 16, 8, 5, -1}, {2, 1, 8, 16, 8, 16, 5, -1},
+    {4, 1, 8, 8, 8, 8, 11, 0},     {4, 2, 8, 4, 8, 8, 19, 1},   {4, 2, 4, 8, 8, 8, 19, 2},
+    {4, 4, 4, 4, 8, 8, 27, 3}};
+
+struct Shared {
+    NbInfo nb[5];  // 0 = current MB (live search state), 1 = A, 2 = B, 3 = C, 4 = D
+    int32_t nb_pm0[3];
+    int8_t nb_i4[3][16];
+    int8_t extA[16], extB[16];  // luma nC from the neighbouring MB (-1 = not available, -2 = inside MB)
+    int8_t extCA[4], extCB[4];  // chroma AC nC from neighbouring MBs
+    uint8_t src[256];
+    uint8_t srcc[2][64];
+    uint8_t rec[256];     // current MB luma recon (intra neighbours read it)
+    int16_t top[25];      // luma row y=-1, x=-1..23 (kNA when not available)
+    int16_t left[16];     // luma column x=-1
+    int16_t ctop[2][9];   // chroma row y=-1, x=-1..7
+    int16_t cleft[2][8];
+    int8_t tc[16];        // live TotalCoeffsLuma
+    int8_t tcc[2][4];     // live TotalCoeffsChromaACCbCr
+    int16_t cac[2][4][16];// live ChromaACLevel
+    int32_t cbp_l, cbp_c; // live CodedBlockPattern{Luma,Chroma}
+    // --- candidate step scratch
+    int16_t cmv[16][2];
+    int32_t be_nz[9][16], be_tc[9][16], be_t1[9][16], be_sctr[9][16], be_bits[9][16], be_dist[9][16];
+    int32_t cd_bits[9], cd_dist[9], cd_single[9], cd_cbp[9], cd_last[9];
+    // --- per (sub)partition search results
+    double bcost[4][4];
+    int32_t bdist[4][4], bsingle[4][4], bcbp[4][4];
+    int16_t bmv[4][4][2], bmvp[4][4][2];
+    // --- best inter decision
+    int16_t best_mv[4][4][2], best_mvp[4][4][2];
+    // --- intra scratch
+    int32_t pred[256];
+    int32_t i16_ac[16][16], i16_dc[16], i16_dcc[16];
+    int32_t i16_called[16], i16_tc[16], i16_t1[16], i16_sctr[16], i16_bits[16], i16_dist[16];
+    int16_t i16_best_ac[16][16], i16_best_dc[16];
+    uint8_t i16_best_rec[256], tmp_rec[256];
+    int32_t i4_cost_ok[9], i4_exact[9], i4_nz[9], i4_tc[9], i4_sctr[9], i4_dist[9];
+    double i4_cost[9];
+    int16_t i4_lv[9][16];
+    uint8_t i4_rec[9][16];
+    int32_t luma_level[16][16];
+    int32_t predc[2][64];
+    int32_t cres_dc[2][4], cres_cac[2][4], cres_cdc[2][4], cres_tc[2][4], cres_sctr[2][4];
+    int32_t cdc_level[2][4];
+    // --- live MB decision fields
+    int32_t flags, pm0, e_type, mb_type, i16mode, chroma_mode, cbp, cbp_l4x4, cbp_cac[2], cbp_cdc[2];
+    int32_t num_part, num_sub[4], sub_type[4];
+    int8_t i4mode[16], prev_flag[16], rem_mode[16];
+    int16_t mvd[4][4][2];
+    int8_t nc_luma[16], nc_cac[2][4], nc_dc;
+};
+
+struct Ctx {
+    const FrameArgs& F;
+    Shared& S;
+    int tid, nthr;
+    int addr, mbx, mby, xL, yL;
+    int chain, fresh, dep;  // rdo.Single_ctr emulation (uniform)
+};
+
+// --------------------------------------------------------------------------
+// small helpers
+// --------------------------------------------------------------------------
+HD int ue_len(unsigned v)
+{
+    int lz = 0;
+    while ((1u << (lz + 1)) <= v + 1) ++lz;
+    return 2 * lz + 1;
+}
+HD int se_len(int n) { return ue_len(n <= 0 ? (unsigned)(-n) << 1 : ((unsigned)n << 1) - 1); }
+
+HD void chain_write(Ctx& c, int sctr)
+{
+    c.chain = sctr;
+    c.fresh = 1;
+}
+
+// Luma 4x4 prediction from the padded quarter-pel planes for integer origin
+// (X, Y) and fraction (xF, yF) -- the 16 cases of 8.4.2.2.1 as computed by
+// interpol.h:162-925 (planes: 0 full, 1 b, 2 h, 3 j).
+static constexpr int8_t kQpelTab[16][6] = {
+    {0, 0, 0, -1, 0, 0}, {0, 0, 0, 1, 0, 0}, {1, 0, 0, -1, 0, 0}, {0, 1, 0, 1, 0, 0},
+    {0, 0, 0, 2, 0, 0},  {1, 0, 0, 2, 0, 0}, {1, 0, 0, 3, 0, 0},  {1, 0, 0, 2, 1, 0},
+    {2, 0, 0, -1, 0, 0}, {2, 0, 0, 3, 0, 0}, {3, 0, 0, -1, 0, 0}, {3, 0, 0, 2, 1, 0},
+    {0, 0, 1, 2, 0, 0},  {2, 0, 0, 1, 0, 1}, {3, 0, 0, 1, 0, 1},  {2, 1, 0, 1, 0, 1}};
+
+HD void pred_luma4x4(const FrameArgs& F, int X, int Y, int xF, int yF, int* p)
+{
+    const int ph = (yF << 2) | xF;
+    const int s = F.pstride;
+    const uint8_t* p1 = F.pl[kQpelTab[ph][0]] + (Y + kPad + kQpelTab[ph][2]) * s + X + kPad + kQpelTab[ph][1];
+    if (kQpelTab[ph][3] < 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) p[j * 4 + i] = p1[j * s + i];
+    }
+    else {
+        const uint8_t* p2 = F.pl[kQpelTab[ph][3]] + (Y + kPad + kQpelTab[ph][5]) * s + X + kPad + kQpelTab[ph][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) p[j * 4 + i] = (p1[j * s + i] + p2[j * s + i] + 1) >> 1;
+    }
+}
+
+// --------------------------------------------------------------------------
+// neighbour derivation (6.4.12, utils.c:61-230)
+// --------------------------------------------------------------------------
+// Which MB holds luma/chroma location (xN, yN) relative to the current MB:
+// 0 current, 1 A, 2 B, 3 C, 4 D, -1 not available.
+HD int nb_loc(const Shared& S, int xN, int yN, int maxW, int maxH, int& xW, int& yW)
+{
+    int w;
+    if (xN >= 0 && xN < maxW && yN >= 0 && yN < maxH) w = 0;
+    else if (xN >= 0 && xN < maxW && yN < 0) w = 2;
+    else if (xN >= maxW && yN < 0) w = 3;
+    else if (xN < 0 && yN < 0) w = 4;
+    else if (xN < 0 && yN >= 0 && yN < maxH) w = 1;
+    else w = -1;
+    if (w > 0 && !S.nb[w].avail) w = -1;
+    xW = (xN + maxW) % maxW;
+    yW = (yN + maxH) % maxH;
+    return w;
+}
+
+HD bool is8x8(int et) { return et == ET_P8x8 || et == ET_P8x8REF0; }
+
+HD void sub_part_idx(const NbInfo& n, int xW, int yW, int& pi, int& spi)  // mb.h:313-339
+{
+    if (n.intra) pi = 0;
+    else pi = (16 / n.part_w) * (yW / n.part_h) + (xW / n.part_w);
+    if (!is8x8(n.e_type)) spi = 0;
+    else spi = (8 / n.sub_w[pi]) * ((yW % 8) / n.sub_h[pi]) + ((xW % 8) / n.sub_w[pi]);
+}
+
+struct NbPart {
+    int w, pi, spi;
+};
+
+// 8.4.1.3.2 neighbouring partitions + motion data (utils.c:854-963)
+HD void nb_motion(const Shared& S, int pi, int spi, NbPart nb[4], int mv[4][2], int ref[4])
+{
+    const NbInfo& cur = S.nb[0];
+    const int x = (pi % (16 / cur.part_w)) * cur.part_w;
+    const int y = (pi / (16 / cur.part_w)) * cur.part_h;
+    int xS = 0, yS = 0, ppw;
+    if (is8x8(cur.e_type)) {
+        xS = (spi % (8 / cur.sub_w[pi])) * cur.sub_w[pi];
+        yS = (spi / (8 / cur.sub_w[pi])) * cur.sub_h[pi];
+    }
+    if (cur.e_type == ET_PSKIP) ppw = 16;
+    else if (is8x8(cur.e_type)) ppw = cur.sub_w[pi];
+    else ppw = cur.part_w;
+    const int xd[4] = {-1, 0, ppw, -1}, yd[4] = {0, -1, -1, -1};
+    for (int N = 0; N < 4; ++N) {
+        int xW, yW;
+        const int w = nb_loc(S, x + xS + xd[N], y + yS + yd[N], 16, 16, xW, yW);
+        nb[N].w = w;
+        nb[N].pi = nb[N].spi = -1;
+        if (w >= 0) {
+            int p, sp;
+            sub_part_idx(S.nb[w], xW, yW, p, sp);
+            if (w == 0 && (p > pi || (p == pi && sp > spi))) nb[N].w = -1;
+            else {
+                nb[N].pi = p;
+                nb[N].spi = sp;
+            }
+        }
+    }
+    if (nb[2].w < 0) nb[2] = nb[3];
+    for (int N = 0; N < 4; ++N) {
+        if (nb[N].w < 0 || S.nb[nb[N].w].intra) {
+            mv[N][0] = mv[N][1] = 0;
+            ref[N] = -1;
+        }
+        else {
+            mv[N][0] = S.nb[nb[N].w].mv[nb[N].pi][nb[N].spi][0];
+            mv[N][1] = S.nb[nb[N].w].mv[nb[N].pi][nb[N].spi][1];
+            ref[N] = 0;  // RefIdxL0 is always 0 with one reference frame
+        }
+    }
+}
+
+HD int median3(int a, int b, int c)
+{
+    const int mx = a > b ? (a > c ? a : c) : (b > c ? b : c);
+    const int mn = a < b ? (a < c ? a : c) : (b < c ? b : c);
+    return a + b + c - mx - mn;
+}
+
+// 8.4.1.3 (utils.c:751-831)
+HD void mvp(const Shared& S, int pi, int spi, int out[2])
+{
+    NbPart nb[4];
+    int mv[4][2], ref[4];
+    nb_motion(S, pi, spi, nb, mv, ref);
+    const NbInfo& cur = S.nb[0];
+    int sel = -1;
+    if (cur.part_w == 16 && cur.part_h == 8 && pi == 0 && ref[1] == 0) sel = 1;
+    else if (cur.part_w == 16 && cur.part_h == 8 && pi == 1 && ref[0] == 0) sel = 0;
+    else if (cur.part_w == 8 && cur.part_h == 16 && pi == 0 && ref[0] == 0) sel = 0;
+    else if (cur.part_w == 8 && cur.part_h == 16 && pi == 1 && ref[2] == 0) sel = 2;
+    if (sel >= 0) {
+        out[0] = mv[sel][0];
+        out[1] = mv[sel][1];
+        return;
+    }
+    if (nb[1].w < 0 && nb[2].w < 0 && nb[0].w >= 0) {
+        mv[1][0] = mv[2][0] = mv[0][0];
+        mv[1][1] = mv[2][1] = mv[0][1];
+        ref[1] = ref[2] = ref[0];
+    }
+    if (ref[0] == 0 && ref[1] != 0 && ref[2] != 0) sel = 0;
+    else if (ref[1] == 0 && ref[2] != 0 && ref[0] != 0) sel = 1;
+    else if (ref[2] == 0 && ref[1] != 0 && ref[0] != 0) sel = 2;
+    if (sel >= 0) {
+        out[0] = mv[sel][0];
+        out[1] = mv[sel][1];
+        return;
+    }
+    out[0] = median3(mv[0][0], mv[1][0], mv[2][0]);
+    out[1] = median3(mv[0][1], mv[1][1], mv[2][1]);
+}
+
+// 8.4.1.1 P_Skip motion vector (utils.c:709-748)
+HD void skip_mv(const Shared& S, int out[2])
+{
+    NbPart nb[4];
+    int mv[4][2], ref[4];
+    nb_motion(S, 0, 0, nb, mv, ref);
+    if (nb[0].w < 0 || nb[1].w < 0 || (ref[0] == 0 && !mv[0][0] && !mv[0][1]) || (ref[1] == 0 && !mv[1][0] && !mv[1][1])) {
+        out[0] = out[1] = 0;
+        return;
+    }
+    mvp(S, 0, 0, out);
+}
+
+// nC of a luma-type block (residual.c:640-755): neighbour values are taken
+// from the external MBs (extA/extB) or, inside the MB, through `inside`.
+template <typename F>
+HD int nc_luma_of(const Shared& S, int bi, F inside)
+{
+    const int bx = kBlkX[bi], by = kBlkY[bi];
+    int nA = 0, nB = 0;
+    bool aA, aB;
+    if (bx == 0) {
+        aA = S.extA[bi] >= 0;
+        nA = aA ? S.extA[bi] : 0;
+    }
+    else {
+        const int ni = blk_idx(bx - 4, by);
+        aA = true;
+        nA = (S.cbp_l & (1 << (ni >> 2))) ? inside(ni) : 0;
+    }
+    if (by == 0) {
+        aB = S.extB[bi] >= 0;
+        nB = aB ? S.extB[bi] : 0;
+    }
+    else {
+        const int ni = blk_idx(bx, by - 4);
+        aB = true;
+        nB = (S.cbp_l & (1 << (ni >> 2))) ? inside(ni) : 0;
+    }
+    if (aA && aB) return (nA + nB + 1) >> 1;
+    if (aA) return nA;
+    if (aB) return nB;
+    return 0;
+}
+// --------------------------------------------------------------------------
+// MB start: load neighbours, source, live state
+// --------------------------------------------------------------------------
+HD void load_nbinfo(const MbState& m, NbInfo& n)
+{
+    n.avail = 1;
+    n.intra = (m.flags & FL_INTRA) ? 1 : 0;
+    n.e_type = m.e_type;
+    n.part_w = m.part_w;
+    n.part_h = m.part_h;
+    for (int i = 0; i < 4; ++i) {
+        n.sub_w[i] = m.sub_w[i];
+        n.sub_h[i] = m.sub_h[i];
+    }
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            n.mv[i][j][0] = m.mv[i][j][0];
+            n.mv[i][j][1] = m.mv[i][j][1];
+        }
+}
+
+HD void mb_begin(Ctx& c)
+{
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    const int tid = c.tid, nthr = c.nthr;
+    const int a = c.addr;
+    const int hasA = c.mbx > 0, hasB = c.mby > 0, hasC = c.mby > 0 && c.mbx < F.mbw - 1, hasD = c.mbx > 0 && c.mby > 0;
+    const int addrs[5] = {a, a - 1, a - F.mbw, a - F.mbw + 1, a - F.mbw - 1};
+    const int av[5] = {1, hasA, hasB, hasC, hasD};
+    // source samples
+    for (int t = tid; t < 256; t += nthr) S.src[t] = F.src[0][(c.yL + (t >> 4)) * F.W + c.xL + (t & 15)];
+    for (int t = tid; t < 128; t += nthr) {
+        const int comp = t >> 6, i = t & 63;
+        S.srcc[comp][i] = F.src[1 + comp][((c.yL >> 1) + (i >> 3)) * F.Wc + (c.xL >> 1) + (i & 7)];
+    }
+    // intra neighbour samples from the (unfiltered) current picture
+    for (int t = tid; t < 25; t += nthr) {
+        const int x = t - 1;
+        int v = kNA;
+        if (x < 0) {
+            if (hasD) v = F.cur[0][(c.yL - 1) * F.W + c.xL - 1];
+        }
+        else if (x < 16) {
+            if (hasB) v = F.cur[0][(c.yL - 1) * F.W + c.xL + x];
+        }
+        else if (x < 20) {
+            if (hasC) v = F.cur[0][(c.yL - 1) * F.W + c.xL + x];
+        }
+        S.top[t] = (int16_t)v;
+    }
+    for (int t = tid; t < 16; t += nthr) S.left[t] = (int16_t)(hasA ? F.cur[0][(c.yL + t) * F.W + c.xL - 1] : kNA);
+    for (int t = tid; t < 18; t += nthr) {
+        const int comp = t / 9, x = t % 9 - 1;
+        int v = kNA;
+        if (x < 0) {
+            if (hasD) v = F.cur[1 + comp][((c.yL >> 1) - 1) * F.Wc + (c.xL >> 1) - 1];
+        }
+        else if (hasB) {
+            v = F.cur[1 + comp][((c.yL >> 1) - 1) * F.Wc + (c.xL >> 1) + x];
+        }
+        S.ctop[comp][x + 1] = (int16_t)v;
+    }
+    for (int t = tid; t < 16; t += nthr) {
+        const int comp = t >> 3, y = t & 7;
+        S.cleft[comp][y] = (int16_t)(hasA ? F.cur[1 + comp][((c.yL >> 1) + y) * F.Wc + (c.xL >> 1) - 1] : kNA);
+    }
+    // neighbour MB summaries
+    for (int t = tid; t < 4; t += nthr) {
+        const int w = t + 1;
+        if (av[w]) load_nbinfo(F.st[addrs[w]], S.nb[w]);
+        else S.nb[w].avail = 0;
+    }
+    for (int t = tid; t < 2; t += nthr) {
+        const int w = t + 1;
+        S.nb_pm0[w] = av[w] ? F.st[addrs[w]].pm0 : 0;
+        for (int i = 0; i < 16; ++i) S.nb_i4[w][i] = av[w] ? F.st[addrs[w]].i4mode[i] : 2;
+    }
+    // external nC contributions (neighbour MBs are final for this frame)
+    for (int t = tid; t < 16; t += nthr) {
+        const int bx = kBlkX[t], by = kBlkY[t];
+        int8_t ea = -2, eb = -2;
+        if (bx == 0) {
+            if (!hasA) ea = -1;
+            else {
+                const MbState& A = F.st[addrs[1]];
+                const int nb = blk_idx(12, by);
+                ea = (A.e_type == ET_PSKIP || !(A.cbp_l & (1 << (nb >> 2)))) ? 0 : A.tc_luma[nb];
+            }
+        }
+        if (by == 0) {
+            if (!hasB) eb = -1;
+            else {
+                const MbState& B = F.st[addrs[2]];
+                const int nb = blk_idx(bx, 12);
+                eb = (B.e_type == ET_PSKIP || !(B.cbp_l & (1 << (nb >> 2)))) ? 0 : B.tc_luma[nb];
+            }
+        }
+        S.extA[t] = ea;
+        S.extB[t] = eb;
+    }
+    // chroma external nC: extCA[c*2 + row], extCB[c*2 + col]
+    for (int t = tid; t < 4; t += nthr) {
+        const int comp = t >> 1, k = t & 1;
+        int8_t ea = -1, eb = -1;
+        if (hasA) {
+            const MbState& A = F.st[addrs[1]];
+            ea = (A.e_type == ET_PSKIP || !(A.cbp_c & 2)) ? 0 : A.tc_cac[comp][k * 2 + 1];
+        }
+        if (hasB) {
+            const MbState& B = F.st[addrs[2]];
+            eb = (B.e_type == ET_PSKIP || !(B.cbp_c & 2)) ? 0 : B.tc_cac[comp][2 + k];
+        }
+        S.extCA[t] = ea;
+        S.extCB[t] = eb;
+    }
+    // live state of this address (stale from the previous frame)
+    const MbState& M = F.st[a];
+    for (int t = tid; t < 16; t += nthr) S.tc[t] = M.tc_luma[t];
+    for (int t = tid; t < 8; t += nthr) S.tcc[t >> 2][t & 3] = M.tc_cac[t >> 2][t & 3];
+    for (int t = tid; t < 128; t += nthr) S.cac[t >> 6][(t >> 4) & 3][t & 15] = M.cac_level[t >> 6][(t >> 4) & 3][t & 15];
+    if (tid == 0) {
+        S.cbp_l = M.cbp_l;
+        S.cbp_c = M.cbp_c;
+        S.cbp_l4x4 = 0;
+        S.cbp_cac[0] = S.cbp_cac[1] = 0;
+        S.cbp_cdc[0] = S.cbp_cdc[1] = 0;
+        S.nb[0].avail = 1;
+        S.nb[0].intra = 0;
+        S.nb[0].e_type = M.e_type;
+        S.num_part = 1;
+        for (int i = 0; i < 4; ++i) {
+            S.num_sub[i] = 1;
+            S.sub_type[i] = -1;
+        }
+        for (int i = 0; i < 16; ++i) {
+            S.i4mode[i] = 2;
+            S.prev_flag[i] = 0;
+            S.rem_mode[i] = 0;
+        }
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) S.mvd[i][j][0] = S.mvd[i][j][1] = 0;
+        S.i16mode = 2;
+        S.chroma_mode = 0;
+        S.mb_type = 0;
+    }
+    HL_SYNC();
+}
+
+// --------------------------------------------------------------------------
+// Inter candidate evaluation (me_ds.c:527-688 for a list of MVs)
+// --------------------------------------------------------------------------
+struct PartGeo {
+    int px, py, pw, ph, nbw, nblk;
+};
+
+// Evaluates S.cmv[0..ncand) for partition g in order.  Leaves per-candidate
+// rbc/dist/single/cbp in S.cd_*, updates S.tc (last writer) and the chain.
+HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand)
+{
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    const int n = ncand * g.nblk;
+    // phase 1: transform / quant / CAVLC statistics / reconstruction per block
+    for (int t = c.tid; t < n; t += c.nthr) {
+        const int ci = t / g.nblk, k = t % g.nblk;
+        const int hx = k % g.nbw, hy = k / g.nbw;
+        const int mvx = S.cmv[ci][0], mvy = S.cmv[ci][1];
+        const int X = clip3(-17, F.W + 17, c.xL + g.px + (mvx >> 2)) + (hx << 2);
+        const int Y = clip3(-17, F.H + 17, c.yL + g.py + (mvy >> 2)) + (hy << 2);
+        const int bx = g.px + (hx << 2), by = g.py + (hy << 2);
+        int pred[16], res[16];
+        pred_luma4x4(F, X, Y, mvx & 3, mvy & 3, pred);
+        bool zero = true;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            res[i] = (int)S.src[(by + (i >> 2)) * 16 + bx + (i & 3)] - pred[i];
+            zero = zero && res[i] == 0;
+        }
+        int nz = 0, dist = 0;
+        CavlcStat st = {0, 0, 0, -1};
+        if (!zero) {
+            int w[16], q[16], lv[16];
+            fwd4x4(res, w);
+            quant4x4(F.qp, false, w, q);
+            bool lz = true;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                lv[i] = q[kZigzag[i]];
+                lz = lz && lv[i] == 0;
+            }
+            if (!lz) {
+                nz = 1;
+                st = cavlc_stat(lv, 16, 15, false);
+                int r[16];
+                dequant_idct(F.qp, q, false, r);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) dist += iabs(res[i] - (clip255(pred[i] + r[i]) - pred[i]));
+            }
+            else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) dist += iabs(res[i]);
+            }
+        }
+        S.be_nz[ci][k] = nz;
+        S.be_tc[ci][k] = st.tc;
+        S.be_t1[ci][k] = st.t1;
+        S.be_sctr[ci][k] = st.sctr;
+        S.be_bits[ci][k] = st.rest;
+        S.be_dist[ci][k] = dist;
+    }
+    HL_SYNC();
+    // phase 2: nC as the reference sees it at this point of the sequence
+    for (int t = c.tid; t < n; t += c.nthr) {
+        const int ci = t / g.nblk, k = t % g.nblk;
+        if (!S.be_nz[ci][k]) continue;
+        const int hx = k % g.nbw, hy = k / g.nbw;
+        const int bi = blk_idx(g.px + (hx << 2), g.py + (hy << 2));
+        const int nC = nc_luma_of(S, bi, [&](int ni) -> int {
+            const int nx = kBlkX[ni] - g.px, ny = kBlkY[ni] - g.py;
+            if (nx >= 0 && ny >= 0 && nx < g.pw && ny < g.ph) {
+                const int kk = (ny >> 2) * g.nbw + (nx >> 2);
+                if (S.be_nz[ci][kk]) return S.be_tc[ci][kk];
+                for (int cj = ci - 1; cj >= 0; --cj)
+                    if (S.be_nz[cj][kk]) return S.be_tc[cj][kk];
+            }
+            return S.tc[ni];
+        });
+        S.be_bits[ci][k] += token_len(nC, S.be_tc[ci][k], S.be_t1[ci][k]);
+    }
+    HL_SYNC();
+    // phase 3: per-candidate sums; live TotalCoeffsLuma = last writer
+    for (int t = c.tid; t < ncand + g.nblk; t += c.nthr) {
+        if (t < ncand) {
+            int bits = 0, dist = 0, single = 0, cbp = 0, last = -1;
+            for (int k = 0; k < g.nblk; ++k) {
+                dist += S.be_dist[t][k];
+                if (S.be_nz[t][k]) {
+                    const int hx = k % g.nbw, hy = k / g.nbw;
+                    bits += S.be_bits[t][k];
+                    single += S.be_sctr[t][k];
+                    cbp |= 1 << blk_idx(g.px + (hx << 2), g.py + (hy << 2));
+                    last = S.be_sctr[t][k];
+                }
+            }
+            S.cd_bits[t] = bits;
+            S.cd_dist[t] = dist;
+            S.cd_single[t] = single;
+            S.cd_cbp[t] = cbp;
+            S.cd_last[t] = last;
+        }
+        else {
+            const int k = t - ncand;
+            const int hx = k % g.nbw, hy = k / g.nbw;
+            const int bi = blk_idx(g.px + (hx << 2), g.py + (hy << 2));
+            for (int cj = ncand - 1; cj >= 0; --cj)
+                if (S.be_nz[cj][k]) {
+                    S.tc[bi] = (int8_t)S.be_tc[cj][k];
+                    break;
+                }
+        }
+    }
+    HL_SYNC();
+    for (int ci = ncand - 1; ci >= 0; --ci)
+        if (S.cd_last[ci] >= 0) {
+            chain_write(c, S.cd_last[ci]);
+            break;
+        }
+}
+
+// Search state of one (sub)partition, uniform across lanes
+struct Best {
+    double cost;
+    int dist, single, cbp, mv[2];
+};
+
+HD double cand_cost(const Ctx& c, int ci, const int pmv[2])
+{
+    const Shared& S = c.S;
+    const int rbc_mv = se_len(S.cmv[ci][0] - pmv[0]) + se_len(S.cmv[ci][1] - pmv[1]);
+    return dadd((double)S.cd_dist[ci], dmul((double)(S.cd_bits[ci] + rbc_mv), c.F.lambda));
+}
+
+// Diamond search of one (sub)partition, me_ds.c:104-477.  Returns true when
+// the P_Skip probe fired (16x16 only).
+HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
+{
+    Shared& S = c.S;
+    const int xP = (pi % (16 / pd.part_w)) * pd.part_w, yP = (pi / (16 / pd.part_w)) * pd.part_h;
+    int xS = 0, yS = 0;
+    if (pd.num_part == 4) {
+        xS = (spi % (8 / pd.sub_w)) * pd.sub_w;
+        yS = (spi / (8 / pd.sub_w)) * pd.sub_h;
+    }
+    PartGeo g;
+    g.px = xP + xS;
+    g.py = yP + yS;
+    g.pw = pd.sub_w;
+    g.ph = pd.sub_h;
+    g.nbw = g.pw >> 2;
+    g.nblk = (g.pw >> 2) * (g.ph >> 2);
+    Best b;
+    b.cost = 1.7976931348623157e308;
+    b.dist = 0x7fffffff;
+    b.single = 9;
+    b.cbp = 0;
+    b.mv[0] = b.mv[1] = 0;
+    bool probably = false;
+    int pmv[2];
+    if (probe) {  // me_ds.c:229-261
+        int smv[2];
+        skip_mv(S, smv);
+        mvp(S, 0, 0, pmv);
+        if (pmv[0] == smv[0] && pmv[1] == smv[1]) {
+            if (c.tid == 0) {
+                S.cmv[0][0] = (int16_t)pmv[0];
+                S.cmv[0][1] = (int16_t)pmv[1];
+            }
+            HL_SYNC();
+            eval_candidates(c, g, 1);
+            if (S.cd_bits[0] == 0 || S.cd_single[0] < 6) {
+                probably = true;
+                b.cost = 0.0;
+                b.single = S.cd_single[0];
+                b.dist = S.cd_dist[0];
+                b.cbp = S.cd_cbp[0];
+                b.mv[0] = pmv[0];
+                b.mv[1] = pmv[1];
+            }
+        }
+    }
+    mvp(S, pi, spi, pmv);
+    // MVP and (0,0) candidates, me_ds.c:280-300
+    const int nc0 = (pmv[0] != 0 || pmv[1] != 0) ? 2 : 1;
+    HL_SYNC();
+    if (c.tid == 0) {
+        S.cmv[0][0] = (int16_t)pmv[0];
+        S.cmv[0][1] = (int16_t)pmv[1];
+        S.cmv[1][0] = S.cmv[1][1] = 0;
+    }
+    HL_SYNC();
+    eval_candidates(c, g, nc0);
+    for (int ci = 0; ci < nc0; ++ci) {
+        const double cost = cand_cost(c, ci, pmv);
+        if (cost < b.cost) {
+            b.cost = cost;
+            b.single = S.cd_single[ci];
+            b.dist = S.cd_dist[ci];
+            b.cbp = S.cd_cbp[ci];
+            b.mv[0] = S.cmv[ci][0];
+            b.mv[1] = S.cmv[ci][1];
+        }
+    }
+    // diamond stages, me_ds.c:302-470
+    static constexpr int8_t kInt[9][2] = {{0, 2}, {-1, 1}, {1, 1}, {-2, 0}, {0, 0}, {2, 0}, {-1, -1}, {1, -1}, {0, -2}};
+    static constexpr int8_t kHalf[5][2] = {{0, 1}, {-1, 0}, {0, -1}, {1, 0}, {0, 0}};
+    static constexpr int8_t kQuar[9][2] = {{-1, 1}, {0, 1}, {1, 1}, {-1, 0}, {0, 0}, {1, 0}, {-1, -1}, {0, -1}, {1, -1}};
+    static constexpr int16_t kMaskInt[9] = {~(16 | 64 | 256 | 128), ~(16 | 32 | 256), ~(16 | 2 | 8 | 64 | 256 | 128),
+                                            ~(16 | 4 | 32 | 128),   ~0,                ~(16 | 2 | 8 | 64),
+                                            ~(16 | 1 | 2 | 128 | 32 | 4), ~(16 | 1 | 2 | 8 | 64 | 4), ~(16 | 4 | 1 | 2)};
+    static constexpr int16_t kMaskHalf[5] = {~(16 | 4), ~(16 | 8), ~(16 | 1), ~(16 | 2), ~0};
+    static constexpr int16_t kMaskQuar[9] = {~(16 | 32 | 256 | 128), ~(16 | 8 | 64 | 128 | 256 | 32), ~(16 | 8 | 1 | 2 | 4 | 32),
+                                             ~(16 | 2 | 4 | 32 | 256 | 128), ~0,                      ~(16 | 1 | 2 | 8 | 64 | 128),
+                                             ~(16 | 2 | 4 | 32),             ~(16 | 1 | 2 | 4 | 8 | 32), ~(16 | 1 | 2 | 8)};
+    const int range = c.F.me_range;
+    int shift = 2, count = 9, flags = 0xFFFFFF;
+    int cx = b.mv[0] >> 2, cy = b.mv[1] >> 2;
+    int left = cx - range, right = cx + range, top = cy - range, bottom = cy + range;
+    int idxsel[9];
+    for (;;) {
+        int ncand = 0;
+        HL_SYNC();
+        for (int i = 0; i < count; ++i) {
+            if (!(flags & (1 << i))) continue;
+            const int dx = shift == 2 ? kInt[i][0] : (shift == 1 ? kHalf[i][0] : kQuar[i][0]);
+            const int dy = shift == 2 ? kInt[i][1] : (shift == 1 ? kHalf[i][1] : kQuar[i][1]);
+            const int mx = cx + dx, my = cy + dy;
+            if (mx < left || mx > right || my < top || my > bottom) continue;
+            if (c.tid == 0) {
+                S.cmv[ncand][0] = (int16_t)(mx << shift);
+                S.cmv[ncand][1] = (int16_t)(my << shift);
+            }
+            idxsel[ncand++] = i;
+        }
+        int best = -1;
+        if (ncand) {
+            HL_SYNC();
+            eval_candidates(c, g, ncand);
+            for (int ci = 0; ci < ncand; ++ci) {
+                const double cost = cand_cost(c, ci, pmv);
+                if (cost < b.cost) {
+                    best = idxsel[ci];
+                    b.cost = cost;
+                    b.single = S.cd_single[ci];
+                    b.dist = S.cd_dist[ci];
+                    b.cbp = S.cd_cbp[ci];
+                    b.mv[0] = S.cmv[ci][0];
+                    b.mv[1] = S.cmv[ci][1];
+                }
+            }
+        }
+        flags = 0xFFFFFF;
+        if (shift == 2 && best == -1) {
+            shift = 1;
+            count = 5;
+            cx = b.mv[0] >> 2;  // integer-pel value used as the half-pel centre (me_ds.c:360)
+            cy = b.mv[1] >> 2;
+        }
+        else if (shift == 1 && best == -1) {
+            shift = 0;
+            count = 9;
+            cx = b.mv[0];
+            cy = b.mv[1];
+        }
+        else if (shift == 0 && best == -1) {
+            break;
+        }
+        else {
+            cx = b.mv[0] >> shift;
+            cy = b.mv[1] >> shift;
+            flags &= shift == 2 ? kMaskInt[best] : (shift == 1 ? kMaskHalf[best] : kMaskQuar[best]);
+            continue;
+        }
+        left = cx - range;
+        right = cx + range;
+        top = cy - range;
+        bottom = cy + range;
+    }
+    HL_SYNC();
+    if (c.tid == 0) {
+        S.bcost[pi][spi] = b.cost;
+        S.bdist[pi][spi] = b.dist;
+        S.bsingle[pi][spi] = b.single;
+        S.bcbp[pi][spi] = b.cbp;
+        S.bmv[pi][spi][0] = (int16_t)b.mv[0];
+        S.bmv[pi][spi][1] = (int16_t)b.mv[1];
+        S.bmvp[pi][spi][0] = (int16_t)pmv[0];
+        S.bmvp[pi][spi][1] = (int16_t)pmv[1];
+        S.nb[0].mv[pi][spi][0] = (int16_t)b.mv[0];  // MvL0 feeds the MVP of later partitions
+        S.nb[0].mv[pi][spi][1] = (int16_t)b.mv[1];
+    }
+    HL_SYNC();
+    return probably;
+}
+
+// --------------------------------------------------------------------------
+// Intra prediction (8.3, pred_intra.c:326-1220)
+// --------------------------------------------------------------------------
+// luma sample at (x, y) relative to the MB origin as intra prediction sees it
+HD int intra_sample(const Shared& S, int x, int y)
+{
+    if (y < 0) return S.top[x + 1];
+    if (x < 0) return S.left[y];
+    return S.rec[y * 16 + x];
+}
+
+HD void i4_neighbours(const Shared& S, int blk, int p[13])
+{
+    const int xO = kBlkX[blk], yO = kBlkY[blk];
+    for (int i = 0; i < 13; ++i) {
+        const int X = i < 5 ? -1 : i - 5, Y = i < 5 ? i - 1 : -1;
+        const int x = xO + X, y = yO + Y;
+        int v;
+        if (x > 15 && y >= 0) v = kNA;
+        else if (X > 3 && (blk == 3 || blk == 11)) v = kNA;
+        else if (x < 0 && y >= 0) v = S.left[y];
+        else if (y < 0) v = S.top[x + 1];
+        else v = S.rec[y * 16 + x];
+        p[i] = v;
+    }
+    if (p[9] == kNA && p[8] != kNA) p[9] = p[10] = p[11] = p[12] = p[8];
+}
+
+#define HL_P4(x, y) p[(x) == -1 ? (y) + 1 : (x) + 5]
+HD bool i4_avail(int mode, const int p[13])
+{
+    if ((mode == 0 || mode == 3 || mode == 7) && p[5] == kNA) return false;
+    if ((mode == 1 || mode == 8) && p[1] == kNA) return false;
+    if ((mode == 4 || mode == 5 || mode == 6) && p[0] == kNA) return false;
+    return true;
+}
+HD void i4_pred(int mode, const int p[13], int* pr)
+{
+    for (int y = 0; y < 4; ++y)
+        for (int x = 0; x < 4; ++x) {
+            int v;
+            switch (mode) {
+            case 0: v = p[5 + x]; break;
+            case 1: v = p[1 + y]; break;
+            case 2: {
+                const bool xa = p[5] != kNA && p[6] != kNA && p[7] != kNA && p[8] != kNA;
+                const bool ya = p[1] != kNA && p[2] != kNA && p[3] != kNA && p[4] != kNA;
+                if (xa && ya) v = (p[5] + p[6] + p[7] + p[8] + p[1] + p[2] + p[3] + p[4] + 4) >> 3;
+                else if (ya) v = (p[1] + p[2] + p[3] + p[4] + 2) >> 2;
+                else if (xa) v = (p[5] + p[6] + p[7] + p[8] + 2) >> 2;
+                else v = 128;
+                break;
+            }
+            case 3:
+                v = (x == 3 && y == 3) ? (p[11] + 3 * p[12] + 2) >> 2
+                                       : (HL_P4(x + y, -1) + 2 * HL_P4(x + y + 1, -1) + HL_P4(x + y + 2, -1) + 2) >> 2;
+                break;
+            case 4:
+                if (x > y) v = (HL_P4(x - y - 2, -1) + 2 * HL_P4(x - y - 1, -1) + HL_P4(x - y, -1) + 2) >> 2;
+                else if (x < y) v = (HL_P4(-1, y - x - 2) + 2 * HL_P4(-1, y - x - 1) + HL_P4(-1, y - x) + 2) >> 2;
+                else v = (p[5] + 2 * p[0] + p[1] + 2) >> 2;
+                break;
+            case 5: {
+                const int z = 2 * x - y;
+                if (z >= 0 && !(z & 1)) v = (HL_P4(x - (y >> 1) - 1, -1) + HL_P4(x - (y >> 1), -1) + 1) >> 1;
+                else if (z >= 0) v = (HL_P4(x - (y >> 1) - 2, -1) + 2 * HL_P4(x - (y >> 1) - 1, -1) + HL_P4(x - (y >> 1), -1) + 2) >> 2;
+                else if (z == -1) v = (p[1] + 2 * p[0] + p[5] + 2) >> 2;
+                else v = (HL_P4(-1, y - 1) + 2 * HL_P4(-1, y - 2) + HL_P4(-1, y - 3) + 2) >> 2;
+                break;
+            }
+            case 6: {
+                const int z = 2 * y - x;
+                if (z >= 0 && !(z & 1)) v = (HL_P4(-1, y - (x >> 1) - 1) + HL_P4(-1, y - (x >> 1)) + 1) >> 1;
+                else if (z >= 0) v = (HL_P4(-1, y - (x >> 1) - 2) + 2 * HL_P4(-1, y - (x >> 1) - 1) + HL_P4(-1, y - (x >> 1)) + 2) >> 2;
+                else if (z == -1) v = (p[1] + 2 * p[0] + p[5] + 2) >> 2;
+                else v = (HL_P4(x - 1, -1) + 2 * HL_P4(x - 2, -1) + HL_P4(x - 3, -1) + 2) >> 2;
+                break;
+            }
+            case 7:
+                if (y == 0) v = (HL_P4(x, -1) + HL_P4(x + 1, -1) + 1) >> 1;
+                else if (y == 2) v = (HL_P4(x + 1, -1) + HL_P4(x + 2, -1) + 1) >> 1;
+                else if (y == 1) v = (HL_P4(x, -1) + 2 * HL_P4(x + 1, -1) + HL_P4(x + 2, -1) + 2) >> 2;
+                else v = (HL_P4(x + 1, -1) + 2 * HL_P4(x + 2, -1) + HL_P4(x + 3, -1) + 2) >> 2;
+                break;
+            default: {
+                const int z = x + 2 * y;
+                if (z == 0 || z == 2 || z == 4) v = (HL_P4(-1, y + (x >> 1)) + HL_P4(-1, y + (x >> 1) + 1) + 1) >> 1;
+                else if (z == 1 || z == 3) v = (HL_P4(-1, y + (x >> 1)) + 2 * HL_P4(-1, y + (x >> 1) + 1) + HL_P4(-1, y + (x >> 1) + 2) + 2) >> 2;
+                else if (z == 5) v = (p[3] + 3 * p[4] + 2) >> 2;
+                else v = p[4];
+                break;
+            }
+            }
+            pr[y * 4 + x] = v;
+        }
+}
+
+// Intra16x16 prediction of sample (x, y) (pred_intra.c:855-1041); p33 layout
+// is S.top / S.left.
+HD int i16_pred(const Shared& S, int mode, int x, int y, int dcv, int pa, int pb, int pc)
+{
+    if (mode == 0) return S.top[1 + x];
+    if (mode == 1) return S.left[y];
+    if (mode == 2) return dcv;
+    return clip255((pa + pb * (x - 7) + pc * (y - 7) + 16) >> 5);
+    (void)pc;
+}
+HD void i16_params(const Shared& S, int mode, int& dcv, int& pa, int& pb, int& pc)
+{
+    dcv = pa = pb = pc = 0;
+    if (mode == 2) {
+        bool xa = true, ya = true;
+        int xs = 0, ys = 0;
+        for (int x = 0; x < 16; ++x) {
+            if (S.top[1 + x] == kNA) {
+                xa = false;
+                break;
+            }
+            xs += S.top[1 + x];
+        }
+        for (int y = 0; y < 16; ++y) {
+            if (S.left[y] == kNA) {
+                ya = false;
+                break;
+            }
+            ys += S.left[y];
+        }
+        if (xa && ya) dcv = (xs + ys + 16) >> 5;
+        else if (ya) dcv = (ys + 8) >> 4;
+        else if (xa) dcv = (xs + 8) >> 4;
+        else dcv = 128;
+    }
+    else if (mode == 3) {
+        int H = 0, V = 0;
+        for (int i = 0; i < 7; ++i) {
+            H += (i + 1) * (S.top[1 + 8 + i] - S.top[1 + 6 - i]);
+            V += (i + 1) * (S.left[8 + i] - S.left[6 - i]);
+        }
+        H += 8 * (S.top[16] - S.top[0]);
+        V += 8 * (S.left[15] - S.top[0]);
+        pa = (S.left[15] + S.top[16]) << 4;
+        pb = (5 * H + 32) >> 6;
+        pc = (5 * V + 32) >> 6;
+    }
+}
+
+// --------------------------------------------------------------------------
+// Chroma reconstruction (rdo.c:2502-2701 + transf.c:161-294)
+// --------------------------------------------------------------------------
+// S.predc holds the chroma prediction; writes recon to the picture.
+HD void reconstruct_chroma(Ctx& c, bool intra_flag)
+{
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    for (int t = c.tid; t < 8; t += c.nthr) {
+        const int comp = t >> 2, b = t & 3, xO = (b & 1) * 4, yO = (b >> 1) * 4;
+        int res[16];
+        bool zero = true;
+        for (int i = 0; i < 16; ++i) {
+            const int o = (yO + (i >> 2)) * 8 + xO + (i & 3);
+            res[i] = (int)S.srcc[comp][o] - S.predc[comp][o];
+            zero = zero && res[i] == 0;
+        }
+        int dc = 0, cacb = 0, cdcb = 0;
+        CavlcStat st = {0, 0, 0, -1};
+        if (!zero) {
+            int w[16], q[16];
+            fwd4x4(res, w);
+            quant4x4(F.qpc, true, w, q);  // intra rounding for every MB (rdo.c:2588,2618)
+            bool az = true;
+            for (int i = 1; i < 16; ++i) {
+                S.cac[comp][b][i - 1] = (int16_t)q[kZigzag[i]];
+                az = az && q[kZigzag[i]] == 0;
+            }
+            az = az && S.cac[comp][b][15] == 0;
+            dc = w[0];
+            cacb = !az;
+            cdcb = w[0] != 0;
+            if (cacb) st = cavlc_stat(S.cac[comp][b], 16, 15, false);
+        }
+        S.cres_dc[comp][b] = dc;
+        S.cres_cac[comp][b] = cacb;
+        S.cres_cdc[comp][b] = cdcb;
+        S.cres_tc[comp][b] = st.tc;
+        S.cres_sctr[comp][b] = st.sctr;
+    }
+    HL_SYNC();
+    // sequential single-coefficient gating (uniform)
+    int single[2] = {0, 0}, tcs[2] = {0, 0}, cac[2] = {0, 0}, cdc[2] = {0, 0};
+    for (int b = 0; b < 4; ++b)
+        for (int comp = 0; comp < 2; ++comp) {
+            cac[comp] |= S.cres_cac[comp][b] << b;
+            cdc[comp] |= S.cres_cdc[comp][b] << b;
+            if (single[comp] < 7 && S.cres_cac[comp][b]) {
+                single[comp] += S.cres_sctr[comp][b];
+                tcs[comp] += S.cres_tc[comp][b];
+                chain_write(c, S.cres_sctr[comp][b]);
+            }
+        }
+    // TotalCoeffs are written only for blocks passed to write_block (lane 0)
+    if (c.tid == 0) {
+        int sg[2] = {0, 0};
+        for (int b = 0; b < 4; ++b)
+            for (int comp = 0; comp < 2; ++comp)
+                if (sg[comp] < 7 && S.cres_cac[comp][b]) {
+                    sg[comp] += S.cres_sctr[comp][b];
+                    S.tcc[comp][b] = (int8_t)S.cres_tc[comp][b];
+                }
+    }
+    for (int comp = 0; comp < 2; ++comp)
+        if (single[comp] < 7 && tcs[comp] == 1) cac[comp] = 0;
+    int dcl[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    for (int comp = 0; comp < 2; ++comp)
+        if (cdc[comp]) {
+            const int* D = S.cres_dc[comp];
+            const int t00 = D[0] + D[2], t01 = D[1] + D[3], t10 = D[0] - D[2], t11 = D[1] - D[3];
+            dcl[comp][0] = quant_dc(F.qpc, intra_flag, t00 + t01);
+            dcl[comp][1] = quant_dc(F.qpc, intra_flag, t00 - t01);
+            dcl[comp][2] = quant_dc(F.qpc, intra_flag, t10 + t11);
+            dcl[comp][3] = quant_dc(F.qpc, intra_flag, t10 - t11);
+            cdc[comp] = (dcl[comp][0] ? 1 : 0) | (dcl[comp][1] ? 2 : 0) | (dcl[comp][2] ? 4 : 0) | (dcl[comp][3] ? 8 : 0);
+        }
+    if (c.tid == 0) {
+        for (int comp = 0; comp < 2; ++comp) {
+            S.cbp_cac[comp] = cac[comp];
+            S.cbp_cdc[comp] = cdc[comp];
+            for (int i = 0; i < 4; ++i) S.cdc_level[comp][i] = dcl[comp][i];
+        }
+    }
+    // decode (transf.c:161-294): thread per 4x4 chroma block
+    for (int t = c.tid; t < 8; t += c.nthr) {
+        const int comp = t >> 2, b = t & 3, xO = (b & 1) * 4, yO = (b >> 1) * 4;
+        int r[16];
+        bool have = false;
+        if (cdc[comp] || cac[comp]) {
+            int dcc = 0;
+            if (cdc[comp]) {
+                const int qP = F.qpc, scale = level_scale(qP % 6, 0, 0);
+                const int* L = dcl[comp];
+                const int f00 = (L[0] + L[2]) + (L[1] + L[3]), f01 = (L[0] + L[2]) - (L[1] + L[3]);
+                const int f10 = (L[0] - L[2]) + (L[1] - L[3]), f11 = (L[0] - L[2]) - (L[1] - L[3]);
+                const int f = b == 0 ? f00 : (b == 1 ? f01 : (b == 2 ? f10 : f11));
+                dcc = ((f * scale) << (qP / 6)) >> 5;
+            }
+            if (dcc || (cac[comp] & (1 << b))) {
+                int list[16], m[16];
+                list[0] = dcc;
+                for (int i = 1; i < 16; ++i) list[i] = S.cac[comp][b][i - 1];
+                unscan(list, m);
+                dequant_idct(F.qpc, m, true, r);
+                have = true;
+            }
+        }
+        for (int i = 0; i < 16; ++i) {
+            const int o = (yO + (i >> 2)) * 8 + xO + (i & 3);
+            const int v = have ? clip255(S.predc[comp][o] + r[i]) : S.predc[comp][o];
+            F.cur[1 + comp][((c.yL >> 1) + yO + (i >> 2)) * F.Wc + (c.xL >> 1) + xO + (i & 3)] = (uint8_t)v;
+        }
+    }
+    HL_SYNC();
+}
+
+HD void guess_cbp(Shared& S)  // rdo.c:2703-2782 (lane 0)
+{
+    if (S.pm0 == PM_I16) S.cbp_l = S.cbp_l4x4 ? 15 : 0;
+    else {
+        S.cbp_l = 0;
+        for (int i8 = 0; i8 < 4; ++i8)
+            if (S.cbp_l4x4 & (0xF << (i8 * 4))) S.cbp_l |= 1 << i8;
+    }
+    if ((S.cbp_cdc[0] || S.cbp_cdc[1]) && (!S.cbp_cac[0] && !S.cbp_cac[1])) S.cbp_c = 1;
+    else if (S.cbp_cac[0] || S.cbp_cac[1]) S.cbp_c = 2;
+    else S.cbp_c = 0;
+    S.cbp = (S.cbp_c << 4) | S.cbp_l;
+    if (S.cbp > 47) {
+        S.cbp -= 16;
+        S.cbp_c = S.cbp >> 4;
+    }
+}
+
+// intra chroma prediction into S.predc (pred_intra.c:1043-1220)
+HD void intra_chroma_pred(Ctx& c, int mode)
+{
+    Shared& S = c.S;
+    for (int t = c.tid; t < 128; t += c.nthr) {
+        const int comp = t >> 6, i = t & 63, x = i & 7, y = i >> 3;
+        const int16_t* top = &S.ctop[comp][1];
+        const int16_t* left = S.cleft[comp];
+        int v;
+        if (mode == 0) {
+            // availability flags are sticky across the four blocks (pred_intra.c:1046)
+            bool xa = true, ya = true;
+            int t4 = 128;
+            for (int b = 0; b <= ((y >> 2) << 1 | (x >> 2)); ++b) {
+                const int xO = (b & 1) * 4, yO = (b >> 1) * 4;
+                int xs = 0, ys = 0;
+                for (int k = 0; k < 4; ++k) {
+                    if (top[xO + k] == kNA) {
+                        xa = false;
+                        break;
+                    }
+                    xs += top[xO + k];
+                }
+                for (int k = 0; k < 4; ++k) {
+                    if (left[yO + k] == kNA) {
+                        ya = false;
+                        break;
+                    }
+                    ys += left[yO + k];
+                }
+                t4 = 128;
+                if ((xO == 0 && yO == 0) || (xO > 0 && yO > 0)) {
+                    if (xa && ya) t4 = (xs + ys + 4) >> 3;
+                    else if (!xa && ya) t4 = (ys + 2) >> 2;
+                    else if (!ya && xa) t4 = (xs + 2) >> 2;
+                }
+                else if (xO > 0 && yO == 0) {
+                    if (xa) t4 = (xs + 2) >> 2;
+                    else if (ya) t4 = (ys + 2) >> 2;
+                }
+                else {
+                    if (ya) t4 = (ys + 2) >> 2;
+                    else if (xa) t4 = (xs + 2) >> 2;
+                }
+            }
+            v = t4;
+        }
+        else if (mode == 1) v = left[y];
+        else if (mode == 2) v = top[x];
+        else {
+            int H = 0, V = 0;
+            for (int k = 0; k < 3; ++k) {
+                H += (k + 1) * (top[4 + k] - top[2 - k]);
+                V += (k + 1) * (left[4 + k] - left[2 - k]);
+            }
+            H += 4 * (top[7] - top[-1]);
+            V += 4 * (left[7] - top[-1]);
+            const int a = (left[7] + top[7]) << 4, bb = (34 * H + 32) >> 6, cc = (34 * V + 32) >> 6;
+            v = clip255((a + bb * (x - 3) + cc * (y - 3) + 16) >> 5);
+        }
+        S.predc[comp][i] = v;
+    }
+    HL_SYNC();
+}
+
+// --------------------------------------------------------------------------
+// Intra 16x16 RDO (rdo.c:1526-1809)
+// --------------------------------------------------------------------------
+HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp)
+{
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    best_cost = 1.7976931348623157e308;
+    best_cbp = 0;
+    if (c.tid == 0) {
+        S.e_type = ET_I16;
+        S.flags = FL_INTRA;
+        S.pm0 = PM_I16;
+        S.i16mode = 2;
+    }
+    for (int mode = 0; mode < 4; ++mode) {
+        if (mode == 0 && S.top[1] == kNA) continue;
+        if (mode == 1 && S.left[0] == kNA) continue;
+        if (mode == 3 && S.top[0] == kNA) continue;
+        int dcv, pa, pb, pc;
+        i16_params(S, mode, dcv, pa, pb, pc);
+        HL_SYNC();
+        for (int t = c.tid; t < 256; t += c.nthr) S.pred[t] = i16_pred(S, mode, t & 15, t >> 4, dcv, pa, pb, pc);
+        HL_SYNC();
+        // blocks: transform, quant, AC stats
+        for (int t = c.tid; t < 16; t += c.nthr) {
+            const int xO = kBlkX[t], yO = kBlkY[t];
+            int res[16], w[16], q[16];
+            for (int i = 0; i < 16; ++i) {
+                const int o = (yO + (i >> 2)) * 16 + xO + (i & 3);
+                res[i] = (int)S.src[o] - S.pred[o];
+            }
+            fwd4x4(res, w);
+            quant4x4(F.qp, true, w, q);
+            bool qz = true;
+            for (int i = 0; i < 16; ++i) qz = qz && q[i] == 0;
+            for (int i = 1; i < 16; ++i) S.i16_ac[t][i - 1] = q[kZigzag[i]];
+            S.i16_ac[t][15] = 0;
+            S.i16_dcc[t] = w[0];
+            S.i16_called[t] = !qz;
+            CavlcStat st = {0, 0, 0, -1};
+            if (!qz) st = cavlc_stat(S.i16_ac[t], 16, 15, false);
+            S.i16_tc[t] = st.tc;
+            S.i16_t1[t] = st.t1;
+            S.i16_sctr[t] = st.sctr;
+            S.i16_bits[t] = st.rest;
+        }
+        HL_SYNC();
+        // nC of the AC writes: inside the MB, blocks written earlier in this
+        // mode show their own TotalCoeff (even 0), others the live state
+        for (int t = c.tid; t < 16; t += c.nthr) {
+            if (!S.i16_called[t]) continue;
+            const int nC = nc_luma_of(S, t, [&](int ni) -> int { return S.i16_called[ni] ? S.i16_tc[ni] : S.tc[ni]; });
+            S.i16_bits[t] += token_len(nC, S.i16_tc[t], S.i16_t1[t]);
+        }
+        HL_SYNC();
+        // uniform: single counter with stale reads, cbp, rate
+        int single = 0, bcbp = 0, rate = 0;
+        for (int b = 0; b < 16; ++b) {
+            if (!S.i16_called[b]) continue;
+            rate += S.i16_bits[b];
+            bcbp |= 1 << b;
+            if (S.i16_tc[b] > 0) chain_write(c, S.i16_sctr[b]);
+            else if (!c.fresh) c.dep = 1;
+            single += c.chain;
+        }
+        for (int t = c.tid; t < 16; t += c.nthr)
+            if (S.i16_called[t]) S.tc[t] = (int8_t)S.i16_tc[t];
+        if (bcbp && single < 6) bcbp = 0;
+        int dist = 0;
+        int dcl[16];
+        if (bcbp) {
+            int h[16], qd[16];
+            for (int b = 0; b < 16; ++b) h[kDcPos[b]] = S.i16_dcc[b];
+            int hh[16];
+            hadamard4x4_fwd(h, hh);
+            for (int i = 0; i < 16; ++i) qd[i] = quant_dc(F.qp, true, hh[i]);
+            for (int i = 0; i < 16; ++i) dcl[i] = qd[kZigzag[i]];
+            const CavlcStat st = cavlc_stat(dcl, 16, 15, false);
+            const int nC = nc_luma_of(S, 0, [&](int ni) -> int { return S.tc[ni]; });
+            rate += st.rest + token_len(nC, st.tc, st.t1);
+            if (st.tc > 0) chain_write(c, st.sctr);
+            HL_SYNC();
+            if (c.tid == 0) S.tc[0] = (int8_t)st.tc;
+            // scale DC (8.5.10) then per block inverse
+            int cm[16], dcY[16];
+            unscan(dcl, cm);
+            {
+                int d[16], f[16];
+                for (int j = 0; j < 4; ++j) {
+                    d[0 * 4 + j] = cm[0 * 4 + j] + cm[1 * 4 + j] + cm[2 * 4 + j] + cm[3 * 4 + j];
+                    d[1 * 4 + j] = cm[0 * 4 + j] + cm[1 * 4 + j] - cm[2 * 4 + j] - cm[3 * 4 + j];
+                    d[2 * 4 + j] = cm[0 * 4 + j] - cm[1 * 4 + j] - cm[2 * 4 + j] + cm[3 * 4 + j];
+                    d[3 * 4 + j] = cm[0 * 4 + j] - cm[1 * 4 + j] + cm[2 * 4 + j] - cm[3 * 4 + j];
+                }
+                for (int i = 0; i < 4; ++i) {
+                    f[i * 4 + 0] = d[i * 4 + 0] + d[i * 4 + 1] + d[i * 4 + 2] + d[i * 4 + 3];
+                    f[i * 4 + 1] = d[i * 4 + 0] + d[i * 4 + 1] - d[i * 4 + 2] - d[i * 4 + 3];
+                    f[i * 4 + 2] = d[i * 4 + 0] - d[i * 4 + 1] - d[i * 4 + 2] + d[i * 4 + 3];
+                    f[i * 4 + 3] = d[i * 4 + 0] - d[i * 4 + 1] + d[i * 4 + 2] - d[i * 4 + 3];
+                }
+                const int scale = level_scale(F.qp % 6, 0, 0), q6 = F.qp / 6;
+                for (int i = 0; i < 16; ++i)
+                    dcY[i] = F.qp >= 36 ? (f[i] * scale) << (q6 - 6) : (f[i] * scale + (1 << (5 - q6))) >> (6 - q6);
+            }
+            for (int t = c.tid; t < 16; t += c.nthr) {
+                const int xO = kBlkX[t], yO = kBlkY[t];
+                int list[16], m[16], r[16];
+                list[0] = dcY[kDcPos[t]];
+                bool nzl = list[0] != 0;
+                for (int i = 1; i < 16; ++i) {
+                    list[i] = S.i16_ac[t][i - 1];
+                    nzl = nzl || list[i] != 0;
+                }
+                if (nzl) {
+                    unscan(list, m);
+                    dequant_idct(F.qp, m, true, r);
+                }
+                int d = 0;
+                for (int i = 0; i < 16; ++i) {
+                    const int o = (yO + (i >> 2)) * 16 + xO + (i & 3);
+                    const int v = nzl ? clip255(S.pred[o] + r[i]) : S.pred[o];
+                    S.tmp_rec[o] = (uint8_t)v;
+                    d += iabs((int)S.src[o] - v);
+                }
+                S.i16_dist[t] = d;
+            }
+        }
+        else {
+            for (int i = 0; i < 16; ++i) dcl[i] = 0;
+            for (int t = c.tid; t < 16; t += c.nthr) {
+                const int xO = kBlkX[t], yO = kBlkY[t];
+                int d = 0;
+                for (int i = 0; i < 16; ++i) {
+                    const int o = (yO + (i >> 2)) * 16 + xO + (i & 3);
+                    S.tmp_rec[o] = (uint8_t)S.pred[o];
+                    d += iabs((int)S.src[o] - S.pred[o]);
+                }
+                S.i16_dist[t] = d;
+            }
+        }
+        HL_SYNC();
+        for (int b = 0; b < 16; ++b) dist += S.i16_dist[b];
+        const double cost = dadd((double)dist, dmul(F.lambda, (double)rate));
+        if (cost < best_cost) {
+            best_cost = cost;
+            best_cbp = bcbp;
+            if (c.tid == 0) {
+                S.i16mode = mode;
+                for (int i = 0; i < 16; ++i) S.i16_best_dc[i] = (int16_t)dcl[i];
+            }
+            for (int t = c.tid; t < 256; t += c.nthr) {
+                S.i16_best_ac[t >> 4][t & 15] = (int16_t)S.i16_ac[t >> 4][t & 15];
+                S.i16_best_rec[t] = S.tmp_rec[t];
+            }
+        }
+        HL_SYNC();
+    }
+}
+
+// --------------------------------------------------------------------------
+// Intra 4x4 RDO (rdo.c:1813-2098)
+// --------------------------------------------------------------------------
+HD void guess_i4(Ctx& c, double& best_cost, int& cbp4)
+{
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    best_cost = 0.0;
+    cbp4 = 0;
+    if (c.tid == 0) {
+        S.e_type = ET_I_NXN;
+        S.flags = FL_INTRA;
+        S.pm0 = PM_I4;
+    }
+    for (int blk = 0; blk < 16; ++blk) {
+        const int xO = kBlkX[blk], yO = kBlkY[blk];
+        int p[13];
+        i4_neighbours(S, blk, p);
+        // nC is the same for all nine modes: they only rewrite this block
+        const int nC = nc_luma_of(S, blk, [&](int ni) -> int { return S.tc[ni]; });
+        HL_SYNC();
+        for (int m = c.tid; m < 9; m += c.nthr) {
+            S.i4_cost_ok[m] = i4_avail(m, p);
+            if (!S.i4_cost_ok[m]) continue;
+            int pred[16], res[16];
+            i4_pred(m, p, pred);
+            bool zero = true;
+            for (int i = 0; i < 16; ++i) {
+                res[i] = (int)S.src[(yO + (i >> 2)) * 16 + xO + (i & 3)] - pred[i];
+                zero = zero && res[i] == 0;
+            }
+            S.i4_exact[m] = zero;
+            S.i4_nz[m] = 0;
+            S.i4_tc[m] = 0;
+            S.i4_sctr[m] = -1;
+            if (zero) {
+                for (int i = 0; i < 16; ++i) {
+                    S.i4_rec[m][i] = (uint8_t)pred[i];
+                    S.i4_lv[m][i] = 0;
+                }
+                S.i4_cost[m] = 0.0;
+                S.i4_dist[m] = 0;
+                continue;
+            }
+            int w[16], q[16], lv[16];
+            fwd4x4(res, w);
+            quant4x4(F.qp, true, w, q);
+            bool lz = true;
+            for (int i = 0; i < 16; ++i) {
+                lv[i] = q[kZigzag[i]];
+                lz = lz && lv[i] == 0;
+                S.i4_lv[m][i] = (int16_t)lv[i];
+            }
+            int bits = 0, d = 0;
+            if (!lz) {
+                const CavlcStat st = cavlc_stat(lv, 16, 15, false);
+                bits = st.rest + token_len(nC, st.tc, st.t1);
+                S.i4_nz[m] = 1;
+                S.i4_tc[m] = st.tc;
+                S.i4_sctr[m] = st.sctr;
+                int r[16];
+                dequant_idct(F.qp, q, false, r);
+                for (int i = 0; i < 16; ++i) {
+                    const int v = clip255(pred[i] + r[i]);
+                    S.i4_rec[m][i] = (uint8_t)v;
+                    d += iabs(res[i] + pred[i] - v);
+                }
+            }
+            else {
+                for (int i = 0; i < 16; ++i) {
+                    S.i4_rec[m][i] = (uint8_t)pred[i];
+                    d += iabs(res[i]);
+                }
+            }
+            S.i4_dist[m] = d;
+            S.i4_cost[m] = dadd((double)d, dmul(F.lambda, (double)bits));
+        }
+        HL_SYNC();
+        // uniform resolution in mode order (rdo.c:1931-2014)
+        double dmin = 1.7976931348623157e308;
+        int best = 2, lastw = -1;
+        bool best_zero = false;
+        for (int m = 0; m < 9; ++m) {
+            if (!S.i4_cost_ok[m]) continue;
+            if (S.i4_exact[m]) {
+                dmin = 0.0;
+                best = m;
+                best_zero = true;
+                break;
+            }
+            if (S.i4_nz[m]) lastw = m;
+            if (S.i4_cost[m] < dmin) {
+                dmin = S.i4_cost[m];
+                best = m;
+                best_zero = !S.i4_nz[m];
+            }
+        }
+        if (lastw >= 0) chain_write(c, S.i4_sctr[lastw]);
+        best_cost = dadd(best_cost, dmin);
+        if (!best_zero) cbp4 |= 1 << blk;
+        for (int t = c.tid; t < 16; t += c.nthr) {
+            S.rec[(yO + (t >> 2)) * 16 + xO + (t & 3)] = S.i4_rec[best][t];
+            S.luma_level[blk][t] = S.i4_exact[best] ? 0 : S.i4_lv[best][t];
+        }
+        if (c.tid == 0) {
+            S.i4mode[blk] = (int8_t)best;
+            if (lastw >= 0) S.tc[blk] = (int8_t)S.i4_tc[lastw];
+        }
+        HL_SYNC();
+    }
+}
+
+HD void pred_modes_4x4(Shared& S)  // pred_intra.c:541-615 (lane 0)
+{
+    for (int blk = 0; blk < 16; ++blk) {
+        const int bx = kBlkX[blk], by = kBlkY[blk];
+        int mA, mB;
+        bool aA, aB;
+        int pmA, pmB, iA, iB;
+        if (bx == 0) {
+            aA = S.nb[1].avail;
+            pmA = S.nb_pm0[1];
+            iA = aA ? S.nb_i4[1][blk_idx(12, by)] : 2;
+        }
+        else {
+            aA = true;
+            pmA = PM_I4;
+            iA = S.i4mode[blk_idx(bx - 4, by)];
+        }
+        if (by == 0) {
+            aB = S.nb[2].avail;
+            pmB = S.nb_pm0[2];
+            iB = aB ? S.nb_i4[2][blk_idx(bx, 12)] : 2;
+        }
+        else {
+            aB = true;
+            pmB = PM_I4;
+            iB = S.i4mode[blk_idx(bx, by - 4)];
+        }
+        const bool dcf = !aA || !aB;
+        mA = (dcf || pmA != PM_I4) ? 2 : iA;
+        mB = (dcf || pmB != PM_I4) ? 2 : iB;
+        const int pred = mA < mB ? mA : mB;
+        if (pred == S.i4mode[blk]) S.prev_flag[blk] = 1;
+        else {
+            S.prev_flag[blk] = 0;
+            S.rem_mode[blk] = (int8_t)(S.i4mode[blk] < pred ? S.i4mode[blk] : S.i4mode[blk] - 1);
+        }
+    }
+}
+
+// hl_codec_264_rdo_mb_guess_best_intra_pred_avc, rdo.c:99-299.  Returns the
+// best intra cost (the reference's static last_best_intra_cost).
+HD double guess_intra(Ctx& c)
+{
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    double c16, c4;
+    int cbp16, cbp4 = 0;
+    guess_i16(c, c16, cbp16);
+    if (c16 == 0.0) c4 = 1.7976931348623157e308;
+    else guess_i4(c, c4, cbp4);
+    HL_SYNC();
+    const int i16mode = S.i16mode;
+    const int cmode = i16mode == 0 ? 2 : (i16mode == 3 ? 3 : (i16mode == 1 ? 1 : 0));
+    bool is_i16 = false;
+    if (c4 < c16) {
+        HL_SYNC();
+        if (c.tid == 0) {
+            S.mb_type = 0;
+            S.e_type = ET_I_NXN;
+            S.flags = FL_INTRA;
+            S.pm0 = PM_I4;
+            S.cbp_l4x4 = cbp4;
+            pred_modes_4x4(S);
+        }
+        HL_SYNC();
+        int nz = 0;
+        for (int b = 0; b < 16; ++b) nz += !S.prev_flag[b];
+        c4 = dadd(c4, dmul(F.lambda, (double)(16 + nz * 3)));
+    }
+    if (c16 <= c4) is_i16 = true;
+    HL_SYNC();
+    if (c.tid == 0) {
+        S.chroma_mode = cmode;
+        if (is_i16) {
+            S.mb_type = 1;
+            S.e_type = ET_I16;
+            S.flags = FL_INTRA;
+            S.pm0 = PM_I16;
+            S.cbp_l4x4 = cbp16;
+        }
+    }
+    HL_SYNC();
+    intra_chroma_pred(c, cmode);
+    reconstruct_chroma(c, true);
+    if (is_i16) {
+        for (int t = c.tid; t < 256; t += c.nthr) S.rec[t] = S.i16_best_rec[t];
+    }
+    HL_SYNC();
+    if (c.tid == 0) {
+        guess_cbp(S);
+        if (is_i16) S.mb_type += (S.cbp_c << 2) + S.i16mode + (S.cbp_l ? 12 : 0);
+        if (!F.is_intra) S.mb_type += 5;
+    }
+    HL_SYNC();
+    return c16 < c4 ? c16 : c4;
+}
+
+// --------------------------------------------------------------------------
+// Inter prediction of the whole MB with the final partitioning
+// --------------------------------------------------------------------------
+HD void part_of(const Shared& S, int lx, int ly, int& pi, int& spi)
+{
+    const NbInfo& n = S.nb[0];
+    pi = (16 / n.part_w) * (ly / n.part_h) + (lx / n.part_w);
+    if (!is8x8(n.e_type)) spi = 0;
+    else spi = (8 / n.sub_w[pi]) * ((ly % 8) / n.sub_h[pi]) + ((lx % 8) / n.sub_w[pi]);
+}
+
+// luma prediction of the MB into S.pred, chroma into S.predc; mv from S.nb[0].mv
+HD void inter_pred_mb(Ctx& c, bool chroma_only_16x16, bool luma)
+{
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    if (luma) {
+        for (int t = c.tid; t < 16; t += c.nthr) {
+            const int bx = kBlkX[t], by = kBlkY[t];
+            int pi, spi;
+            part_of(S, bx, by, pi, spi);
+            const NbInfo& n = S.nb[0];
+            const int xP = (pi % (16 / n.part_w)) * n.part_w, yP = (pi / (16 / n.part_w)) * n.part_h;
+            int xS = 0, yS = 0;
+            if (is8x8(n.e_type)) {
+                xS = (spi % (8 / n.sub_w[pi])) * n.sub_w[pi];
+                yS = (spi / (8 / n.sub_w[pi])) * n.sub_h[pi];
+            }
+            const int mvx = n.mv[pi][spi][0], mvy = n.mv[pi][spi][1];
+            const int X = clip3(-17, F.W + 17, c.xL + xP + xS + (mvx >> 2)) + bx - xP - xS;
+            const int Y = clip3(-17, F.H + 17, c.yL + yP + yS + (mvy >> 2)) + by - yP - yS;
+            int p[16];
+            pred_luma4x4(F, X, Y, mvx & 3, mvy & 3, p);
+            for (int i = 0; i < 16; ++i) S.pred[(by + (i >> 2)) * 16 + bx + (i & 3)] = p[i];
+        }
+    }
+    for (int t = c.tid; t < 64; t += c.nthr) {
+        const int cx = t & 7, cy = t >> 3;
+        int pi = 0, spi = 0;
+        if (!chroma_only_16x16) part_of(S, cx * 2, cy * 2, pi, spi);
+        const int mvx = S.nb[0].mv[pi][spi][0], mvy = S.nb[0].mv[pi][spi][1];
+        const int xi = (c.xL >> 1) + cx + (mvx >> 3), yi = (c.yL >> 1) + cy + (mvy >> 3);
+        const int xF = mvx & 7, yF = mvy & 7;
+        const int xa = clip3(0, F.Wc - 1, xi), xb = clip3(0, F.Wc - 1, xi + 1);
+        const int ya = clip3(0, F.Hc - 1, yi), yb = clip3(0, F.Hc - 1, yi + 1);
+        for (int comp = 0; comp < 2; ++comp) {
+            const uint8_t* r = F.ref[1 + comp];
+            S.predc[comp][t] = ((8 - xF) * (8 - yF) * r[ya * F.Wc + xa] + xF * (8 - yF) * r[ya * F.Wc + xb] +
+                                (8 - xF) * yF * r[yb * F.Wc + xa] + xF * yF * r[yb * F.Wc + xb] + 32) >> 6;
+        }
+    }
+    HL_SYNC();
+}
+
+// rdo.c:2274-2500 luma part (chroma via reconstruct_chroma)
+HD void reconstruct_inter_luma(Ctx& c, int single_luma)
+{
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    for (int t = c.tid; t < 16; t += c.nthr) {
+        const int xO = kBlkX[t], yO = kBlkY[t];
+        int res[16], pred[16];
+        bool zero = true;
+        for (int i = 0; i < 16; ++i) {
+            const int o = (yO + (i >> 2)) * 16 + xO + (i & 3);
+            pred[i] = S.pred[o];
+            res[i] = (int)S.src[o] - pred[i];
+            zero = zero && res[i] == 0;
+        }
+        bool coded = false;
+        int q[16];
+        if (single_luma >= 6) {
+            if (!zero) {
+                int w[16];
+                fwd4x4(res, w);
+                quant4x4(F.qp, false, w, q);
+                bool qz = true;
+                for (int i = 0; i < 16; ++i) qz = qz && q[i] == 0;
+                coded = !qz;
+            }
+            for (int i = 0; i < 16; ++i) S.luma_level[t][i] = coded ? q[kZigzag[i]] : 0;
+        }
+        int r[16];
+        if (coded) dequant_idct(F.qp, q, false, r);
+        for (int i = 0; i < 16; ++i) {
+            const int o = (yO + (i >> 2)) * 16 + xO + (i & 3);
+            S.rec[o] = (uint8_t)(coded ? clip255(pred[i] + r[i]) : pred[i]);
+        }
+        S.i16_called[t] = coded;  // reuse as per-block coded flag
+    }
+    HL_SYNC();
+    if (c.tid == 0) {
+        int cbp = 0;
+        for (int b = 0; b < 16; ++b) cbp |= S.i16_called[b] << b;
+        S.cbp_l4x4 = cbp;
+    }
+    HL_SYNC();
+}
+
+// --------------------------------------------------------------------------
+// P macroblock decision, rdo.c:678-1271
+// --------------------------------------------------------------------------
+HD void guess_inter(Ctx& c)
+{
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    static constexpr int kFamFirst[5] = {0, 1, 2, 3, 7};
+    static constexpr int32_t kFamType[4] = {ET_P16x16, ET_P16x8, ET_P8x16, ET_P8x8REF0};
+    double best_cost = 1.7976931348623157e308;
+    int best_single = 9, best_part = -1, best_fam = -1;
+    bool best_found = false, pskip = false;
+    if (c.tid == 0) S.flags = FL_INTER;
+    for (int fam = 0; fam < 4 && !best_found; ++fam) {
+        bool probably = false;
+        for (int j = kFamFirst[fam]; j < kFamFirst[fam + 1]; ++j) {
+            const PartDef& pd = kParts[j];
+            HL_SYNC();
+            if (c.tid == 0) {
+                S.e_type = kFamType[fam];
+                S.nb[0].e_type = kFamType[fam];
+                S.nb[0].part_w = pd.part_w;
+                S.nb[0].part_h = pd.part_h;
+                for (int i = 0; i < 4; ++i) {
+                    S.nb[0].sub_w[i] = pd.sub_w;
+                    S.nb[0].sub_h[i] = pd.sub_h;
+                }
+            }
+            HL_SYNC();
+            bool prob = false;
+            for (int pi = 0; pi < pd.num_part; ++pi)
+                for (int spi = 0; spi < pd.num_sub; ++spi) {
+                    const bool p = search_partition(c, pd, pi, spi, j == 0 && pi == 0 && spi == 0);
+                    if (j == 0 && pi == 0 && spi == 0) prob = p;
+                }
+            probably = prob;
+            double cost_sum = 0.0;
+            int single_sum = 0;
+            for (int pi = 0; pi < pd.num_part; ++pi)
+                for (int spi = 0; spi < pd.num_sub; ++spi) {
+                    cost_sum = dadd(cost_sum, S.bcost[pi][spi]);
+                    single_sum += S.bsingle[pi][spi];
+                }
+            if (!probably && cost_sum != 0.0 && single_sum < 6 && fam == 0) {
+                int smv[2];
+                skip_mv(S, smv);
+                probably = smv[0] == S.bmvp[0][0][0] && smv[1] == S.bmvp[0][0][1] && S.bmv[0][0][0] == S.bmvp[0][0][0] &&
+                           S.bmv[0][0][1] == S.bmvp[0][0][1];
+            }
+            cost_sum = dadd(cost_sum, dmul(F.lambda, (double)pd.hdr_bits));
+            if (cost_sum < best_cost) {
+                best_cost = cost_sum;
+                best_single = single_sum;
+                best_part = j;
+                best_fam = fam;
+                HL_SYNC();
+                if (c.tid == 0) {
+                    for (int pi = 0; pi < pd.num_part; ++pi)
+                        for (int spi = 0; spi < pd.num_sub; ++spi) {
+                            S.best_mv[pi][spi][0] = S.bmv[pi][spi][0];
+                            S.best_mv[pi][spi][1] = S.bmv[pi][spi][1];
+                            S.best_mvp[pi][spi][0] = S.bmvp[pi][spi][0];
+                            S.best_mvp[pi][spi][1] = S.bmvp[pi][spi][1];
+                        }
+                }
+                HL_SYNC();
+            }
+        }
+        pskip = probably;
+        if (pskip) {  // _is_zeros_inter16x16_chroma, rdo.c:2140-2215
+            HL_SYNC();
+            if (c.tid == 0) {
+                S.nb[0].mv[0][0][0] = S.best_mv[0][0][0];
+                S.nb[0].mv[0][0][1] = S.best_mv[0][0][1];
+            }
+            HL_SYNC();
+            inter_pred_mb(c, true, false);
+            reconstruct_chroma(c, false);
+            pskip = !S.cbp_cac[0] && !S.cbp_cac[1] && !S.cbp_cdc[0] && !S.cbp_cdc[1];
+        }
+        best_found = best_found || best_cost == 0.0 || pskip;
+    }
+    if (!pskip) {
+        const double ic = guess_intra(c);
+        if (ic <= best_cost) return;
+    }
+    // finalize (rdo.c:1167-1262)
+    const PartDef& bp = kParts[best_part];
+    HL_SYNC();
+    if (c.tid == 0) {
+        S.flags = FL_INTER;
+        S.pm0 = PM_L0;
+        S.e_type = kFamType[best_fam];
+        S.mb_type = S.e_type - 301;
+        S.num_part = bp.num_part;
+        S.nb[0].intra = 0;
+        S.nb[0].e_type = S.e_type;
+        S.nb[0].part_w = bp.part_w;
+        S.nb[0].part_h = bp.part_h;
+        for (int pi = 0; pi < 4; ++pi) {
+            S.nb[0].sub_w[pi] = bp.sub_w;
+            S.nb[0].sub_h[pi] = bp.sub_h;
+            S.num_sub[pi] = pi < bp.num_part ? bp.num_sub : 1;
+            S.sub_type[pi] = pi < bp.num_part ? bp.sub_type : -1;
+        }
+        for (int pi = 0; pi < bp.num_part; ++pi)
+            for (int spi = 0; spi < bp.num_sub; ++spi) {
+                S.nb[0].mv[pi][spi][0] = S.best_mv[pi][spi][0];
+                S.nb[0].mv[pi][spi][1] = S.best_mv[pi][spi][1];
+                S.mvd[pi][spi][0] = (int16_t)(S.best_mv[pi][spi][0] - S.best_mvp[pi][spi][0]);
+                S.mvd[pi][spi][1] = (int16_t)(S.best_mv[pi][spi][1] - S.best_mvp[pi][spi][1]);
+            }
+    }
+    HL_SYNC();
+    if (pskip) {
+        inter_pred_mb(c, false, true);
+        for (int t = c.tid; t < 256; t += c.nthr) S.rec[t] = (uint8_t)S.pred[t];
+        HL_SYNC();
+        if (c.tid == 0) {
+            S.e_type = ET_PSKIP;
+            S.nb[0].e_type = ET_PSKIP;
+            S.flags = FL_INTER | FL_SKIP;
+            S.mb_type = ET_PSKIP - 301;
+            S.cbp = 0;
+            S.cbp_c = 0;
+            S.cbp_l4x4 = 0;
+            S.cbp_l = 0;
+        }
+        HL_SYNC();
+    }
+    else {
+        inter_pred_mb(c, false, true);
+        reconstruct_inter_luma(c, best_single);
+        reconstruct_chroma(c, false);
+        if (c.tid == 0) guess_cbp(S);
+        HL_SYNC();
+    }
+    if (!(S.flags & FL_SKIP) && S.cbp == 0 && S.e_type == ET_P16x16 && S.mvd[0][0][0] == 0 && S.mvd[0][0][1] == 0) {
+        int smv[2];
+        skip_mv(S, smv);
+        if (smv[0] == S.best_mvp[0][0][0] && smv[1] == S.best_mvp[0][0][1]) {
+            HL_SYNC();
+            if (c.tid == 0) {
+                S.e_type = ET_PSKIP;
+                S.nb[0].e_type = ET_PSKIP;
+                S.mb_type = ET_PSKIP - 301;
+            }
+            HL_SYNC();
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// Final CAVLC write side effects (mb.c:543-892): TotalCoeff updates and the
+// nC of every written block, recorded for the host writer.  Lane 0.
+// --------------------------------------------------------------------------
+template <typename T>
+HD int count_tc(const T* lv, int n)
+{
+    int k = 0;
+    for (int i = 0; i < n; ++i) k += lv[i] != 0;
+    return k;
+}
+
+HD void final_write(Shared& S)
+{
+    for (int i = 0; i < 16; ++i) S.nc_luma[i] = 0;
+    for (int i = 0; i < 8; ++i) S.nc_cac[i >> 2][i & 3] = 0;
+    S.nc_dc = 0;
+    if (S.e_type == ET_PSKIP) return;
+    if (!(S.cbp_l > 0 || S.cbp_c > 0 || S.pm0 == PM_I16)) return;
+    auto inside = [&](int ni) -> int { return S.tc[ni]; };
+    if (S.pm0 == PM_I16) {
+        S.nc_dc = (int8_t)nc_luma_of(S, 0, inside);
+        S.tc[0] = (int8_t)count_tc(S.i16_best_dc, 16);
+    }
+    for (int i8 = 0; i8 < 4; ++i8)
+        for (int i4 = 0; i4 < 4; ++i4)
+            if (S.cbp_l & (1 << i8)) {
+                const int blk = i8 * 4 + i4;
+                S.nc_luma[blk] = (int8_t)nc_luma_of(S, blk, inside);
+                S.tc[blk] = (int8_t)(S.pm0 == PM_I16 ? count_tc(S.i16_best_ac[blk], 15) : count_tc(S.luma_level[blk], 16));
+            }
+    for (int comp = 0; comp < 2; ++comp)
+        for (int i4 = 0; i4 < 4; ++i4)
+            if (S.cbp_c & 2) {
+                int nA, nB;
+                bool aA, aB;
+                if (i4 & 1) {
+                    aA = true;
+                    nA = (S.cbp_c & 2) ? S.tcc[comp][i4 - 1] : 0;
+                }
+                else {
+                    aA = S.extCA[comp * 2 + (i4 >> 1)] >= 0;
+                    nA = aA ? S.extCA[comp * 2 + (i4 >> 1)] : 0;
+                }
+                if (i4 & 2) {
+                    aB = true;
+                    nB = (S.cbp_c & 2) ? S.tcc[comp][i4 - 2] : 0;
+                }
+                else {
+                    aB = S.extCB[comp * 2 + (i4 & 1)] >= 0;
+                    nB = aB ? S.extCB[comp * 2 + (i4 & 1)] : 0;
+                }
+                S.nc_cac[comp][i4] = (int8_t)(aA && aB ? (nA + nB + 1) >> 1 : (aA ? nA : (aB ? nB : 0)));
+                S.tcc[comp][i4] = (int8_t)((S.cbp_cac[comp] & (1 << i4)) ? count_tc(S.cac[comp][i4], 15) : 0);
+            }
+}
+
+// --------------------------------------------------------------------------
+// MB end: write recon, persistent state and the record
+// --------------------------------------------------------------------------
+HD void mb_end(Ctx& c)
+{
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    for (int t = c.tid; t < 256; t += c.nthr) F.cur[0][(c.yL + (t >> 4)) * F.W + c.xL + (t & 15)] = S.rec[t];
+    if (c.tid == 0) final_write(S);
+    HL_SYNC();
+    MbState& M = F.st[c.addr];
+    MbRecord& R = F.rec[c.addr];
+    for (int t = c.tid; t < 128; t += c.nthr) {
+        M.cac_level[t >> 6][(t >> 4) & 3][t & 15] = S.cac[t >> 6][(t >> 4) & 3][t & 15];
+        R.cac[t >> 6][(t >> 4) & 3][t & 15] = S.cac[t >> 6][(t >> 4) & 3][t & 15];
+    }
+    for (int t = c.tid; t < 256; t += c.nthr) {
+        const int b = t >> 4, i = t & 15;
+        R.luma[b][i] = (int16_t)(S.pm0 == PM_I16 ? S.i16_best_ac[b][i] : S.luma_level[b][i]);
+    }
+    if (c.tid == 0) {
+        M.e_type = S.e_type;
+        M.flags = S.flags;
+        M.pm0 = S.pm0;
+        M.cbp_l = S.cbp_l;
+        M.cbp_c = S.cbp_c;
+        M.cbp_l4x4 = S.cbp_l4x4;
+        const bool intra = (S.flags & FL_INTRA) != 0;
+        if (!intra) {
+            M.num_part = S.num_part;
+            M.part_w = S.nb[0].part_w;
+            M.part_h = S.nb[0].part_h;
+            for (int i = 0; i < 4; ++i) {
+                M.sub_w[i] = S.nb[0].sub_w[i];
+                M.sub_h[i] = S.nb[0].sub_h[i];
+            }
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j) {
+                    M.mv[i][j][0] = S.nb[0].mv[i][j][0];
+                    M.mv[i][j][1] = S.nb[0].mv[i][j][1];
+                }
+        }
+        for (int i = 0; i < 16; ++i) {
+            M.i4mode[i] = S.i4mode[i];
+            M.tc_luma[i] = S.tc[i];
+        }
+        for (int i = 0; i < 8; ++i) M.tc_cac[i >> 2][i & 3] = S.tcc[i >> 2][i & 3];
+        R.e_type = S.e_type;
+        R.mb_type = S.mb_type;
+        R.flags = S.flags;
+        R.pm0 = S.pm0;
+        R.cbp = S.cbp;
+        R.cbp_l = S.cbp_l;
+        R.cbp_c = S.cbp_c;
+        R.cbp_l4x4 = S.cbp_l4x4;
+        for (int i = 0; i < 2; ++i) {
+            R.cbp_cdc[i] = S.cbp_cdc[i];
+            R.cbp_cac[i] = S.cbp_cac[i];
+        }
+        R.num_part = S.num_part;
+        for (int i = 0; i < 4; ++i) {
+            R.num_sub[i] = S.num_sub[i];
+            R.sub_mb_type[i] = S.sub_type[i];
+        }
+        R.chroma_mode = S.chroma_mode;
+        R.i16mode = S.i16mode;
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) {
+                R.mvd[i][j][0] = S.mvd[i][j][0];
+                R.mvd[i][j][1] = S.mvd[i][j][1];
+                R.mv[i][j][0] = S.nb[0].mv[i][j][0];
+                R.mv[i][j][1] = S.nb[0].mv[i][j][1];
+            }
+        for (int i = 0; i < 16; ++i) {
+            R.prev_flag[i] = S.prev_flag[i];
+            R.rem_mode[i] = S.rem_mode[i];
+            R.i4mode[i] = S.i4mode[i];
+            R.nc_luma[i] = S.nc_luma[i];
+            R.i16dc[i] = S.i16_best_dc[i];
+        }
+        for (int i = 0; i < 8; ++i) {
+            R.nc_cac[i >> 2][i & 3] = S.nc_cac[i >> 2][i & 3];
+            R.cdc[i >> 2][i & 3] = (int16_t)S.cdc_level[i >> 2][i & 3];
+        }
+        R.nc_dc = S.nc_dc;
+        MbChain& ch = F.chain[c.addr];
+        ch.s_out = c.chain;
+        ch.dep = c.dep;
+        ch.fresh = c.fresh;
+    }
+    HL_SYNC();
+}
+
+// One macroblock, start to end.  s_in = rdo.Single_ctr on entry.
+HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, int s_in)
+{
+    Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0};
+    if (tid == 0) F.chain[addr].s_in = s_in;
+    mb_begin(c);
+    if (F.is_intra) guess_intra(c);
+    else guess_inter(c);
+    mb_end(c);
+}
+
+}  // namespace hl

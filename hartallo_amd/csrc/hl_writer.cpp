@@ -1,0 +1,371 @@
+// hl_writer.cpp -- see hl_writer.h.
+#include "hl_writer.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "hl_prims.h"
+
+namespace hl {
+
+BitWriter::BitWriter(uint8_t* buf, size_t cap, int64_t limit)
+    : buf_(buf), cap_(cap), limit_(limit < 0 ? (int64_t)cap - 1 : limit), nbits_(0), overflow_(false)
+{
+}
+
+void BitWriter::u(uint32_t v, int n)
+{
+    for (int i = n - 1; i >= 0; --i) {
+        if ((nbits_ >> 3) > limit_) {
+            overflow_ = true;
+            return;
+        }
+        const size_t byte = (size_t)(nbits_ >> 3);
+        const int bit = 7 - (int)(nbits_ & 7);
+        if (byte < cap_) {
+            if ((v >> i) & 1u) buf_[byte] |= (uint8_t)(1u << bit);
+            else buf_[byte] &= (uint8_t)~(1u << bit);
+        }
+        else {
+            overflow_ = true;
+        }
+        ++nbits_;
+    }
+}
+
+void BitWriter::ue(uint32_t v)
+{
+    int lz = 0;
+    while ((1ull << (lz + 1)) <= (uint64_t)v + 1) ++lz;
+    u(0, lz);
+    u(v + 1, lz + 1);
+}
+
+void BitWriter::se(int32_t v) { ue(v <= 0 ? (uint32_t)(-(int64_t)v) << 1 : ((uint32_t)v << 1) - 1); }
+
+void BitWriter::trailing()
+{
+    const bool aligned = (nbits_ & 7) == 0;
+    if (!aligned || !(buf_[(nbits_ >> 3) - 1] & 1)) {
+        const int left = 8 - (int)(nbits_ & 7);
+        u(1u << (left - 1), left);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// CAVLC level table, generated exactly like cavlc.c:59-103 (inclusive suffix
+// bound; entries past the generated range stay {0,0,0}).
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr int kMaxLevelCode = 62545;
+struct LevelCode {
+    uint16_t prefix, size;
+    uint32_t suffix;
+};
+std::vector<LevelCode>* g_levels = nullptr;
+std::once_flag g_levels_once;
+
+void init_levels()
+{
+    g_levels = new std::vector<LevelCode>(7 * (kMaxLevelCode + 1), LevelCode{0, 0, 0});
+    for (int lp = 0; lp <= 15; ++lp)
+        for (int sl = 0; sl <= 6; ++sl) {
+            int size = sl;
+            if (lp == 14 && sl == 0) size = 4;
+            else if (lp >= 15) size = lp - 3;
+            for (int ls = 0; ls <= (1 << size); ++ls) {
+                int lc = (lp < 15 ? lp : 15) << sl;
+                if (sl > 0 || lp >= 14) lc += ls;
+                if (lp >= 15 && sl == 0) lc += 15;
+                (*g_levels)[(size_t)sl * (kMaxLevelCode + 1) + lc] = LevelCode{(uint16_t)lp, (uint16_t)size, (uint32_t)ls};
+            }
+        }
+}
+
+const LevelCode& level_code(int sl, int lc)
+{
+    std::call_once(g_levels_once, init_levels);
+    if (lc > kMaxLevelCode) lc = kMaxLevelCode;
+    return (*g_levels)[(size_t)sl * (kMaxLevelCode + 1) + lc];
+}
+
+// me(v) coded_block_pattern -> codeNum, Table 9-4 [cbp][0 = Intra_4x4, 1 = Inter]
+constexpr uint8_t kCbpCode[48][2] = {
+    {3, 0},   {29, 2},  {30, 3},  {17, 7},  {31, 4},  {18, 8},  {37, 17}, {8, 13},  {32, 5},  {38, 18}, {19, 9},  {9, 14},
+    {20, 10}, {10, 15}, {11, 16}, {2, 11},  {16, 1},  {33, 32}, {34, 33}, {21, 36}, {35, 34}, {22, 37}, {39, 44}, {4, 40},
+    {36, 35}, {40, 45}, {23, 38}, {5, 41},  {24, 39}, {6, 42},  {7, 43},  {1, 19},  {41, 6},  {42, 24}, {43, 25}, {25, 20},
+    {44, 26}, {26, 21}, {46, 46}, {12, 28}, {45, 27}, {47, 47}, {27, 22}, {13, 29}, {28, 23}, {14, 30}, {15, 31}, {0, 12}};
+
+// residual_block_cavlc, residual.c:587-901 (write path)
+template <typename T>
+void write_block(BitWriter& bw, const T* coeffLevel, int endIdx, int maxNumCoef, int nC)
+{
+    static constexpr int32_t kThr[7] = {0, 3, 6, 12, 24, 48, 1 << 15};
+    int nz[16], run_before[16] = {0};
+    int tc = 0, t1 = 0, total_zeros = 0, k = -1;
+    bool countT1 = true, countTZ = false;
+    for (int j = 0; j < maxNumCoef; ++j) {
+        const int c = coeffLevel[maxNumCoef - 1 - j];
+        if (c) {
+            nz[tc++] = c;
+            countTZ = true;
+            ++k;
+            if (countT1) {
+                if (c == 1 || c == -1) {
+                    ++t1;
+                    countT1 = t1 < 3;
+                }
+                else {
+                    countT1 = false;
+                }
+            }
+        }
+        else if (countTZ) {
+            ++run_before[k];
+        }
+        if (countTZ && c == 0) ++total_zeros;
+    }
+    if (nC >= 0) {
+        if (nC >= 8) bw.u(tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u, 6);
+        else {
+            const int vlc = nC < 2 ? 0 : (nC < 4 ? 1 : 2);
+            bw.u(kTokCode[vlc][t1][tc], kTokLen[vlc][t1][tc]);
+        }
+    }
+    else {
+        bw.u(kTokCdcCode[t1][tc], kTokCdcLen[t1][tc]);
+    }
+    if (tc == 0) return;
+    int suffixLength = (tc > 10 && t1 < 3) ? 1 : 0;
+    for (int j = 0; j < tc; ++j) {
+        if (j < t1) {
+            bw.u1((uint32_t)((1 - nz[j]) >> 1));
+            continue;
+        }
+        int lc = nz[j] >= 0 ? (nz[j] << 1) - 2 : -(nz[j] << 1) - 1;
+        if (j == t1 && t1 < 3 && lc >= 2) lc -= 2;
+        const LevelCode& L = level_code(suffixLength, lc);
+        if (L.prefix > 0) bw.u(0, L.prefix);
+        bw.u1(1);
+        if (L.size) bw.u(L.suffix, L.size);
+        if (suffixLength == 0) suffixLength = 1;
+        if (iabs(nz[j]) > kThr[suffixLength]) ++suffixLength;
+    }
+    int zerosLeft = 0;
+    if (tc < endIdx + 1) {
+        if (nC >= 0) bw.u(kTzCode[tc - 1][total_zeros], kTzLen[tc - 1][total_zeros]);
+        else bw.u(kTzCdcCode[tc - 1][total_zeros], kTzCdcLen[tc - 1][total_zeros]);
+        zerosLeft = total_zeros;
+    }
+    for (k = 0; k < tc - 1 && zerosLeft > 0; ++k) {
+        const int row = zerosLeft <= 6 ? zerosLeft - 1 : 6;
+        bw.u(kRbCode[row][run_before[k]], kRbLen[row][run_before[k]]);
+        zerosLeft -= run_before[k];
+    }
+}
+
+int guess_level(int w, int h)  // utils.c:14-58
+{
+    static const int L[16][3] = {{10, 128, 96},   {9, 128, 96},    {11, 176, 144},  {12, 320, 240},  {13, 352, 288},  {20, 352, 288},
+                                 {21, 352, 480},  {22, 352, 480},  {30, 720, 480},  {31, 1280, 720}, {32, 1280, 720}, {40, 2048, 1024},
+                                 {41, 2048, 1024}, {42, 2048, 1080}, {50, 2560, 1920}, {51, 3840, 2160}};
+    for (int i = 0; i < 16; ++i)
+        if (L[i][1] >= w && L[i][2] >= h) return L[i][0];
+    return 51;
+}
+
+size_t put_nal(uint8_t* out, size_t cap, const uint8_t* rbsp, size_t n)
+{
+    if (cap < n + 3) return 0;
+    out[0] = 0;
+    out[1] = 0;
+    out[2] = 1;
+    memcpy(out + 3, rbsp, n);
+    return n + 3;
+}
+
+}  // namespace
+
+size_t write_stream_headers(const StreamParams& p, uint8_t* out, size_t cap)
+{
+    uint8_t buf[64];
+    size_t n = 0;
+    {
+        memset(buf, 0, sizeof(buf));
+        BitWriter bw(buf, sizeof(buf));
+        bw.u(0, 1);
+        bw.u(1, 2);
+        bw.u(7, 5);     // nal_unit_type SPS
+        bw.u(66, 8);    // profile_idc Baseline
+        bw.u1(1);       // constraint_set0..2 = 1 (sps.c:555-560)
+        bw.u1(1);
+        bw.u1(1);
+        bw.u1(0);
+        bw.u1(0);
+        bw.u1(0);
+        bw.u(0, 2);
+        bw.u((uint32_t)guess_level(p.width, p.height), 8);
+        bw.ue(0);  // seq_parameter_set_id
+        bw.ue(4);  // log2_max_frame_num_minus4
+        bw.ue(2);  // pic_order_cnt_type
+        bw.ue(1);  // max_num_ref_frames
+        bw.u1(0);
+        bw.ue((uint32_t)(p.width / 16 - 1));
+        bw.ue((uint32_t)(p.height / 16 - 1));
+        bw.u1(1);  // frame_mbs_only_flag
+        bw.u1(0);  // direct_8x8_inference_flag
+        bw.u1(0);  // frame_cropping_flag
+        bw.u1(0);  // vui_parameters_present_flag
+        bw.trailing();
+        n += put_nal(out + n, cap - n, buf, bw.bytes());
+    }
+    {
+        memset(buf, 0, sizeof(buf));
+        BitWriter bw(buf, sizeof(buf));
+        bw.u(0, 1);
+        bw.u(1, 2);
+        bw.u(8, 5);  // nal_unit_type PPS
+        bw.ue(0);
+        bw.ue(0);
+        bw.u1(0);    // entropy_coding_mode_flag (CAVLC)
+        bw.u1(0);
+        bw.ue(0);    // num_slice_groups_minus1
+        bw.ue(0);
+        bw.ue(0);
+        bw.u1(0);
+        bw.u(0, 2);
+        bw.se(p.qp - 26);
+        bw.se(0);
+        bw.se(0);
+        bw.u1(1);  // deblocking_filter_control_present_flag
+        bw.u1(0);
+        bw.u1(0);
+        bw.trailing();
+        n += put_nal(out + n, cap - n, buf, bw.bytes());
+    }
+    return n;
+}
+
+size_t slice_scratch_bytes(const StreamParams& p)
+{
+    const size_t nmb = (size_t)(p.width / 16) * (p.height / 16);
+    return (size_t)p.width * p.height * 3 / 2 + 4096 + (nmb << 8);
+}
+
+size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap)
+{
+    static const int16_t kZeros[16] = {0};
+    const size_t scap = slice_scratch_bytes(p);
+    const int nmb = (p.width / 16) * (p.height / 16);
+    // the reference builds the slice NAL in a (mb_count << 8) + 4096 byte
+    // buffer (encode.c:192) and drops writes past its end
+    const size_t esd_size = ((size_t)nmb << 8) + 4096;
+    memset(scratch, 0, scap);
+    BitWriter bw(scratch, scap, (int64_t)esd_size);
+    // slice header, slice.c:660-900
+    bw.u(0, 1);
+    bw.u(1, 2);
+    bw.u(s.idr ? 5 : 1, 5);
+    bw.ue(0);                // first_mb_in_slice
+    bw.ue(s.idr ? 2 : 0);    // slice_type I / P
+    bw.ue(0);                // pic_parameter_set_id
+    bw.u((uint32_t)s.frame_num & 0xFF, 8);
+    if (s.idr) bw.ue((uint32_t)s.idr_pic_id);
+    if (!s.idr) {
+        bw.u1(1);            // num_ref_idx_active_override_flag
+        bw.ue(0);
+        bw.u1(0);            // ref_pic_list_modification_flag_l0
+        bw.u1(0);            // adaptive_ref_pic_marking_mode_flag
+    }
+    else {
+        bw.u1(0);            // no_output_of_prior_pics_flag
+        bw.u1(0);            // long_term_reference_flag
+    }
+    bw.se(0);                // slice_qp_delta
+    bw.ue(p.deblock ? 0 : 1);
+    if (p.deblock) {
+        bw.se(0);
+        bw.se(0);
+    }
+    // slice_data, mb.c:543-892
+    int skip_run = 0;
+    for (int a = 0; a < nmb; ++a) {
+        const MbRecord& m = recs[a];
+        if (!s.idr) {
+            if (m.e_type == ET_PSKIP) {
+                ++skip_run;
+                if (a == nmb - 1) bw.ue((uint32_t)skip_run);
+                continue;
+            }
+            bw.ue((uint32_t)skip_run);
+            skip_run = 0;
+        }
+        bw.ue((uint32_t)m.mb_type);
+        const bool intra = (m.flags & FL_INTRA) != 0;
+        if (m.e_type != ET_I_NXN && m.pm0 != PM_I16 && m.num_part == 4 && !intra) {
+            for (int pi = 0; pi < 4; ++pi) bw.ue((uint32_t)m.sub_mb_type[pi]);
+            for (int pi = 0; pi < 4; ++pi)
+                for (int spi = 0; spi < m.num_sub[pi]; ++spi) {
+                    bw.se(m.mvd[pi][spi][0]);
+                    bw.se(m.mvd[pi][spi][1]);
+                }
+        }
+        else if (m.pm0 == PM_I4 || m.pm0 == PM_I16) {
+            if (m.pm0 == PM_I4)
+                for (int b = 0; b < 16; ++b) {
+                    bw.u1((uint32_t)m.prev_flag[b]);
+                    if (!m.prev_flag[b]) bw.u((uint32_t)m.rem_mode[b], 3);
+                }
+            bw.ue((uint32_t)m.chroma_mode);
+        }
+        else {
+            for (int pi = 0; pi < m.num_part; ++pi) {
+                bw.se(m.mvd[pi][0][0]);
+                bw.se(m.mvd[pi][0][1]);
+            }
+        }
+        if (m.pm0 != PM_I16) bw.ue(kCbpCode[m.cbp][m.pm0 == PM_I4 ? 0 : 1]);
+        if (m.cbp_l > 0 || m.cbp_c > 0 || m.pm0 == PM_I16) {
+            bw.se(0);  // mb_qp_delta
+            if (m.pm0 == PM_I16) write_block(bw, m.i16dc, 15, 16, m.nc_dc);
+            for (int i8 = 0; i8 < 4; ++i8)
+                for (int i4 = 0; i4 < 4; ++i4)
+                    if (m.cbp_l & (1 << i8)) {
+                        const int blk = i8 * 4 + i4;
+                        if (m.pm0 == PM_I16) write_block(bw, m.luma[blk], 14, 15, m.nc_luma[blk]);
+                        else write_block(bw, m.luma[blk], 15, 16, m.nc_luma[blk]);
+                    }
+            if (m.cbp_c & 3)
+                for (int c = 0; c < 2; ++c) write_block(bw, m.cbp_cdc[c] ? m.cdc[c] : kZeros, 3, 4, -1);
+            for (int c = 0; c < 2; ++c)
+                for (int i4 = 0; i4 < 4; ++i4)
+                    if (m.cbp_c & 2) write_block(bw, (m.cbp_cac[c] & (1 << i4)) ? m.cac[c][i4] : kZeros, 14, 15, m.nc_cac[c][i4]);
+        }
+    }
+    bw.trailing();
+    size_t n = bw.bytes();
+    // emulation prevention, rbsp.c:609-632: only 00 00 01 is escaped and the
+    // caller keeps the unescaped length (encode.c:443-444)
+    {
+        size_t zeros = 0, len = n;
+        for (size_t i = 0; i < len; ++i) {
+            if (zeros == 2) {
+                if (scratch[i] == 0x01) {
+                    if (len + 1 >= esd_size) return 0;  // HL_ERROR_TOOSHORT, rbsp.c:617-620
+                    memmove(&scratch[i + 1], &scratch[i], len - i + 1);
+                    len++;
+                    scratch[i++] = 0x03;
+                }
+                zeros = 0;
+            }
+            zeros = scratch[i] ? 0 : zeros + 1;
+        }
+    }
+    return put_nal(out, cap, scratch, n);
+}
+
+}  // namespace hl

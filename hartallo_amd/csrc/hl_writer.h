@@ -1,0 +1,56 @@
+// hl_writer.h -- host-side H.264 Baseline bitstream writer of the encoder:
+// SPS/PPS (sps.c:535-800, pps.c:265-400), slice header (slice.c:660-900),
+// macroblock_layer() + CAVLC residual (mb.c:543-892, residual.c:587-1094),
+// rbsp trailing bits and emulation prevention (rbsp.c:162-170, 609-632).
+//
+// The GPU hands over one MbRecord per macroblock with every syntax value and
+// every nC context already resolved, so this pass is serialisation only.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "hl_types.h"
+
+namespace hl {
+
+struct StreamParams {
+    int32_t width, height, qp, deblock;
+};
+
+class BitWriter {
+public:
+    // limit: last writable byte index; bits beyond it are dropped like the
+    // reference's end-of-buffer handling (bits.h:236-246, 612-626); -1 = cap
+    BitWriter(uint8_t* buf, size_t cap, int64_t limit = -1);
+    void u(uint32_t v, int n);
+    void u1(uint32_t v) { u(v & 1u, 1); }
+    void ue(uint32_t v);
+    void se(int32_t v);
+    void trailing();  // rbsp_trailing_bits with the reference's aligned-stream quirk
+    size_t bytes() const { return (size_t)((nbits_ + 7) >> 3); }
+    int64_t bits() const { return nbits_; }
+    bool overflow() const { return overflow_; }
+
+private:
+    uint8_t* buf_;
+    size_t cap_;
+    int64_t limit_;
+    int64_t nbits_;
+    bool overflow_;
+};
+
+// Writes the 00 00 01-prefixed SPS and PPS NAL units; returns bytes written.
+size_t write_stream_headers(const StreamParams& p, uint8_t* out, size_t cap);
+
+struct SliceState {
+    int32_t idr, frame_num, idr_pic_id;
+};
+
+// Writes "00 00 01" + one escaped slice NAL for the frame's MB records.
+// scratch must hold at least slice_scratch_bytes(); returns bytes written to
+// out, or 0 when out is too small or the reference would fail the frame with
+// HL_ERROR_TOOSHORT (an escape that does not fit its slice buffer).
+size_t slice_scratch_bytes(const StreamParams& p);
+size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap);
+
+}  // namespace hl

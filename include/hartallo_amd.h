@@ -1,0 +1,111 @@
+/*
+ * hartallo_amd.h -- C ABI of the MI355X (gfx950) H.264 encode path.
+ *
+ * Drop-in boundary.  hartallo reaches an encoder through one plugin slot:
+ *
+ *   HL_ERROR_T (*encode)(struct hl_codec_s*, const struct hl_frame_s*,
+ *                        struct hl_codec_result_s*);
+ *     include/hartallo/hl_codec.h:173-184 (hl_codec_plugin_def_t.encode),
+ *     called by hl_codec_encode, source/hl_codec.c:152-159.
+ *
+ * The H.264 plugin behind it (hl_codec_264_encode, source/h264/
+ * hl_codec_264.c:637-1006) turns one planar YUV420 frame into headers +
+ * one slice NAL.  The functions below are that operation with plain C types:
+ * a maintainer registers a plugin def whose encode() forwards here (see
+ * INTEGRATION.md), and hartallo's public API is unchanged.
+ *
+ * Semantics follow the reference:
+ *   - parameters are the hl_codec_t fields the encoder reads
+ *     (hl_codec.h:33-80): qp, gop_size, me_range, deblock_flag,
+ *     me_early_term_flag; threads_count is 1 and max_ref_frame is 1;
+ *   - width and height must be multiples of 16 (1088, not 1080 -- the
+ *     reference rejects cropping, hl_codec_264.c:430-438);
+ *   - result.type carries HL_CODEC_RESULT_TYPE_DATA / _HDR bits
+ *     (hl_types.h:158-163); result.hdr holds "00 00 01"-prefixed SPS+PPS
+ *     on the first frame (hl_codec_264.c:675-686), result.data the slice
+ *     NAL without its start code (hl_codec_264.c:1000-1006);
+ *   - the output buffers are owned by the encoder and valid until the next
+ *     call (hl_codec_264.c:1000-1006);
+ *   - errors are HL_ERROR_T values (hl_types.h:101-122).
+ * Output is bit-identical to the reference encoder on the same input.
+ */
+#ifndef HARTALLO_AMD_H
+#define HARTALLO_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* HL_ERROR_T values, hl_types.h:101-122 */
+enum {
+    HL_AMD_SUCCESS = 0,
+    HL_AMD_ERROR_INVALID_PARAMETER = 1,
+    HL_AMD_ERROR_INVALID_STATE = 3,
+    HL_AMD_ERROR_INVALID_FORMAT = 4,
+    HL_AMD_ERROR_NOT_IMPLEMENTED = 7,
+    HL_AMD_ERROR_OUTOFMEMMORY = 8,
+    HL_AMD_ERROR_SYSTEM = 13,
+    HL_AMD_ERROR_TOOSHORT = 15
+};
+
+/* HL_CODEC_RESULT_TYPE_T bits, hl_types.h:158-163 */
+enum { HL_AMD_RESULT_TYPE_DATA = 1, HL_AMD_RESULT_TYPE_HDR = 2 };
+
+typedef struct hl_amd_params_s {
+    int32_t width;          /* hl_codec_t.width  (multiple of 16) */
+    int32_t height;         /* hl_codec_t.height (multiple of 16) */
+    int32_t qp;             /* hl_codec_t.qp, 0..51 */
+    int32_t me_range;       /* hl_codec_t.me_range, clipped to [1,64] (rdo.c:847) */
+    int32_t deblock;        /* hl_codec_t.deblock_flag */
+    int32_t gop_size;       /* hl_codec_t.gop_size */
+    int32_t me_early_term;  /* hl_codec_t.me_early_term_flag; only 0 is supported */
+    int32_t device;         /* HIP device ordinal */
+} hl_amd_params_t;
+
+typedef struct hl_amd_result_s {
+    int32_t type;            /* HL_AMD_RESULT_TYPE_* bits */
+    const uint8_t* hdr;      /* SPS + PPS with start codes, when type & HDR */
+    size_t hdr_size;
+    const uint8_t* data;     /* slice NAL without start code, when type & DATA */
+    size_t data_size;
+} hl_amd_result_t;
+
+typedef struct hl_amd_encoder_s hl_amd_encoder_t;
+
+/* hl_codec_create + option setting for HL_CODEC_TYPE_H264 (hl_codec.c:24-150) */
+int32_t hl_amd_encoder_create(const hl_amd_params_t* params, hl_amd_encoder_t** encoder);
+void hl_amd_encoder_destroy(hl_amd_encoder_t* encoder);
+
+/* plugin encode() for a planar YUV420 frame in host memory
+ * (hl_frame_video_t data_ptr[0..2], hl_frame.h:278-291) */
+int32_t hl_amd_encode(hl_amd_encoder_t* encoder, const uint8_t* y, const uint8_t* u, const uint8_t* v,
+                      hl_amd_result_t* result);
+
+/* same, with the planes already resident in device memory (HBM) */
+int32_t hl_amd_encode_device(hl_amd_encoder_t* encoder, const uint8_t* y, const uint8_t* u, const uint8_t* v,
+                             hl_amd_result_t* result);
+
+/* reconstructed (deblocked) picture of the last encoded frame, i.e. the
+ * reference picture the next frame predicts from (dpb.c:160-170) */
+int32_t hl_amd_get_recon(hl_amd_encoder_t* encoder, uint8_t* y, uint8_t* u, uint8_t* v);
+
+/* GPU time of the last encode call, in milliseconds, split by stage:
+ * [0] quarter-pel planes, [1] macroblock decision, [2] deblocking,
+ * [3] whole device part of the frame.  Filled only when timing is on. */
+int32_t hl_amd_set_timing(hl_amd_encoder_t* encoder, int32_t enable);
+int32_t hl_amd_get_timing(hl_amd_encoder_t* encoder, float* ms4);
+
+/* number of row-start re-runs the last frame needed (rdo.Single_ctr
+ * speculation) -- diagnostics */
+int32_t hl_amd_last_reruns(hl_amd_encoder_t* encoder);
+
+const char* hl_amd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -171,9 +171,10 @@ typedef struct {
     uint8_t* buf;
     size_t cap;
     int64_t nbits;
+    int64_t limit; /* last writable byte index (pc_end - pc_start), 0 = none */
 } bw_t;
 
-static void bw_init(bw_t* b, uint8_t* buf, size_t cap) { b->buf = buf; b->cap = cap; b->nbits = 0; }
+static void bw_init(bw_t* b, uint8_t* buf, size_t cap) { b->buf = buf; b->cap = cap; b->nbits = 0; b->limit = 0; }
 
 static void bw_u(bw_t* b, uint32_t v, int n)
 {
@@ -181,6 +182,7 @@ static void bw_u(bw_t* b, uint32_t v, int n)
         int i;
         for (i = n - 1; i >= 0; --i) {
             int64_t pos = b->nbits;
+            if (b->limit && (pos >> 3) > b->limit) return; /* EoB: bits_write_u1 drops (bits.h:236-246) */
             size_t byte = (size_t)(pos >> 3);
             int bit = 7 - (int)(pos & 7);
             if (byte < b->cap) {
@@ -285,7 +287,6 @@ struct hlo_enc_s {
 /* Small helpers                                                             */
 /* ------------------------------------------------------------------------- */
 static int is_intra(const mb_t* m) { return (m->flags & FL_INTRA) != 0; }
-static int is_inter(const mb_t* m) { return (m->flags & FL_INTER) != 0; }
 static int inv_raster(int a, int b, int c, int d, int e) { return e == 0 ? (a % (d / b)) * b : (a / (d / b)) * c; }
 static int luma_blk_idx(int x, int y) { return 8 * (y / 8) + 4 * (x / 8) + 2 * ((y % 8) / 4) + ((x % 8) / 4); }
 static int sad4x4(const uint8_t* a, int sa, const uint8_t* b, int sb)
@@ -2259,14 +2260,16 @@ static void write_slice_header(hlo_enc_t* e, bw_t* bw)
 }
 
 /* rbsp.c:609-632: escapes only 00 00 01 and never updates the caller's
- * length (encode.c:443-444), so each escape drops the last byte. */
-static void escape_inplace(uint8_t* p, size_t n, size_t cap)
+ * length (encode.c:443-444), so each escape drops the last byte.  size is
+ * the slice buffer size (encode.c:192). */
+static int escape_inplace(uint8_t* p, size_t n, size_t size)
 {
     size_t i, zeros = 0;
     for (i = 0; i < n; ++i) {
         if (zeros == 2) {
             if (p[i] == 0x01) {
-                if (n + 1 < cap) memmove(&p[i + 1], &p[i], n - i + 1);
+                if (n + 1 >= size) return -1; /* HL_ERROR_TOOSHORT (rbsp.c:617-620) */
+                memmove(&p[i + 1], &p[i], n - i + 1);
                 n++;
                 p[i++] = 0x03;
             }
@@ -2274,6 +2277,7 @@ static void escape_inplace(uint8_t* p, size_t n, size_t cap)
         }
         zeros = p[i] ? 0 : zeros + 1;
     }
+    return 0;
 }
 
 /* ------------------------------------------------------------------------- */
@@ -2348,6 +2352,9 @@ int hlo_encode_frame(hlo_enc_t* e, const uint8_t* y, const uint8_t* u, const uin
     e->skip_run = 0;
     memset(e->slice_buf, 0, e->slice_cap);
     bw_init(&bw, e->slice_buf, e->slice_cap);
+    /* the slice NAL is built in a (mb_count << 8) + 4096 byte buffer
+     * (encode.c:192); writes past its end are dropped (bits.h:236-246) */
+    bw.limit = ((int64_t)e->nmb << 8) + 4096;
     write_slice_header(e, &bw);
     for (a = 0; a < e->nmb; ++a) {
         mb_t* m = &e->mbs[a];
@@ -2361,7 +2368,7 @@ int hlo_encode_frame(hlo_enc_t* e, const uint8_t* y, const uint8_t* u, const uin
     if (e->p.deblock) deblock_picture(e);
     bw_trailing(&bw);
     slice_len = (size_t)((bw.nbits + 7) >> 3);
-    escape_inplace(e->slice_buf, slice_len, e->slice_cap);
+    if (escape_inplace(e->slice_buf, slice_len, (size_t)bw.limit)) return -3;
     out[n++] = 0;
     out[n++] = 0;
     out[n++] = 1;

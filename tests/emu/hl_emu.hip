@@ -1,0 +1,160 @@
+// hl_emu.hip -- TEST INFRASTRUCTURE.  Runs the product's macroblock kernel
+// logic (hartallo_amd/csrc/hl_mbcore.h, hl_filters.h) on the host, one lane
+// per workgroup (nthr = 1), in raster order, followed by the product's host
+// bitstream writer.  It lets tests/ diff the gfx950 kernel logic against the
+// oracle without a GPU.  The product library never links this file; it
+// fails loudly without a GPU instead of falling back to it.
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../hartallo_amd/csrc/hl_filters.h"
+#include "../../hartallo_amd/csrc/hl_writer.h"
+
+using namespace hl;
+
+struct EmuEnc {
+    int W, H, Wc, Hc, mbw, mbh, nmb, qp, qpc, me_range, deblock, gop;
+    int pstride;
+    std::vector<uint8_t> pic[2][3];
+    std::vector<uint8_t> pl[4];
+    std::vector<MbState> st;
+    std::vector<MbRecord> rec;
+    std::vector<MbChain> chain;
+    std::vector<int32_t> spec;
+    std::vector<uint8_t> scratch, out, hdr;
+    int cur, frame_index, gop_left, pict_count, idr_pic_id, chain_end;
+    Shared* S;
+};
+
+extern "C" void* emu_create(int W, int H, int qp, int me_range, int deblock, int gop)
+{
+    if (W <= 0 || H <= 0 || (W & 15) || (H & 15)) return nullptr;
+    EmuEnc* e = new EmuEnc();
+    e->W = W;
+    e->H = H;
+    e->Wc = W / 2;
+    e->Hc = H / 2;
+    e->mbw = W / 16;
+    e->mbh = H / 16;
+    e->nmb = e->mbw * e->mbh;
+    e->qp = qp;
+    e->qpc = kQpToQpc[qp];
+    e->me_range = me_range < 1 ? 1 : (me_range > 64 ? 64 : me_range);
+    e->deblock = deblock;
+    e->gop = gop;
+    e->pstride = W + 2 * kPad;
+    for (int k = 0; k < 2; ++k)
+        for (int c = 0; c < 3; ++c) e->pic[k][c].assign(c ? (size_t)e->Wc * e->Hc : (size_t)W * H, 0);
+    for (int i = 0; i < 4; ++i) e->pl[i].assign((size_t)e->pstride * (H + 2 * kPad), 0);
+    e->st.assign(e->nmb, MbState{});
+    memset(e->st.data(), 0, sizeof(MbState) * e->nmb);
+    e->rec.assign(e->nmb, MbRecord{});
+    e->chain.assign(e->nmb, MbChain{});
+    e->spec.assign(e->mbh, 0);
+    const StreamParams sp{W, H, qp, deblock};
+    e->scratch.resize(slice_scratch_bytes(sp));
+    e->out.resize(slice_scratch_bytes(sp) + 64);
+    e->hdr.resize(256);
+    e->hdr.resize(write_stream_headers(sp, e->hdr.data(), e->hdr.size()));
+    e->S = (Shared*)calloc(1, sizeof(Shared));
+    return e;
+}
+
+extern "C" void emu_destroy(void* h)
+{
+    EmuEnc* e = (EmuEnc*)h;
+    if (!e) return;
+    free(e->S);
+    delete e;
+}
+
+// Writes hdr (first frame) + 00 00 01 + slice into out; returns bytes or -1.
+extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, const uint8_t* v, uint8_t* out, long cap)
+{
+    EmuEnc* e = (EmuEnc*)h;
+    const bool intra = e->gop_left <= 0;
+    if (intra) e->gop_left = e->gop;
+    auto& cur = e->pic[e->cur];
+    auto& ref = e->pic[e->cur ^ 1];
+    if (!intra)
+        for (int p = 0; p < 4; ++p)
+            for (int py = 0; py < e->H + 2 * kPad; ++py)
+                for (int px = 0; px < e->W + 2 * kPad; ++px)
+                    e->pl[p][(size_t)py * e->pstride + px] = qpel_plane_sample(ref[0].data(), e->W, e->H, p, px - kPad, py - kPad);
+    FrameArgs F;
+    F.W = e->W;
+    F.H = e->H;
+    F.Wc = e->Wc;
+    F.Hc = e->Hc;
+    F.mbw = e->mbw;
+    F.mbh = e->mbh;
+    F.qp = e->qp;
+    F.qpc = e->qpc;
+    F.is_intra = intra;
+    F.me_range = e->me_range;
+    F.lambda = 0.852 * (double)(1 << ((e->qp - 12) / 3));
+    F.src[0] = y;
+    F.src[1] = u;
+    F.src[2] = v;
+    for (int c = 0; c < 3; ++c) {
+        F.cur[c] = cur[c].data();
+        F.ref[c] = ref[c].data();
+    }
+    for (int i = 0; i < 4; ++i) F.pl[i] = e->pl[i].data();
+    F.pstride = e->pstride;
+    F.st = e->st.data();
+    F.rec = e->rec.data();
+    F.chain = e->chain.data();
+    F.spec = e->spec.data();
+    int chain = e->chain_end;
+    for (int a = 0; a < e->nmb; ++a) {
+        encode_mb(F, *e->S, a, 0, 1, chain);
+        chain = e->chain[a].s_out;
+    }
+    e->chain_end = chain;
+    if (e->deblock) {
+        DeblockArgs D;
+        D.W = e->W;
+        D.H = e->H;
+        D.Wc = e->Wc;
+        D.mbw = e->mbw;
+        D.qp = e->qp;
+        D.qpc = e->qpc;
+        for (int c = 0; c < 3; ++c) D.pic[c] = cur[c].data();
+        D.st = e->st.data();
+        for (int a = 0; a < e->nmb; ++a)
+            for (int step = 0; step < 8; ++step)
+                for (int lane = 0; lane < 32; ++lane) deblock_mb_step(D, a, step, lane);
+    }
+    const StreamParams sp{e->W, e->H, e->qp, e->deblock};
+    const SliceState ss{intra ? 1 : 0, e->pict_count, e->idr_pic_id};
+    size_t n = 0;
+    if (e->frame_index == 0) {
+        if ((long)e->hdr.size() > cap) return -1;
+        memcpy(out, e->hdr.data(), e->hdr.size());
+        n = e->hdr.size();
+    }
+    const size_t m = write_slice(sp, ss, e->rec.data(), e->scratch.data(), out + n, (size_t)cap - n);
+    if (!m) return -1;
+    n += m;
+    e->cur ^= 1;
+    ++e->pict_count;
+    if (intra) ++e->idr_pic_id;
+    --e->gop_left;
+    ++e->frame_index;
+    return (long)n;
+}
+
+extern "C" const uint8_t* emu_recon(void* h, int plane)
+{
+    EmuEnc* e = (EmuEnc*)h;
+    return e->pic[e->cur ^ 1][plane].data();
+}
+
+extern "C" const void* emu_records(void* h) { return ((EmuEnc*)h)->rec.data(); }
+extern "C" int emu_record_size(void) { return (int)sizeof(MbRecord); }
+extern "C" const void* emu_states(void* h) { return ((EmuEnc*)h)->st.data(); }
+extern "C" int emu_state_size(void) { return (int)sizeof(MbState); }

@@ -1,0 +1,55 @@
+"""Regenerates tests/golden/ from the reference encoder itself.
+
+Each configuration in tests/hl_testlib.GOLDEN_CONFIGS is synthesised with
+hartallo_amd.synth (seeded), encoded by oracle/_ref/ref_enc (the reference's
+own C sources compiled by oracle/Makefile, driven through hl_codec_encode as
+source/test_encoder.c does), and stored as:
+  <name>.264        the reference's Annex-B output
+  golden.json       per-config parameters, stream MD5 and per-frame MD5 of
+                    the reference's reconstructed (deblocked) pictures
+
+Run in the build container (needs /root/reference):  python tests/golden/make_golden.py
+"""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import numpy as np  # noqa: E402
+
+from hl_testlib import GOLDEN_CONFIGS, REF_ENC, golden_input, md5  # noqa: E402
+
+
+def main():
+    if not os.path.exists(REF_ENC):
+        sys.exit(f"{REF_ENC} missing: run `make -C oracle ref` where /root/reference exists")
+    table = {}
+    with tempfile.TemporaryDirectory() as td:
+        for cfg in GOLDEN_CONFIGS:
+            name, w, h, n, qp, mer, db, gop, seed = cfg
+            clip = golden_input(cfg)
+            inp = os.path.join(td, name + ".yuv")
+            clip.tofile(inp)
+            pre = os.path.join(td, name)
+            subprocess.run([REF_ENC, str(w), str(h), str(n), str(qp), str(mer), str(db), str(gop), "0", inp, pre], check=True,
+                           stdout=subprocess.DEVNULL)
+            stream = open(pre + ".264", "rb").read()
+            rec = np.fromfile(pre + ".rec.yuv", dtype=np.uint8).reshape(n, -1)
+            with open(os.path.join(HERE, name + ".264"), "wb") as f:
+                f.write(stream)
+            table[name] = {
+                "width": w, "height": h, "frames": n, "qp": qp, "me_range": mer, "deblock": db, "gop": gop, "seed": seed,
+                "stream_md5": md5(stream), "stream_bytes": len(stream),
+                "recon_md5": [md5(r) for r in rec],
+            }
+            print(f"{name}: {len(stream)} bytes")
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(table, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,181 @@
+"""Test support: ctypes bindings of the CPU oracle (oracle/_build/
+libhloracle.so), of the host emulation of the kernel logic (tests/emu/
+libhl_emu.so) and shared helpers.  TEST INFRASTRUCTURE ONLY -- the product
+(hartallo_amd/) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from hartallo_amd import synth  # noqa: E402
+
+ORACLE_LIB = os.path.join(ROOT, "oracle", "_build", "libhloracle.so")
+EMU_LIB = os.path.join(ROOT, "tests", "emu", "libhl_emu.so")
+REF_ENC = os.path.join(ROOT, "oracle", "_ref", "ref_enc")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+class _OParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("width", "height", "qp", "me_range", "deblock", "gop_size", "early_term")]
+
+
+_oracle = None
+_emu = None
+
+
+def oracle_lib():
+    global _oracle
+    if _oracle is None:
+        lib = ctypes.CDLL(ORACLE_LIB)
+        lib.hlo_create.argtypes = [ctypes.POINTER(_OParams)]
+        lib.hlo_create.restype = ctypes.c_void_p
+        lib.hlo_destroy.argtypes = [ctypes.c_void_p]
+        lib.hlo_encode_frame.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+        lib.hlo_encode_frame.restype = ctypes.c_int
+        lib.hlo_recon.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        lib.hlo_recon.restype = ctypes.c_void_p
+        lib.hlo_rdo_overflows.argtypes = [ctypes.c_void_p]
+        lib.hlo_rdo_overflows.restype = ctypes.c_int64
+        _oracle = lib
+    return _oracle
+
+
+def emu_lib():
+    global _emu
+    if _emu is None:
+        lib = ctypes.CDLL(EMU_LIB)
+        lib.emu_create.restype = ctypes.c_void_p
+        lib.emu_create.argtypes = [ctypes.c_int] * 6
+        lib.emu_destroy.argtypes = [ctypes.c_void_p]
+        lib.emu_encode_frame.restype = ctypes.c_long
+        lib.emu_encode_frame.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_long]
+        lib.emu_recon.restype = ctypes.c_void_p
+        lib.emu_recon.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        _emu = lib
+    return _emu
+
+
+def _planes(frame: np.ndarray, w: int, h: int):
+    n = w * h
+    return frame[:n], frame[n:n + n // 4], frame[n + n // 4:n * 3 // 2]
+
+
+def _recon(ptr_fn, w: int, h: int) -> np.ndarray:
+    n = w * h
+    parts = []
+    for p, sz in ((0, n), (1, n // 4), (2, n // 4)):
+        parts.append(np.ctypeslib.as_array(ctypes.cast(ptr_fn(p), ctypes.POINTER(ctypes.c_uint8)), shape=(sz,)).copy())
+    return np.concatenate(parts)
+
+
+class OracleEncoder:
+    """CPU restatement of the reference encoder (oracle/hl_oracle.c)."""
+
+    def __init__(self, w, h, qp=28, me_range=16, deblock=1, gop=30):
+        self.lib = oracle_lib()
+        self.w, self.h = w, h
+        p = _OParams(w, h, qp, me_range, deblock, gop, 0)
+        self.h_ = self.lib.hlo_create(ctypes.byref(p))
+        if not self.h_:
+            raise ValueError("oracle rejected parameters")
+        self.out = np.zeros(w * h * 4 + (1 << 20), np.uint8)
+
+    def encode(self, frame: np.ndarray) -> bytes:
+        y, u, v = _planes(frame, self.w, self.h)
+        n = ctypes.c_size_t()
+        rc = self.lib.hlo_encode_frame(ctypes.c_void_p(self.h_), y.ctypes.data, u.ctypes.data, v.ctypes.data, self.out.ctypes.data,
+                                       self.out.size, ctypes.byref(n))
+        assert rc == 0
+        return self.out[:n.value].tobytes()
+
+    def recon(self) -> np.ndarray:
+        return _recon(lambda p: self.lib.hlo_recon(ctypes.c_void_p(self.h_), p), self.w, self.h)
+
+    def rdo_overflows(self) -> int:
+        return self.lib.hlo_rdo_overflows(ctypes.c_void_p(self.h_))
+
+    def __del__(self):
+        if getattr(self, "h_", None):
+            self.lib.hlo_destroy(ctypes.c_void_p(self.h_))
+
+
+class EmuEncoder:
+    """Host build of the gfx950 kernel logic (tests/emu/hl_emu.hip)."""
+
+    def __init__(self, w, h, qp=28, me_range=16, deblock=1, gop=30):
+        self.lib = emu_lib()
+        self.w, self.h = w, h
+        self.h_ = self.lib.emu_create(w, h, qp, me_range, deblock, gop)
+        self.out = np.zeros(w * h * 4 + (1 << 20), np.uint8)
+
+    def encode(self, frame: np.ndarray) -> bytes:
+        y, u, v = _planes(frame, self.w, self.h)
+        n = self.lib.emu_encode_frame(ctypes.c_void_p(self.h_), y.ctypes.data, u.ctypes.data, v.ctypes.data, self.out.ctypes.data,
+                                      self.out.size)
+        assert n > 0
+        return self.out[:n].tobytes()
+
+    def recon(self) -> np.ndarray:
+        return _recon(lambda p: self.lib.emu_recon(ctypes.c_void_p(self.h_), p), self.w, self.h)
+
+    def __del__(self):
+        if getattr(self, "h_", None):
+            self.lib.emu_destroy(ctypes.c_void_p(self.h_))
+
+
+class GpuEncoder:
+    """The product (libhartallo_amd.so) with the same encode() shape."""
+
+    def __init__(self, w, h, qp=28, me_range=16, deblock=1, gop=30):
+        from hartallo_amd import Encoder
+
+        self.enc = Encoder(w, h, qp, me_range, deblock, gop)
+        self.w, self.h = w, h
+
+    def encode(self, frame: np.ndarray) -> bytes:
+        y, u, v = _planes(frame, self.w, self.h)
+        return self.enc.encode(y, u, v).annexb()
+
+    def recon(self) -> np.ndarray:
+        return np.concatenate(self.enc.recon())
+
+
+def md5(b) -> str:
+    return hashlib.md5(bytes(b)).hexdigest()
+
+
+def first_diff(a: bytes, b: bytes) -> int:
+    for i in range(min(len(a), len(b))):
+        if a[i] != b[i]:
+            return i
+    return -1 if len(a) == len(b) else min(len(a), len(b))
+
+
+# Golden configurations: (name, W, H, frames, qp, me_range, deblock, gop, seed).
+# tests/golden/make_golden.py encodes them with the reference (oracle/_ref/ref_enc).
+GOLDEN_CONFIGS = [
+    ("cif_i_qp31", 352, 288, 1, 31, 8, 0, 400, 1),           # config 1: test_encoder.c settings
+    ("cif_ippp_qp31_me8", 352, 288, 6, 31, 8, 0, 400, 2),
+    ("qcif_ippp_qp28_db", 176, 144, 8, 28, 16, 1, 30, 3),
+    ("qcif_gop3_qp20_me4", 176, 144, 8, 20, 4, 1, 3, 4),
+    ("qcif_qp40_me16_gop4", 176, 144, 8, 40, 16, 1, 4, 5),
+    ("qcif_qp12_me2", 176, 144, 4, 12, 2, 1, 400, 6),
+    ("qcif_qp51", 176, 144, 4, 51, 8, 1, 400, 7),
+    ("tiny_32x16_qp26", 32, 16, 6, 26, 8, 1, 2, 8),
+    ("qcif_qp0_me1", 176, 144, 3, 0, 1, 1, 400, 9),
+    ("w480_h272_qp28_me16", 480, 272, 4, 28, 16, 1, 30, 10),
+]
+
+
+def golden_input(cfg) -> np.ndarray:
+    _, w, h, n, _, _, _, _, seed = cfg
+    return synth.clip(w, h, n, seed)
