@@ -1,0 +1,156 @@
+#!/usr/bin/env python3
+"""bench.py -- encoded 1920x1088 frames/s (bit-exact H.264 Baseline), MI355X.
+
+Workload (BASELINE.json configs[2] as the reference can express it, SURVEY
+§8(d) c3): 1920x1088 YUV420 IPPP, GOP 30, QP 28, ME range 16, deblocking on,
+synthetic input (hartallo_amd.synth, seeded per rank).  A step is one frame
+through the whole encode path (quarter-pel planes, MB decisions, deblocking,
+CAVLC bitstream); inputs are resident in HBM before the timed region.
+
+Multi-GPU: one independent stream per GPU (frame-sharded throughput mode,
+SURVEY §8(e) c5) -- weak scaling, no data-path collective; torch.distributed
+(gloo) carries only the barrier and the max-over-ranks of the elapsed time.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+W, H = 1920, 1088
+QP, ME_RANGE, DEBLOCK, GOP = 28, 16, 1, 30
+BYTES_PER_MB = 2752  # compulsory HBM bytes per macroblock, DESIGN.md / SURVEY §8(d)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def cpu_baseline(frames_host, n_frames):
+    """Times the reference encoder (oracle/_ref/ref_enc, built from the
+    reference's own sources) -- or, without it, the bit-exact C restatement --
+    on the first n_frames of this rank's workload, single thread."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_enc")
+    orc = os.path.join(ROOT, "oracle", "_build", "hlenc_oracle")
+    exe, kind = (ref, "reference") if os.path.exists(ref) else (orc, "port")
+    if not os.path.exists(exe):
+        return None
+    with tempfile.TemporaryDirectory() as td:
+        inp = os.path.join(td, "in.yuv")
+        frames_host[:n_frames].tofile(inp)
+        cmd = [exe, str(W), str(H), str(n_frames), str(QP), str(ME_RANGE), str(DEBLOCK), str(GOP), "0", inp, os.path.join(td, "o"), "quiet"]
+        r = subprocess.run(cmd, capture_output=True, text=True, check=True)
+        info = json.loads(r.stdout.strip().splitlines()[-1])
+    return {
+        "value": round(info["fps"], 4),
+        "unit": "frames/s",
+        "cores": 1,
+        "kind": kind,
+        "sample": f"first {n_frames} frames (1 I + {n_frames - 1} P) of the same 1920x1088 QP{QP} stream, encode time only, 1 thread",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--cpu-frames", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+
+    from hartallo_amd import Encoder, synth
+
+    n_frames = args.warmup + args.steps
+    frames_host = synth.clip(W, H, n_frames, 11 + rank)
+    # inputs resident in HBM before timing
+    dev = torch.from_numpy(frames_host).to(f"cuda:{local}")
+    torch.cuda.synchronize()
+    ny, nc = W * H, W * H // 4
+    ptrs = [(dev[i].data_ptr(), dev[i].data_ptr() + ny, dev[i].data_ptr() + ny + nc) for i in range(n_frames)]
+
+    enc = Encoder(W, H, QP, ME_RANGE, DEBLOCK, GOP, 0, local)
+    for i in range(args.warmup):
+        enc.encode_device(*ptrs[i], collect=False)
+    enc.set_timing(True)
+    mb_ms = mb_launches = 0.0
+    out_bytes = 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, n_frames):
+        out_bytes += enc.encode_device(*ptrs[i], collect=False)
+        ms = enc.timing_ms()
+        mb_ms += ms[1]
+        mb_launches += enc.last_mb_launches()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    base = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        base = cpu_baseline(frames_host, min(args.cpu_frames, n_frames))
+
+    if rank == 0:
+        total = world * args.steps
+        fps = total / elapsed
+        nmb = (W // 16) * (H // 16)
+        # dominant kernel: k_mb_diag; algorithmic bytes per launch = 2752 B x MBs per launch
+        avg_launch_s = (mb_ms / 1e3) / mb_launches
+        bytes_per_launch = BYTES_PER_MB * nmb * args.steps / mb_launches
+        achieved = bytes_per_launch / avg_launch_s / 1e9
+        line = {
+            "metric": "1080p encoded frames/sec (bit-exact) at 1/2/4/8 MI355X; macroblocks/sec/GPU",
+            "value": round(fps, 4),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8/int32",
+            "data": "synthetic (hartallo_amd.synth, seeded per rank)",
+            "config": {"workload": "1920x1088 YUV420 IPPP GOP30 QP28 ME16 deblock, one stream per GPU", "width": W, "height": H,
+                       "qp": QP, "me_range": ME_RANGE, "deblock": DEBLOCK, "gop": GOP, "parallelism": f"streams{world}"},
+            "mb_per_s_per_gpu": round(fps / world * nmb, 1),
+            "bitstream_bytes_per_frame": round(out_bytes / args.steps, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_mb_diag", "avg_launch_us": round(avg_launch_s * 1e6, 2),
+                         "launches_per_frame": round(mb_launches / args.steps, 1),
+                         "note": "latency-bound MB wavefront; achieved = 2752 B/MB x MBs per launch / mean launch time"},
+            "cpu_baseline": base,
+        }
+        print(json.dumps(line), flush=True)
+    enc.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -35,6 +35,7 @@ EXPORTED_SYMBOLS = (
     "hl_amd_set_timing",
     "hl_amd_get_timing",
     "hl_amd_last_reruns",
+    "hl_amd_last_mb_launches",
     "hl_amd_version",
 )
 
@@ -92,6 +93,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_get_timing.restype = i32
     lib.hl_amd_last_reruns.argtypes = [vp]
     lib.hl_amd_last_reruns.restype = i32
+    lib.hl_amd_last_mb_launches.argtypes = [vp]
+    lib.hl_amd_last_mb_launches.restype = i32
     lib.hl_amd_version.argtypes = []
     lib.hl_amd_version.restype = ctypes.c_char_p
     _lib = lib
@@ -186,3 +189,6 @@ class Encoder:
 
     def last_reruns(self) -> int:
         return self.lib.hl_amd_last_reruns(self._h)
+
+    def last_mb_launches(self) -> int:
+        return self.lib.hl_amd_last_mb_launches(self._h)

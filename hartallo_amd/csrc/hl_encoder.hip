@@ -109,8 +109,9 @@ struct hl_amd_encoder_s {
     std::vector<uint8_t> hdr, out, scratch;
     int32_t frame_index, gop_left, pict_count, idr_pic_id, chain_end, reruns;
     bool timing;
-    hipEvent_t ev[4];
+    hipEvent_t ev[6];
     float ms[4];
+    int32_t mb_launches;
 };
 
 static void free_all(hl_amd_encoder_t* e)
@@ -130,7 +131,7 @@ static void free_all(hl_amd_encoder_t* e)
     (void)hipHostFree(e->h_chain);
     (void)hipHostFree(e->h_spec);
     if (e->stream) (void)hipStreamDestroy(e->stream);
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 6; ++i)
         if (e->ev[i]) (void)hipEventDestroy(e->ev[i]);
 }
 
@@ -169,7 +170,7 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
          hipHostMalloc(&e->h_chain, sizeof(MbChain) * e->nmb, hipHostMallocDefault) == hipSuccess &&
          hipHostMalloc(&e->h_spec, sizeof(int32_t) * e->mbh, hipHostMallocDefault) == hipSuccess;
     ok = ok && hipMemset(e->d_st, 0, sizeof(MbState) * e->nmb) == hipSuccess;
-    for (int i = 0; i < 4 && ok; ++i) ok = hipEventCreate(&e->ev[i]) == hipSuccess;
+    for (int i = 0; i < 6 && ok; ++i) ok = hipEventCreate(&e->ev[i]) == hipSuccess;
     if (!ok) {
         free_all(e);
         delete e;
@@ -201,6 +202,7 @@ static hipError_t run_wavefront(hl_amd_encoder_t* e, const FrameArgs& F, int row
         const int n = diag_count(e->mbw, rows, d);
         if (!n) continue;
         k_mb_diag<<<n, kMbThreads, 0, e->stream>>>(F, d, row0);
+        ++e->mb_launches;
     }
     return hipGetLastError();
 }
@@ -273,11 +275,20 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
     for (int yy = 1; yy < e->mbh; ++yy) e->h_spec[yy] = 9;
     int row0 = 0, chain_end = 0;
     e->reruns = 0;
+    e->mb_launches = 0;
+    e->ms[1] = 0.f;
     for (;;) {
         HL_HIP_CHECK(hipMemcpyAsync(e->d_spec, e->h_spec, sizeof(int32_t) * e->mbh, hipMemcpyHostToDevice, e->stream));
+        if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[4], e->stream));
         HL_HIP_CHECK(run_wavefront(e, F, row0));
+        if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[5], e->stream));
         HL_HIP_CHECK(hipMemcpyAsync(e->h_chain, e->d_chain, sizeof(MbChain) * e->nmb, hipMemcpyDeviceToHost, e->stream));
         HL_HIP_CHECK(hipStreamSynchronize(e->stream));
+        if (e->timing) {
+            float t = 0.f;
+            (void)hipEventElapsedTime(&t, e->ev[4], e->ev[5]);
+            e->ms[1] += t;
+        }
         const int bad = validate_chain(e, row0, chain_end);
         if (bad < 0) break;
         ++e->reruns;
@@ -309,7 +320,6 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
     HL_HIP_CHECK(hipStreamSynchronize(e->stream));
     if (e->timing) {
         (void)hipEventElapsedTime(&e->ms[0], e->ev[0], e->ev[1]);
-        (void)hipEventElapsedTime(&e->ms[1], e->ev[1], e->ev[2]);
         (void)hipEventElapsedTime(&e->ms[2], e->ev[2], e->ev[3]);
         (void)hipEventElapsedTime(&e->ms[3], e->ev[0], e->ev[3]);
     }
@@ -373,5 +383,7 @@ extern "C" int32_t hl_amd_get_timing(hl_amd_encoder_t* e, float* ms4)
 }
 
 extern "C" int32_t hl_amd_last_reruns(hl_amd_encoder_t* e) { return e ? e->reruns : -1; }
+
+extern "C" int32_t hl_amd_last_mb_launches(hl_amd_encoder_t* e) { return e ? e->mb_launches : -1; }
 
 extern "C" const char* hl_amd_version(void) { return "hartallo_amd 0.1 (gfx950)"; }

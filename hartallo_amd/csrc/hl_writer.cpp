@@ -190,6 +190,12 @@ size_t put_nal(uint8_t* out, size_t cap, const uint8_t* rbsp, size_t n)
 
 }  // namespace
 
+int level_code_bits(int suffix_length, int code)
+{
+    const LevelCode& L = level_code(suffix_length, code);
+    return L.prefix + 1 + L.size;
+}
+
 size_t write_stream_headers(const StreamParams& p, uint8_t* out, size_t cap)
 {
     uint8_t buf[64];

@@ -51,6 +51,11 @@ struct SliceState {
 // out, or 0 when out is too small or the reference would fail the frame with
 // HL_ERROR_TOOSHORT (an escape that does not fit its slice buffer).
 size_t slice_scratch_bytes(const StreamParams& p);
+
+// Bits of one level code (level_prefix + 1 + level_suffix) from the table the
+// writer serialises with; the GPU bit counter (hl_prims.h level_code_len)
+// must agree with it for every (suffixLength, levelCode).
+int level_code_bits(int suffix_length, int level_code);
 size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap);
 
 }  // namespace hl

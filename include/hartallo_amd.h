@@ -93,14 +93,19 @@ int32_t hl_amd_encode_device(hl_amd_encoder_t* encoder, const uint8_t* y, const 
 int32_t hl_amd_get_recon(hl_amd_encoder_t* encoder, uint8_t* y, uint8_t* u, uint8_t* v);
 
 /* GPU time of the last encode call, in milliseconds, split by stage:
- * [0] quarter-pel planes, [1] macroblock decision, [2] deblocking,
- * [3] whole device part of the frame.  Filled only when timing is on. */
+ * [0] quarter-pel planes kernel, [1] macroblock-decision kernels (sum over
+ * the wavefront launches, re-runs included), [2] deblocking kernels,
+ * [3] the frame's device timeline from planes to deblock end (host
+ * validation gaps included).  Filled only when timing is on. */
 int32_t hl_amd_set_timing(hl_amd_encoder_t* encoder, int32_t enable);
 int32_t hl_amd_get_timing(hl_amd_encoder_t* encoder, float* ms4);
 
 /* number of row-start re-runs the last frame needed (rdo.Single_ctr
  * speculation) -- diagnostics */
 int32_t hl_amd_last_reruns(hl_amd_encoder_t* encoder);
+
+/* number of macroblock-decision kernel launches of the last frame */
+int32_t hl_amd_last_mb_launches(hl_amd_encoder_t* encoder);
 
 const char* hl_amd_version(void);
 

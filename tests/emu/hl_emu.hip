@@ -158,3 +158,7 @@ extern "C" const void* emu_records(void* h) { return ((EmuEnc*)h)->rec.data(); }
 extern "C" int emu_record_size(void) { return (int)sizeof(MbRecord); }
 extern "C" const void* emu_states(void* h) { return ((EmuEnc*)h)->st.data(); }
 extern "C" int emu_state_size(void) { return (int)sizeof(MbState); }
+
+// unit hooks: GPU-side bit counting vs the writer's table
+extern "C" int emu_level_code_len(int sl, int lc) { return level_code_len(sl, lc); }
+extern "C" int emu_writer_level_bits(int sl, int lc) { return level_code_bits(sl, lc); }
