@@ -64,22 +64,15 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    import numpy as np
     import torch
-    import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hartallo_amd import Encoder, dist, synth
+
+    rank, world, local = dist.init_from_env()
     torch.cuda.set_device(local)
 
-    from hartallo_amd import Encoder, synth
-
     n_frames = args.warmup + args.steps
-    frames_host = synth.clip(W, H, n_frames, 11 + rank)
+    frames_host = synth.clip(W, H, n_frames, dist.stream_seed(rank))
     # inputs resident in HBM before timing
     dev = torch.from_numpy(frames_host).to(f"cuda:{local}")
     torch.cuda.synchronize()
@@ -92,8 +85,7 @@ def main():
     enc.set_timing(True)
     mb_ms = mb_launches = 0.0
     out_bytes = 0
-    if world > 1:
-        dist.barrier()
+    dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.warmup, n_frames):
@@ -102,13 +94,8 @@ def main():
         mb_ms += ms[1]
         mb_launches += enc.last_mb_launches()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    dist.barrier()
+    elapsed = dist.max_over_ranks(time.perf_counter() - t0)
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -148,8 +135,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     enc.close()
-    if world > 1:
-        dist.destroy_process_group()
+    dist.shutdown()
 
 
 if __name__ == "__main__":
