@@ -9,7 +9,7 @@ HDRS    := $(wildcard $(CSRC)/*.h) include/hartallo_amd.h
 # -ffp-contract=off: the RDO costs are IEEE double and must round exactly like the reference
 CXXFLAGS := -std=c++17 -O3 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-variable
 
-.PHONY: all product emu oracle clean
+.PHONY: all product emu oracle profile clean
 all: product emu oracle
 
 product: hartallo_amd/libhartallo_amd.so
@@ -20,6 +20,12 @@ hartallo_amd/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp $(
 
 tests/emu/libhl_emu.so: tests/emu/hl_emu.hip $(CSRC)/hl_writer.cpp $(HDRS)
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -O2 -shared -o $@ tests/emu/hl_emu.hip $(CSRC)/hl_writer.cpp
+
+# profiling build: same library with per-phase clock64 counters (tools/phase_profile.py)
+profile: build/prof/hartallo_amd/libhartallo_amd.so
+build/prof/hartallo_amd/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp $(HDRS)
+	mkdir -p build/prof/hartallo_amd
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DHL_PROFILE=1 -shared -o $@ $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp
 
 oracle:
 	$(MAKE) -C oracle

@@ -36,6 +36,7 @@ EXPORTED_SYMBOLS = (
     "hl_amd_get_timing",
     "hl_amd_last_reruns",
     "hl_amd_last_mb_launches",
+    "hl_amd_profile_counters",
     "hl_amd_version",
 )
 
@@ -95,6 +96,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_last_reruns.restype = i32
     lib.hl_amd_last_mb_launches.argtypes = [vp]
     lib.hl_amd_last_mb_launches.restype = i32
+    lib.hl_amd_profile_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong), i32]
+    lib.hl_amd_profile_counters.restype = i32
     lib.hl_amd_version.argtypes = []
     lib.hl_amd_version.restype = ctypes.c_char_p
     _lib = lib
@@ -189,6 +192,11 @@ class Encoder:
 
     def last_reruns(self) -> int:
         return self.lib.hl_amd_last_reruns(self._h)
+
+    def profile_counters(self, n: int = 32):
+        a = (ctypes.c_ulonglong * n)()
+        self.lib.hl_amd_profile_counters(self._h, a, n)
+        return list(a)
 
     def last_mb_launches(self) -> int:
         return self.lib.hl_amd_last_mb_launches(self._h)

@@ -112,6 +112,7 @@ struct hl_amd_encoder_s {
     hipEvent_t ev[6];
     float ms[4];
     int32_t mb_launches;
+    unsigned long long* d_prof;  // phase counters (HL_PROFILE builds)
 };
 
 static void free_all(hl_amd_encoder_t* e)
@@ -127,6 +128,7 @@ static void free_all(hl_amd_encoder_t* e)
     (void)hipFree(e->d_rec);
     (void)hipFree(e->d_chain);
     (void)hipFree(e->d_spec);
+    (void)hipFree(e->d_prof);
     (void)hipHostFree(e->h_rec);
     (void)hipHostFree(e->h_chain);
     (void)hipHostFree(e->h_spec);
@@ -170,6 +172,10 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
          hipHostMalloc(&e->h_chain, sizeof(MbChain) * e->nmb, hipHostMallocDefault) == hipSuccess &&
          hipHostMalloc(&e->h_spec, sizeof(int32_t) * e->mbh, hipHostMallocDefault) == hipSuccess;
     ok = ok && hipMemset(e->d_st, 0, sizeof(MbState) * e->nmb) == hipSuccess;
+#if defined(HL_PROFILE)
+    ok = ok && hipMalloc(&e->d_prof, 64 * sizeof(unsigned long long)) == hipSuccess &&
+         hipMemset(e->d_prof, 0, 64 * sizeof(unsigned long long)) == hipSuccess;
+#endif
     for (int i = 0; i < 6 && ok; ++i) ok = hipEventCreate(&e->ev[i]) == hipSuccess;
     if (!ok) {
         free_all(e);
@@ -262,6 +268,7 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
     F.rec = e->d_rec;
     F.chain = e->d_chain;
     F.spec = e->d_spec;
+    F.prof = e->d_prof;
 
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[0], e->stream));
     if (!intra) {
@@ -385,5 +392,16 @@ extern "C" int32_t hl_amd_get_timing(hl_amd_encoder_t* e, float* ms4)
 extern "C" int32_t hl_amd_last_reruns(hl_amd_encoder_t* e) { return e ? e->reruns : -1; }
 
 extern "C" int32_t hl_amd_last_mb_launches(hl_amd_encoder_t* e) { return e ? e->mb_launches : -1; }
+
+// Phase cycle counters of HL_PROFILE builds (zeros otherwise); n <= 64.
+extern "C" int32_t hl_amd_profile_counters(hl_amd_encoder_t* e, unsigned long long* out, int32_t n)
+{
+    if (!e || !out || n > 64) return HL_AMD_ERROR_INVALID_PARAMETER;
+    memset(out, 0, sizeof(unsigned long long) * n);
+    if (!e->d_prof) return HL_AMD_SUCCESS;
+    HL_HIP_CHECK(hipMemcpy(out, e->d_prof, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
+    HL_HIP_CHECK(hipMemset(e->d_prof, 0, sizeof(unsigned long long) * 64));
+    return HL_AMD_SUCCESS;
+}
 
 extern "C" const char* hl_amd_version(void) { return "hartallo_amd 0.1 (gfx950)"; }

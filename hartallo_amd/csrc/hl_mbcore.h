@@ -39,6 +39,22 @@ namespace hl {
 #define HL_SYNC() ((void)0)
 #endif
 
+// Optional phase timing (profiling build only, -DHL_PROFILE): lane 0
+// accumulates shader-clock cycles per phase into FrameArgs::prof.
+#if defined(HL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+#define HL_PROF_T(v) const unsigned long long v = clock64()
+#define HL_PROF_ADD(c, slot, t0)                                                  \
+    do {                                                                        \
+        if ((c).tid == 0 && (c).F.prof) {                                       \
+            atomicAdd(&(c).F.prof[2 * (slot)], (unsigned long long)(clock64() - (t0))); \
+            atomicAdd(&(c).F.prof[2 * (slot) + 1], 1ull);                        \
+        }                                                                       \
+    } while (0)
+#else
+#define HL_PROF_T(v) const unsigned long long v = 0
+#define HL_PROF_ADD(c, slot, t0) ((void)(t0))
+#endif
+
 constexpr int kPad = 40;  // padding of the luma reference planes (origin clip is +-17, block 16, tap 3)
 constexpr int kNA = -1;   // not-available sample marker
 
@@ -55,6 +71,7 @@ struct FrameArgs {
     MbRecord* rec;
     MbChain* chain;
     const int32_t* spec;  // speculated Single_ctr at each row start
+    unsigned long long* prof;  // phase cycle counters (profiling build), may be null
 };
 
 struct NbInfo {
@@ -496,11 +513,21 @@ struct PartGeo {
 
 // Evaluates S.cmv[0..ncand) for partition g in order.  Leaves per-candidate
 // rbc/dist/single/cbp in S.cd_*, updates S.tc (last writer) and the chain.
+#if defined(HL_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+extern long long g_hl_stats[8];
+#endif
 HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand)
 {
+#if defined(HL_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+    g_hl_stats[0]++;
+    g_hl_stats[1] += ncand;
+    g_hl_stats[2] += ncand * g.nblk;
+    g_hl_stats[3 + (g.nblk == 16 ? 0 : (g.nblk == 4 ? 1 : (g.nblk == 2 ? 2 : 3)))]++;
+#endif
     const FrameArgs& F = c.F;
     Shared& S = c.S;
     const int n = ncand * g.nblk;
+    HL_PROF_T(tp0);
     // phase 1: transform / quant / CAVLC statistics / reconstruction per block
     for (int t = c.tid; t < n; t += c.nthr) {
         const int ci = t / g.nblk, k = t % g.nblk;
@@ -550,6 +577,8 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand)
         S.be_dist[ci][k] = dist;
     }
     HL_SYNC();
+    HL_PROF_ADD(c, 0, tp0);
+    HL_PROF_T(tp1);
     // phase 2: nC as the reference sees it at this point of the sequence
     for (int t = c.tid; t < n; t += c.nthr) {
         const int ci = t / g.nblk, k = t % g.nblk;
@@ -569,6 +598,8 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand)
         S.be_bits[ci][k] += token_len(nC, S.be_tc[ci][k], S.be_t1[ci][k]);
     }
     HL_SYNC();
+    HL_PROF_ADD(c, 1, tp1);
+    HL_PROF_T(tp2);
     // phase 3: per-candidate sums; live TotalCoeffsLuma = last writer
     for (int t = c.tid; t < ncand + g.nblk; t += c.nthr) {
         if (t < ncand) {
@@ -601,6 +632,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand)
         }
     }
     HL_SYNC();
+    HL_PROF_ADD(c, 2, tp2);
     for (int ci = ncand - 1; ci >= 0; --ci)
         if (S.cd_last[ci] >= 0) {
             chain_write(c, S.cd_last[ci]);
@@ -626,6 +658,7 @@ HD double cand_cost(const Ctx& c, int ci, const int pmv[2])
 HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
 {
     Shared& S = c.S;
+    HL_PROF_T(tsp);
     const int xP = (pi % (16 / pd.part_w)) * pd.part_w, yP = (pi / (16 / pd.part_w)) * pd.part_h;
     int xS = 0, yS = 0;
     if (pd.num_part == 4) {
@@ -669,7 +702,11 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
             }
         }
     }
-    mvp(S, pi, spi, pmv);
+    {
+        HL_PROF_T(tm);
+        mvp(S, pi, spi, pmv);
+        HL_PROF_ADD(c, 4, tm);
+    }
     // MVP and (0,0) candidates, me_ds.c:280-300
     const int nc0 = (pmv[0] != 0 || pmv[1] != 0) ? 2 : 1;
     HL_SYNC();
@@ -780,6 +817,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         S.nb[0].mv[pi][spi][1] = (int16_t)b.mv[1];
     }
     HL_SYNC();
+    HL_PROF_ADD(c, 3, tsp);
     return probably;
 }
 
@@ -1679,7 +1717,9 @@ HD void guess_inter(Ctx& c)
         best_found = best_found || best_cost == 0.0 || pskip;
     }
     if (!pskip) {
+        HL_PROF_T(ti);
         const double ic = guess_intra(c);
+        HL_PROF_ADD(c, 5, ti);
         if (ic <= best_cost) return;
     }
     // finalize (rdo.c:1167-1262)
@@ -1903,10 +1943,15 @@ HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, in
 {
     Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0};
     if (tid == 0) F.chain[addr].s_in = s_in;
+    HL_PROF_T(t0);
     mb_begin(c);
+    HL_PROF_ADD(c, 6, t0);
     if (F.is_intra) guess_intra(c);
     else guess_inter(c);
+    HL_PROF_T(t1);
     mb_end(c);
+    HL_PROF_ADD(c, 7, t1);
+    HL_PROF_ADD(c, 8, t0);
 }
 
 }  // namespace hl

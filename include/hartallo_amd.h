@@ -107,6 +107,11 @@ int32_t hl_amd_last_reruns(hl_amd_encoder_t* encoder);
 /* number of macroblock-decision kernel launches of the last frame */
 int32_t hl_amd_last_mb_launches(hl_amd_encoder_t* encoder);
 
+/* per-phase shader-clock counters of the macroblock kernel; filled only by
+ * the profiling build (make profile); out[2k] = cycles, out[2k+1] = calls.
+ * The counters are cleared by the call. */
+int32_t hl_amd_profile_counters(hl_amd_encoder_t* encoder, unsigned long long* out, int32_t n);
+
 const char* hl_amd_version(void);
 
 #ifdef __cplusplus

@@ -109,6 +109,7 @@ extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, co
     F.rec = e->rec.data();
     F.chain = e->chain.data();
     F.spec = e->spec.data();
+    F.prof = nullptr;
     int chain = e->chain_end;
     for (int a = 0; a < e->nmb; ++a) {
         encode_mb(F, *e->S, a, 0, 1, chain);
