@@ -1,0 +1,265 @@
+// hl_coop.h -- the 4x4 residual pipeline of the macroblock search with one
+// 16-lane DPP row per 4x4 block (gfx950 only).
+//
+// Lane p of a row holds raster coefficient (r, c) = (p >> 2, p & 3) of the
+// block.  The two 1-D passes of every transform are register exchanges:
+// the horizontal pass reads the other lanes of the quad (DPP quad_perm), the
+// vertical pass the same column of the other quads (DPP row_ror 4/8/12).
+// CAVLC statistics come from two 16-bit masks in scan order (non-zero, +-1)
+// built with a row OR-reduction; everything except the level_prefix /
+// suffix chain (suffixLength adapts level by level) is then closed-form per
+// lane.  Results are bit-identical to the scalar reference paths:
+//   forward transform      hl_codec_264_transf.c:716-772   (fwd4x4)
+//   quantisation           hl_codec_264_quant.c:116-137     (quant4x4)
+//   dequant + inverse      hl_codec_264_transf.c:376-458    (dequant_idct)
+//   CAVLC bit count        hl_codec_264_residual.c:587-901  (cavlc_stat)
+#pragma once
+#include "hl_prims.h"
+
+namespace hl {
+
+template <int CTRL>
+__device__ __forceinline__ int dpp(int v)
+{
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+constexpr int kQ0 = 0x00, kQ1 = 0x55, kQ2 = 0xAA, kQ3 = 0xFF;  // quad_perm broadcast of quad lane j
+constexpr int kRor1 = 0x121, kRor2 = 0x122, kRor4 = 0x124, kRor8 = 0x128, kRor12 = 0x12C;
+
+// sum / or / max over the 16 lanes of a DPP row (every lane gets the result)
+__device__ __forceinline__ int row_sum(int x)
+{
+    x += dpp<kRor8>(x);
+    x += dpp<kRor4>(x);
+    x += dpp<kRor2>(x);
+    return x + dpp<kRor1>(x);
+}
+__device__ __forceinline__ int row_or(int x)
+{
+    x |= dpp<kRor8>(x);
+    x |= dpp<kRor4>(x);
+    x |= dpp<kRor2>(x);
+    return x | dpp<kRor1>(x);
+}
+__device__ __forceinline__ int row_max(int x)
+{
+    x = max(x, dpp<kRor8>(x));
+    x = max(x, dpp<kRor4>(x));
+    x = max(x, dpp<kRor2>(x));
+    return max(x, dpp<kRor1>(x));
+}
+
+// Per-lane constants.  The coefficient fields are packed 4 bits per source
+// (signed 3-bit coefficient + a shift bit for the IDCT's >>1 terms) and
+// decoded with bit-field extracts.
+struct LaneK {
+    int p, s;          // raster position in the block, zig-zag scan index
+    uint32_t fwd;      // [0..15] horizontal, [16..31] vertical forward coefficients
+    uint32_t inv;      // same for the inverse transform (coef | shift << 3)
+    int mf, mfc;       // quant multiplier at qp / qpc for this position
+    int ls, lsc;       // dequant level scale at qp / qpc for this position
+};
+
+// forward core matrix and the IDCT's (coefficient, shift) for out o, in i
+HD int fwd_m(int o, int i)
+{
+    const int m[4][4] = {{1, 1, 1, 1}, {2, 1, -1, -2}, {1, -1, -1, 1}, {1, -2, 2, -1}};
+    return m[o][i];
+}
+HD int inv_c(int o, int i)
+{
+    if (i == 0) return 1;
+    if (i == 2) return (o == 0 || o == 3) ? 1 : -1;
+    if (i == 1) return o < 2 ? 1 : -1;
+    return (o & 1) ? -1 : 1;
+}
+HD int inv_s(int o, int i)
+{
+    if (i == 1) return (o == 1 || o == 2) ? 1 : 0;
+    if (i == 3) return (o == 0 || o == 3) ? 1 : 0;
+    return 0;
+}
+
+__device__ __forceinline__ LaneK make_lanek(int tid, int qp, int qpc)
+{
+    static constexpr uint8_t kZzInv[16] = {0, 1, 5, 6, 2, 4, 7, 12, 3, 8, 11, 13, 9, 10, 14, 15};
+    LaneK K;
+    const int p = tid & 15, r = p >> 2, c = p & 3;
+    K.p = p;
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s = (p == i) ? kZzInv[i] : s;
+    K.s = s;
+    // source rows the vertical rotations read (direction-agnostic: rotate the row index itself)
+    const int rr[4] = {r, dpp<kRor4>(tid & 15) >> 2, dpp<kRor8>(tid & 15) >> 2, dpp<kRor12>(tid & 15) >> 2};
+    uint32_t fw = 0, iv = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        fw |= (uint32_t)(fwd_m(c, j) & 0xF) << (4 * j);
+        fw |= (uint32_t)(fwd_m(r, rr[j]) & 0xF) << (16 + 4 * j);
+        iv |= (uint32_t)((inv_c(c, j) & 7) | (inv_s(c, j) << 3)) << (4 * j);
+        iv |= (uint32_t)((inv_c(r, rr[j]) & 7) | (inv_s(r, rr[j]) << 3)) << (16 + 4 * j);
+    }
+    K.fwd = fw;
+    K.inv = iv;
+    const int cls = ((r & 1) == 0 && (c & 1) == 0) ? 0 : (((r & 1) && (c & 1)) ? 1 : 2);
+    int mf = 0, mfc = 0, ls = 0, lsc = 0;
+#pragma unroll
+    for (int m = 0; m < 6; ++m)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (m == qp % 6 && k == cls) {
+                mf = kQuantMF[m][k];
+                ls = 16 * kScaleV[m][k];
+            }
+            if (m == qpc % 6 && k == cls) {
+                mfc = kQuantMF[m][k];
+                lsc = 16 * kScaleV[m][k];
+            }
+        }
+    K.mf = mf;
+    K.mfc = mfc;
+    K.ls = ls;
+    K.lsc = lsc;
+    return K;
+}
+
+__device__ __forceinline__ int fld_s3(uint32_t w, int pos) { return ((int)(w << (29 - pos))) >> 29; }  // signed bits [pos, pos+2]
+__device__ __forceinline__ int fld_u1(uint32_t w, int pos) { return (w >> (pos + 3)) & 1; }
+
+// Forward core transform of one coefficient per lane.
+__device__ __forceinline__ int coop_fwd(const LaneK& K, int x)
+{
+    const int q0 = dpp<kQ0>(x), q1 = dpp<kQ1>(x), q2 = dpp<kQ2>(x), q3 = dpp<kQ3>(x);
+    const uint32_t f = K.fwd;
+    const int h = fld_s3(f, 0) * q0 + fld_s3(f, 4) * q1 + fld_s3(f, 8) * q2 + fld_s3(f, 12) * q3;
+    const int v1 = dpp<kRor4>(h), v2 = dpp<kRor8>(h), v3 = dpp<kRor12>(h);
+    return fld_s3(f, 16) * h + fld_s3(f, 20) * v1 + fld_s3(f, 24) * v2 + fld_s3(f, 28) * v3;
+}
+
+// Inverse core transform (rows, then columns, then (x + 32) >> 6).
+__device__ __forceinline__ int coop_idct(const LaneK& K, int d)
+{
+    const int q0 = dpp<kQ0>(d), q1 = dpp<kQ1>(d), q2 = dpp<kQ2>(d), q3 = dpp<kQ3>(d);
+    const uint32_t w = K.inv;
+    const int f = fld_s3(w, 0) * (q0 >> fld_u1(w, 0)) + fld_s3(w, 4) * (q1 >> fld_u1(w, 4)) + fld_s3(w, 8) * (q2 >> fld_u1(w, 8)) +
+                  fld_s3(w, 12) * (q3 >> fld_u1(w, 12));
+    const int v1 = dpp<kRor4>(f), v2 = dpp<kRor8>(f), v3 = dpp<kRor12>(f);
+    const int h = fld_s3(w, 16) * (f >> fld_u1(w, 16)) + fld_s3(w, 20) * (v1 >> fld_u1(w, 20)) + fld_s3(w, 24) * (v2 >> fld_u1(w, 24)) +
+                  fld_s3(w, 28) * (v3 >> fld_u1(w, 28));
+    return (h + 32) >> 6;
+}
+
+// LDS tables of the cooperative pipeline
+struct CoopTables {
+    uint8_t tz[15][16];      // total_zeros lengths
+    uint8_t tok[3][4][17];   // coeff_token lengths, nC < 8
+    uint8_t pad[4];
+};
+
+__device__ __forceinline__ void coop_tables_init(CoopTables& T, int tid, int nthr)
+{
+    for (int i = tid; i < 15 * 16; i += nthr) T.tz[i >> 4][i & 15] = kTzLen[i >> 4][i & 15];
+    for (int i = tid; i < 3 * 4 * 17; i += nthr) T.tok[i / 68][(i / 17) % 4][i % 17] = kTokLen[i / 68][(i / 17) % 4][i % 17];
+}
+
+__device__ __forceinline__ int coop_token_len(const CoopTables& T, int nC, int tc, int t1)
+{
+    return nC >= 8 ? 6 : T.tok[nC < 2 ? 0 : (nC < 4 ? 1 : 2)][t1][tc];
+}
+
+// run_before length, Table 9-10 (kRbLen) in closed form
+__device__ __forceinline__ int rb_len(int zl, int run)
+{
+    if (zl > 6) return run < 7 ? 3 : run - 3;
+    // rows zerosLeft 1..6, two bits per run value
+    const uint32_t rows[6] = {0x5u, 0x29u, 0xAAu, 0x3EAu, 0xFFAu, 0x3FFEu};
+    uint32_t w = rows[0];
+#pragma unroll
+    for (int i = 1; i < 6; ++i) w = zl == i + 1 ? rows[i] : w;
+    return (w >> (2 * run)) & 3;
+}
+
+__device__ __forceinline__ int level_len(int sl, int lc)
+{
+    if (sl == 0) return lc < 14 ? lc + 1 : (lc < 30 ? 19 : (lc <= 4126 ? 28 : 1));
+    if (lc < (14 << sl)) return (lc >> sl) + 1 + sl;
+    if (lc < (15 << sl)) return 15 + sl;
+    return lc <= (15 << sl) + 4096 ? 28 : 1;
+}
+
+struct CoopStat {
+    int tc, t1, rest, sctr;  // as CavlcStat (uniform over the row)
+};
+
+// CAVLC statistics of the row's block (cavlc_stat with maxNumCoef 16,
+// endIdx 15).  L = this lane's level, li = its list index (scan index, or
+// scan index - 1 for AC blocks; -1 = not part of the list).  lvs = 16 words
+// of LDS scratch owned by this row.  Also returns this lane's run_before bits
+// through the row reduction, so every lane of the row gets the same result.
+__device__ __forceinline__ CoopStat coop_cavlc(const CoopTables& T, int L, int li, int* lvs)
+{
+    const int aL = L < 0 ? -L : L;
+    const bool nzl = li >= 0 && L != 0;
+    const uint32_t masks = (uint32_t)row_or(nzl ? (int)((1u << li) | ((uint32_t)(aL == 1) << (li + 16))) : 0);
+    const uint32_t nz = masks & 0xFFFFu, ones = masks >> 16;
+    CoopStat st;
+    st.tc = __popc(nz);
+    st.t1 = 0;
+    st.rest = 0;
+    st.sctr = -1;
+    if (st.tc == 0) return st;  // uniform over the row
+    const int hi = 31 - __clz(nz);
+    const uint32_t big = nz & ~ones;
+    const int hb = big ? 31 - __clz(big) : -1;
+    const int t1 = min(3, __popc(nz >> (hb + 1)));
+    const int tc = st.tc;
+    // this lane's order from the top, run_before and level slot
+    int rb = 0;
+    if (nzl) {
+        const int j = __popc(nz >> (li + 1));
+        const uint32_t lower = nz & ((1u << li) - 1u);
+        const int zl = li - __popc(lower);
+        const int run = lower ? li - 1 - (31 - __clz(lower)) : li;
+        if (j < tc - 1 && zl > 0) rb = rb_len(zl, run);
+        const int m = j - t1;
+        if (m >= 0) {
+            int lc = L > 0 ? (L << 1) - 2 : -(L << 1) - 1;
+            if (m == 0 && t1 < 3 && lc >= 2) lc -= 2;
+            lvs[m] = (lc << 16) | aL;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int bits = t1 + row_sum(rb);
+    int sl = (tc > 10 && t1 < 3) ? 1 : 0;
+    for (int m = 0; m < tc - t1; ++m) {
+        const int v = lvs[m];
+        const int lc = v >> 16, a = v & 0xFFFF;
+        bits += level_len(sl, lc);
+        if (sl == 0) sl = 1;
+        const int thr = sl == 1 ? 3 : (sl == 2 ? 6 : (sl == 3 ? 12 : (sl == 4 ? 24 : (sl == 5 ? 48 : 32768))));
+        if (a > thr) ++sl;
+    }
+    if (tc < 16) bits += T.tz[tc - 1][hi + 1 - tc];
+    st.t1 = t1;
+    st.rest = bits;
+    st.sctr = 9;
+    if (tc == 1 && ones == nz) st.sctr = hi == 0 ? 3 : (hi < 3 ? 2 : (hi < 6 ? 1 : 0));
+    return st;
+}
+
+// quantisation of one coefficient: f = 2^qbits / 3 (intra) or / 6 (inter)
+__device__ __forceinline__ int coop_quant(int w, int mf, int qbits, int f)
+{
+    const int v = ((w < 0 ? -w : w) * mf + f) >> qbits;
+    return w >= 0 ? v : -v;
+}
+__device__ __forceinline__ int coop_dequant(int c, int ls, int qP)
+{
+    const int q6 = qP / 6;
+    return qP >= 24 ? (c * ls) << (q6 - 4) : (c * ls + (1 << (3 - q6))) >> (4 - q6);
+}
+
+}  // namespace hl

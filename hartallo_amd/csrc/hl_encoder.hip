@@ -4,7 +4,7 @@
 //   1. k_planes      quarter-pel planes of the reference picture (HBM-bound)
 //   2. k_mb_diag     macroblock decisions on an anti-diagonal wavefront:
 //                    MB (x, y) runs after (x-1, y) and (x+1, y-1), i.e. in
-//                    launch d = x + 2y; one 256-lane workgroup per MB
+//                    launch d = x + 2y; one 1024-lane workgroup per MB
 //   3. row-start validation of the rdo.Single_ctr speculation (host), with a
 //      re-run of the wavefront from the first mispredicted row
 //   4. k_deblock_diag the in-place Baseline deblocking, same wavefront order
@@ -31,7 +31,7 @@ using namespace hl;
         }                                                                                \
     } while (0)
 
-constexpr int kMbThreads = 256;
+constexpr int kMbThreads = 1024;  // 64 rows of 16 lanes: one row per (candidate, 4x4 block)
 
 // ---------------------------------------------------------------------------
 // kernels
@@ -98,7 +98,8 @@ struct hl_amd_encoder_s {
     uint8_t* d_in[3];
     uint8_t* d_pic[2][3];  // [cur/ref swap][plane]
     int cur;
-    uint8_t* d_pl[4];
+    uint8_t* d_pl[4];  // one allocation: d_pl[i] = d_pl[0] + i * plsz
+    size_t plsz;
     MbState *d_st, *d_snap;
     MbRecord* d_rec;
     MbChain* d_chain;
@@ -122,7 +123,7 @@ static void free_all(hl_amd_encoder_t* e)
         (void)hipFree(e->d_pic[0][c]);
         (void)hipFree(e->d_pic[1][c]);
     }
-    for (int i = 0; i < 4; ++i) (void)hipFree(e->d_pl[i]);
+    (void)hipFree(e->d_pl[0]);
     (void)hipFree(e->d_st);
     (void)hipFree(e->d_snap);
     (void)hipFree(e->d_rec);
@@ -164,7 +165,9 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
              hipMalloc(&e->d_pic[1][c], sz) == hipSuccess && hipMemset(e->d_pic[0][c], 0, sz) == hipSuccess &&
              hipMemset(e->d_pic[1][c], 0, sz) == hipSuccess;
     }
-    for (int i = 0; i < 4 && ok; ++i) ok = hipMalloc(&e->d_pl[i], pls) == hipSuccess;
+    e->plsz = pls;
+    ok = ok && hipMalloc(&e->d_pl[0], 4 * pls) == hipSuccess;
+    for (int i = 1; i < 4 && ok; ++i) e->d_pl[i] = e->d_pl[0] + i * pls;
     ok = ok && hipMalloc(&e->d_st, sizeof(MbState) * e->nmb) == hipSuccess && hipMalloc(&e->d_snap, sizeof(MbState) * e->nmb) == hipSuccess &&
          hipMalloc(&e->d_rec, sizeof(MbRecord) * e->nmb) == hipSuccess && hipMalloc(&e->d_chain, sizeof(MbChain) * e->nmb) == hipSuccess &&
          hipMalloc(&e->d_spec, sizeof(int32_t) * e->mbh) == hipSuccess &&
@@ -264,6 +267,7 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
     }
     for (int i = 0; i < 4; ++i) F.pl[i] = e->d_pl[i];
     F.pstride = e->pstride;
+    F.plsz = (int32_t)e->plsz;
     F.st = e->d_st;
     F.rec = e->d_rec;
     F.chain = e->d_chain;

@@ -28,6 +28,7 @@
 //    I16x16 RDO; it is carried in Ctx::chain and recorded in MbChain so the
 //    host can validate row-start speculation.
 #pragma once
+#include "hl_coop.h"
 #include "hl_prims.h"
 #include "hl_types.h"
 
@@ -56,6 +57,7 @@ namespace hl {
 #endif
 
 constexpr int kPad = 40;  // padding of the luma reference planes (origin clip is +-17, block 16, tap 3)
+constexpr int kMaxWaves = 16;  // workgroup of up to 1024 lanes per macroblock
 constexpr int kNA = -1;   // not-available sample marker
 
 struct FrameArgs {
@@ -67,6 +69,7 @@ struct FrameArgs {
     const uint8_t* ref[3];  // ref[0] unused (luma goes through pl[])
     const uint8_t* pl[4];   // padded luma reference: full, half-h (b), half-v (h), centre (j)
     int32_t pstride;
+    int32_t plsz;           // pl[i] = pl[0] + i * plsz (device buffers)
     MbState* st;
     MbRecord* rec;
     MbChain* chain;
@@ -107,8 +110,14 @@ struct Shared {
     int16_t cac[2][4][16];// live ChromaACLevel
     int32_t cbp_l, cbp_c; // live CodedBlockPattern{Luma,Chroma}
     // --- candidate step scratch
-    int16_t cmv[16][2];
+    int16_t wcmv[kMaxWaves][9][2];  // candidate MVs, one copy per wave (each wave writes its own)
     int32_t be_nz[9][16], be_tc[9][16], be_t1[9][16], be_sctr[9][16], be_bits[9][16], be_dist[9][16];
+    int32_t be_w0[9][16], be_w1[9][16];                  // packed block statistics (device path)
+    alignas(16) uint8_t be_nzb[16][16], be_tcb[16][16];  // [block][candidate]
+    int32_t lvs[kMaxWaves * 4][16];                      // per-row level scratch of coop_cavlc
+    CoopTables ct;
+    uint32_t qtab[16];                                   // packed quarter-pel phase table
+    double cd_cost[9];
     int32_t cd_bits[9], cd_dist[9], cd_single[9], cd_cbp[9], cd_last[9];
     // --- per (sub)partition search results
     double bcost[4][4];
@@ -144,6 +153,7 @@ struct Ctx {
     int tid, nthr;
     int addr, mbx, mby, xL, yL;
     int chain, fresh, dep;  // rdo.Single_ctr emulation (uniform)
+    LaneK K;                // per-lane constants of the 16-lane block pipeline (device)
 };
 
 // --------------------------------------------------------------------------
@@ -329,7 +339,7 @@ HD void skip_mv(const Shared& S, int out[2])
 template <typename F>
 HD int nc_luma_of(const Shared& S, int bi, F inside)
 {
-    const int bx = kBlkX[bi], by = kBlkY[bi];
+    const int bx = blk_x(bi), by = blk_y(bi);
     int nA = 0, nB = 0;
     bool aA, aB;
     if (bx == 0) {
@@ -385,6 +395,13 @@ HD void mb_begin(Ctx& c)
     const int hasA = c.mbx > 0, hasB = c.mby > 0, hasC = c.mby > 0 && c.mbx < F.mbw - 1, hasD = c.mbx > 0 && c.mby > 0;
     const int addrs[5] = {a, a - 1, a - F.mbw, a - F.mbw + 1, a - F.mbw - 1};
     const int av[5] = {1, hasA, hasB, hasC, hasD};
+#if defined(__HIP_DEVICE_COMPILE__)
+    coop_tables_init(S.ct, tid, nthr);
+    for (int t = tid; t < 16; t += nthr) {
+        const int8_t* e = kQpelTab[t];
+        S.qtab[t] = (uint32_t)(e[0] | (e[1] << 2) | (e[2] << 3) | ((e[3] >= 0) << 4) | ((e[3] >= 0 ? e[3] : 0) << 5) | (e[4] << 7) | (e[5] << 8));
+    }
+#endif
     // source samples
     for (int t = tid; t < 256; t += nthr) S.src[t] = F.src[0][(c.yL + (t >> 4)) * F.W + c.xL + (t & 15)];
     for (int t = tid; t < 128; t += nthr) {
@@ -508,15 +525,56 @@ HD void mb_begin(Ctx& c)
 // Inter candidate evaluation (me_ds.c:527-688 for a list of MVs)
 // --------------------------------------------------------------------------
 struct PartGeo {
-    int px, py, pw, ph, nbw, nblk;
+    int px, py, pw, ph, nbw, nblk, lbw, lnb;  // lbw / lnb = log2(nbw) / log2(nblk)
 };
 
-// Evaluates S.cmv[0..ncand) for partition g in order.  Leaves per-candidate
-// rbc/dist/single/cbp in S.cd_*, updates S.tc (last writer) and the chain.
+// The candidate list of a step is uniform; each wave keeps its own copy in
+// LDS so that no barrier is needed between choosing and evaluating it.
+HD void put_cand(Ctx& c, int i, int mx, int my)
+{
+    const int w = c.tid >> 6;
+    c.S.wcmv[w][i][0] = (int16_t)mx;
+    c.S.wcmv[w][i][1] = (int16_t)my;
+}
+
+HD double mv_cost(const FrameArgs& F, int dist, int bits, int mvx, int mvy, const int pmv[2])
+{
+    const int rbc_mv = se_len(mvx - pmv[0]) + se_len(mvy - pmv[1]);
+    return dadd((double)dist, dmul((double)(bits + rbc_mv), F.lambda));
+}
+
 #if defined(HL_STATS) && !defined(__HIP_DEVICE_COMPILE__)
 extern long long g_hl_stats[8];
 #endif
-HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand)
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// Luma prediction sample at integer (X, Y) for fraction (xF, yF) from the
+// contiguous quarter-pel planes; S.qtab packs kQpelTab.
+__device__ __forceinline__ int pred_luma_px(const FrameArgs& F, const Shared& S, int X, int Y, int xF, int yF)
+{
+    const uint32_t e = S.qtab[(yF << 2) | xF];
+    const uint8_t* base = F.pl[0];
+    const int a = base[(int)(e & 3) * F.plsz + (Y + kPad + (int)((e >> 3) & 1)) * F.pstride + X + kPad + (int)((e >> 2) & 1)];
+    if (!(e & 16)) return a;
+    const int b = base[(int)((e >> 5) & 3) * F.plsz + (Y + kPad + (int)((e >> 8) & 1)) * F.pstride + X + kPad + (int)((e >> 7) & 1)];
+    return (a + b + 1) >> 1;
+}
+
+// non-zero flags of block k over the candidates of the step, as a bit mask
+__device__ __forceinline__ uint32_t nz_mask(const Shared& S, int k)
+{
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(S.be_nzb[k]);
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m |= ((((w[i] & 0x01010101u) * 0x01020408u) >> 24) & 0xFu) << (4 * i);
+    return m;
+}
+#endif
+
+// Evaluates the candidates S.wcmv[wave][0..ncand) of partition g in order.
+// Leaves per-candidate cost/rbc/dist/single/cbp in S.cd_*, updates the live
+// TotalCoeffsLuma S.tc (last writer) and the Single_ctr chain.
+HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
 {
 #if defined(HL_STATS) && !defined(__HIP_DEVICE_COMPILE__)
     g_hl_stats[0]++;
@@ -526,20 +584,99 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand)
 #endif
     const FrameArgs& F = c.F;
     Shared& S = c.S;
-    const int n = ncand * g.nblk;
     HL_PROF_T(tp0);
+#if defined(__HIP_DEVICE_COMPILE__)
+    // phase 1: one 16-lane row per (candidate, 4x4 block)
+    {
+        const int wave = c.tid >> 6, grp = c.tid >> 4, ngrp = c.nthr >> 4;
+        const int n = ncand << g.lnb;
+        const int qbits = 15 + F.qp / 6, f = (1 << qbits) / 6;
+        const int pr = c.K.p >> 2, pc = c.K.p & 3;
+        for (int item = grp; item < n; item += ngrp) {
+            const int ci = item >> g.lnb, k = item & (g.nblk - 1);
+            const int hx = k & (g.nbw - 1), hy = k >> g.lbw;
+            const int mvx = S.wcmv[wave][ci][0], mvy = S.wcmv[wave][ci][1];
+            const int X = clip3(-17, F.W + 17, c.xL + g.px + (mvx >> 2)) + (hx << 2) + pc;
+            const int Y = clip3(-17, F.H + 17, c.yL + g.py + (mvy >> 2)) + (hy << 2) + pr;
+            const int pred = pred_luma_px(F, S, X, Y, mvx & 3, mvy & 3);
+            const int sv = S.src[(g.py + (hy << 2) + pr) * 16 + g.px + (hx << 2) + pc];
+            const int q = coop_quant(coop_fwd(c.K, sv - pred), c.K.mf, qbits, f);
+            const CoopStat st = coop_cavlc(S.ct, q, c.K.s, S.lvs[grp]);
+            const int r = coop_idct(c.K, coop_dequant(q, c.K.ls, F.qp));
+            const int dist = row_sum(iabs(sv - clip255(pred + r)));
+            if (c.K.p == 0) {
+                S.be_w0[ci][k] = st.tc | (st.t1 << 5) | ((st.sctr + 1) << 8);
+                S.be_w1[ci][k] = st.rest | (dist << 16);
+                S.be_nzb[k][ci] = st.tc > 0;
+                S.be_tcb[k][ci] = (uint8_t)st.tc;
+            }
+        }
+    }
+    HL_SYNC();
+    HL_PROF_ADD(c, 0, tp0);
+    HL_PROF_T(tp1);
+    // phase 2: one row per candidate, one lane per block: nC as the reference
+    // sees it at this point of the sequence, coeff_token, candidate sums, cost
+    if (c.tid < (ncand << 4)) {
+        const int wave = c.tid >> 6, ci = c.tid >> 4, k = c.tid & 15;
+        int bits = 0, dist = 0, cs = 0, last = 0;
+        if (k < g.nblk) {
+            const int w0 = S.be_w0[ci][k], w1 = S.be_w1[ci][k];
+            const int tc = w0 & 31, t1 = (w0 >> 5) & 7, sctr = ((w0 >> 8) & 15) - 1;
+            dist = w1 >> 16;
+            if (tc) {
+                const int hx = k & (g.nbw - 1), hy = k >> g.lbw;
+                const int bi = blk_idx(g.px + (hx << 2), g.py + (hy << 2));
+                const int nC = nc_luma_of(S, bi, [&](int ni) -> int {
+                    const int nx = blk_x(ni) - g.px, ny = blk_y(ni) - g.py;
+                    if (nx >= 0 && ny >= 0 && nx < g.pw && ny < g.ph) {
+                        const int kk = ((ny >> 2) << g.lbw) + (nx >> 2);
+                        const uint32_t m = nz_mask(S, kk) & ((2u << ci) - 1u);  // candidates 0..ci
+                        if (m) return S.be_tcb[kk][31 - __clz(m)];
+                    }
+                    return S.tc[ni];
+                });
+                bits = (w1 & 0xFFFF) + coop_token_len(S.ct, nC, tc, t1);
+                cs = (1 << bi) | (sctr << 16);
+                last = ((k + 1) << 4) | sctr;
+            }
+        }
+        bits = row_sum(bits);
+        dist = row_sum(dist);
+        cs = row_sum(cs);
+        last = row_max(last);
+        if (k == 0) {
+            S.cd_cost[ci] = mv_cost(F, dist, bits, S.wcmv[wave][ci][0], S.wcmv[wave][ci][1], pmv);
+            S.cd_bits[ci] = bits;
+            S.cd_dist[ci] = dist;
+            S.cd_single[ci] = cs >> 16;
+            S.cd_cbp[ci] = cs & 0xFFFF;
+            S.cd_last[ci] = last ? (last & 15) : -1;
+        }
+    }
+    HL_SYNC();
+    HL_PROF_ADD(c, 1, tp1);
+    HL_PROF_T(tp2);
+    // live TotalCoeffsLuma = last writer; the next reader is behind a barrier
+    if (c.tid < g.nblk) {
+        const int k = c.tid;
+        const uint32_t m = nz_mask(S, k) & ((1u << ncand) - 1u);
+        if (m) S.tc[blk_idx(g.px + ((k & (g.nbw - 1)) << 2), g.py + ((k >> g.lbw) << 2))] = (int8_t)S.be_tcb[k][31 - __clz(m)];
+    }
+#else
+    HL_PROF_T(tp2);
+    const int n = ncand * g.nblk;
     // phase 1: transform / quant / CAVLC statistics / reconstruction per block
     for (int t = c.tid; t < n; t += c.nthr) {
         const int ci = t / g.nblk, k = t % g.nblk;
         const int hx = k % g.nbw, hy = k / g.nbw;
-        const int mvx = S.cmv[ci][0], mvy = S.cmv[ci][1];
+        const int mvx = S.wcmv[0][ci][0], mvy = S.wcmv[0][ci][1];
         const int X = clip3(-17, F.W + 17, c.xL + g.px + (mvx >> 2)) + (hx << 2);
         const int Y = clip3(-17, F.H + 17, c.yL + g.py + (mvy >> 2)) + (hy << 2);
         const int bx = g.px + (hx << 2), by = g.py + (hy << 2);
         int pred[16], res[16];
         pred_luma4x4(F, X, Y, mvx & 3, mvy & 3, pred);
         bool zero = true;
-#pragma unroll
         for (int i = 0; i < 16; ++i) {
             res[i] = (int)S.src[(by + (i >> 2)) * 16 + bx + (i & 3)] - pred[i];
             zero = zero && res[i] == 0;
@@ -551,7 +688,6 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand)
             fwd4x4(res, w);
             quant4x4(F.qp, false, w, q);
             bool lz = true;
-#pragma unroll
             for (int i = 0; i < 16; ++i) {
                 lv[i] = q[kZigzag[i]];
                 lz = lz && lv[i] == 0;
@@ -561,11 +697,9 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand)
                 st = cavlc_stat(lv, 16, 15, false);
                 int r[16];
                 dequant_idct(F.qp, q, false, r);
-#pragma unroll
                 for (int i = 0; i < 16; ++i) dist += iabs(res[i] - (clip255(pred[i] + r[i]) - pred[i]));
             }
             else {
-#pragma unroll
                 for (int i = 0; i < 16; ++i) dist += iabs(res[i]);
             }
         }
@@ -576,9 +710,6 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand)
         S.be_bits[ci][k] = st.rest;
         S.be_dist[ci][k] = dist;
     }
-    HL_SYNC();
-    HL_PROF_ADD(c, 0, tp0);
-    HL_PROF_T(tp1);
     // phase 2: nC as the reference sees it at this point of the sequence
     for (int t = c.tid; t < n; t += c.nthr) {
         const int ci = t / g.nblk, k = t % g.nblk;
@@ -586,7 +717,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand)
         const int hx = k % g.nbw, hy = k / g.nbw;
         const int bi = blk_idx(g.px + (hx << 2), g.py + (hy << 2));
         const int nC = nc_luma_of(S, bi, [&](int ni) -> int {
-            const int nx = kBlkX[ni] - g.px, ny = kBlkY[ni] - g.py;
+            const int nx = blk_x(ni) - g.px, ny = blk_y(ni) - g.py;
             if (nx >= 0 && ny >= 0 && nx < g.pw && ny < g.ph) {
                 const int kk = (ny >> 2) * g.nbw + (nx >> 2);
                 if (S.be_nz[ci][kk]) return S.be_tc[ci][kk];
@@ -597,41 +728,36 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand)
         });
         S.be_bits[ci][k] += token_len(nC, S.be_tc[ci][k], S.be_t1[ci][k]);
     }
-    HL_SYNC();
-    HL_PROF_ADD(c, 1, tp1);
-    HL_PROF_T(tp2);
     // phase 3: per-candidate sums; live TotalCoeffsLuma = last writer
-    for (int t = c.tid; t < ncand + g.nblk; t += c.nthr) {
-        if (t < ncand) {
-            int bits = 0, dist = 0, single = 0, cbp = 0, last = -1;
-            for (int k = 0; k < g.nblk; ++k) {
-                dist += S.be_dist[t][k];
-                if (S.be_nz[t][k]) {
-                    const int hx = k % g.nbw, hy = k / g.nbw;
-                    bits += S.be_bits[t][k];
-                    single += S.be_sctr[t][k];
-                    cbp |= 1 << blk_idx(g.px + (hx << 2), g.py + (hy << 2));
-                    last = S.be_sctr[t][k];
-                }
+    for (int t = 0; t < ncand; ++t) {
+        int bits = 0, dist = 0, single = 0, cbp = 0, last = -1;
+        for (int k = 0; k < g.nblk; ++k) {
+            dist += S.be_dist[t][k];
+            if (S.be_nz[t][k]) {
+                const int hx = k % g.nbw, hy = k / g.nbw;
+                bits += S.be_bits[t][k];
+                single += S.be_sctr[t][k];
+                cbp |= 1 << blk_idx(g.px + (hx << 2), g.py + (hy << 2));
+                last = S.be_sctr[t][k];
             }
-            S.cd_bits[t] = bits;
-            S.cd_dist[t] = dist;
-            S.cd_single[t] = single;
-            S.cd_cbp[t] = cbp;
-            S.cd_last[t] = last;
         }
-        else {
-            const int k = t - ncand;
-            const int hx = k % g.nbw, hy = k / g.nbw;
-            const int bi = blk_idx(g.px + (hx << 2), g.py + (hy << 2));
-            for (int cj = ncand - 1; cj >= 0; --cj)
-                if (S.be_nz[cj][k]) {
-                    S.tc[bi] = (int8_t)S.be_tc[cj][k];
-                    break;
-                }
-        }
+        S.cd_cost[t] = mv_cost(F, dist, bits, S.wcmv[0][t][0], S.wcmv[0][t][1], pmv);
+        S.cd_bits[t] = bits;
+        S.cd_dist[t] = dist;
+        S.cd_single[t] = single;
+        S.cd_cbp[t] = cbp;
+        S.cd_last[t] = last;
     }
-    HL_SYNC();
+    for (int k = 0; k < g.nblk; ++k) {
+        const int hx = k % g.nbw, hy = k / g.nbw;
+        const int bi = blk_idx(g.px + (hx << 2), g.py + (hy << 2));
+        for (int cj = ncand - 1; cj >= 0; --cj)
+            if (S.be_nz[cj][k]) {
+                S.tc[bi] = (int8_t)S.be_tc[cj][k];
+                break;
+            }
+    }
+#endif
     HL_PROF_ADD(c, 2, tp2);
     for (int ci = ncand - 1; ci >= 0; --ci)
         if (S.cd_last[ci] >= 0) {
@@ -646,12 +772,7 @@ struct Best {
     int dist, single, cbp, mv[2];
 };
 
-HD double cand_cost(const Ctx& c, int ci, const int pmv[2])
-{
-    const Shared& S = c.S;
-    const int rbc_mv = se_len(S.cmv[ci][0] - pmv[0]) + se_len(S.cmv[ci][1] - pmv[1]);
-    return dadd((double)S.cd_dist[ci], dmul((double)(S.cd_bits[ci] + rbc_mv), c.F.lambda));
-}
+HD int ilog2_small(int v) { return v >= 16 ? 4 : (v >= 8 ? 3 : (v >= 4 ? 2 : (v >= 2 ? 1 : 0))); }
 
 // Diamond search of one (sub)partition, me_ds.c:104-477.  Returns true when
 // the P_Skip probe fired (16x16 only).
@@ -672,6 +793,8 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     g.ph = pd.sub_h;
     g.nbw = g.pw >> 2;
     g.nblk = (g.pw >> 2) * (g.ph >> 2);
+    g.lbw = ilog2_small(g.nbw);
+    g.lnb = ilog2_small(g.nblk);
     Best b;
     b.cost = 1.7976931348623157e308;
     b.dist = 0x7fffffff;
@@ -685,12 +808,8 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         skip_mv(S, smv);
         mvp(S, 0, 0, pmv);
         if (pmv[0] == smv[0] && pmv[1] == smv[1]) {
-            if (c.tid == 0) {
-                S.cmv[0][0] = (int16_t)pmv[0];
-                S.cmv[0][1] = (int16_t)pmv[1];
-            }
-            HL_SYNC();
-            eval_candidates(c, g, 1);
+            put_cand(c, 0, pmv[0], pmv[1]);
+            eval_candidates(c, g, 1, pmv);
             if (S.cd_bits[0] == 0 || S.cd_single[0] < 6) {
                 probably = true;
                 b.cost = 0.0;
@@ -709,23 +828,22 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     }
     // MVP and (0,0) candidates, me_ds.c:280-300
     const int nc0 = (pmv[0] != 0 || pmv[1] != 0) ? 2 : 1;
-    HL_SYNC();
-    if (c.tid == 0) {
-        S.cmv[0][0] = (int16_t)pmv[0];
-        S.cmv[0][1] = (int16_t)pmv[1];
-        S.cmv[1][0] = S.cmv[1][1] = 0;
-    }
-    HL_SYNC();
-    eval_candidates(c, g, nc0);
+    int cand[9][2];
+    cand[0][0] = pmv[0];
+    cand[0][1] = pmv[1];
+    cand[1][0] = cand[1][1] = 0;
+    put_cand(c, 0, pmv[0], pmv[1]);
+    put_cand(c, 1, 0, 0);
+    eval_candidates(c, g, nc0, pmv);
     for (int ci = 0; ci < nc0; ++ci) {
-        const double cost = cand_cost(c, ci, pmv);
+        const double cost = S.cd_cost[ci];
         if (cost < b.cost) {
             b.cost = cost;
             b.single = S.cd_single[ci];
             b.dist = S.cd_dist[ci];
             b.cbp = S.cd_cbp[ci];
-            b.mv[0] = S.cmv[ci][0];
-            b.mv[1] = S.cmv[ci][1];
+            b.mv[0] = cand[ci][0];
+            b.mv[1] = cand[ci][1];
         }
     }
     // diamond stages, me_ds.c:302-470
@@ -746,33 +864,30 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     int idxsel[9];
     for (;;) {
         int ncand = 0;
-        HL_SYNC();
         for (int i = 0; i < count; ++i) {
             if (!(flags & (1 << i))) continue;
             const int dx = shift == 2 ? kInt[i][0] : (shift == 1 ? kHalf[i][0] : kQuar[i][0]);
             const int dy = shift == 2 ? kInt[i][1] : (shift == 1 ? kHalf[i][1] : kQuar[i][1]);
             const int mx = cx + dx, my = cy + dy;
             if (mx < left || mx > right || my < top || my > bottom) continue;
-            if (c.tid == 0) {
-                S.cmv[ncand][0] = (int16_t)(mx << shift);
-                S.cmv[ncand][1] = (int16_t)(my << shift);
-            }
+            cand[ncand][0] = mx << shift;
+            cand[ncand][1] = my << shift;
+            put_cand(c, ncand, mx << shift, my << shift);
             idxsel[ncand++] = i;
         }
         int best = -1;
         if (ncand) {
-            HL_SYNC();
-            eval_candidates(c, g, ncand);
+            eval_candidates(c, g, ncand, pmv);
             for (int ci = 0; ci < ncand; ++ci) {
-                const double cost = cand_cost(c, ci, pmv);
+                const double cost = S.cd_cost[ci];
                 if (cost < b.cost) {
                     best = idxsel[ci];
                     b.cost = cost;
                     b.single = S.cd_single[ci];
                     b.dist = S.cd_dist[ci];
                     b.cbp = S.cd_cbp[ci];
-                    b.mv[0] = S.cmv[ci][0];
-                    b.mv[1] = S.cmv[ci][1];
+                    b.mv[0] = cand[ci][0];
+                    b.mv[1] = cand[ci][1];
                 }
             }
         }
@@ -820,7 +935,6 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     HL_PROF_ADD(c, 3, tsp);
     return probably;
 }
-
 // --------------------------------------------------------------------------
 // Intra prediction (8.3, pred_intra.c:326-1220)
 // --------------------------------------------------------------------------
@@ -1941,7 +2055,10 @@ HD void mb_end(Ctx& c)
 // One macroblock, start to end.  s_in = rdo.Single_ctr on entry.
 HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, int s_in)
 {
-    Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0};
+    Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0, LaneK{}};
+#if defined(__HIP_DEVICE_COMPILE__)
+    c.K = make_lanek(tid, F.qp, F.qpc);
+#endif
     if (tid == 0) F.chain[addr].s_in = s_in;
     HL_PROF_T(t0);
     mb_begin(c);

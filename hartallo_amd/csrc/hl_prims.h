@@ -62,6 +62,9 @@ static constexpr uint8_t kBlkY[16] = {0, 0, 4, 4, 0, 0, 4, 4, 8, 8, 12, 12, 8, 8
 // I16x16 DC matrix position of luma block idx (raster index into 4x4 DC matrix)
 static constexpr uint8_t kDcPos[16] = {0, 1, 4, 5, 2, 3, 6, 7, 8, 9, 12, 13, 10, 11, 14, 15};
 HD int blk_idx(int x, int y) { return 8 * (y >> 3) + 4 * (x >> 3) + 2 * ((y & 7) >> 2) + ((x & 7) >> 2); }
+// kBlkX / kBlkY as bit arithmetic (no table load for lane-varying indices)
+HD int blk_x(int bi) { return ((bi >> 2) & 1) * 8 + (bi & 1) * 4; }
+HD int blk_y(int bi) { return ((bi >> 3) & 1) * 8 + ((bi >> 1) & 1) * 4; }
 
 static constexpr uint8_t kQpToQpc[52] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17,
                                          18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 29, 30, 31, 32, 32, 33,
