@@ -56,6 +56,7 @@ struct LaneK {
     int p, s;          // raster position in the block, zig-zag scan index
     uint32_t fwd;      // [0..15] horizontal, [16..31] vertical forward coefficients
     uint32_t inv;      // same for the inverse transform (coef | shift << 3)
+    uint32_t had;      // same for the 4x4 Hadamard (I16x16 DC)
     int mf, mfc;       // quant multiplier at qp / qpc for this position
     int ls, lsc;       // dequant level scale at qp / qpc for this position
 };
@@ -64,6 +65,11 @@ struct LaneK {
 HD int fwd_m(int o, int i)
 {
     const int m[4][4] = {{1, 1, 1, 1}, {2, 1, -1, -2}, {1, -1, -1, 1}, {1, -2, 2, -1}};
+    return m[o][i];
+}
+HD int had_m(int o, int i)
+{
+    const int m[4][4] = {{1, 1, 1, 1}, {1, 1, -1, -1}, {1, -1, -1, 1}, {1, -1, 1, -1}};
     return m[o][i];
 }
 HD int inv_c(int o, int i)
@@ -92,16 +98,19 @@ __device__ __forceinline__ LaneK make_lanek(int tid, int qp, int qpc)
     K.s = s;
     // source rows the vertical rotations read (direction-agnostic: rotate the row index itself)
     const int rr[4] = {r, dpp<kRor4>(tid & 15) >> 2, dpp<kRor8>(tid & 15) >> 2, dpp<kRor12>(tid & 15) >> 2};
-    uint32_t fw = 0, iv = 0;
+    uint32_t fw = 0, iv = 0, hd = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         fw |= (uint32_t)(fwd_m(c, j) & 0xF) << (4 * j);
         fw |= (uint32_t)(fwd_m(r, rr[j]) & 0xF) << (16 + 4 * j);
+        hd |= (uint32_t)(had_m(c, j) & 0xF) << (4 * j);
+        hd |= (uint32_t)(had_m(r, rr[j]) & 0xF) << (16 + 4 * j);
         iv |= (uint32_t)((inv_c(c, j) & 7) | (inv_s(c, j) << 3)) << (4 * j);
         iv |= (uint32_t)((inv_c(r, rr[j]) & 7) | (inv_s(r, rr[j]) << 3)) << (16 + 4 * j);
     }
     K.fwd = fw;
     K.inv = iv;
+    K.had = hd;
     const int cls = ((r & 1) == 0 && (c & 1) == 0) ? 0 : (((r & 1) && (c & 1)) ? 1 : 2);
     int mf = 0, mfc = 0, ls = 0, lsc = 0;
 #pragma unroll
@@ -127,15 +136,17 @@ __device__ __forceinline__ LaneK make_lanek(int tid, int qp, int qpc)
 __device__ __forceinline__ int fld_s3(uint32_t w, int pos) { return ((int)(w << (29 - pos))) >> 29; }  // signed bits [pos, pos+2]
 __device__ __forceinline__ int fld_u1(uint32_t w, int pos) { return (w >> (pos + 3)) & 1; }
 
-// Forward core transform of one coefficient per lane.
-__device__ __forceinline__ int coop_fwd(const LaneK& K, int x)
+// M X M^T for the packed matrix f (exact integer arithmetic), one
+// coefficient per lane.
+__device__ __forceinline__ int coop_lin(uint32_t f, int x)
 {
     const int q0 = dpp<kQ0>(x), q1 = dpp<kQ1>(x), q2 = dpp<kQ2>(x), q3 = dpp<kQ3>(x);
-    const uint32_t f = K.fwd;
     const int h = fld_s3(f, 0) * q0 + fld_s3(f, 4) * q1 + fld_s3(f, 8) * q2 + fld_s3(f, 12) * q3;
     const int v1 = dpp<kRor4>(h), v2 = dpp<kRor8>(h), v3 = dpp<kRor12>(h);
     return fld_s3(f, 16) * h + fld_s3(f, 20) * v1 + fld_s3(f, 24) * v2 + fld_s3(f, 28) * v3;
 }
+// forward core transform (transf.c:716-772)
+__device__ __forceinline__ int coop_fwd(const LaneK& K, int x) { return coop_lin(K.fwd, x); }
 
 // Inverse core transform (rows, then columns, then (x + 32) >> 6).
 __device__ __forceinline__ int coop_idct(const LaneK& K, int d)

@@ -4,7 +4,7 @@
 //   1. k_planes      quarter-pel planes of the reference picture (HBM-bound)
 //   2. k_mb_diag     macroblock decisions on an anti-diagonal wavefront:
 //                    MB (x, y) runs after (x-1, y) and (x+1, y-1), i.e. in
-//                    launch d = x + 2y; one 1024-lane workgroup per MB
+//                    launch d = x + 2y; one 512-lane workgroup per MB
 //   3. row-start validation of the rdo.Single_ctr speculation (host), with a
 //      re-run of the wavefront from the first mispredicted row
 //   4. k_deblock_diag the in-place Baseline deblocking, same wavefront order
@@ -31,7 +31,10 @@ using namespace hl;
         }                                                                                \
     } while (0)
 
-constexpr int kMbThreads = 1024;  // 64 rows of 16 lanes: one row per (candidate, 4x4 block)
+#ifndef HL_MB_THREADS
+#define HL_MB_THREADS 512
+#endif
+constexpr int kMbThreads = HL_MB_THREADS;  // rows of 16 lanes: one row per (candidate, 4x4 block)
 
 // ---------------------------------------------------------------------------
 // kernels

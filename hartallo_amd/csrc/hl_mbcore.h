@@ -40,17 +40,17 @@ namespace hl {
 #define HL_SYNC() ((void)0)
 #endif
 
-// Optional phase timing (profiling build only, -DHL_PROFILE): lane 0
-// accumulates shader-clock cycles per phase into FrameArgs::prof.
+// Optional phase timing (profiling build only, -DHL_PROFILE): every wave
+// accumulates shader-clock cycles per phase in registers (Ctx::pacc); lane 0
+// adds them to FrameArgs::prof once per macroblock.
 #if defined(HL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
-#define HL_PROF_T(v) const unsigned long long v = clock64()
-#define HL_PROF_ADD(c, slot, t0)                                                  \
-    do {                                                                        \
-        if ((c).tid == 0 && (c).F.prof) {                                       \
-            atomicAdd(&(c).F.prof[2 * (slot)], (unsigned long long)(clock64() - (t0))); \
-            atomicAdd(&(c).F.prof[2 * (slot) + 1], 1ull);                        \
-        }                                                                       \
+#define HL_PROF_T(v) const unsigned long long v = __builtin_readcyclecounter()
+#define HL_PROF_ADD(c, slot, t0)                                 \
+    do {                                                         \
+        (c).pacc[slot] += __builtin_readcyclecounter() - (t0);   \
+        (c).pcnt[slot] += 1;                                     \
     } while (0)
+constexpr int kProfSlots = 12;
 #else
 #define HL_PROF_T(v) const unsigned long long v = 0
 #define HL_PROF_ADD(c, slot, t0) ((void)(t0))
@@ -94,6 +94,8 @@ static constexpr PartDef kParts[7] = {
 
 struct Shared {
     NbInfo nb[5];  // 0 = current MB (live search state), 1 = A, 2 = B, 3 = C, 4 = D
+    int32_t mvg[5][6];  // motion grid, see MvN
+    int8_t mvs[5][6];
     int32_t nb_pm0[3];
     int8_t nb_i4[3][16];
     int8_t extA[16], extB[16];  // luma nC from the neighbouring MB (-1 = not available, -2 = inside MB)
@@ -136,6 +138,10 @@ struct Shared {
     int16_t i4_lv[9][16];
     uint8_t i4_rec[9][16];
     int32_t luma_level[16][16];
+    int16_t i4nb[16];            // neighbours of the current 4x4 block (p[13] layout)
+    int32_t dcY[16];             // I16x16: scaled DC per DC-matrix position
+    int16_t i16_dcl[16];         // I16x16: DC levels of the current mode (scan order)
+    int32_t dcrow[4];            // I16x16: DC block rate, TotalCoeff, single counter
     int32_t predc[2][64];
     int32_t cres_dc[2][4], cres_cac[2][4], cres_cdc[2][4], cres_tc[2][4], cres_sctr[2][4];
     int32_t cdc_level[2][4];
@@ -154,6 +160,10 @@ struct Ctx {
     int addr, mbx, mby, xL, yL;
     int chain, fresh, dep;  // rdo.Single_ctr emulation (uniform)
     LaneK K;                // per-lane constants of the 16-lane block pipeline (device)
+#if defined(HL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+    unsigned long long pacc[kProfSlots] = {};
+    unsigned pcnt[kProfSlots] = {};
+#endif
 };
 
 // --------------------------------------------------------------------------
@@ -232,12 +242,48 @@ HD void sub_part_idx(const NbInfo& n, int xW, int yW, int& pi, int& spi)  // mb.
     else spi = (8 / n.sub_w[pi]) * ((yW % 8) / n.sub_h[pi]) + ((xW % 8) / n.sub_w[pi]);
 }
 
-struct NbPart {
-    int w, pi, spi;
+// Motion of the 4x4 blocks around and inside the current MB, in LDS:
+// S.mvg / S.mvs [by + 1][bx + 1] for block coordinates bx -1..4, by -1..3
+// (row -1 = MBs D, B, C; column -1 = MB A; inside = partitions of the
+// current partitioning already searched).  State 0 = not available,
+// 1 = available intra (refIdx -1), 2 = inter (refIdx 0).  This is the
+// neighbour derivation of 8.4.1.3.2 (utils.c:854-963) with the partition
+// lookup done once per MB instead of per predictor.
+struct MvN {
+    int st, mv[2];
 };
 
-// 8.4.1.3.2 neighbouring partitions + motion data (utils.c:854-963)
-HD void nb_motion(const Shared& S, int pi, int spi, NbPart nb[4], int mv[4][2], int ref[4])
+HD MvN mv_at(const Shared& S, int bx, int by)
+{
+    MvN n;
+    n.st = S.mvs[by + 1][bx + 1];
+    const int v = S.mvg[by + 1][bx + 1];
+    n.mv[0] = n.st == 2 ? (int)(int16_t)(v & 0xFFFF) : 0;
+    n.mv[1] = n.st == 2 ? (v >> 16) : 0;
+    return n;
+}
+
+// A, B, C (C replaced by D when not available) of the (sub)partition at
+// luma (x, y) of width ppw
+HD void nb_motion(const Shared& S, int x, int y, int ppw, MvN nb[3])
+{
+    const int bx = x >> 2, by = y >> 2;
+    nb[0] = mv_at(S, bx - 1, by);
+    nb[1] = mv_at(S, bx, by - 1);
+    const int cx = (x + ppw) >> 2;
+    nb[2] = (cx <= 4 && !(cx == 4 && by > 0)) ? mv_at(S, cx, by - 1) : MvN{0, {0, 0}};
+    if (nb[2].st == 0) nb[2] = mv_at(S, bx - 1, by - 1);
+}
+
+HD int median3(int a, int b, int c)
+{
+    const int mx = a > b ? (a > c ? a : c) : (b > c ? b : c);
+    const int mn = a < b ? (a < c ? a : c) : (b < c ? b : c);
+    return a + b + c - mx - mn;
+}
+
+// 8.4.1.3 (utils.c:751-831) for partition (pi, spi) of the current partitioning
+HD void mvp(const Shared& S, int pi, int spi, int out[2])
 {
     const NbInfo& cur = S.nb[0];
     const int x = (pi % (16 / cur.part_w)) * cur.part_w;
@@ -250,88 +296,63 @@ HD void nb_motion(const Shared& S, int pi, int spi, NbPart nb[4], int mv[4][2], 
     if (cur.e_type == ET_PSKIP) ppw = 16;
     else if (is8x8(cur.e_type)) ppw = cur.sub_w[pi];
     else ppw = cur.part_w;
-    const int xd[4] = {-1, 0, ppw, -1}, yd[4] = {0, -1, -1, -1};
-    for (int N = 0; N < 4; ++N) {
-        int xW, yW;
-        const int w = nb_loc(S, x + xS + xd[N], y + yS + yd[N], 16, 16, xW, yW);
-        nb[N].w = w;
-        nb[N].pi = nb[N].spi = -1;
-        if (w >= 0) {
-            int p, sp;
-            sub_part_idx(S.nb[w], xW, yW, p, sp);
-            if (w == 0 && (p > pi || (p == pi && sp > spi))) nb[N].w = -1;
-            else {
-                nb[N].pi = p;
-                nb[N].spi = sp;
-            }
-        }
-    }
-    if (nb[2].w < 0) nb[2] = nb[3];
-    for (int N = 0; N < 4; ++N) {
-        if (nb[N].w < 0 || S.nb[nb[N].w].intra) {
-            mv[N][0] = mv[N][1] = 0;
-            ref[N] = -1;
-        }
-        else {
-            mv[N][0] = S.nb[nb[N].w].mv[nb[N].pi][nb[N].spi][0];
-            mv[N][1] = S.nb[nb[N].w].mv[nb[N].pi][nb[N].spi][1];
-            ref[N] = 0;  // RefIdxL0 is always 0 with one reference frame
-        }
-    }
-}
-
-HD int median3(int a, int b, int c)
-{
-    const int mx = a > b ? (a > c ? a : c) : (b > c ? b : c);
-    const int mn = a < b ? (a < c ? a : c) : (b < c ? b : c);
-    return a + b + c - mx - mn;
-}
-
-// 8.4.1.3 (utils.c:751-831)
-HD void mvp(const Shared& S, int pi, int spi, int out[2])
-{
-    NbPart nb[4];
-    int mv[4][2], ref[4];
-    nb_motion(S, pi, spi, nb, mv, ref);
-    const NbInfo& cur = S.nb[0];
+    MvN nb[3];
+    nb_motion(S, x + xS, y + yS, ppw, nb);
+    int ref[3];
+    for (int N = 0; N < 3; ++N) ref[N] = nb[N].st == 2 ? 0 : -1;
     int sel = -1;
     if (cur.part_w == 16 && cur.part_h == 8 && pi == 0 && ref[1] == 0) sel = 1;
     else if (cur.part_w == 16 && cur.part_h == 8 && pi == 1 && ref[0] == 0) sel = 0;
     else if (cur.part_w == 8 && cur.part_h == 16 && pi == 0 && ref[0] == 0) sel = 0;
     else if (cur.part_w == 8 && cur.part_h == 16 && pi == 1 && ref[2] == 0) sel = 2;
     if (sel >= 0) {
-        out[0] = mv[sel][0];
-        out[1] = mv[sel][1];
+        out[0] = nb[sel].mv[0];
+        out[1] = nb[sel].mv[1];
         return;
     }
-    if (nb[1].w < 0 && nb[2].w < 0 && nb[0].w >= 0) {
-        mv[1][0] = mv[2][0] = mv[0][0];
-        mv[1][1] = mv[2][1] = mv[0][1];
+    if (nb[1].st == 0 && nb[2].st == 0 && nb[0].st != 0) {
+        nb[1] = nb[2] = nb[0];
         ref[1] = ref[2] = ref[0];
     }
     if (ref[0] == 0 && ref[1] != 0 && ref[2] != 0) sel = 0;
     else if (ref[1] == 0 && ref[2] != 0 && ref[0] != 0) sel = 1;
     else if (ref[2] == 0 && ref[1] != 0 && ref[0] != 0) sel = 2;
     if (sel >= 0) {
-        out[0] = mv[sel][0];
-        out[1] = mv[sel][1];
+        out[0] = nb[sel].mv[0];
+        out[1] = nb[sel].mv[1];
         return;
     }
-    out[0] = median3(mv[0][0], mv[1][0], mv[2][0]);
-    out[1] = median3(mv[0][1], mv[1][1], mv[2][1]);
+    out[0] = median3(nb[0].mv[0], nb[1].mv[0], nb[2].mv[0]);
+    out[1] = median3(nb[0].mv[1], nb[1].mv[1], nb[2].mv[1]);
 }
 
-// 8.4.1.1 P_Skip motion vector (utils.c:709-748)
+// 8.4.1.1 P_Skip motion vector (utils.c:709-748); the current partitioning
+// is 16x16 whenever this is asked
 HD void skip_mv(const Shared& S, int out[2])
 {
-    NbPart nb[4];
-    int mv[4][2], ref[4];
-    nb_motion(S, 0, 0, nb, mv, ref);
-    if (nb[0].w < 0 || nb[1].w < 0 || (ref[0] == 0 && !mv[0][0] && !mv[0][1]) || (ref[1] == 0 && !mv[1][0] && !mv[1][1])) {
+    MvN nb[3];
+    nb_motion(S, 0, 0, 16, nb);
+    if (nb[0].st == 0 || nb[1].st == 0 || (nb[0].st == 2 && !nb[0].mv[0] && !nb[0].mv[1]) ||
+        (nb[1].st == 2 && !nb[1].mv[0] && !nb[1].mv[1])) {
         out[0] = out[1] = 0;
         return;
     }
     mvp(S, 0, 0, out);
+}
+
+// marks the 4x4 blocks of the luma rectangle as decided with motion mv
+HD void grid_set(Shared& S, int x, int y, int w, int h, int mvx, int mvy)
+{
+    for (int by = y >> 2; by < (y + h) >> 2; ++by)
+        for (int bx = x >> 2; bx < (x + w) >> 2; ++bx) {
+            S.mvs[by + 1][bx + 1] = 2;
+            S.mvg[by + 1][bx + 1] = (mvx & 0xFFFF) | (mvy << 16);
+        }
+}
+HD void grid_reset_inside(Shared& S)
+{
+    for (int by = 0; by < 4; ++by)
+        for (int bx = 0; bx < 4; ++bx) S.mvs[by + 1][bx + 1] = 0;
 }
 
 // nC of a luma-type block (residual.c:640-755): neighbour values are taken
@@ -444,6 +465,27 @@ HD void mb_begin(Ctx& c)
         const int w = t + 1;
         if (av[w]) load_nbinfo(F.st[addrs[w]], S.nb[w]);
         else S.nb[w].avail = 0;
+    }
+    // motion grid: row -1 from D / B / C, column -1 from A, inside undecided
+    for (int t = tid; t < 30; t += nthr) {
+        const int gy = t / 6, gx = t % 6, bx = gx - 1, by = gy - 1;
+        int w = 0, st = 0, v = 0;
+        if (by < 0) w = bx < 0 ? 4 : (bx < 4 ? 2 : 3);
+        else if (bx < 0) w = 1;
+        if (w && av[w]) {
+            const MbState& M = F.st[addrs[w]];
+            const int xW = (bx + 4) & 3, yW = (by + 4) & 3;  // 4x4 block of the neighbour
+            if (M.flags & FL_INTRA) st = 1;
+            else {
+                const int x = xW * 4, y = yW * 4;
+                const int pi = (16 / M.part_w) * (y / M.part_h) + (x / M.part_w);
+                const int spi = is8x8(M.e_type) ? (8 / M.sub_w[pi]) * ((y % 8) / M.sub_h[pi]) + ((x % 8) / M.sub_w[pi]) : 0;
+                st = 2;
+                v = (M.mv[pi][spi][0] & 0xFFFF) | (M.mv[pi][spi][1] << 16);
+            }
+        }
+        S.mvs[gy][gx] = (int8_t)st;
+        S.mvg[gy][gx] = v;
     }
     for (int t = tid; t < 2; t += nthr) {
         const int w = t + 1;
@@ -760,8 +802,8 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
 #endif
     HL_PROF_ADD(c, 2, tp2);
     for (int ci = ncand - 1; ci >= 0; --ci)
-        if (S.cd_last[ci] >= 0) {
-            chain_write(c, S.cd_last[ci]);
+        if (uni(S.cd_last[ci]) >= 0) {
+            chain_write(c, uni(S.cd_last[ci]));
             break;
         }
 }
@@ -807,15 +849,19 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         int smv[2];
         skip_mv(S, smv);
         mvp(S, 0, 0, pmv);
+        smv[0] = uni(smv[0]);
+        smv[1] = uni(smv[1]);
+        pmv[0] = uni(pmv[0]);
+        pmv[1] = uni(pmv[1]);
         if (pmv[0] == smv[0] && pmv[1] == smv[1]) {
             put_cand(c, 0, pmv[0], pmv[1]);
             eval_candidates(c, g, 1, pmv);
-            if (S.cd_bits[0] == 0 || S.cd_single[0] < 6) {
+            if (uni(S.cd_bits[0]) == 0 || uni(S.cd_single[0]) < 6) {
                 probably = true;
                 b.cost = 0.0;
-                b.single = S.cd_single[0];
-                b.dist = S.cd_dist[0];
-                b.cbp = S.cd_cbp[0];
+                b.single = uni(S.cd_single[0]);
+                b.dist = uni(S.cd_dist[0]);
+                b.cbp = uni(S.cd_cbp[0]);
                 b.mv[0] = pmv[0];
                 b.mv[1] = pmv[1];
             }
@@ -824,6 +870,8 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     {
         HL_PROF_T(tm);
         mvp(S, pi, spi, pmv);
+        pmv[0] = uni(pmv[0]);
+        pmv[1] = uni(pmv[1]);
         HL_PROF_ADD(c, 4, tm);
     }
     // MVP and (0,0) candidates, me_ds.c:280-300
@@ -836,12 +884,12 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     put_cand(c, 1, 0, 0);
     eval_candidates(c, g, nc0, pmv);
     for (int ci = 0; ci < nc0; ++ci) {
-        const double cost = S.cd_cost[ci];
+        const double cost = uni(S.cd_cost[ci]);
         if (cost < b.cost) {
             b.cost = cost;
-            b.single = S.cd_single[ci];
-            b.dist = S.cd_dist[ci];
-            b.cbp = S.cd_cbp[ci];
+            b.single = uni(S.cd_single[ci]);
+            b.dist = uni(S.cd_dist[ci]);
+            b.cbp = uni(S.cd_cbp[ci]);
             b.mv[0] = cand[ci][0];
             b.mv[1] = cand[ci][1];
         }
@@ -879,13 +927,13 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         if (ncand) {
             eval_candidates(c, g, ncand, pmv);
             for (int ci = 0; ci < ncand; ++ci) {
-                const double cost = S.cd_cost[ci];
+                const double cost = uni(S.cd_cost[ci]);
                 if (cost < b.cost) {
                     best = idxsel[ci];
                     b.cost = cost;
-                    b.single = S.cd_single[ci];
-                    b.dist = S.cd_dist[ci];
-                    b.cbp = S.cd_cbp[ci];
+                    b.single = uni(S.cd_single[ci]);
+                    b.dist = uni(S.cd_dist[ci]);
+                    b.cbp = uni(S.cd_cbp[ci]);
                     b.mv[0] = cand[ci][0];
                     b.mv[1] = cand[ci][1];
                 }
@@ -930,6 +978,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         S.bmvp[pi][spi][1] = (int16_t)pmv[1];
         S.nb[0].mv[pi][spi][0] = (int16_t)b.mv[0];  // MvL0 feeds the MVP of later partitions
         S.nb[0].mv[pi][spi][1] = (int16_t)b.mv[1];
+        grid_set(S, g.px, g.py, g.pw, g.ph, b.mv[0], b.mv[1]);
     }
     HL_SYNC();
     HL_PROF_ADD(c, 3, tsp);
@@ -964,17 +1013,21 @@ HD void i4_neighbours(const Shared& S, int blk, int p[13])
 }
 
 #define HL_P4(x, y) p[(x) == -1 ? (y) + 1 : (x) + 5]
-HD bool i4_avail(int mode, const int p[13])
+template <typename PT>
+HD bool i4_avail(int mode, const PT& p)
 {
     if ((mode == 0 || mode == 3 || mode == 7) && p[5] == kNA) return false;
     if ((mode == 1 || mode == 8) && p[1] == kNA) return false;
     if ((mode == 4 || mode == 5 || mode == 6) && p[0] == kNA) return false;
     return true;
 }
-HD void i4_pred(int mode, const int p[13], int* pr)
+// Intra4x4 prediction of sample (x, y), modes 0-8 (8.3.1.2); p is the
+// 13-sample neighbour array (p[0] = corner, p[1..4] left, p[5..12] top).
+template <typename PT>
+HD int i4_pred_px(int mode, const PT& p, int x, int y)
 {
-    for (int y = 0; y < 4; ++y)
-        for (int x = 0; x < 4; ++x) {
+    {
+        {
             int v;
             switch (mode) {
             case 0: v = p[5 + x]; break;
@@ -1028,8 +1081,14 @@ HD void i4_pred(int mode, const int p[13], int* pr)
                 break;
             }
             }
-            pr[y * 4 + x] = v;
+            return v;
         }
+    }
+}
+HD void i4_pred(int mode, const int p[13], int* pr)
+{
+    for (int y = 0; y < 4; ++y)
+        for (int x = 0; x < 4; ++x) pr[y * 4 + x] = i4_pred_px(mode, p, x, y);
 }
 
 // Intra16x16 prediction of sample (x, y) (pred_intra.c:855-1041); p33 layout
@@ -1295,6 +1354,110 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp)
         S.pm0 = PM_I16;
         S.i16mode = 2;
     }
+#if defined(__HIP_DEVICE_COMPILE__)
+    // one 16-lane row per 4x4 block (rows 0-15), modes in order
+    const int row = c.tid >> 4;
+    const int qbits = 15 + F.qp / 6, fq = (1 << qbits) / 3;
+    const int x = blk_x(row & 15) + (c.K.p & 3), y = blk_y(row & 15) + (c.K.p >> 2);
+    for (int mode = 0; mode < 4; ++mode) {
+        if (mode == 0 && uni(S.top[1]) == kNA) continue;
+        if (mode == 1 && uni(S.left[0]) == kNA) continue;
+        if (mode == 3 && uni(S.top[0]) == kNA) continue;
+        int dcv, pa, pb, pc;
+        i16_params(S, mode, dcv, pa, pb, pc);
+        dcv = uni(dcv);
+        pa = uni(pa);
+        pb = uni(pb);
+        pc = uni(pc);
+        int pred = 0, sv = 0;
+        if (row < 16) {  // blocks: transform, quant, AC statistics
+            const int t = row;
+            pred = i16_pred(S, mode, x, y, dcv, pa, pb, pc);
+            sv = S.src[y * 16 + x];
+            const int w = coop_fwd(c.K, sv - pred);
+            const int q = coop_quant(w, c.K.mf, qbits, fq);
+            const bool qz = row_or(q != 0) == 0;
+            const CoopStat st = coop_cavlc(S.ct, q, c.K.s - 1, S.lvs[row]);
+            S.i16_ac[t][c.K.s == 0 ? 15 : c.K.s - 1] = c.K.s == 0 ? 0 : q;
+            if (c.K.p == 0) {
+                S.i16_dcc[t] = w;
+                S.i16_called[t] = !qz;
+                S.i16_tc[t] = st.tc;
+                S.i16_t1[t] = st.t1;
+                S.i16_sctr[t] = st.sctr;
+                S.i16_bits[t] = st.rest;
+            }
+        }
+        HL_SYNC();
+        // nC of the AC writes: inside the MB, blocks written earlier in this
+        // mode show their own TotalCoeff (even 0), others the live state
+        if (c.tid < 16) {
+            const int t = c.tid;
+            if (S.i16_called[t]) {
+                const int nC = nc_luma_of(S, t, [&](int ni) -> int { return S.i16_called[ni] ? S.i16_tc[ni] : S.tc[ni]; });
+                S.i16_bits[t] += coop_token_len(S.ct, nC, S.i16_tc[t], S.i16_t1[t]);
+                S.tc[t] = (int8_t)S.i16_tc[t];
+            }
+        }
+        HL_SYNC();
+        // uniform: single counter with stale reads, cbp, rate
+        int single = 0, bcbp = 0, rate = 0;
+        for (int b = 0; b < 16; ++b) {
+            if (!uni(S.i16_called[b])) continue;
+            rate += uni(S.i16_bits[b]);
+            bcbp |= 1 << b;
+            if (uni(S.i16_tc[b]) > 0) chain_write(c, uni(S.i16_sctr[b]));
+            else if (!c.fresh) c.dep = 1;
+            single += c.chain;
+        }
+        if (bcbp && single < 6) bcbp = 0;
+        if (bcbp) {
+            if (c.tid < 16) {  // the DC block: Hadamard, quant, CAVLC, inverse
+                const int hh = coop_lin(c.K.had, S.i16_dcc[kDcPos[c.K.p]]) >> 1;
+                const int qd = quant_dc(F.qp, true, hh);
+                const CoopStat st = coop_cavlc(S.ct, qd, c.K.s, S.lvs[0]);
+                S.i16_dcl[c.K.s] = (int16_t)qd;
+                const int f = coop_lin(c.K.had, qd);
+                const int scale = level_scale(F.qp % 6, 0, 0), q6 = F.qp / 6;
+                S.dcY[c.K.p] = F.qp >= 36 ? (f * scale) << (q6 - 6) : (f * scale + (1 << (5 - q6))) >> (6 - q6);
+                if (c.tid == 0) {
+                    const int nC = nc_luma_of(S, 0, [&](int ni) -> int { return S.tc[ni]; });
+                    S.dcrow[0] = st.rest + coop_token_len(S.ct, nC, st.tc, st.t1);
+                    S.dcrow[1] = st.tc;
+                    S.dcrow[2] = st.sctr;
+                    S.tc[0] = (int8_t)st.tc;
+                }
+            }
+            HL_SYNC();
+            rate += uni(S.dcrow[0]);
+            if (uni(S.dcrow[1]) > 0) chain_write(c, uni(S.dcrow[2]));
+        }
+        if (row < 16) {  // reconstruction and distortion of each block
+            const int t = row;
+            const int cv = !bcbp ? 0 : (c.K.p == 0 ? S.dcY[kDcPos[t]] : S.i16_ac[t][c.K.s - 1]);
+            const int r = coop_idct(c.K, c.K.p == 0 ? cv : coop_dequant(cv, c.K.ls, F.qp));
+            const int rec = clip255(pred + r);
+            S.tmp_rec[y * 16 + x] = (uint8_t)rec;
+            const int d = row_sum(iabs(sv - rec));
+            if (c.K.p == 0) S.i16_dist[t] = d;
+        }
+        HL_SYNC();
+        int dist = 0;
+        for (int b = 0; b < 16; ++b) dist += uni(S.i16_dist[b]);
+        const double cost = dadd((double)dist, dmul(F.lambda, (double)rate));
+        if (cost < best_cost) {
+            best_cost = cost;
+            best_cbp = bcbp;
+            if (c.tid == 0) S.i16mode = mode;
+            if (c.tid < 16) S.i16_best_dc[c.tid] = bcbp ? S.i16_dcl[c.tid] : 0;
+            for (int t = c.tid; t < 256; t += c.nthr) {
+                S.i16_best_ac[t >> 4][t & 15] = (int16_t)S.i16_ac[t >> 4][t & 15];
+                S.i16_best_rec[t] = S.tmp_rec[t];
+            }
+        }
+        HL_SYNC();
+    }
+#else
     for (int mode = 0; mode < 4; ++mode) {
         if (mode == 0 && S.top[1] == kNA) continue;
         if (mode == 1 && S.left[0] == kNA) continue;
@@ -1438,6 +1601,7 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp)
         }
         HL_SYNC();
     }
+#endif
 }
 
 // --------------------------------------------------------------------------
@@ -1454,6 +1618,84 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4)
         S.flags = FL_INTRA;
         S.pm0 = PM_I4;
     }
+#if defined(__HIP_DEVICE_COMPILE__)
+    // one 16-lane row per mode (rows 0-8), blocks in order
+    const int row = c.tid >> 4;
+    const int qbits = 15 + F.qp / 6, fq = (1 << qbits) / 3;
+    for (int blk = 0; blk < 16; ++blk) {
+        const int xO = blk_x(blk), yO = blk_y(blk);
+        if (c.tid < 13) {
+            int p[13];
+            i4_neighbours(S, blk, p);
+            S.i4nb[c.tid] = (int16_t)p[c.tid];
+        }
+        HL_SYNC();
+        // nC is the same for all nine modes: they only rewrite this block
+        const int nC = uni(nc_luma_of(S, blk, [&](int ni) -> int { return S.tc[ni]; }));
+        if (row < 9) {
+            const int m = row;
+            const bool ok = i4_avail(m, S.i4nb);
+            if (ok) {
+                const int x = c.K.p & 3, y = c.K.p >> 2;
+                const int pred = i4_pred_px(m, S.i4nb, x, y);
+                const int sv = S.src[(yO + y) * 16 + xO + x];
+                const int res = sv - pred;
+                const bool exact = row_or(res != 0) == 0;
+                const int q = coop_quant(coop_fwd(c.K, res), c.K.mf, qbits, fq);
+                const CoopStat st = coop_cavlc(S.ct, q, c.K.s, S.lvs[row]);
+                const int r = coop_idct(c.K, coop_dequant(q, c.K.ls, F.qp));
+                const int rec = clip255(pred + r);
+                const int d = row_sum(iabs(sv - rec));
+                S.i4_rec[m][c.K.p] = (uint8_t)rec;
+                S.i4_lv[m][c.K.s] = (int16_t)q;
+                if (c.K.p == 0) {
+                    const int bits = st.tc ? st.rest + coop_token_len(S.ct, nC, st.tc, st.t1) : 0;
+                    S.i4_exact[m] = exact;
+                    S.i4_nz[m] = st.tc > 0;
+                    S.i4_tc[m] = st.tc;
+                    S.i4_sctr[m] = st.sctr;
+                    S.i4_dist[m] = d;
+                    S.i4_cost[m] = exact ? 0.0 : dadd((double)d, dmul(F.lambda, (double)bits));
+                }
+            }
+            if (c.K.p == 0) S.i4_cost_ok[m] = ok;
+        }
+        HL_SYNC();
+        // uniform resolution in mode order (rdo.c:1931-2014)
+        double dmin = 1.7976931348623157e308;
+        int best = 2, lastw = -1;
+        bool best_zero = false;
+        for (int m = 0; m < 9; ++m) {
+            if (!uni(S.i4_cost_ok[m])) continue;
+            if (uni(S.i4_exact[m])) {
+                dmin = 0.0;
+                best = m;
+                best_zero = true;
+                break;
+            }
+            const int nz = uni(S.i4_nz[m]);
+            if (nz) lastw = m;
+            const double cm = uni(S.i4_cost[m]);
+            if (cm < dmin) {
+                dmin = cm;
+                best = m;
+                best_zero = !nz;
+            }
+        }
+        if (lastw >= 0) chain_write(c, uni(S.i4_sctr[lastw]));
+        best_cost = dadd(best_cost, dmin);
+        if (!best_zero) cbp4 |= 1 << blk;
+        if (c.tid < 16) {
+            S.rec[(yO + (c.tid >> 2)) * 16 + xO + (c.tid & 3)] = S.i4_rec[best][c.tid];
+            S.luma_level[blk][c.tid] = S.i4_lv[best][c.tid];
+        }
+        if (c.tid == 0) {
+            S.i4mode[blk] = (int8_t)best;
+            if (lastw >= 0) S.tc[blk] = (int8_t)S.i4_tc[lastw];
+        }
+        HL_SYNC();
+    }
+#else
     for (int blk = 0; blk < 16; ++blk) {
         const int xO = kBlkX[blk], yO = kBlkY[blk];
         int p[13];
@@ -1550,6 +1792,7 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4)
         }
         HL_SYNC();
     }
+#endif
 }
 
 HD void pred_modes_4x4(Shared& S)  // pred_intra.c:541-615 (lane 0)
@@ -1599,9 +1842,13 @@ HD double guess_intra(Ctx& c)
     Shared& S = c.S;
     double c16, c4;
     int cbp16, cbp4 = 0;
+    HL_PROF_T(t16);
     guess_i16(c, c16, cbp16);
+    HL_PROF_ADD(c, 10, t16);
+    HL_PROF_T(t4);
     if (c16 == 0.0) c4 = 1.7976931348623157e308;
     else guess_i4(c, c4, cbp4);
+    HL_PROF_ADD(c, 11, t4);
     HL_SYNC();
     const int i16mode = S.i16mode;
     const int cmode = i16mode == 0 ? 2 : (i16mode == 3 ? 3 : (i16mode == 1 ? 1 : 0));
@@ -1775,6 +2022,7 @@ HD void guess_inter(Ctx& c)
                     S.nb[0].sub_w[i] = pd.sub_w;
                     S.nb[0].sub_h[i] = pd.sub_h;
                 }
+                grid_reset_inside(S);
             }
             HL_SYNC();
             bool prob = false;
@@ -1788,14 +2036,14 @@ HD void guess_inter(Ctx& c)
             int single_sum = 0;
             for (int pi = 0; pi < pd.num_part; ++pi)
                 for (int spi = 0; spi < pd.num_sub; ++spi) {
-                    cost_sum = dadd(cost_sum, S.bcost[pi][spi]);
-                    single_sum += S.bsingle[pi][spi];
+                    cost_sum = dadd(cost_sum, uni(S.bcost[pi][spi]));
+                    single_sum += uni(S.bsingle[pi][spi]);
                 }
             if (!probably && cost_sum != 0.0 && single_sum < 6 && fam == 0) {
                 int smv[2];
                 skip_mv(S, smv);
-                probably = smv[0] == S.bmvp[0][0][0] && smv[1] == S.bmvp[0][0][1] && S.bmv[0][0][0] == S.bmvp[0][0][0] &&
-                           S.bmv[0][0][1] == S.bmvp[0][0][1];
+                probably = uni(smv[0]) == uni(S.bmvp[0][0][0]) && uni(smv[1]) == uni(S.bmvp[0][0][1]) &&
+                           uni(S.bmv[0][0][0]) == uni(S.bmvp[0][0][0]) && uni(S.bmv[0][0][1]) == uni(S.bmvp[0][0][1]);
             }
             cost_sum = dadd(cost_sum, dmul(F.lambda, (double)pd.hdr_bits));
             if (cost_sum < best_cost) {
@@ -1826,7 +2074,7 @@ HD void guess_inter(Ctx& c)
             HL_SYNC();
             inter_pred_mb(c, true, false);
             reconstruct_chroma(c, false);
-            pskip = !S.cbp_cac[0] && !S.cbp_cac[1] && !S.cbp_cdc[0] && !S.cbp_cdc[1];
+            pskip = !uni(S.cbp_cac[0]) && !uni(S.cbp_cac[1]) && !uni(S.cbp_cdc[0]) && !uni(S.cbp_cdc[1]);
         }
         best_found = best_found || best_cost == 0.0 || pskip;
     }
@@ -1887,10 +2135,10 @@ HD void guess_inter(Ctx& c)
         if (c.tid == 0) guess_cbp(S);
         HL_SYNC();
     }
-    if (!(S.flags & FL_SKIP) && S.cbp == 0 && S.e_type == ET_P16x16 && S.mvd[0][0][0] == 0 && S.mvd[0][0][1] == 0) {
+    if (!(uni(S.flags) & FL_SKIP) && uni(S.cbp) == 0 && uni(S.e_type) == ET_P16x16 && uni(S.mvd[0][0][0]) == 0 && uni(S.mvd[0][0][1]) == 0) {
         int smv[2];
         skip_mv(S, smv);
-        if (smv[0] == S.best_mvp[0][0][0] && smv[1] == S.best_mvp[0][0][1]) {
+        if (uni(smv[0]) == uni(S.best_mvp[0][0][0]) && uni(smv[1]) == uni(S.best_mvp[0][0][1])) {
             HL_SYNC();
             if (c.tid == 0) {
                 S.e_type = ET_PSKIP;
@@ -2069,6 +2317,13 @@ HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, in
     mb_end(c);
     HL_PROF_ADD(c, 7, t1);
     HL_PROF_ADD(c, 8, t0);
+#if defined(HL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+    if (tid == 0 && F.prof)
+        for (int i = 0; i < kProfSlots; ++i) {
+            atomicAdd(&F.prof[2 * i], c.pacc[i]);
+            atomicAdd(&F.prof[2 * i + 1], (unsigned long long)c.pcnt[i]);
+        }
+#endif
 }
 
 }  // namespace hl

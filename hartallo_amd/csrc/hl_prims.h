@@ -38,6 +38,28 @@ HD double dmul(double a, double b)
 #endif
 }
 
+// Values every lane computes identically from LDS: tell the compiler they
+// are wave-uniform (SGPRs, scalar branches) instead of divergent VGPRs.
+HD int uni(int v)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_readfirstlane(v);
+#else
+    return v;
+#endif
+}
+HD double uni(double v)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)b);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32));
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+#else
+    return v;
+#endif
+}
+
 HD int iabs(int x) { return x < 0 ? -x : x; }
 HD int isign(int x) { return x >= 0 ? 1 : -1; }
 HD int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }

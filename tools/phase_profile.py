@@ -13,7 +13,8 @@ sys.path.insert(0, ROOT)
 import hartallo_amd  # noqa: E402
 from hartallo_amd import _lib, synth  # noqa: E402
 
-PHASES = ["eval:block", "eval:nC", "eval:reduce", "search_partition", "mvp", "guess_intra(P)", "mb_begin", "mb_end", "whole MB"]
+PHASES = ["eval:block", "eval:nC", "eval:reduce", "search_partition", "mvp", "guess_intra(P)", "mb_begin", "mb_end", "whole MB",
+          "-", "intra:i16", "intra:i4"]
 
 
 def main():
