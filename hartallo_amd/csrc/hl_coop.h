@@ -49,6 +49,21 @@ __device__ __forceinline__ int row_max(int x)
     return max(x, dpp<kRor1>(x));
 }
 
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v)
+{
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)dpp<CTRL>((int)(unsigned)b), hi = (unsigned)dpp<CTRL>((int)(unsigned)(b >> 32));
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double row_min_f64(double x)
+{
+    x = fmin(x, dpp_f64<kRor8>(x));
+    x = fmin(x, dpp_f64<kRor4>(x));
+    x = fmin(x, dpp_f64<kRor2>(x));
+    return fmin(x, dpp_f64<kRor1>(x));
+}
+
 // Per-lane constants.  The coefficient fields are packed 4 bits per source
 // (signed 3-bit coefficient + a shift bit for the IDCT's >>1 terms) and
 // decoded with bit-field extracts.
@@ -141,9 +156,10 @@ __device__ __forceinline__ int fld_u1(uint32_t w, int pos) { return (w >> (pos +
 __device__ __forceinline__ int coop_lin(uint32_t f, int x)
 {
     const int q0 = dpp<kQ0>(x), q1 = dpp<kQ1>(x), q2 = dpp<kQ2>(x), q3 = dpp<kQ3>(x);
-    const int h = fld_s3(f, 0) * q0 + fld_s3(f, 4) * q1 + fld_s3(f, 8) * q2 + fld_s3(f, 12) * q3;
+    // |values| < 2^23 on every path (residuals, DC sums), so 24-bit multiplies are exact
+    const int h = __mul24(fld_s3(f, 0), q0) + __mul24(fld_s3(f, 4), q1) + __mul24(fld_s3(f, 8), q2) + __mul24(fld_s3(f, 12), q3);
     const int v1 = dpp<kRor4>(h), v2 = dpp<kRor8>(h), v3 = dpp<kRor12>(h);
-    return fld_s3(f, 16) * h + fld_s3(f, 20) * v1 + fld_s3(f, 24) * v2 + fld_s3(f, 28) * v3;
+    return __mul24(fld_s3(f, 16), h) + __mul24(fld_s3(f, 20), v1) + __mul24(fld_s3(f, 24), v2) + __mul24(fld_s3(f, 28), v3);
 }
 // forward core transform (transf.c:716-772)
 __device__ __forceinline__ int coop_fwd(const LaneK& K, int x) { return coop_lin(K.fwd, x); }
@@ -153,11 +169,12 @@ __device__ __forceinline__ int coop_idct(const LaneK& K, int d)
 {
     const int q0 = dpp<kQ0>(d), q1 = dpp<kQ1>(d), q2 = dpp<kQ2>(d), q3 = dpp<kQ3>(d);
     const uint32_t w = K.inv;
-    const int f = fld_s3(w, 0) * (q0 >> fld_u1(w, 0)) + fld_s3(w, 4) * (q1 >> fld_u1(w, 4)) + fld_s3(w, 8) * (q2 >> fld_u1(w, 8)) +
-                  fld_s3(w, 12) * (q3 >> fld_u1(w, 12));
+    // dequantised coefficients stay below 2^22 in magnitude (level < 2^13, scale <= 464)
+    const int f = __mul24(fld_s3(w, 0), q0 >> fld_u1(w, 0)) + __mul24(fld_s3(w, 4), q1 >> fld_u1(w, 4)) +
+                  __mul24(fld_s3(w, 8), q2 >> fld_u1(w, 8)) + __mul24(fld_s3(w, 12), q3 >> fld_u1(w, 12));
     const int v1 = dpp<kRor4>(f), v2 = dpp<kRor8>(f), v3 = dpp<kRor12>(f);
-    const int h = fld_s3(w, 16) * (f >> fld_u1(w, 16)) + fld_s3(w, 20) * (v1 >> fld_u1(w, 20)) + fld_s3(w, 24) * (v2 >> fld_u1(w, 24)) +
-                  fld_s3(w, 28) * (v3 >> fld_u1(w, 28));
+    const int h = __mul24(fld_s3(w, 16), f >> fld_u1(w, 16)) + __mul24(fld_s3(w, 20), v1 >> fld_u1(w, 20)) +
+                  __mul24(fld_s3(w, 24), v2 >> fld_u1(w, 24)) + __mul24(fld_s3(w, 28), v3 >> fld_u1(w, 28));
     return (h + 32) >> 6;
 }
 
@@ -264,13 +281,14 @@ __device__ __forceinline__ CoopStat coop_cavlc(const CoopTables& T, int L, int l
 // quantisation of one coefficient: f = 2^qbits / 3 (intra) or / 6 (inter)
 __device__ __forceinline__ int coop_quant(int w, int mf, int qbits, int f)
 {
-    const int v = ((w < 0 ? -w : w) * mf + f) >> qbits;
+    const int v = (int)((__umul24((unsigned)(w < 0 ? -w : w), (unsigned)mf) + (unsigned)f) >> qbits);  // < 2^32
     return w >= 0 ? v : -v;
 }
 __device__ __forceinline__ int coop_dequant(int c, int ls, int qP)
 {
     const int q6 = qP / 6;
-    return qP >= 24 ? (c * ls) << (q6 - 4) : (c * ls + (1 << (3 - q6))) >> (4 - q6);
+    const int p = __mul24(c, ls);
+    return qP >= 24 ? p << (q6 - 4) : (p + (1 << (3 - q6))) >> (4 - q6);
 }
 
 }  // namespace hl

@@ -31,10 +31,6 @@ using namespace hl;
         }                                                                                \
     } while (0)
 
-#ifndef HL_MB_THREADS
-#define HL_MB_THREADS 512
-#endif
-constexpr int kMbThreads = HL_MB_THREADS;  // rows of 16 lanes: one row per (candidate, 4x4 block)
 
 // ---------------------------------------------------------------------------
 // kernels

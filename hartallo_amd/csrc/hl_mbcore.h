@@ -58,6 +58,20 @@ constexpr int kProfSlots = 12;
 
 constexpr int kPad = 40;  // padding of the luma reference planes (origin clip is +-17, block 16, tap 3)
 constexpr int kMaxWaves = 16;  // workgroup of up to 1024 lanes per macroblock
+#ifndef HL_MB_THREADS
+#define HL_MB_THREADS 512
+#endif
+constexpr int kMbThreads = HL_MB_THREADS;          // lanes of the macroblock workgroup
+constexpr int kMbRows = kMbThreads / 16;           // 16-lane rows
+constexpr int kMaxPass = (9 * 16 + kMbRows - 1) / kMbRows;  // rows per lane for the largest step
+
+// One candidate of a step: plane offsets of its quarter-pel prediction
+// (second plane = first when the phase needs no average) and its MV.
+struct alignas(16) CandSlot {
+    int32_t off1, off2;
+    int16_t mvx, mvy;
+    int32_t pad;
+};
 constexpr int kNA = -1;   // not-available sample marker
 
 struct FrameArgs {
@@ -112,10 +126,10 @@ struct Shared {
     int16_t cac[2][4][16];// live ChromaACLevel
     int32_t cbp_l, cbp_c; // live CodedBlockPattern{Luma,Chroma}
     // --- candidate step scratch
-    int16_t wcmv[kMaxWaves][9][2];  // candidate MVs, one copy per wave (each wave writes its own)
+    CandSlot wc[kMaxWaves][9];  // candidates of the step, one copy per wave (each wave writes its own)
     int32_t be_nz[9][16], be_tc[9][16], be_t1[9][16], be_sctr[9][16], be_bits[9][16], be_dist[9][16];
-    int32_t be_w0[9][16], be_w1[9][16];                  // packed block statistics (device path)
-    alignas(16) uint8_t be_nzb[16][16], be_tcb[16][16];  // [block][candidate]
+    int32_t be_w0[9][16], be_w1[9][16], be_w2[9][16];    // packed block statistics (device path)
+    alignas(16) uint8_t be_tcb[16][16];                  // TotalCoeff [block][candidate]
     int32_t lvs[kMaxWaves * 4][16];                      // per-row level scratch of coop_cavlc
     CoopTables ct;
     uint32_t qtab[16];                                   // packed quarter-pel phase table
@@ -264,15 +278,17 @@ HD MvN mv_at(const Shared& S, int bx, int by)
 }
 
 // A, B, C (C replaced by D when not available) of the (sub)partition at
-// luma (x, y) of width ppw
+// luma (x, y) of width ppw; all four cells are read in one batch
 HD void nb_motion(const Shared& S, int x, int y, int ppw, MvN nb[3])
 {
     const int bx = x >> 2, by = y >> 2;
-    nb[0] = mv_at(S, bx - 1, by);
-    nb[1] = mv_at(S, bx, by - 1);
     const int cx = (x + ppw) >> 2;
-    nb[2] = (cx <= 4 && !(cx == 4 && by > 0)) ? mv_at(S, cx, by - 1) : MvN{0, {0, 0}};
-    if (nb[2].st == 0) nb[2] = mv_at(S, bx - 1, by - 1);
+    const bool c_in = cx <= 4 && !(cx == 4 && by > 0);
+    const MvN a = mv_at(S, bx - 1, by), b = mv_at(S, bx, by - 1), d = mv_at(S, bx - 1, by - 1);
+    const MvN cc = mv_at(S, c_in ? cx : bx - 1, by - 1);
+    nb[0] = a;
+    nb[1] = b;
+    nb[2] = (c_in && cc.st != 0) ? cc : d;
 }
 
 HD int median3(int a, int b, int c)
@@ -282,52 +298,52 @@ HD int median3(int a, int b, int c)
     return a + b + c - mx - mn;
 }
 
-// 8.4.1.3 (utils.c:751-831) for partition (pi, spi) of the current partitioning
-HD void mvp(const Shared& S, int pi, int spi, int out[2])
+// shape of the partitioning being searched (registers, not LDS)
+struct PartShape {
+    int part_w, part_h, sub_w, sub_h, is8;
+};
+
+// 8.4.1.3 (utils.c:751-831) for partition (pi, spi) of partitioning ps
+HD void mvp(const Shared& S, const PartShape& ps, int pi, int spi, int out[2])
 {
-    const NbInfo& cur = S.nb[0];
-    const int x = (pi % (16 / cur.part_w)) * cur.part_w;
-    const int y = (pi / (16 / cur.part_w)) * cur.part_h;
-    int xS = 0, yS = 0, ppw;
-    if (is8x8(cur.e_type)) {
-        xS = (spi % (8 / cur.sub_w[pi])) * cur.sub_w[pi];
-        yS = (spi / (8 / cur.sub_w[pi])) * cur.sub_h[pi];
+    const int x = (pi % (16 / ps.part_w)) * ps.part_w;
+    const int y = (pi / (16 / ps.part_w)) * ps.part_h;
+    int xS = 0, yS = 0, ppw = ps.part_w;
+    if (ps.is8) {
+        xS = (spi % (8 / ps.sub_w)) * ps.sub_w;
+        yS = (spi / (8 / ps.sub_w)) * ps.sub_h;
+        ppw = ps.sub_w;
     }
-    if (cur.e_type == ET_PSKIP) ppw = 16;
-    else if (is8x8(cur.e_type)) ppw = cur.sub_w[pi];
-    else ppw = cur.part_w;
     MvN nb[3];
     nb_motion(S, x + xS, y + yS, ppw, nb);
-    int ref[3];
-    for (int N = 0; N < 3; ++N) ref[N] = nb[N].st == 2 ? 0 : -1;
+    // named values + selects (no dynamically indexed arrays: they go to scratch)
+    MvN A = nb[0], B = nb[1], C = nb[2];
+    int rA = A.st == 2 ? 0 : -1, rB = B.st == 2 ? 0 : -1, rC = C.st == 2 ? 0 : -1;
     int sel = -1;
-    if (cur.part_w == 16 && cur.part_h == 8 && pi == 0 && ref[1] == 0) sel = 1;
-    else if (cur.part_w == 16 && cur.part_h == 8 && pi == 1 && ref[0] == 0) sel = 0;
-    else if (cur.part_w == 8 && cur.part_h == 16 && pi == 0 && ref[0] == 0) sel = 0;
-    else if (cur.part_w == 8 && cur.part_h == 16 && pi == 1 && ref[2] == 0) sel = 2;
+    if (ps.part_w == 16 && ps.part_h == 8 && pi == 0 && rB == 0) sel = 1;
+    else if (ps.part_w == 16 && ps.part_h == 8 && pi == 1 && rA == 0) sel = 0;
+    else if (ps.part_w == 8 && ps.part_h == 16 && pi == 0 && rA == 0) sel = 0;
+    else if (ps.part_w == 8 && ps.part_h == 16 && pi == 1 && rC == 0) sel = 2;
+    if (sel < 0) {
+        if (B.st == 0 && C.st == 0 && A.st != 0) {
+            B = A;
+            C = A;
+            rB = rC = rA;
+        }
+        if (rA == 0 && rB != 0 && rC != 0) sel = 0;
+        else if (rB == 0 && rC != 0 && rA != 0) sel = 1;
+        else if (rC == 0 && rB != 0 && rA != 0) sel = 2;
+    }
     if (sel >= 0) {
-        out[0] = nb[sel].mv[0];
-        out[1] = nb[sel].mv[1];
+        out[0] = sel == 0 ? A.mv[0] : (sel == 1 ? B.mv[0] : C.mv[0]);
+        out[1] = sel == 0 ? A.mv[1] : (sel == 1 ? B.mv[1] : C.mv[1]);
         return;
     }
-    if (nb[1].st == 0 && nb[2].st == 0 && nb[0].st != 0) {
-        nb[1] = nb[2] = nb[0];
-        ref[1] = ref[2] = ref[0];
-    }
-    if (ref[0] == 0 && ref[1] != 0 && ref[2] != 0) sel = 0;
-    else if (ref[1] == 0 && ref[2] != 0 && ref[0] != 0) sel = 1;
-    else if (ref[2] == 0 && ref[1] != 0 && ref[0] != 0) sel = 2;
-    if (sel >= 0) {
-        out[0] = nb[sel].mv[0];
-        out[1] = nb[sel].mv[1];
-        return;
-    }
-    out[0] = median3(nb[0].mv[0], nb[1].mv[0], nb[2].mv[0]);
-    out[1] = median3(nb[0].mv[1], nb[1].mv[1], nb[2].mv[1]);
+    out[0] = median3(A.mv[0], B.mv[0], C.mv[0]);
+    out[1] = median3(A.mv[1], B.mv[1], C.mv[1]);
 }
 
-// 8.4.1.1 P_Skip motion vector (utils.c:709-748); the current partitioning
-// is 16x16 whenever this is asked
+// 8.4.1.1 P_Skip motion vector (utils.c:709-748)
 HD void skip_mv(const Shared& S, int out[2])
 {
     MvN nb[3];
@@ -337,7 +353,8 @@ HD void skip_mv(const Shared& S, int out[2])
         out[0] = out[1] = 0;
         return;
     }
-    mvp(S, 0, 0, out);
+    const PartShape p16{16, 16, 16, 16, 0};
+    mvp(S, p16, 0, 0, out);
 }
 
 // marks the 4x4 blocks of the luma rectangle as decided with motion mv
@@ -494,7 +511,7 @@ HD void mb_begin(Ctx& c)
     }
     // external nC contributions (neighbour MBs are final for this frame)
     for (int t = tid; t < 16; t += nthr) {
-        const int bx = kBlkX[t], by = kBlkY[t];
+        const int bx = blk_x(t), by = blk_y(t);
         int8_t ea = -2, eb = -2;
         if (bx == 0) {
             if (!hasA) ea = -1;
@@ -570,13 +587,38 @@ struct PartGeo {
     int px, py, pw, ph, nbw, nblk, lbw, lnb;  // lbw / lnb = log2(nbw) / log2(nblk)
 };
 
+// Quarter-pel phase table kQpelTab packed 9 bits per phase:
+// plane1 | dx1 << 2 | dy1 << 3 | has2 << 4 | plane2 << 5 | dx2 << 7 | dy2 << 8
+HD constexpr uint32_t qpel_entry(int ph)
+{
+    return (uint32_t)(kQpelTab[ph][0] | (kQpelTab[ph][1] << 2) | (kQpelTab[ph][2] << 3) | ((kQpelTab[ph][3] >= 0) << 4) |
+                      ((kQpelTab[ph][3] >= 0 ? kQpelTab[ph][3] : 0) << 5) | (kQpelTab[ph][4] << 7) | (kQpelTab[ph][5] << 8));
+}
+HD constexpr uint64_t qpel_pack(int first, int n)
+{
+    uint64_t r = 0;
+    for (int i = 0; i < n; ++i) r |= (uint64_t)qpel_entry(first + i) << (9 * i);
+    return r;
+}
+
 // The candidate list of a step is uniform; each wave keeps its own copy in
 // LDS so that no barrier is needed between choosing and evaluating it.
-HD void put_cand(Ctx& c, int i, int mx, int my)
+// (xo, yo) = luma origin of the partition inside the MB.
+HD void put_cand(Ctx& c, int xo, int yo, int i, int mx, int my, int pt = 0, bool writer = true)
 {
-    const int w = c.tid >> 6;
-    c.S.wcmv[w][i][0] = (int16_t)mx;
-    c.S.wcmv[w][i][1] = (int16_t)my;
+    const FrameArgs& F = c.F;
+    constexpr uint64_t q0 = qpel_pack(0, 7), q1 = qpel_pack(7, 7), q2 = qpel_pack(14, 2);
+    const int ph = ((my & 3) << 2) | (mx & 3);
+    const uint64_t w = ph < 7 ? q0 : (ph < 14 ? q1 : q2);
+    const uint32_t e = (uint32_t)(w >> (9 * (ph < 7 ? ph : (ph < 14 ? ph - 7 : ph - 14)))) & 0x1FF;
+    const int X = clip3(-17, F.W + 17, c.xL + xo + (mx >> 2)) + kPad, Y = clip3(-17, F.H + 17, c.yL + yo + (my >> 2)) + kPad;
+    CandSlot cs;
+    cs.off1 = (int)(e & 3) * F.plsz + (Y + (int)((e >> 3) & 1)) * F.pstride + X + (int)((e >> 2) & 1);
+    cs.off2 = (e & 16) ? (int)((e >> 5) & 3) * F.plsz + (Y + (int)((e >> 8) & 1)) * F.pstride + X + (int)((e >> 7) & 1) : cs.off1;
+    cs.mvx = (int16_t)mx;
+    cs.mvy = (int16_t)my;
+    cs.pad = pt;  // diamond point index
+    if (writer) c.S.wc[c.tid >> 6][i] = cs;
 }
 
 HD double mv_cost(const FrameArgs& F, int dist, int bits, int mvx, int mvy, const int pmv[2])
@@ -590,30 +632,25 @@ extern long long g_hl_stats[8];
 #endif
 
 #if defined(__HIP_DEVICE_COMPILE__)
-// Luma prediction sample at integer (X, Y) for fraction (xF, yF) from the
-// contiguous quarter-pel planes; S.qtab packs kQpelTab.
-__device__ __forceinline__ int pred_luma_px(const FrameArgs& F, const Shared& S, int X, int Y, int xF, int yF)
+// bit i set iff byte i of w is non-zero
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t w)
 {
-    const uint32_t e = S.qtab[(yF << 2) | xF];
-    const uint8_t* base = F.pl[0];
-    const int a = base[(int)(e & 3) * F.plsz + (Y + kPad + (int)((e >> 3) & 1)) * F.pstride + X + kPad + (int)((e >> 2) & 1)];
-    if (!(e & 16)) return a;
-    const int b = base[(int)((e >> 5) & 3) * F.plsz + (Y + kPad + (int)((e >> 8) & 1)) * F.pstride + X + kPad + (int)((e >> 7) & 1)];
-    return (a + b + 1) >> 1;
+    const uint32_t t = ((w | ((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu)) >> 7) & 0x01010101u;
+    return (t * 0x01020408u) >> 24;
 }
-
-// non-zero flags of block k over the candidates of the step, as a bit mask
-__device__ __forceinline__ uint32_t nz_mask(const Shared& S, int k)
+// Last candidate (bit set in `allow`) whose TotalCoeff in the block row r is
+// non-zero: returns its TotalCoeff, or -1.
+__device__ __forceinline__ int tcb_last(const uint4& r, uint32_t allow)
 {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(S.be_nzb[k]);
-    uint32_t m = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) m |= ((((w[i] & 0x01010101u) * 0x01020408u) >> 24) & 0xFu) << (4 * i);
-    return m;
+    const uint32_t m = (nz_bytes(r.x) | (nz_bytes(r.y) << 4) | (nz_bytes(r.z) << 8) | (nz_bytes(r.w) << 12)) & allow;
+    if (!m) return -1;
+    const int j = 31 - __clz(m);
+    const uint32_t w = j < 4 ? r.x : (j < 8 ? r.y : (j < 12 ? r.z : r.w));
+    return (int)((w >> ((j & 3) * 8)) & 0xFF);
 }
 #endif
 
-// Evaluates the candidates S.wcmv[wave][0..ncand) of partition g in order.
+// Evaluates the candidates S.wc[wave][0..ncand) of partition g in order.
 // Leaves per-candidate cost/rbc/dist/single/cbp in S.cd_*, updates the live
 // TotalCoeffsLuma S.tc (last writer) and the Single_ctr chain.
 HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
@@ -628,29 +665,54 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
     Shared& S = c.S;
     HL_PROF_T(tp0);
 #if defined(__HIP_DEVICE_COMPILE__)
-    // phase 1: one 16-lane row per (candidate, 4x4 block)
+    // phase 1: one 16-lane row per (candidate, 4x4 block); every row of the
+    // wave issues its prediction loads for all its passes before computing
     {
         const int wave = c.tid >> 6, grp = c.tid >> 4, ngrp = c.nthr >> 4;
         const int n = ncand << g.lnb;
         const int qbits = 15 + F.qp / 6, f = (1 << qbits) / 6;
         const int pr = c.K.p >> 2, pc = c.K.p & 3;
-        for (int item = grp; item < n; item += ngrp) {
+        const uint8_t* base = F.pl[0];
+        int pa[kMaxPass], pb[kMaxPass], sv[kMaxPass];
+        // slots and source samples first (one LDS round trip), then all loads
+        int o1[kMaxPass], o2[kMaxPass];
+#pragma unroll
+        for (int j = 0; j < kMaxPass; ++j) {
+            const int item = min(grp + j * ngrp, n - 1);  // clamped: no divergence, valid addresses
             const int ci = item >> g.lnb, k = item & (g.nblk - 1);
             const int hx = k & (g.nbw - 1), hy = k >> g.lbw;
-            const int mvx = S.wcmv[wave][ci][0], mvy = S.wcmv[wave][ci][1];
-            const int X = clip3(-17, F.W + 17, c.xL + g.px + (mvx >> 2)) + (hx << 2) + pc;
-            const int Y = clip3(-17, F.H + 17, c.yL + g.py + (mvy >> 2)) + (hy << 2) + pr;
-            const int pred = pred_luma_px(F, S, X, Y, mvx & 3, mvy & 3);
-            const int sv = S.src[(g.py + (hy << 2) + pr) * 16 + g.px + (hx << 2) + pc];
-            const int q = coop_quant(coop_fwd(c.K, sv - pred), c.K.mf, qbits, f);
-            const CoopStat st = coop_cavlc(S.ct, q, c.K.s, S.lvs[grp]);
-            const int r = coop_idct(c.K, coop_dequant(q, c.K.ls, F.qp));
-            const int dist = row_sum(iabs(sv - clip255(pred + r)));
-            if (c.K.p == 0) {
-                S.be_w0[ci][k] = st.tc | (st.t1 << 5) | ((st.sctr + 1) << 8);
-                S.be_w1[ci][k] = st.rest | (dist << 16);
-                S.be_nzb[k][ci] = st.tc > 0;
-                S.be_tcb[k][ci] = (uint8_t)st.tc;
+            const int2 cs = *reinterpret_cast<const int2*>(&S.wc[wave][ci]);
+            const int o = ((hy << 2) + pr) * F.pstride + (hx << 2) + pc;
+            o1[j] = cs.x + o;
+            o2[j] = cs.y + o;
+            sv[j] = S.src[(g.py + (hy << 2) + pr) * 16 + g.px + (hx << 2) + pc];
+        }
+#pragma unroll
+        for (int j = 0; j < kMaxPass; ++j) {
+            if (grp + j * ngrp < n) {
+                pa[j] = base[o1[j]];
+                pb[j] = base[o2[j]];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kMaxPass; ++j) {
+            const int item = grp + j * ngrp;
+            if (item < n) {
+                const int ci = item >> g.lnb, k = item & (g.nblk - 1);
+                const int pred = (pa[j] + pb[j] + 1) >> 1;
+                const int q = coop_quant(coop_fwd(c.K, sv[j] - pred), c.K.mf, qbits, f);
+                const CoopStat st = coop_cavlc(S.ct, q, c.K.s, S.lvs[grp]);
+                int tok = 0;
+                if (c.K.p == 0 && st.tc)  // coeff_token lengths for the four nC classes
+                    tok = S.ct.tok[0][st.t1][st.tc] | (S.ct.tok[1][st.t1][st.tc] << 5) | (S.ct.tok[2][st.t1][st.tc] << 10) | (6 << 15);
+                const int r = coop_idct(c.K, coop_dequant(q, c.K.ls, F.qp));
+                const int dist = row_sum(iabs(sv[j] - clip255(pred + r)));
+                if (c.K.p == 0) {
+                    S.be_w0[ci][k] = st.tc | (st.t1 << 5) | ((st.sctr + 1) << 8);
+                    S.be_w1[ci][k] = st.rest | (dist << 16);
+                    S.be_w2[ci][k] = tok;
+                    S.be_tcb[k][ci] = (uint8_t)st.tc;
+                }
             }
         }
     }
@@ -658,41 +720,65 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
     HL_PROF_ADD(c, 0, tp0);
     HL_PROF_T(tp1);
     // phase 2: one row per candidate, one lane per block: nC as the reference
-    // sees it at this point of the sequence, coeff_token, candidate sums, cost
+    // sees it at this point of the sequence (residual.c:640-755 with the live
+    // TotalCoeffs of quirk 1), coeff_token, candidate sums, cost.  All LDS
+    // reads are issued up front.
     if (c.tid < (ncand << 4)) {
-        const int wave = c.tid >> 6, ci = c.tid >> 4, k = c.tid & 15;
-        int bits = 0, dist = 0, cs = 0, last = 0;
-        if (k < g.nblk) {
-            const int w0 = S.be_w0[ci][k], w1 = S.be_w1[ci][k];
-            const int tc = w0 & 31, t1 = (w0 >> 5) & 7, sctr = ((w0 >> 8) & 15) - 1;
+        const int wave = c.tid >> 6, ci = c.tid >> 4, k0 = c.tid & 15;
+        const bool valid = k0 < g.nblk;
+        const int k = valid ? k0 : 0;
+        const int hx = k & (g.nbw - 1), hy = k >> g.lbw;
+        const int bx = g.px + (hx << 2), by = g.py + (hy << 2);
+        const int bi = blk_idx(bx, by);
+        const int niA = bx ? blk_idx(bx - 4, by) : 0, niB = by ? blk_idx(bx, by - 4) : 0;
+        const bool inA = bx - 4 >= g.px, inB = by - 4 >= g.py;  // neighbour inside the partition
+        const int kkA = inA ? ((hy << g.lbw) + hx - 1) : 0, kkB = inB ? (((hy - 1) << g.lbw) + hx) : 0;
+        const int w0 = S.be_w0[ci][k], w1 = S.be_w1[ci][k], w2 = S.be_w2[ci][k];
+        const int eA = S.extA[bi], eB = S.extB[bi], cbp = S.cbp_l, tA = S.tc[niA], tB = S.tc[niB];
+        const uint4 rA = *reinterpret_cast<const uint4*>(S.be_tcb[kkA]), rB = *reinterpret_cast<const uint4*>(S.be_tcb[kkB]);
+        const CandSlot cs = S.wc[wave][ci];
+        int bits = 0, dist = 0, cs_sum = 0, last = 0;
+        const int tc = w0 & 31;
+        if (valid) {
             dist = w1 >> 16;
             if (tc) {
-                const int hx = k & (g.nbw - 1), hy = k >> g.lbw;
-                const int bi = blk_idx(g.px + (hx << 2), g.py + (hy << 2));
-                const int nC = nc_luma_of(S, bi, [&](int ni) -> int {
-                    const int nx = blk_x(ni) - g.px, ny = blk_y(ni) - g.py;
-                    if (nx >= 0 && ny >= 0 && nx < g.pw && ny < g.ph) {
-                        const int kk = ((ny >> 2) << g.lbw) + (nx >> 2);
-                        const uint32_t m = nz_mask(S, kk) & ((2u << ci) - 1u);  // candidates 0..ci
-                        if (m) return S.be_tcb[kk][31 - __clz(m)];
-                    }
-                    return S.tc[ni];
-                });
-                bits = (w1 & 0xFFFF) + coop_token_len(S.ct, nC, tc, t1);
-                cs = (1 << bi) | (sctr << 16);
+                const uint32_t allow = (2u << ci) - 1u;  // candidates 0..ci
+                int nA = 0, nB = 0;
+                bool aA = true, aB = true;
+                if (bx == 0) {
+                    aA = eA >= 0;
+                    nA = aA ? eA : 0;
+                }
+                else if (cbp & (1 << (niA >> 2))) {
+                    const int v = inA ? tcb_last(rA, allow) : -1;
+                    nA = v >= 0 ? v : tA;
+                }
+                if (by == 0) {
+                    aB = eB >= 0;
+                    nB = aB ? eB : 0;
+                }
+                else if (cbp & (1 << (niB >> 2))) {
+                    const int v = inB ? tcb_last(rB, allow) : -1;
+                    nB = v >= 0 ? v : tB;
+                }
+                const int nC = (aA && aB) ? (nA + nB + 1) >> 1 : (aA ? nA : (aB ? nB : 0));
+                const int cls = nC < 2 ? 0 : (nC < 4 ? 1 : (nC < 8 ? 2 : 3));
+                const int sctr = ((w0 >> 8) & 15) - 1;
+                bits = (w1 & 0xFFFF) + ((w2 >> (5 * cls)) & 31);
+                cs_sum = (1 << bi) | (sctr << 16);
                 last = ((k + 1) << 4) | sctr;
             }
         }
         bits = row_sum(bits);
         dist = row_sum(dist);
-        cs = row_sum(cs);
+        cs_sum = row_sum(cs_sum);
         last = row_max(last);
-        if (k == 0) {
-            S.cd_cost[ci] = mv_cost(F, dist, bits, S.wcmv[wave][ci][0], S.wcmv[wave][ci][1], pmv);
+        if (k0 == 0) {
+            S.cd_cost[ci] = mv_cost(F, dist, bits, cs.mvx, cs.mvy, pmv);
             S.cd_bits[ci] = bits;
             S.cd_dist[ci] = dist;
-            S.cd_single[ci] = cs >> 16;
-            S.cd_cbp[ci] = cs & 0xFFFF;
+            S.cd_single[ci] = cs_sum >> 16;
+            S.cd_cbp[ci] = cs_sum & 0xFFFF;
             S.cd_last[ci] = last ? (last & 15) : -1;
         }
     }
@@ -702,8 +788,8 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
     // live TotalCoeffsLuma = last writer; the next reader is behind a barrier
     if (c.tid < g.nblk) {
         const int k = c.tid;
-        const uint32_t m = nz_mask(S, k) & ((1u << ncand) - 1u);
-        if (m) S.tc[blk_idx(g.px + ((k & (g.nbw - 1)) << 2), g.py + ((k >> g.lbw) << 2))] = (int8_t)S.be_tcb[k][31 - __clz(m)];
+        const int v = tcb_last(*reinterpret_cast<const uint4*>(S.be_tcb[k]), (1u << ncand) - 1u);
+        if (v >= 0) S.tc[blk_idx(g.px + ((k & (g.nbw - 1)) << 2), g.py + ((k >> g.lbw) << 2))] = (int8_t)v;
     }
 #else
     HL_PROF_T(tp2);
@@ -712,7 +798,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
     for (int t = c.tid; t < n; t += c.nthr) {
         const int ci = t / g.nblk, k = t % g.nblk;
         const int hx = k % g.nbw, hy = k / g.nbw;
-        const int mvx = S.wcmv[0][ci][0], mvy = S.wcmv[0][ci][1];
+        const int mvx = S.wc[0][ci].mvx, mvy = S.wc[0][ci].mvy;
         const int X = clip3(-17, F.W + 17, c.xL + g.px + (mvx >> 2)) + (hx << 2);
         const int Y = clip3(-17, F.H + 17, c.yL + g.py + (mvy >> 2)) + (hy << 2);
         const int bx = g.px + (hx << 2), by = g.py + (hy << 2);
@@ -783,7 +869,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                 last = S.be_sctr[t][k];
             }
         }
-        S.cd_cost[t] = mv_cost(F, dist, bits, S.wcmv[0][t][0], S.wcmv[0][t][1], pmv);
+        S.cd_cost[t] = mv_cost(F, dist, bits, S.wc[0][t].mvx, S.wc[0][t].mvy, pmv);
         S.cd_bits[t] = bits;
         S.cd_dist[t] = dist;
         S.cd_single[t] = single;
@@ -801,11 +887,44 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
     }
 #endif
     HL_PROF_ADD(c, 2, tp2);
+#if defined(__HIP_DEVICE_COMPILE__)
+    {  // last candidate that wrote the counter (vectorised over the step)
+        const int l = c.tid & 15;
+        const int v = l < ncand ? S.cd_last[l] : -1;
+        const unsigned long long bal = __ballot(v >= 0) & 0xFFFFull;
+        if (bal) chain_write(c, __builtin_amdgcn_readlane(v, 63 - __clzll((long long)bal)));
+    }
+#else
     for (int ci = ncand - 1; ci >= 0; --ci)
-        if (uni(S.cd_last[ci]) >= 0) {
-            chain_write(c, uni(S.cd_last[ci]));
+        if (S.cd_last[ci] >= 0) {
+            chain_write(c, S.cd_last[ci]);
             break;
         }
+#endif
+}
+
+// The sequential strict-< scan of one step's candidates (me_ds.c:339-347):
+// index of the first candidate with the smallest cost, and that cost.
+HD int pick_first_min(const Ctx& c, int ncand, double& m)
+{
+    const Shared& S = c.S;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int l = c.tid & 15;
+    const double v = l < ncand ? S.cd_cost[l] : 1.7976931348623157e308;
+    const double mn = row_min_f64(v);
+    const unsigned long long bal = __ballot(l < ncand && v == mn) & 0xFFFFull;
+    m = uni(mn);
+    return uni(__ffsll((long long)bal) - 1);
+#else
+    int bi = 0;
+    m = S.cd_cost[0];
+    for (int ci = 1; ci < ncand; ++ci)
+        if (S.cd_cost[ci] < m) {
+            m = S.cd_cost[ci];
+            bi = ci;
+        }
+    return bi;
+#endif
 }
 
 // Search state of one (sub)partition, uniform across lanes
@@ -848,13 +967,14 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     if (probe) {  // me_ds.c:229-261
         int smv[2];
         skip_mv(S, smv);
-        mvp(S, 0, 0, pmv);
+        const PartShape p16{16, 16, 16, 16, 0};
+        mvp(S, p16, 0, 0, pmv);
         smv[0] = uni(smv[0]);
         smv[1] = uni(smv[1]);
         pmv[0] = uni(pmv[0]);
         pmv[1] = uni(pmv[1]);
         if (pmv[0] == smv[0] && pmv[1] == smv[1]) {
-            put_cand(c, 0, pmv[0], pmv[1]);
+            put_cand(c, g.px, g.py, 0, pmv[0], pmv[1], 0, (c.tid & 63) == 0);
             eval_candidates(c, g, 1, pmv);
             if (uni(S.cd_bits[0]) == 0 || uni(S.cd_single[0]) < 6) {
                 probably = true;
@@ -869,74 +989,108 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     }
     {
         HL_PROF_T(tm);
-        mvp(S, pi, spi, pmv);
+        const PartShape ps{pd.part_w, pd.part_h, pd.sub_w, pd.sub_h, pd.num_part == 4};
+        mvp(S, ps, pi, spi, pmv);
         pmv[0] = uni(pmv[0]);
         pmv[1] = uni(pmv[1]);
         HL_PROF_ADD(c, 4, tm);
     }
     // MVP and (0,0) candidates, me_ds.c:280-300
     const int nc0 = (pmv[0] != 0 || pmv[1] != 0) ? 2 : 1;
-    int cand[9][2];
-    cand[0][0] = pmv[0];
-    cand[0][1] = pmv[1];
-    cand[1][0] = cand[1][1] = 0;
-    put_cand(c, 0, pmv[0], pmv[1]);
-    put_cand(c, 1, 0, 0);
+    put_cand(c, g.px, g.py, 0, pmv[0], pmv[1], 0, (c.tid & 63) == 0);
+    put_cand(c, g.px, g.py, 1, 0, 0, 0, (c.tid & 63) == 0);
     eval_candidates(c, g, nc0, pmv);
-    for (int ci = 0; ci < nc0; ++ci) {
-        const double cost = uni(S.cd_cost[ci]);
-        if (cost < b.cost) {
-            b.cost = cost;
-            b.single = uni(S.cd_single[ci]);
-            b.dist = uni(S.cd_dist[ci]);
-            b.cbp = uni(S.cd_cbp[ci]);
-            b.mv[0] = cand[ci][0];
-            b.mv[1] = cand[ci][1];
+    {
+        double m;
+        const int bi = pick_first_min(c, nc0, m);
+        if (m < b.cost) {
+            b.cost = m;
+            b.single = uni(S.cd_single[bi]);
+            b.dist = uni(S.cd_dist[bi]);
+            b.cbp = uni(S.cd_cbp[bi]);
+            b.mv[0] = bi ? 0 : pmv[0];
+            b.mv[1] = bi ? 0 : pmv[1];
         }
     }
-    // diamond stages, me_ds.c:302-470
-    static constexpr int8_t kInt[9][2] = {{0, 2}, {-1, 1}, {1, 1}, {-2, 0}, {0, 0}, {2, 0}, {-1, -1}, {1, -1}, {0, -2}};
-    static constexpr int8_t kHalf[5][2] = {{0, 1}, {-1, 0}, {0, -1}, {1, 0}, {0, 0}};
-    static constexpr int8_t kQuar[9][2] = {{-1, 1}, {0, 1}, {1, 1}, {-1, 0}, {0, 0}, {1, 0}, {-1, -1}, {0, -1}, {1, -1}};
-    static constexpr int16_t kMaskInt[9] = {~(16 | 64 | 256 | 128), ~(16 | 32 | 256), ~(16 | 2 | 8 | 64 | 256 | 128),
-                                            ~(16 | 4 | 32 | 128),   ~0,                ~(16 | 2 | 8 | 64),
-                                            ~(16 | 1 | 2 | 128 | 32 | 4), ~(16 | 1 | 2 | 8 | 64 | 4), ~(16 | 4 | 1 | 2)};
-    static constexpr int16_t kMaskHalf[5] = {~(16 | 4), ~(16 | 8), ~(16 | 1), ~(16 | 2), ~0};
-    static constexpr int16_t kMaskQuar[9] = {~(16 | 32 | 256 | 128), ~(16 | 8 | 64 | 128 | 256 | 32), ~(16 | 8 | 1 | 2 | 4 | 32),
-                                             ~(16 | 2 | 4 | 32 | 256 | 128), ~0,                      ~(16 | 1 | 2 | 8 | 64 | 128),
-                                             ~(16 | 2 | 4 | 32),             ~(16 | 1 | 2 | 4 | 8 | 32), ~(16 | 1 | 2 | 8)};
+    // diamond stages, me_ds.c:302-470.  The point offsets and visited-point
+    // masks are packed into immediates (3-bit offsets + 2, 9-bit masks).
+    // integer: {0,2},{-1,1},{1,1},{-2,0},{0,0},{2,0},{-1,-1},{1,-1},{0,-2}
+    // half:    {0,1},{-1,0},{0,-1},{1,0},{0,0}
+    // quarter: {-1,1},{0,1},{1,1},{-1,0},{0,0},{1,0},{-1,-1},{0,-1},{1,-1}
+    auto pk3 = [](const int* v, int n) -> uint32_t {
+        uint32_t r = 0;
+        for (int i = 0; i < n; ++i) r |= (uint32_t)(v[i] + 2) << (3 * i);
+        return r;
+    };
+    static constexpr int kIntX[9] = {0, -1, 1, -2, 0, 2, -1, 1, 0}, kIntY[9] = {2, 1, 1, 0, 0, 0, -1, -1, -2};
+    static constexpr int kHalfX[5] = {0, -1, 0, 1, 0}, kHalfY[5] = {1, 0, -1, 0, 0};
+    static constexpr int kQuarX[9] = {-1, 0, 1, -1, 0, 1, -1, 0, 1}, kQuarY[9] = {1, 1, 1, 0, 0, 0, -1, -1, -1};
+    const uint32_t pIntX = pk3(kIntX, 9), pIntY = pk3(kIntY, 9), pHalfX = pk3(kHalfX, 5), pHalfY = pk3(kHalfY, 5);
+    const uint32_t pQuarX = pk3(kQuarX, 9), pQuarY = pk3(kQuarY, 9);
+    // visited-point masks after a move to point i (low 9 bits; bit 4 = centre)
+    auto mask_of = [](int shift, int i) -> int {
+        constexpr uint64_t mi0 = (uint64_t)(0x1FF & ~(16 | 64 | 256 | 128)) | (uint64_t)(0x1FF & ~(16 | 32 | 256)) << 9 |
+                                 (uint64_t)(0x1FF & ~(16 | 2 | 8 | 64 | 256 | 128)) << 18 | (uint64_t)(0x1FF & ~(16 | 4 | 32 | 128)) << 27 |
+                                 (uint64_t)0x1FF << 36 | (uint64_t)(0x1FF & ~(16 | 2 | 8 | 64)) << 45 |
+                                 (uint64_t)(0x1FF & ~(16 | 1 | 2 | 128 | 32 | 4)) << 54;
+        constexpr uint32_t mi1 = (0x1FF & ~(16 | 1 | 2 | 8 | 64 | 4)) | (0x1FF & ~(16 | 4 | 1 | 2)) << 9;
+        constexpr uint64_t mh = (uint64_t)(0x1FF & ~(16 | 4)) | (uint64_t)(0x1FF & ~(16 | 8)) << 9 | (uint64_t)(0x1FF & ~(16 | 1)) << 18 |
+                                (uint64_t)(0x1FF & ~(16 | 2)) << 27 | (uint64_t)0x1FF << 36;
+        constexpr uint64_t mq0 = (uint64_t)(0x1FF & ~(16 | 32 | 256 | 128)) | (uint64_t)(0x1FF & ~(16 | 8 | 64 | 128 | 256 | 32)) << 9 |
+                                 (uint64_t)(0x1FF & ~(16 | 8 | 1 | 2 | 4 | 32)) << 18 | (uint64_t)(0x1FF & ~(16 | 2 | 4 | 32 | 256 | 128)) << 27 |
+                                 (uint64_t)0x1FF << 36 | (uint64_t)(0x1FF & ~(16 | 1 | 2 | 8 | 64 | 128)) << 45 |
+                                 (uint64_t)(0x1FF & ~(16 | 2 | 4 | 32)) << 54;
+        constexpr uint32_t mq1 = (0x1FF & ~(16 | 1 | 2 | 4 | 8 | 32)) | (0x1FF & ~(16 | 1 | 2 | 8)) << 9;
+        uint64_t w;
+        int k = i;
+        if (shift == 1) w = mh;
+        else if (i < 7) w = shift == 2 ? mi0 : mq0;
+        else {
+            w = shift == 2 ? mi1 : mq1;
+            k = i - 7;
+        }
+        return (int)((w >> (9 * k)) & 0x1FF);
+    };
     const int range = c.F.me_range;
     int shift = 2, count = 9, flags = 0xFFFFFF;
     int cx = b.mv[0] >> 2, cy = b.mv[1] >> 2;
     int left = cx - range, right = cx + range, top = cy - range, bottom = cy + range;
-    int idxsel[9];
     for (;;) {
         int ncand = 0;
+        const uint32_t pkx = shift == 2 ? pIntX : (shift == 1 ? pHalfX : pQuarX);
+        const uint32_t pky = shift == 2 ? pIntY : (shift == 1 ? pHalfY : pQuarY);
+#if defined(__HIP_DEVICE_COMPILE__)
+        {  // lane i of every wave checks diamond point i; enabled points are compacted in order
+            const int i = c.tid & 63, ii = min(i, 8);
+            const int mx = cx + (int)((pkx >> (3 * ii)) & 7) - 2, my = cy + (int)((pky >> (3 * ii)) & 7) - 2;
+            const bool en = i < count && ((flags >> i) & 1) && mx >= left && mx <= right && my >= top && my <= bottom;
+            const unsigned long long bal = __ballot(en);
+            ncand = __popcll(bal);
+            if (en) put_cand(c, g.px, g.py, __popcll(bal & ((1ull << i) - 1ull)), mx << shift, my << shift, i, true);
+        }
+#else
         for (int i = 0; i < count; ++i) {
             if (!(flags & (1 << i))) continue;
-            const int dx = shift == 2 ? kInt[i][0] : (shift == 1 ? kHalf[i][0] : kQuar[i][0]);
-            const int dy = shift == 2 ? kInt[i][1] : (shift == 1 ? kHalf[i][1] : kQuar[i][1]);
+            const int dx = (int)((pkx >> (3 * i)) & 7) - 2, dy = (int)((pky >> (3 * i)) & 7) - 2;
             const int mx = cx + dx, my = cy + dy;
             if (mx < left || mx > right || my < top || my > bottom) continue;
-            cand[ncand][0] = mx << shift;
-            cand[ncand][1] = my << shift;
-            put_cand(c, ncand, mx << shift, my << shift);
-            idxsel[ncand++] = i;
+            put_cand(c, g.px, g.py, ncand, mx << shift, my << shift, i, true);
+            ++ncand;
         }
+#endif
         int best = -1;
         if (ncand) {
             eval_candidates(c, g, ncand, pmv);
-            for (int ci = 0; ci < ncand; ++ci) {
-                const double cost = uni(S.cd_cost[ci]);
-                if (cost < b.cost) {
-                    best = idxsel[ci];
-                    b.cost = cost;
-                    b.single = uni(S.cd_single[ci]);
-                    b.dist = uni(S.cd_dist[ci]);
-                    b.cbp = uni(S.cd_cbp[ci]);
-                    b.mv[0] = cand[ci][0];
-                    b.mv[1] = cand[ci][1];
-                }
+            double m;
+            const int bi = pick_first_min(c, ncand, m);
+            if (m < b.cost) {
+                best = uni(S.wc[c.tid >> 6][bi].pad);
+                b.cost = m;
+                b.single = uni(S.cd_single[bi]);
+                b.dist = uni(S.cd_dist[bi]);
+                b.cbp = uni(S.cd_cbp[bi]);
+                b.mv[0] = uni((int)S.wc[c.tid >> 6][bi].mvx);
+                b.mv[1] = uni((int)S.wc[c.tid >> 6][bi].mvy);
             }
         }
         flags = 0xFFFFFF;
@@ -958,7 +1112,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         else {
             cx = b.mv[0] >> shift;
             cy = b.mv[1] >> shift;
-            flags &= shift == 2 ? kMaskInt[best] : (shift == 1 ? kMaskHalf[best] : kMaskQuar[best]);
+            flags &= mask_of(shift, best) | ~0x1FF;
             continue;
         }
         left = cx - range;
@@ -997,7 +1151,7 @@ HD int intra_sample(const Shared& S, int x, int y)
 
 HD void i4_neighbours(const Shared& S, int blk, int p[13])
 {
-    const int xO = kBlkX[blk], yO = kBlkY[blk];
+    const int xO = blk_x(blk), yO = blk_y(blk);
     for (int i = 0; i < 13; ++i) {
         const int X = i < 5 ? -1 : i - 5, Y = i < 5 ? i - 1 : -1;
         const int x = xO + X, y = yO + Y;
@@ -1469,7 +1623,7 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp)
         HL_SYNC();
         // blocks: transform, quant, AC stats
         for (int t = c.tid; t < 16; t += c.nthr) {
-            const int xO = kBlkX[t], yO = kBlkY[t];
+            const int xO = blk_x(t), yO = blk_y(t);
             int res[16], w[16], q[16];
             for (int i = 0; i < 16; ++i) {
                 const int o = (yO + (i >> 2)) * 16 + xO + (i & 3);
@@ -1549,7 +1703,7 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp)
                     dcY[i] = F.qp >= 36 ? (f[i] * scale) << (q6 - 6) : (f[i] * scale + (1 << (5 - q6))) >> (6 - q6);
             }
             for (int t = c.tid; t < 16; t += c.nthr) {
-                const int xO = kBlkX[t], yO = kBlkY[t];
+                const int xO = blk_x(t), yO = blk_y(t);
                 int list[16], m[16], r[16];
                 list[0] = dcY[kDcPos[t]];
                 bool nzl = list[0] != 0;
@@ -1574,7 +1728,7 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp)
         else {
             for (int i = 0; i < 16; ++i) dcl[i] = 0;
             for (int t = c.tid; t < 16; t += c.nthr) {
-                const int xO = kBlkX[t], yO = kBlkY[t];
+                const int xO = blk_x(t), yO = blk_y(t);
                 int d = 0;
                 for (int i = 0; i < 16; ++i) {
                     const int o = (yO + (i >> 2)) * 16 + xO + (i & 3);
@@ -1661,28 +1815,35 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4)
             if (c.K.p == 0) S.i4_cost_ok[m] = ok;
         }
         HL_SYNC();
-        // uniform resolution in mode order (rdo.c:1931-2014)
-        double dmin = 1.7976931348623157e308;
-        int best = 2, lastw = -1;
-        bool best_zero = false;
-        for (int m = 0; m < 9; ++m) {
-            if (!uni(S.i4_cost_ok[m])) continue;
-            if (uni(S.i4_exact[m])) {
+        // resolution in mode order (rdo.c:1931-2014), vectorised: the scan
+        // stops at the first exact mode; before it, the last coded mode
+        // writes the counter and the first strict minimum wins
+        double dmin;
+        int best, lastw;
+        bool best_zero;
+        {
+            const int l = c.tid & 15;
+            const bool ok = l < 9 && S.i4_cost_ok[l];
+            const bool ex = ok && S.i4_exact[l], nz = ok && S.i4_nz[l];
+            const unsigned E = (unsigned)(__ballot(ex) & 0xFFFFull);
+            const int limit = E ? __ffs(E) - 1 : 9;
+            const unsigned W = (unsigned)(__ballot(nz) & 0xFFFFull) & ((1u << limit) - 1u);
+            lastw = W ? 31 - __clz(W) : -1;
+            const int sct = l < 9 ? S.i4_sctr[l] : 0;
+            if (lastw >= 0) chain_write(c, __builtin_amdgcn_readlane(sct, lastw));
+            if (E) {
                 dmin = 0.0;
-                best = m;
+                best = limit;
                 best_zero = true;
-                break;
             }
-            const int nz = uni(S.i4_nz[m]);
-            if (nz) lastw = m;
-            const double cm = uni(S.i4_cost[m]);
-            if (cm < dmin) {
-                dmin = cm;
-                best = m;
-                best_zero = !nz;
+            else {
+                const double v = ok ? S.i4_cost[l] : 1.7976931348623157e308;
+                const double mn = row_min_f64(v);
+                dmin = uni(mn);
+                best = __ffs((unsigned)(__ballot(ok && v == mn) & 0xFFFFull)) - 1;
+                best_zero = !((W >> best) & 1);
             }
         }
-        if (lastw >= 0) chain_write(c, uni(S.i4_sctr[lastw]));
         best_cost = dadd(best_cost, dmin);
         if (!best_zero) cbp4 |= 1 << blk;
         if (c.tid < 16) {
@@ -1697,7 +1858,7 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4)
     }
 #else
     for (int blk = 0; blk < 16; ++blk) {
-        const int xO = kBlkX[blk], yO = kBlkY[blk];
+        const int xO = blk_x(blk), yO = blk_y(blk);
         int p[13];
         i4_neighbours(S, blk, p);
         // nC is the same for all nine modes: they only rewrite this block
@@ -1798,7 +1959,7 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4)
 HD void pred_modes_4x4(Shared& S)  // pred_intra.c:541-615 (lane 0)
 {
     for (int blk = 0; blk < 16; ++blk) {
-        const int bx = kBlkX[blk], by = kBlkY[blk];
+        const int bx = blk_x(blk), by = blk_y(blk);
         int mA, mB;
         bool aA, aB;
         int pmA, pmB, iA, iB;
@@ -1914,7 +2075,7 @@ HD void inter_pred_mb(Ctx& c, bool chroma_only_16x16, bool luma)
     Shared& S = c.S;
     if (luma) {
         for (int t = c.tid; t < 16; t += c.nthr) {
-            const int bx = kBlkX[t], by = kBlkY[t];
+            const int bx = blk_x(t), by = blk_y(t);
             int pi, spi;
             part_of(S, bx, by, pi, spi);
             const NbInfo& n = S.nb[0];
@@ -1956,7 +2117,7 @@ HD void reconstruct_inter_luma(Ctx& c, int single_luma)
     const FrameArgs& F = c.F;
     Shared& S = c.S;
     for (int t = c.tid; t < 16; t += c.nthr) {
-        const int xO = kBlkX[t], yO = kBlkY[t];
+        const int xO = blk_x(t), yO = blk_y(t);
         int res[16], pred[16];
         bool zero = true;
         for (int i = 0; i < 16; ++i) {
@@ -2002,20 +2163,20 @@ HD void guess_inter(Ctx& c)
 {
     const FrameArgs& F = c.F;
     Shared& S = c.S;
-    static constexpr int kFamFirst[5] = {0, 1, 2, 3, 7};
-    static constexpr int32_t kFamType[4] = {ET_P16x16, ET_P16x8, ET_P8x16, ET_P8x8REF0};
+    auto fam_first = [](int f) -> int { return f < 4 ? f : 7; };  // {0, 1, 2, 3, 7}
+    auto fam_type = [](int f) -> int32_t { return f < 3 ? ET_P16x16 + f : ET_P8x8REF0; };
     double best_cost = 1.7976931348623157e308;
     int best_single = 9, best_part = -1, best_fam = -1;
     bool best_found = false, pskip = false;
     if (c.tid == 0) S.flags = FL_INTER;
     for (int fam = 0; fam < 4 && !best_found; ++fam) {
         bool probably = false;
-        for (int j = kFamFirst[fam]; j < kFamFirst[fam + 1]; ++j) {
+        for (int j = fam_first(fam); j < fam_first(fam + 1); ++j) {
             const PartDef& pd = kParts[j];
             HL_SYNC();
             if (c.tid == 0) {
-                S.e_type = kFamType[fam];
-                S.nb[0].e_type = kFamType[fam];
+                S.e_type = fam_type(fam);
+                S.nb[0].e_type = fam_type(fam);
                 S.nb[0].part_w = pd.part_w;
                 S.nb[0].part_h = pd.part_h;
                 for (int i = 0; i < 4; ++i) {
@@ -2090,7 +2251,7 @@ HD void guess_inter(Ctx& c)
     if (c.tid == 0) {
         S.flags = FL_INTER;
         S.pm0 = PM_L0;
-        S.e_type = kFamType[best_fam];
+        S.e_type = fam_type(best_fam);
         S.mb_type = S.e_type - 301;
         S.num_part = bp.num_part;
         S.nb[0].intra = 0;
