@@ -31,6 +31,8 @@ EXPORTED_SYMBOLS = (
     "hl_amd_encoder_destroy",
     "hl_amd_encode",
     "hl_amd_encode_device",
+    "hl_amd_encode_batch",
+    "hl_amd_set_pipeline",
     "hl_amd_get_recon",
     "hl_amd_set_timing",
     "hl_amd_get_timing",
@@ -86,6 +88,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     for f in (lib.hl_amd_encode, lib.hl_amd_encode_device):
         f.argtypes = [vp, vp, vp, vp, ctypes.POINTER(_Result)]
         f.restype = i32
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    lib.hl_amd_encode_batch.argtypes = [vp, i32, pp, pp, pp, ctypes.POINTER(_Result)]
+    lib.hl_amd_encode_batch.restype = i32
+    lib.hl_amd_set_pipeline.argtypes = [vp, i32, i32, i32]
+    lib.hl_amd_set_pipeline.restype = i32
     lib.hl_amd_get_recon.argtypes = [vp, vp, vp, vp]
     lib.hl_amd_get_recon.restype = i32
     lib.hl_amd_set_timing.argtypes = [vp, i32]
@@ -170,6 +177,24 @@ class Encoder:
         if rc != HL_AMD_SUCCESS:
             raise HlAmdError(rc, "hl_amd_encode_device")
         return self._result(r) if collect else r.data_size
+
+    def encode_batch_device(self, ptrs, collect: bool = True):
+        """Encodes consecutive frames already resident in device memory;
+        ptrs = [(y_ptr, u_ptr, v_ptr), ...].  Runs of P pictures are
+        frame-pipelined (hl_amd_encode_batch); returns one result per frame
+        (or, with collect=False, the total bitstream bytes)."""
+        n = len(ptrs)
+        arr = [(ctypes.c_void_p * n)(*[p[i] for p in ptrs]) for i in range(3)]
+        res = (_Result * n)()
+        rc = self.lib.hl_amd_encode_batch(self._h, n, arr[0], arr[1], arr[2], res)
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_encode_batch")
+        return [self._result(r) for r in res] if collect else sum(r.data_size for r in res)
+
+    def set_pipeline(self, slots: int, wg_per_slot: int, reach: int):
+        rc = self.lib.hl_amd_set_pipeline(self._h, slots, wg_per_slot, reach)
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_set_pipeline")
 
     def recon(self):
         import numpy as np

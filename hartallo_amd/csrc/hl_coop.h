@@ -208,12 +208,19 @@ __device__ __forceinline__ int rb_len(int zl, int run)
     return (w >> (2 * run)) & 3;
 }
 
+// level_prefix + level_suffix length (level_code_len of hl_prims.h), branch-free
 __device__ __forceinline__ int level_len(int sl, int lc)
 {
-    if (sl == 0) return lc < 14 ? lc + 1 : (lc < 30 ? 19 : (lc <= 4126 ? 28 : 1));
-    if (lc < (14 << sl)) return (lc >> sl) + 1 + sl;
-    if (lc < (15 << sl)) return 15 + sl;
-    return lc <= (15 << sl) + 4096 ? 28 : 1;
+    const int l0 = lc < 14 ? lc + 1 : (lc < 30 ? 19 : (lc <= 4126 ? 28 : 1));
+    const int l1 = lc < (14 << sl) ? (lc >> sl) + 1 + sl : (lc < (15 << sl) ? 15 + sl : (lc <= (15 << sl) + 4096 ? 28 : 1));
+    return sl == 0 ? l0 : l1;
+}
+// suffixLength update after a level of magnitude a (residual.c:813-858)
+__device__ __forceinline__ int next_sl(int sl, int a)
+{
+    const int s1 = sl == 0 ? 1 : sl;
+    const int thr = s1 < 6 ? 3 << (s1 - 1) : 32768;
+    return s1 + (a > thr ? 1 : 0);
 }
 
 struct CoopStat {
@@ -223,8 +230,7 @@ struct CoopStat {
 // CAVLC statistics of the row's block (cavlc_stat with maxNumCoef 16,
 // endIdx 15).  L = this lane's level, li = its list index (scan index, or
 // scan index - 1 for AC blocks; -1 = not part of the list).  lvs = 16 words
-// of LDS scratch owned by this row.  Also returns this lane's run_before bits
-// through the row reduction, so every lane of the row gets the same result.
+// of LDS scratch owned by this row (16-byte aligned).
 __device__ __forceinline__ CoopStat coop_cavlc(const CoopTables& T, int L, int li, int* lvs)
 {
     const int aL = L < 0 ? -L : L;
@@ -232,49 +238,50 @@ __device__ __forceinline__ CoopStat coop_cavlc(const CoopTables& T, int L, int l
     const uint32_t masks = (uint32_t)row_or(nzl ? (int)((1u << li) | ((uint32_t)(aL == 1) << (li + 16))) : 0);
     const uint32_t nz = masks & 0xFFFFu, ones = masks >> 16;
     CoopStat st;
-    st.tc = __popc(nz);
-    st.t1 = 0;
-    st.rest = 0;
-    st.sctr = -1;
-    if (st.tc == 0) return st;  // uniform over the row
-    const int hi = 31 - __clz(nz);
+    const int tc = __popc(nz);
+    const int hi = 31 - __clz(nz | 1u);
     const uint32_t big = nz & ~ones;
     const int hb = big ? 31 - __clz(big) : -1;
-    const int t1 = min(3, __popc(nz >> (hb + 1)));
-    const int tc = st.tc;
-    // this lane's order from the top, run_before and level slot
-    int rb = 0;
-    if (nzl) {
-        const int j = __popc(nz >> (li + 1));
-        const uint32_t lower = nz & ((1u << li) - 1u);
-        const int zl = li - __popc(lower);
-        const int run = lower ? li - 1 - (31 - __clz(lower)) : li;
-        if (j < tc - 1 && zl > 0) rb = rb_len(zl, run);
-        const int m = j - t1;
-        if (m >= 0) {
-            int lc = L > 0 ? (L << 1) - 2 : -(L << 1) - 1;
-            if (m == 0 && t1 < 3 && lc >= 2) lc -= 2;
-            lvs[m] = (lc << 16) | aL;
+    const int t1a = __popc(nz >> (hb + 1));
+    const int t1 = t1a < 3 ? t1a : 3;
+    // total_zeros length (issued early: independent of the level chain)
+    const int tzb = (tc > 0 && tc < 16) ? T.tz[tc - 1][hi + 1 - tc] : 0;
+    // this lane's order from the top, run_before and level code
+    const int lis = li < 0 ? 0 : li;
+    const int j = __popc(nz >> (lis + 1));
+    const uint32_t lower = nz & ((1u << lis) - 1u);
+    const int zl = lis - __popc(lower);
+    const int run = lower ? lis - 1 - (31 - __clz(lower)) : lis;
+    const int rb = (nzl && j < tc - 1 && zl > 0) ? rb_len(zl, run) : 0;
+    const int m = j - t1;
+    int lc = L > 0 ? (L << 1) - 2 : -(L << 1) - 1;
+    lc -= (m == 0 && t1 < 3 && lc >= 2) ? 2 : 0;
+    const bool lvl = nzl && m >= 0;  // a level coded with level_prefix/suffix
+    const int sl0 = (tc > 10 && t1 < 3) ? 1 : 0;
+    // Fast path: no level above 3 in magnitude.  suffixLength is then sl0 for
+    // the first level and 1 for every later one (it only grows past 1 for
+    // |level| > 3), so every length is known without the chain:
+    // suffixLength 0: lc + 1 (lc < 14), 1: (lc >> 1) + 2 (lc < 28).
+    const int row_in_wave = (__lane_id() >> 4) & 3;
+    const bool slow = ((__ballot(lvl && aL > 3) >> (16 * row_in_wave)) & 0xFFFFull) != 0;  // uniform per row
+    const int len = (lvl && !slow) ? ((m == 0 && sl0 == 0) ? lc + 1 : (lc >> 1) + 2) : 0;
+    int bits = t1 + tzb + row_sum(rb + len);
+    if (slow) {
+        if (lvl) lvs[m] = (lc << 16) | aL;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        int sl = sl0;
+        for (int k = 0; k < tc - t1; ++k) {
+            const int v = lvs[k];
+            bits += level_len(sl, v >> 16);
+            sl = next_sl(sl, v & 0xFFFF);
         }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    int bits = t1 + row_sum(rb);
-    int sl = (tc > 10 && t1 < 3) ? 1 : 0;
-    for (int m = 0; m < tc - t1; ++m) {
-        const int v = lvs[m];
-        const int lc = v >> 16, a = v & 0xFFFF;
-        bits += level_len(sl, lc);
-        if (sl == 0) sl = 1;
-        const int thr = sl == 1 ? 3 : (sl == 2 ? 6 : (sl == 3 ? 12 : (sl == 4 ? 24 : (sl == 5 ? 48 : 32768))));
-        if (a > thr) ++sl;
-    }
-    if (tc < 16) bits += T.tz[tc - 1][hi + 1 - tc];
-    st.t1 = t1;
-    st.rest = bits;
-    st.sctr = 9;
-    if (tc == 1 && ones == nz) st.sctr = hi == 0 ? 3 : (hi < 3 ? 2 : (hi < 6 ? 1 : 0));
+    st.tc = tc;
+    st.t1 = tc ? t1 : 0;
+    st.rest = tc ? bits : 0;
+    st.sctr = tc == 0 ? -1 : ((tc == 1 && ones == nz) ? (hi == 0 ? 3 : (hi < 3 ? 2 : (hi < 6 ? 1 : 0))) : 9);
     return st;
 }
 

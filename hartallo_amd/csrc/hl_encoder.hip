@@ -17,7 +17,7 @@
 #include <vector>
 
 #include "../../include/hartallo_amd.h"
-#include "hl_filters.h"
+#include "hl_pipeline.h"
 #include "hl_writer.h"
 
 using namespace hl;
@@ -80,6 +80,69 @@ __global__ __launch_bounds__(64) void k_deblock_diag(DeblockArgs D, int mbh, int
     }
 }
 
+// Pipelined run of P pictures (hl_pipeline.h): persistent workgroups, slot
+// = blockIdx % slots, tasks taken in wavefront order picture by picture.
+__global__ __launch_bounds__(kMbThreads) void k_pipeline(PipeArgs P, int mbw, int mbh)
+{
+    __shared__ Shared S;
+    __shared__ int32_t s_task;
+    const int tid = threadIdx.x, nmb = mbw * mbh;
+    const int slot = blockIdx.x % P.slots;
+    int32_t* own = P.done + slot * nmb;
+    for (;;) {
+        if (tid == 0) s_task = atomicAdd(&P.next[slot], 1);
+        __syncthreads();
+        const int t = __builtin_amdgcn_readfirstlane(s_task);
+        const int f = slot + P.slots * (t / nmb);
+        if (f >= P.nframes) break;
+        const PipeFrame& PF = P.fr[f];
+        const int addr = P.order[t % nmb];
+        const int x = addr % mbw, y = addr / mbw;
+        int gx = 1 << 20, gy = 1 << 20;
+        if (f > 0) {
+            gx = min(x + P.reach, mbw - 1);
+            gy = min(y + P.reach, mbh - 1);
+        }
+        // wait for the wavefront neighbours and the reference region
+        if (tid == 0) {
+            if (x > 0) spin_ge(own + addr - 1, f + 1, P.err);
+            if (y > 0) spin_ge(own + addr - mbw + (x + 1 < mbw ? 1 : 0), f + 1, P.err);
+            if (f > 0)
+                spin_ge(P.done + ((f - 1) % P.slots) * nmb + min(y + P.reach + 2, mbh - 1) * mbw + min(x + P.reach + 3, mbw - 1), f,
+                        P.err);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const int s_in = x == 0 ? PF.F.spec[y] : PF.F.chain[addr - 1].s_out;
+        encode_mb(PF.F, S, addr, tid, kMbThreads, s_in, gx, gy);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // deblocking, then quarter-pel planes, this decision completed
+        int blk[kMaxTaskBlocks][2];
+        const int nd = PF.deblock ? task_blocks(0, x, y, mbw, mbh, blk) : 0;
+        for (int i = 0; i < nd; ++i) {
+            const int a = blk[i][1] * mbw + blk[i][0];
+            for (int step = 0; step < 8; ++step) {
+                if (tid < 32) deblock_mb_step(PF.D, a, step, tid);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+            }
+        }
+        const int np = task_blocks(1, x, y, mbw, mbh, blk);
+        for (int i = 0; i < np; ++i)
+            plane_block(PF.F.cur[0], PF.F.W, PF.F.H, mbw, mbh, PF.pl_out, PF.F.pstride, PF.F.plsz, blk[i][0], blk[i][1], tid, kMbThreads);
+        // publish (Guideline 16: every wave drained, barrier, release, flag)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            st_relaxed(own + addr, f + 1);
+        }
+    }
+}
+
 static int diag_count(int mbw, int rows, int diag)
 {
     const int ylo = std::max(0, (diag - mbw + 2) / 2);
@@ -113,6 +176,15 @@ struct hl_amd_encoder_s {
     float ms[4];
     int32_t mb_launches;
     unsigned long long* d_prof;  // phase counters (HL_PROFILE builds)
+    // pipelined runs of P pictures (hl_pipeline.h)
+    int slots, wg_per_slot, reach;  // 4 x 60 workgroups, R = 2 MBs by default
+    int bcap;                       // pictures the run buffers hold
+    uint8_t *d_bpic, *d_bpl;        // per picture: recon (Y|U|V), quarter-pel planes
+    MbRecord *d_brec, *h_brec;
+    MbChain *d_bchain, *h_bchain;
+    int32_t *d_bspec, *d_done, *d_next, *d_err, *d_order;
+    PipeFrame *d_pf, *h_pf;
+    std::vector<std::vector<uint8_t>> bout;  // bitstreams of the last hl_amd_encode_batch
 };
 
 static void free_all(hl_amd_encoder_t* e)
@@ -129,6 +201,19 @@ static void free_all(hl_amd_encoder_t* e)
     (void)hipFree(e->d_chain);
     (void)hipFree(e->d_spec);
     (void)hipFree(e->d_prof);
+    (void)hipFree(e->d_bpic);
+    (void)hipFree(e->d_bpl);
+    (void)hipFree(e->d_brec);
+    (void)hipFree(e->d_bchain);
+    (void)hipFree(e->d_bspec);
+    (void)hipFree(e->d_done);
+    (void)hipFree(e->d_next);
+    (void)hipFree(e->d_err);
+    (void)hipFree(e->d_order);
+    (void)hipFree(e->d_pf);
+    (void)hipHostFree(e->h_brec);
+    (void)hipHostFree(e->h_bchain);
+    (void)hipHostFree(e->h_pf);
     (void)hipHostFree(e->h_rec);
     (void)hipHostFree(e->h_chain);
     (void)hipHostFree(e->h_spec);
@@ -175,8 +260,9 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
          hipHostMalloc(&e->h_spec, sizeof(int32_t) * e->mbh, hipHostMallocDefault) == hipSuccess;
     ok = ok && hipMemset(e->d_st, 0, sizeof(MbState) * e->nmb) == hipSuccess;
 #if defined(HL_PROFILE)
-    ok = ok && hipMalloc(&e->d_prof, 64 * sizeof(unsigned long long)) == hipSuccess &&
-         hipMemset(e->d_prof, 0, 64 * sizeof(unsigned long long)) == hipSuccess;
+    // 64 phase counters, then the cycles of every macroblock of the last frame
+    ok = ok && hipMalloc(&e->d_prof, (64 + e->nmb) * sizeof(unsigned long long)) == hipSuccess &&
+         hipMemset(e->d_prof, 0, (64 + e->nmb) * sizeof(unsigned long long)) == hipSuccess;
 #endif
     for (int i = 0; i < 6 && ok; ++i) ok = hipEventCreate(&e->ev[i]) == hipSuccess;
     if (!ok) {
@@ -184,6 +270,9 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
         delete e;
         return HL_AMD_ERROR_OUTOFMEMMORY;
     }
+    e->slots = 4;
+    e->wg_per_slot = 60;
+    e->reach = 2;
     const StreamParams sp{e->W, e->H, p->qp, p->deblock};
     e->scratch.resize(slice_scratch_bytes(sp));
     e->out.resize(slice_scratch_bytes(sp) + 64);
@@ -245,7 +334,7 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
     if (intra) e->gop_left = e->p.gop_size;
     uint8_t** cur = e->d_pic[e->cur];
     uint8_t** ref = e->d_pic[e->cur ^ 1];
-    FrameArgs F;
+    FrameArgs F{};  // ref_done = null: the per-picture path needs no reference waits
     F.W = e->W;
     F.H = e->H;
     F.Wc = e->Wc;
@@ -352,6 +441,262 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
     return HL_AMD_SUCCESS;
 }
 
+// ---------------------------------------------------------------------------
+// pipelined runs of P pictures
+// ---------------------------------------------------------------------------
+static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
+{
+    if (n <= e->bcap) return hipSuccess;
+    const size_t pic = (size_t)e->W * e->H * 3 / 2, nmb = e->nmb;
+    (void)hipFree(e->d_bpic);
+    (void)hipFree(e->d_bpl);
+    (void)hipFree(e->d_brec);
+    (void)hipFree(e->d_bchain);
+    (void)hipFree(e->d_bspec);
+    (void)hipFree(e->d_pf);
+    (void)hipHostFree(e->h_brec);
+    (void)hipHostFree(e->h_bchain);
+    (void)hipHostFree(e->h_pf);
+    e->bcap = 0;
+    hipError_t r;
+    if ((r = hipMalloc(&e->d_bpic, pic * n)) || (r = hipMalloc(&e->d_bpl, 4 * e->plsz * n)) ||
+        (r = hipMalloc(&e->d_brec, sizeof(MbRecord) * nmb * n)) || (r = hipMalloc(&e->d_bchain, sizeof(MbChain) * nmb * n)) ||
+        (r = hipMalloc(&e->d_bspec, sizeof(int32_t) * e->mbh * n)) || (r = hipMalloc(&e->d_pf, sizeof(PipeFrame) * n)) ||
+        (r = hipHostMalloc(&e->h_brec, sizeof(MbRecord) * nmb * n, hipHostMallocDefault)) ||
+        (r = hipHostMalloc(&e->h_bchain, sizeof(MbChain) * nmb * n, hipHostMallocDefault)) ||
+        (r = hipHostMalloc(&e->h_pf, sizeof(PipeFrame) * n, hipHostMallocDefault)))
+        return r;
+    if (!e->d_done) {
+        if ((r = hipMalloc(&e->d_done, sizeof(int32_t) * nmb * 16)) || (r = hipMalloc(&e->d_next, sizeof(int32_t) * 16)) ||
+            (r = hipMalloc(&e->d_err, sizeof(int32_t) * 4)) || (r = hipMalloc(&e->d_order, sizeof(int32_t) * nmb)))
+            return r;
+        std::vector<int32_t> order;  // wavefront order: anti-diagonals d = x + 2y, top to bottom
+        for (int d = 0; d < e->mbw + 2 * e->mbh; ++d)
+            for (int y = 0; y < e->mbh; ++y) {
+                const int x = d - 2 * y;
+                if (x >= 0 && x < e->mbw) order.push_back(y * e->mbw + x);
+            }
+        if ((r = hipMemcpy(e->d_order, order.data(), sizeof(int32_t) * nmb, hipMemcpyHostToDevice))) return r;
+    }
+    std::vector<int32_t> spec((size_t)e->mbh * n, 9);  // speculated rdo.Single_ctr at every row start
+    if ((r = hipMemcpy(e->d_bspec, spec.data(), sizeof(int32_t) * spec.size(), hipMemcpyHostToDevice))) return r;
+    e->bcap = n;
+    return hipSuccess;
+}
+
+// Exact rdo.Single_ctr walk of one picture whose row starts were speculated
+// as `spec`; false when a macroblock read a mispredicted value.
+static bool validate_rows(const MbChain* ch, int mbw, int mbh, int spec, int32_t& carry)
+{
+    for (int y = 0; y < mbh; ++y) {
+        const MbChain* row = ch + (size_t)y * mbw;
+        if (spec != carry)
+            for (int x = 0; x < mbw; ++x) {
+                if (row[x].dep) return false;
+                if (row[x].fresh) break;
+            }
+        bool any_fresh = false;
+        for (int x = 0; x < mbw && !any_fresh; ++x) any_fresh = row[x].fresh != 0;
+        if (any_fresh) carry = row[mbw - 1].s_out;
+    }
+    return true;
+}
+
+static FrameArgs frame_args(hl_amd_encoder_t* e, bool intra)
+{
+    FrameArgs F{};
+    F.W = e->W;
+    F.H = e->H;
+    F.Wc = e->Wc;
+    F.Hc = e->Hc;
+    F.mbw = e->mbw;
+    F.mbh = e->mbh;
+    F.qp = e->p.qp;
+    F.qpc = e->qpc;
+    F.is_intra = intra;
+    F.me_range = std::min(64, std::max(1, e->p.me_range));
+    F.lambda = 0.852 * (double)(1 << ((e->p.qp - 12) / 3));
+    F.pstride = e->pstride;
+    F.plsz = (int32_t)e->plsz;
+    F.st = e->d_st;
+    F.prof = e->d_prof;
+    return F;
+}
+
+static void store_result(hl_amd_encoder_t* e, int i, const hl_amd_result_t& src, hl_amd_result_t* dst)
+{
+    e->bout[i].assign((const uint8_t*)src.data, (const uint8_t*)src.data + src.data_size);
+    *dst = src;
+    dst->data = e->bout[i].data();
+}
+
+// m consecutive P pictures in one pipelined launch; falls back to the
+// per-picture path when a row-start speculation turns out to matter.
+static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, const uint8_t* const* U, const uint8_t* const* V,
+                          hl_amd_result_t* res, int base)
+{
+    HL_HIP_CHECK(ensure_batch(e, m));
+    const size_t pic = (size_t)e->W * e->H * 3 / 2, nmb = e->nmb;
+    uint8_t** ref0 = e->d_pic[e->cur ^ 1];
+    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[0], e->stream));
+    {  // quarter-pel planes of the picture before the run
+        dim3 grid((e->W + 2 * kPad + 63) / 64, (e->H + 2 * kPad + 3) / 4);
+        k_planes<<<grid, 256, 0, e->stream>>>(ref0[0], e->W, e->H, e->d_pl[0], e->d_pl[1], e->d_pl[2], e->d_pl[3], e->pstride);
+        HL_HIP_CHECK(hipGetLastError());
+    }
+    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[1], e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(e->d_snap, e->d_st, sizeof(MbState) * nmb, hipMemcpyDeviceToDevice, e->stream));
+    HL_HIP_CHECK(hipStreamSynchronize(e->stream));  // h_pf may still be read by a previous copy
+    for (int k = 0; k < m; ++k) {
+        PipeFrame& pf = e->h_pf[k];
+        pf = PipeFrame{};
+        FrameArgs& F = pf.F;
+        F = frame_args(e, false);
+        uint8_t* cur = e->d_bpic + pic * k;
+        F.src[0] = Y[k];
+        F.src[1] = U[k];
+        F.src[2] = V[k];
+        F.cur[0] = cur;
+        F.cur[1] = cur + (size_t)e->W * e->H;
+        F.cur[2] = cur + (size_t)e->W * e->H * 5 / 4;
+        if (k == 0)
+            for (int c = 0; c < 3; ++c) F.ref[c] = ref0[c];
+        else {
+            const uint8_t* rp = e->d_bpic + pic * (k - 1);
+            F.ref[0] = rp;
+            F.ref[1] = rp + (size_t)e->W * e->H;
+            F.ref[2] = rp + (size_t)e->W * e->H * 5 / 4;
+        }
+        const uint8_t* plb = k == 0 ? e->d_pl[0] : e->d_bpl + 4 * e->plsz * (k - 1);
+        for (int i = 0; i < 4; ++i) F.pl[i] = plb + i * e->plsz;
+        F.rec = e->d_brec + nmb * k;
+        F.chain = e->d_bchain + nmb * k;
+        F.spec = e->d_bspec + e->mbh * k;
+        F.ref_done = k == 0 ? nullptr : e->d_done + ((k - 1) % e->slots) * nmb;
+        F.ref_epoch = k;
+        F.perr = e->d_err;
+        pf.D.W = e->W;
+        pf.D.H = e->H;
+        pf.D.Wc = e->Wc;
+        pf.D.mbw = e->mbw;
+        pf.D.qp = e->p.qp;
+        pf.D.qpc = e->qpc;
+        for (int c = 0; c < 3; ++c) pf.D.pic[c] = F.cur[c];
+        pf.D.st = e->d_st;
+        pf.pl_out = e->d_bpl + 4 * e->plsz * k;
+        pf.deblock = e->p.deblock;
+    }
+    HL_HIP_CHECK(hipMemcpyAsync(e->d_pf, e->h_pf, sizeof(PipeFrame) * m, hipMemcpyHostToDevice, e->stream));
+    HL_HIP_CHECK(hipMemsetAsync(e->d_done, 0, sizeof(int32_t) * nmb * e->slots, e->stream));
+    HL_HIP_CHECK(hipMemsetAsync(e->d_next, 0, sizeof(int32_t) * 16, e->stream));
+    HL_HIP_CHECK(hipMemsetAsync(e->d_err, 0, sizeof(int32_t) * 4, e->stream));
+    PipeArgs P;
+    P.fr = e->d_pf;
+    P.nframes = m;
+    P.slots = e->slots;
+    P.order = e->d_order;
+    P.done = e->d_done;
+    P.next = e->d_next;
+    P.err = e->d_err;
+    P.reach = e->reach;
+    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[4], e->stream));
+    k_pipeline<<<e->slots * e->wg_per_slot, kMbThreads, 0, e->stream>>>(P, e->mbw, e->mbh);
+    HL_HIP_CHECK(hipGetLastError());
+    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[5], e->stream));
+    int32_t err = 0;
+    HL_HIP_CHECK(hipMemcpyAsync(e->h_bchain, e->d_bchain, sizeof(MbChain) * nmb * m, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(e->h_brec, e->d_brec, sizeof(MbRecord) * nmb * m, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(&err, e->d_err, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipStreamSynchronize(e->stream));
+    if (e->timing) {
+        (void)hipEventElapsedTime(&e->ms[0], e->ev[0], e->ev[1]);
+        (void)hipEventElapsedTime(&e->ms[1], e->ev[4], e->ev[5]);
+        e->ms[2] = 0.f;
+        (void)hipEventElapsedTime(&e->ms[3], e->ev[0], e->ev[5]);
+    }
+    e->mb_launches = 1;
+    e->reruns = 0;
+    if (err) {
+        fprintf(stderr, "hartallo_amd: pipelined run: %d bounded waits gave up\n", err);
+        return HL_AMD_ERROR_SYSTEM;
+    }
+    int32_t carry = e->chain_end;
+    bool ok = true;
+    for (int k = 0; k < m && ok; ++k) ok = validate_rows(e->h_bchain + nmb * k, e->mbw, e->mbh, 9, carry);
+    if (!ok) {  // a speculated row start mattered: redo the run picture by picture
+        HL_HIP_CHECK(hipMemcpyAsync(e->d_st, e->d_snap, sizeof(MbState) * nmb, hipMemcpyDeviceToDevice, e->stream));
+        for (int k = 0; k < m; ++k) {
+            hl_amd_result_t r;
+            const int32_t rc = encode_frame(e, Y[k], U[k], V[k], &r);
+            if (rc) return rc;
+            store_result(e, base + k, r, &res[k]);
+        }
+        e->reruns = 1;
+        return HL_AMD_SUCCESS;
+    }
+    const StreamParams sp{e->W, e->H, e->p.qp, e->p.deblock};
+    for (int k = 0; k < m; ++k) {
+        const SliceState ss{0, e->pict_count, e->idr_pic_id};
+        const size_t n = write_slice(sp, ss, e->h_brec + nmb * k, e->scratch.data(), e->out.data(), e->out.size());
+        if (!n) return HL_AMD_ERROR_TOOSHORT;
+        hl_amd_result_t r;
+        r.type = HL_AMD_RESULT_TYPE_DATA;
+        r.data = e->out.data() + 3;
+        r.data_size = n - 3;
+        r.hdr = e->hdr.data();
+        r.hdr_size = e->hdr.size();
+        if (e->frame_index == 0) r.type |= HL_AMD_RESULT_TYPE_HDR;
+        store_result(e, base + k, r, &res[k]);
+        ++e->pict_count;
+        --e->gop_left;
+        ++e->frame_index;
+    }
+    e->chain_end = carry;
+    // the last picture of the run becomes the reference
+    uint8_t** dst = e->d_pic[e->cur];
+    const uint8_t* last = e->d_bpic + pic * (m - 1);
+    HL_HIP_CHECK(hipMemcpyAsync(dst[0], last, (size_t)e->W * e->H, hipMemcpyDeviceToDevice, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(dst[1], last + (size_t)e->W * e->H, (size_t)e->Wc * e->Hc, hipMemcpyDeviceToDevice, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(dst[2], last + (size_t)e->W * e->H * 5 / 4, (size_t)e->Wc * e->Hc, hipMemcpyDeviceToDevice, e->stream));
+    HL_HIP_CHECK(hipStreamSynchronize(e->stream));
+    e->cur ^= 1;
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_encode_batch(hl_amd_encoder_t* e, int32_t n, const uint8_t* const* y, const uint8_t* const* u,
+                                       const uint8_t* const* v, hl_amd_result_t* results)
+{
+    if (!e || n <= 0 || !y || !u || !v || !results) return HL_AMD_ERROR_INVALID_PARAMETER;
+    for (int i = 0; i < n; ++i)
+        if (!y[i] || !u[i] || !v[i]) return HL_AMD_ERROR_INVALID_PARAMETER;
+    e->bout.resize(n);
+    int i = 0;
+    while (i < n) {
+        if (e->gop_left <= 0 || n - i == 1) {  // IDR pictures (and a lone P picture) take the per-picture path
+            hl_amd_result_t r;
+            const int32_t rc = encode_frame(e, y[i], u[i], v[i], &r);
+            if (rc) return rc;
+            store_result(e, i, r, &results[i]);
+            ++i;
+            continue;
+        }
+        const int m = std::min(n - i, e->gop_left);
+        const int32_t rc = encode_run(e, m, y + i, u + i, v + i, results + i, i);
+        if (rc) return rc;
+        i += m;
+    }
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_set_pipeline(hl_amd_encoder_t* e, int32_t slots, int32_t wg_per_slot, int32_t reach)
+{
+    if (!e || slots < 1 || slots > 16 || wg_per_slot < 1 || slots * wg_per_slot > 256 || reach < 0) return HL_AMD_ERROR_INVALID_PARAMETER;
+    e->slots = slots;
+    e->wg_per_slot = wg_per_slot;
+    e->reach = reach;
+    return HL_AMD_SUCCESS;
+}
+
 extern "C" int32_t hl_amd_encode_device(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t* u, const uint8_t* v, hl_amd_result_t* r)
 {
     if (!e || !y || !u || !v || !r) return HL_AMD_ERROR_INVALID_PARAMETER;
@@ -396,10 +741,11 @@ extern "C" int32_t hl_amd_last_reruns(hl_amd_encoder_t* e) { return e ? e->rerun
 
 extern "C" int32_t hl_amd_last_mb_launches(hl_amd_encoder_t* e) { return e ? e->mb_launches : -1; }
 
-// Phase cycle counters of HL_PROFILE builds (zeros otherwise); n <= 64.
+// Phase cycle counters of HL_PROFILE builds (zeros otherwise): 64 phase
+// counters, then (n > 64) the cycles of each macroblock of the last frame.
 extern "C" int32_t hl_amd_profile_counters(hl_amd_encoder_t* e, unsigned long long* out, int32_t n)
 {
-    if (!e || !out || n > 64) return HL_AMD_ERROR_INVALID_PARAMETER;
+    if (!e || !out || n < 0 || n > 64 + e->nmb) return HL_AMD_ERROR_INVALID_PARAMETER;
     memset(out, 0, sizeof(unsigned long long) * n);
     if (!e->d_prof) return HL_AMD_SUCCESS;
     HL_HIP_CHECK(hipMemcpy(out, e->d_prof, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));

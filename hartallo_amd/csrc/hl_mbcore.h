@@ -89,6 +89,10 @@ struct FrameArgs {
     MbChain* chain;
     const int32_t* spec;  // speculated Single_ctr at each row start
     unsigned long long* prof;  // phase cycle counters (profiling build), may be null
+    // pipelined runs (hl_pipeline.h); ref_done is null in the per-picture path
+    const int32_t* ref_done;  // task flags of the reference picture's slot
+    int32_t ref_epoch;        // flag value once a task of the reference picture finished
+    int32_t* perr;            // bounded-spin failures
 };
 
 struct NbInfo {
@@ -130,7 +134,7 @@ struct Shared {
     int32_t be_nz[9][16], be_tc[9][16], be_t1[9][16], be_sctr[9][16], be_bits[9][16], be_dist[9][16];
     int32_t be_w0[9][16], be_w1[9][16], be_w2[9][16];    // packed block statistics (device path)
     alignas(16) uint8_t be_tcb[16][16];                  // TotalCoeff [block][candidate]
-    int32_t lvs[kMaxWaves * 4][16];                      // per-row level scratch of coop_cavlc
+    alignas(16) int32_t lvs[kMaxWaves * 4][16];          // per-row level scratch of coop_cavlc
     CoopTables ct;
     uint32_t qtab[16];                                   // packed quarter-pel phase table
     double cd_cost[9];
@@ -174,6 +178,7 @@ struct Ctx {
     int addr, mbx, mby, xL, yL;
     int chain, fresh, dep;  // rdo.Single_ctr emulation (uniform)
     LaneK K;                // per-lane constants of the 16-lane block pipeline (device)
+    int gx, gy;             // reference planes known complete for MBs (X <= gx, Y <= gy) (pipelined runs)
 #if defined(HL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
     unsigned long long pacc[kProfSlots] = {};
     unsigned pcnt[kProfSlots] = {};
@@ -676,6 +681,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         int pa[kMaxPass], pb[kMaxPass], sv[kMaxPass];
         // slots and source samples first (one LDS round trip), then all loads
         int o1[kMaxPass], o2[kMaxPass];
+        HL_PROF_T(ta0);
 #pragma unroll
         for (int j = 0; j < kMaxPass; ++j) {
             const int item = min(grp + j * ngrp, n - 1);  // clamped: no divergence, valid addresses
@@ -694,19 +700,42 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                 pb[j] = base[o2[j]];
             }
         }
+#if defined(HL_STEP_PROF)
+        sv[0] += pa[0] * 0;  // wait for the loads here (profiling only)
+        HL_PROF_ADD(c, 3, ta0);
+        HL_PROF_T(ta1);
+#endif
 #pragma unroll
         for (int j = 0; j < kMaxPass; ++j) {
             const int item = grp + j * ngrp;
             if (item < n) {
                 const int ci = item >> g.lnb, k = item & (g.nblk - 1);
                 const int pred = (pa[j] + pb[j] + 1) >> 1;
-                const int q = coop_quant(coop_fwd(c.K, sv[j] - pred), c.K.mf, qbits, f);
-                const CoopStat st = coop_cavlc(S.ct, q, c.K.s, S.lvs[grp]);
-                int tok = 0;
-                if (c.K.p == 0 && st.tc)  // coeff_token lengths for the four nC classes
-                    tok = S.ct.tok[0][st.t1][st.tc] | (S.ct.tok[1][st.t1][st.tc] << 5) | (S.ct.tok[2][st.t1][st.tc] << 10) | (6 << 15);
-                const int r = coop_idct(c.K, coop_dequant(q, c.K.ls, F.qp));
-                const int dist = row_sum(iabs(sv[j] - clip255(pred + r)));
+                const int res = sv[j] - pred;
+                const int q = coop_quant(coop_fwd(c.K, res), c.K.mf, qbits, f);
+#if defined(HL_STEP_PROF)
+                HL_PROF_ADD(c, 4, ta1);
+                HL_PROF_T(ta2);
+#endif
+                CoopStat st{0, 0, 0, -1};
+                int tok = 0, dist;
+                if (__ballot(q != 0) == 0) {  // every block of the wave quantised to zero
+                    dist = row_sum(iabs(res));
+                }
+                else {
+                    st = coop_cavlc(S.ct, q, c.K.s, S.lvs[grp]);
+                    if (c.K.p == 0 && st.tc)  // coeff_token lengths for the four nC classes
+                        tok = S.ct.tok[0][st.t1][st.tc] | (S.ct.tok[1][st.t1][st.tc] << 5) | (S.ct.tok[2][st.t1][st.tc] << 10) | (6 << 15);
+                    const int r = coop_idct(c.K, coop_dequant(q, c.K.ls, F.qp));
+                    dist = row_sum(iabs(sv[j] - clip255(pred + r)));
+                }
+#if defined(HL_STEP_PROF)
+                HL_PROF_ADD(c, 5, ta2);
+                HL_PROF_T(ta3);
+#endif
+#if defined(HL_STEP_PROF)
+                HL_PROF_ADD(c, 6, ta3);
+#endif
                 if (c.K.p == 0) {
                     S.be_w0[ci][k] = st.tc | (st.t1 << 5) | ((st.sctr + 1) << 8);
                     S.be_w1[ci][k] = st.rest | (dist << 16);
@@ -935,6 +964,40 @@ struct Best {
 
 HD int ilog2_small(int v) { return v >= 16 ? 4 : (v >= 8 ? 3 : (v >= 4 ? 2 : (v >= 2 ? 1 : 0))); }
 
+// Pipelined runs: before a partition search, make sure the reference
+// picture's planes cover its motion window.  The diamond window is the
+// initial centre (the MVP or (0,0)) +- me_range in the integer stage, and
+// the half / quarter stages move at most me_range / 2 + me_range / 4 more,
+// so +-2 * me_range (+4 for rounding and the second tap plane) bounds every
+// fetch.  The task start guarantees MBs up to (gx, gy); a window reaching
+// further waits for the reference picture's task whose staircase covers it
+// (hl_pipeline.h).  Negative directions are always covered.
+HD void reach_wait(Ctx& c, const PartGeo& g, const int pmv[2])
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const FrameArgs& F = c.F;
+    if (!F.ref_done) return;
+    const int px = c.xL + g.px + g.pw + (pmv[0] > 0 ? pmv[0] >> 2 : 0) + 2 * F.me_range + 4;
+    const int py = c.yL + g.py + g.ph + (pmv[1] > 0 ? pmv[1] >> 2 : 0) + 2 * F.me_range + 4;
+    int X = min(F.mbw - 1, max(0, px >> 4)), Y = min(F.mbh - 1, max(0, py >> 4));
+    if (X <= c.gx && Y <= c.gy) return;
+    X = max(X, c.gx);
+    Y = max(Y, c.gy);
+    if (c.tid == 0) {
+        spin_ge(F.ref_done + min(Y + 2, F.mbh - 1) * F.mbw + min(X + 3, F.mbw - 1), F.ref_epoch, F.perr);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    HL_SYNC();
+    c.gx = X;
+    c.gy = Y;
+#else
+    (void)c;
+    (void)g;
+    (void)pmv;
+#endif
+}
+
 // Diamond search of one (sub)partition, me_ds.c:104-477.  Returns true when
 // the P_Skip probe fired (16x16 only).
 HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
@@ -964,15 +1027,20 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     b.mv[0] = b.mv[1] = 0;
     bool probably = false;
     int pmv[2];
-    if (probe) {  // me_ds.c:229-261
-        int smv[2];
-        skip_mv(S, smv);
-        const PartShape p16{16, 16, 16, 16, 0};
-        mvp(S, p16, 0, 0, pmv);
-        smv[0] = uni(smv[0]);
-        smv[1] = uni(smv[1]);
+    {
+        HL_PROF_T(tm);
+        const PartShape ps{pd.part_w, pd.part_h, pd.sub_w, pd.sub_h, pd.num_part == 4};
+        mvp(S, ps, pi, spi, pmv);
         pmv[0] = uni(pmv[0]);
         pmv[1] = uni(pmv[1]);
+        HL_PROF_ADD(c, 4, tm);
+    }
+    reach_wait(c, g, pmv);
+    if (probe) {  // me_ds.c:229-261 (the probe's predictor is the 16x16 one, pmv)
+        int smv[2];
+        skip_mv(S, smv);
+        smv[0] = uni(smv[0]);
+        smv[1] = uni(smv[1]);
         if (pmv[0] == smv[0] && pmv[1] == smv[1]) {
             put_cand(c, g.px, g.py, 0, pmv[0], pmv[1], 0, (c.tid & 63) == 0);
             eval_candidates(c, g, 1, pmv);
@@ -986,14 +1054,6 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
                 b.mv[1] = pmv[1];
             }
         }
-    }
-    {
-        HL_PROF_T(tm);
-        const PartShape ps{pd.part_w, pd.part_h, pd.sub_w, pd.sub_h, pd.num_part == 4};
-        mvp(S, ps, pi, spi, pmv);
-        pmv[0] = uni(pmv[0]);
-        pmv[1] = uni(pmv[1]);
-        HL_PROF_ADD(c, 4, tm);
     }
     // MVP and (0,0) candidates, me_ds.c:280-300
     const int nc0 = (pmv[0] != 0 || pmv[1] != 0) ? 2 : 1;
@@ -2461,10 +2521,11 @@ HD void mb_end(Ctx& c)
     HL_SYNC();
 }
 
-// One macroblock, start to end.  s_in = rdo.Single_ctr on entry.
-HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, int s_in)
+// One macroblock, start to end.  s_in = rdo.Single_ctr on entry; (gx, gy) =
+// reference region already known complete (pipelined runs; see reach_wait).
+HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, int s_in, int gx = 1 << 20, int gy = 1 << 20)
 {
-    Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0, LaneK{}};
+    Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0, LaneK{}, gx, gy};
 #if defined(__HIP_DEVICE_COMPILE__)
     c.K = make_lanek(tid, F.qp, F.qpc);
 #endif
@@ -2479,11 +2540,13 @@ HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, in
     HL_PROF_ADD(c, 7, t1);
     HL_PROF_ADD(c, 8, t0);
 #if defined(HL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
-    if (tid == 0 && F.prof)
+    if (tid == 0 && F.prof) {
         for (int i = 0; i < kProfSlots; ++i) {
             atomicAdd(&F.prof[2 * i], c.pacc[i]);
             atomicAdd(&F.prof[2 * i + 1], (unsigned long long)c.pcnt[i]);
         }
+        F.prof[64 + addr] = c.pacc[8];
+    }
 #endif
 }
 

@@ -384,4 +384,29 @@ HD void unscan(const T* list, int* m)
     for (int i = 0; i < 16; ++i) m[kZigzag[i]] = list[i];
 }
 
+// Inter-workgroup flags (agent scope, see hl_pipeline.h)
+typedef __attribute__((address_space(1))) int32_t gi32;
+
+__device__ __forceinline__ int32_t ld_relaxed(const int32_t* p)
+{
+    return __hip_atomic_load((gi32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_relaxed(int32_t* p, int32_t v)
+{
+    __hip_atomic_store((gi32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One lane polls until *flag >= want (bounded: ~0.5 s, then counts an error).
+__device__ __forceinline__ void spin_ge(const int32_t* flag, int32_t want, int32_t* err)
+{
+    for (unsigned i = 0; ld_relaxed(flag) < want; ++i) {
+        __builtin_amdgcn_s_sleep(2);
+        if (i > (1u << 23)) {
+            atomicAdd(err, 1);
+            return;
+        }
+    }
+}
+
+
 }  // namespace hl

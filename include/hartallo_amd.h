@@ -88,6 +88,22 @@ int32_t hl_amd_encode(hl_amd_encoder_t* encoder, const uint8_t* y, const uint8_t
 int32_t hl_amd_encode_device(hl_amd_encoder_t* encoder, const uint8_t* y, const uint8_t* u, const uint8_t* v,
                              hl_amd_result_t* result);
 
+/* n consecutive frames of the stream (planes resident in device memory),
+ * encoded as if by n calls of hl_amd_encode_device, with results[i] the
+ * i-th call's result (bitstreams identical).  Runs of P pictures are encoded
+ * in one frame-pipelined launch: picture f+1 starts as soon as picture f has
+ * finished the region its motion search can reach.  The data of every
+ * result stays valid until the next call on this encoder.  No reference
+ * interface: a throughput entry point for callers that hold several frames
+ * (hl_codec_encode takes one frame per call, hl_codec.c:152-159). */
+int32_t hl_amd_encode_batch(hl_amd_encoder_t* encoder, int32_t n, const uint8_t* const* y, const uint8_t* const* u,
+                            const uint8_t* const* v, hl_amd_result_t* results);
+
+/* pipelined-run geometry: picture slots x workgroups per slot (<= 256 in
+ * all, one workgroup per CU) and the reference reach R (in MBs) guaranteed
+ * at the start of every macroblock task; defaults 4 x 60, R = 2 */
+int32_t hl_amd_set_pipeline(hl_amd_encoder_t* encoder, int32_t slots, int32_t wg_per_slot, int32_t reach);
+
 /* reconstructed (deblocked) picture of the last encoded frame, i.e. the
  * reference picture the next frame predicts from (dpb.c:160-170) */
 int32_t hl_amd_get_recon(hl_amd_encoder_t* encoder, uint8_t* y, uint8_t* u, uint8_t* v);
@@ -108,8 +124,9 @@ int32_t hl_amd_last_reruns(hl_amd_encoder_t* encoder);
 int32_t hl_amd_last_mb_launches(hl_amd_encoder_t* encoder);
 
 /* per-phase shader-clock counters of the macroblock kernel; filled only by
- * the profiling build (make profile); out[2k] = cycles, out[2k+1] = calls.
- * The counters are cleared by the call. */
+ * the profiling build (make profile); out[2k] = cycles, out[2k+1] = calls
+ * for k < 32, then out[64 + addr] = cycles of macroblock addr in the last
+ * frame (n <= 64 + macroblocks).  The phase counters are cleared by the call. */
 int32_t hl_amd_profile_counters(hl_amd_encoder_t* encoder, unsigned long long* out, int32_t n);
 
 const char* hl_amd_version(void);

@@ -1,0 +1,107 @@
+"""Parity of frame-pipelined runs (hl_amd_encode_batch, hl_pipeline.h).
+
+A batch must produce exactly the bitstream and reconstruction of the same
+frames encoded one call at a time -- which test_gpu_parity.py pins to the
+reference -- and of the golden streams the reference itself produced.  The
+pipeline geometry is varied so that the cross-picture waits are exercised
+with few workgroups, several slots and no guaranteed reach (every partition
+search then waits on the reference picture's progress).
+Tolerance: none.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from hartallo_amd import Encoder, synth
+from hl_testlib import GOLDEN, GOLDEN_CONFIGS, OracleEncoder, first_diff, golden_input, md5
+
+pytestmark = pytest.mark.gpu
+
+GOLD = json.load(open(os.path.join(GOLDEN, "golden.json")))
+
+
+def _device_frames(clip, w, h):
+    dev = torch.from_numpy(np.ascontiguousarray(clip)).cuda()
+    torch.cuda.synchronize()
+    n = w * h
+    return dev, [(dev[i].data_ptr(), dev[i].data_ptr() + n, dev[i].data_ptr() + n + n // 4) for i in range(len(clip))]
+
+
+def _batch(w, h, qp, mer, db, gop, clip, geometry=None, split=None):
+    enc = Encoder(w, h, qp, mer, db, gop)
+    if geometry:
+        enc.set_pipeline(*geometry)
+    dev, ptrs = _device_frames(clip, w, h)
+    out, bounds = [], split or [len(ptrs)]
+    i = 0
+    for n in bounds:
+        out += enc.encode_batch_device(ptrs[i:i + n])
+        i += n
+    rec = np.concatenate(enc.recon())
+    enc.close()
+    return [r.annexb() for r in out], rec
+
+
+def _single(w, h, qp, mer, db, gop, clip):
+    enc = Encoder(w, h, qp, mer, db, gop)
+    dev, ptrs = _device_frames(clip, w, h)
+    out = [enc.encode_device(*p).annexb() for p in ptrs]
+    rec = np.concatenate(enc.recon())
+    enc.close()
+    return out, rec
+
+
+@pytest.mark.parametrize("cfg", [c for c in GOLDEN_CONFIGS if c[3] >= 3], ids=[c[0] for c in GOLDEN_CONFIGS if c[3] >= 3])
+def test_batch_golden_streams(gpu, cfg):
+    name, w, h, n, qp, mer, db, gop, seed = cfg
+    ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()
+    out, rec = _batch(w, h, qp, mer, db, gop, golden_input(cfg))
+    got = b"".join(out)
+    assert got == ref, f"{name}: first differing byte {first_diff(got, ref)}"
+    assert md5(rec) == GOLD[name]["recon_md5"][n - 1]
+
+
+@pytest.mark.parametrize("geometry", [(4, 60, 2), (2, 8, 0), (3, 5, 1), (6, 2, 0), (1, 16, 2)], ids=lambda g: "x".join(map(str, g)))
+def test_batch_equals_single_calls(gpu, geometry):
+    w, h, n = 320, 240, 9
+    clip = synth.clip(w, h, n, 31)
+    a, ra = _single(w, h, 26, 16, 1, 30, clip)
+    b, rb = _batch(w, h, 26, 16, 1, 30, clip, geometry, split=[1, 5, 3])
+    for f in range(n):
+        assert a[f] == b[f], f"frame {f}: first differing byte {first_diff(a[f], b[f])}"
+    assert np.array_equal(ra, rb)
+
+
+def test_batch_gop_boundaries(gpu):
+    # IDR pictures inside the batch split it into pipelined P runs
+    w, h, n = 176, 144, 11
+    clip = synth.clip(w, h, n, 32)
+    a, ra = _single(w, h, 30, 8, 1, 4, clip)
+    b, rb = _batch(w, h, 30, 8, 1, 4, clip, (2, 6, 0))
+    assert a == b
+    assert np.array_equal(ra, rb)
+
+
+def test_batch_720p_vs_oracle(gpu):
+    w, h, n = 1280, 720, 4
+    clip = synth.clip(w, h, n, 7)
+    out, rec = _batch(w, h, 28, 16, 1, 30, clip)
+    o = OracleEncoder(w, h, 28, 16, 1, 30)
+    for f in range(n):
+        ob = o.encode(clip[f])
+        assert out[f] == ob, f"frame {f}: first differing byte {first_diff(out[f], ob)}"
+    assert np.array_equal(rec, o.recon())
+
+
+def test_batch_1088p_equals_single_calls(gpu):
+    # the bench workload: 1920x1088, QP28, ME 16, deblocking
+    w, h, n = 1920, 1088, 5
+    clip = synth.clip(w, h, n, 11)
+    a, ra = _single(w, h, 28, 16, 1, 30, clip)
+    b, rb = _batch(w, h, 28, 16, 1, 30, clip)
+    for f in range(n):
+        assert a[f] == b[f], f"frame {f}: first differing byte {first_diff(a[f], b[f])}"
+    assert np.array_equal(ra, rb)

@@ -7,6 +7,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
@@ -30,9 +32,20 @@ def main():
         enc.encode(y[:W * H], y[W * H:W * H * 5 // 4], y[W * H * 5 // 4:])
         dt = time.perf_counter() - t
         ms = enc.timing_ms()
-        cnt = enc.profile_counters(2 * len(PHASES))
         print(f"frame {f}: wall {dt * 1e3:.1f} ms  planes {ms[0]:.2f}  mb {ms[1]:.1f}  deblock {ms[2]:.2f}  device {ms[3]:.1f} ms  reruns {enc.last_reruns()}")
         nmb = (W // 16) * (H // 16)
+        cnt = enc.profile_counters(64 + nmb)
+        mbc = np.array(cnt[64:64 + nmb], dtype=np.float64).reshape(H // 16, W // 16)
+        # launch-per-diagonal time (sum of per-diagonal maxima) vs the dataflow
+        # critical path (MB (x, y) after (x-1, y) and (x+1, y-1))
+        mbh, mbw = mbc.shape
+        diag_max = sum(max((mbc[y, d - 2 * y] for y in range(mbh) if 0 <= d - 2 * y < mbw), default=0.0) for d in range(mbw + 2 * mbh))
+        fin = np.zeros_like(mbc)
+        for y in range(mbh):
+            for x in range(mbw):
+                dep = max(fin[y, x - 1] if x else 0.0, fin[y - 1, x + 1] if y and x + 1 < mbw else (fin[y - 1, x] if y else 0.0))
+                fin[y, x] = dep + mbc[y, x]
+        print(f"   MB cycles: mean {mbc.mean():.0f}  max {mbc.max():.0f}  sum-of-diagonal-max {diag_max / 1e6:.1f} M  dataflow critical path {fin.max() / 1e6:.1f} M")
         for i, name in enumerate(PHASES):
             cyc, calls = cnt[2 * i], cnt[2 * i + 1]
             if calls:
