@@ -270,8 +270,8 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
         delete e;
         return HL_AMD_ERROR_OUTOFMEMMORY;
     }
-    e->slots = 4;
-    e->wg_per_slot = 60;
+    e->slots = 8;
+    e->wg_per_slot = 32;
     e->reach = 2;
     const StreamParams sp{e->W, e->H, p->qp, p->deblock};
     e->scratch.resize(slice_scratch_bytes(sp));
@@ -616,14 +616,11 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     }
     e->mb_launches = 1;
     e->reruns = 0;
-    if (err) {
-        fprintf(stderr, "hartallo_amd: pipelined run: %d bounded waits gave up\n", err);
-        return HL_AMD_ERROR_SYSTEM;
-    }
+    if (err) fprintf(stderr, "hartallo_amd: pipelined run: %d bounded waits gave up; re-encoding the run picture by picture\n", err);
     int32_t carry = e->chain_end;
-    bool ok = true;
+    bool ok = err == 0;
     for (int k = 0; k < m && ok; ++k) ok = validate_rows(e->h_bchain + nmb * k, e->mbw, e->mbh, 9, carry);
-    if (!ok) {  // a speculated row start mattered: redo the run picture by picture
+    if (!ok) {  // a speculated row start mattered (or a wait gave up): redo the run picture by picture
         HL_HIP_CHECK(hipMemcpyAsync(e->d_st, e->d_snap, sizeof(MbState) * nmb, hipMemcpyDeviceToDevice, e->stream));
         for (int k = 0; k < m; ++k) {
             hl_amd_result_t r;

@@ -396,12 +396,13 @@ __device__ __forceinline__ void st_relaxed(int32_t* p, int32_t v)
     __hip_atomic_store((gi32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One lane polls until *flag >= want (bounded: ~0.5 s, then counts an error).
+// One lane polls until *flag >= want (bounded: a few seconds, then counts an
+// error; the host then re-encodes the run picture by picture).
 __device__ __forceinline__ void spin_ge(const int32_t* flag, int32_t want, int32_t* err)
 {
     for (unsigned i = 0; ld_relaxed(flag) < want; ++i) {
         __builtin_amdgcn_s_sleep(2);
-        if (i > (1u << 23)) {
+        if (i > (1u << 26)) {
             atomicAdd(err, 1);
             return;
         }

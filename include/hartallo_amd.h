@@ -101,7 +101,7 @@ int32_t hl_amd_encode_batch(hl_amd_encoder_t* encoder, int32_t n, const uint8_t*
 
 /* pipelined-run geometry: picture slots x workgroups per slot (<= 256 in
  * all, one workgroup per CU) and the reference reach R (in MBs) guaranteed
- * at the start of every macroblock task; defaults 4 x 60, R = 2 */
+ * at the start of every macroblock task; defaults 8 x 32, R = 2 */
 int32_t hl_amd_set_pipeline(hl_amd_encoder_t* encoder, int32_t slots, int32_t wg_per_slot, int32_t reach);
 
 /* reconstructed (deblocked) picture of the last encoded frame, i.e. the
