@@ -31,6 +31,9 @@ sys.path.insert(0, ROOT)
 W, H = 1920, 1088
 QP, ME_RANGE, DEBLOCK, GOP = 28, 16, 1, 30
 BYTES_PER_MB = 2752  # compulsory HBM bytes per macroblock, DESIGN.md / SURVEY §8(d)
+# HBM traffic of k_pipeline per macroblock, from rocprofv3 FETCH_SIZE / WRITE_SIZE
+# passes on this workload (tools/pmc_traffic.sh, corrected per MI355X_MICROARCH.md)
+PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_traffic_k_pipeline.json")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 
@@ -112,6 +115,9 @@ def main():
         avg_launch_s = (mb_ms / 1e3) / mb_launches
         bytes_per_launch = BYTES_PER_MB * nmb * run_frames / mb_launches
         achieved = bytes_per_launch / avg_launch_s / 1e9
+        traffic = None
+        if mb_launches == 1 and os.path.exists(PMC_TRAFFIC):
+            traffic = round(json.load(open(PMC_TRAFFIC))["traffic_bytes_per_mb"] * nmb * run_frames)
         line = {
             "metric": "1080p encoded frames/sec (bit-exact) at 1/2/4/8 MI355X; macroblocks/sec/GPU",
             "value": round(fps, 4),
@@ -130,7 +136,7 @@ def main():
             "mb_per_s_per_gpu": round(fps / world * nmb, 1),
             "bitstream_bytes_per_frame": round(out_bytes / args.steps, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_pipeline", "avg_launch_us": round(avg_launch_s * 1e6, 2),
                          "frames_per_launch": run_frames,
                          "note": "latency-bound MB wavefront, frames pipelined; achieved = 2752 B/MB x MBs per launch / launch time"},

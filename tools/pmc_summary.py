@@ -1,0 +1,38 @@
+"""Summarises rocprofv3 FETCH_SIZE / WRITE_SIZE passes for the pipelined
+kernel into bytes per launch and per macroblock (JSON on stdout).
+
+FETCH_SIZE is doubled as MI355X_MICROARCH.md (HBM) prescribes for gfx950
+(it tallies 128-B requests at 64 B); both counters are in KiB units as
+rocprofv3 reports them (TCC_EA0_*REQ x 64 B / 1024).
+"""
+import collections
+import csv
+import json
+import sys
+
+
+def per_kernel(path):
+    acc = collections.defaultdict(lambda: [0.0, 0])
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"].split("(")[0]
+        acc[(k, r["Counter_Name"])][0] += float(r["Counter_Value"])
+        acc[(k, r["Counter_Name"])][1] += 1
+    return acc
+
+
+def main():
+    f, w = per_kernel(sys.argv[1]), per_kernel(sys.argv[2])
+    fetch = f[("k_pipeline", "FETCH_SIZE")]
+    write = w[("k_pipeline", "WRITE_SIZE")]
+    launches = fetch[1]
+    mbs = 12 * (1920 // 16) * (1088 // 16)  # bench: 12 pipelined pictures per launch
+    rd = 2.0 * fetch[0] * 1024 / launches
+    wr = write[0] * 1024 / launches
+    out = {"kernel": "k_pipeline", "launches": launches, "macroblocks_per_launch": mbs, "fetch_bytes_per_launch_x2": rd,
+           "write_bytes_per_launch": wr, "traffic_bytes_per_launch": rd + wr, "traffic_bytes_per_mb": (rd + wr) / mbs,
+           "note": "FETCH_SIZE x2 (gfx950 correction, calibrated for 16 B/lane reads; this kernel's byte gathers are uncalibrated)"}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
