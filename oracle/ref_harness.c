@@ -130,7 +130,7 @@ int main(int argc, char** argv)
     static const uint8_t scp[3] = { 0, 0, 1 };
     int32_t rec[MBR_STRIDE];
     int n = 0;
-    double tot = 0;
+    double tot = 0, tp = 0;  /* tp: time of the P pictures (every picture after the first) */
     while (n < N && fread(buf, 1, fs, fi) == fs) {
         struct timespec t0, t1;
         hl_frame_video_fill(f, HL_VIDEO_CHROMA_YUV420, W, H, buf, fs);
@@ -139,7 +139,9 @@ int main(int argc, char** argv)
         int e = hl_codec_encode(c, (hl_frame_t*)f, r);
         clock_gettime(CLOCK_MONOTONIC, &t1);
         if (e) { fprintf(stderr, "encode err %d at frame %d\n", e, n); return 4; }
-        tot += (t1.tv_sec - t0.tv_sec) + (t1.tv_nsec - t0.tv_nsec) * 1e-9;
+        const double dt = (t1.tv_sec - t0.tv_sec) + (t1.tv_nsec - t0.tv_nsec) * 1e-9;
+        tot += dt;
+        if (n > 0) tp += dt;
         if (r->type & HL_CODEC_RESULT_TYPE_HDR) fwrite(c->hdr_bytes, 1, c->hdr_bytes_count, fo);
         if (r->type & HL_CODEC_RESULT_TYPE_DATA) { fwrite(scp, 1, 3, fo); fwrite(r->data_ptr, 1, r->data_size, fo); }
         if (!quiet) {
@@ -159,7 +161,7 @@ int main(int argc, char** argv)
     fclose(fo);
     if (frec) fclose(frec);
     if (fmb) fclose(fmb);
-    printf("{\"frames\": %d, \"seconds\": %.6f, \"fps\": %.4f, \"mb_per_s\": %.1f}\n",
-           n, tot, n / tot, (double)n * (W / 16) * (H / 16) / tot);
+    printf("{\"frames\": %d, \"seconds\": %.6f, \"fps\": %.4f, \"mb_per_s\": %.1f, \"p_seconds\": %.6f, \"p_fps\": %.4f}\n",
+           n, tot, n / tot, (double)n * (W / 16) * (H / 16) / tot, tp, n > 1 ? (n - 1) / tp : 0.0);
     return 0;
 }

@@ -10,7 +10,7 @@
 
 #include <vector>
 
-#include "../../hartallo_amd/csrc/hl_filters.h"
+#include "../../hartallo_amd/csrc/hl_pipeline.h"
 #include "../../hartallo_amd/csrc/hl_writer.h"
 
 using namespace hl;
@@ -163,3 +163,16 @@ extern "C" int emu_state_size(void) { return (int)sizeof(MbState); }
 // unit hooks: GPU-side bit counting vs the writer's table
 extern "C" int emu_level_code_len(int sl, int lc) { return level_code_len(sl, lc); }
 extern "C" int emu_writer_level_bits(int sl, int lc) { return level_code_bits(sl, lc); }
+
+// The pipelined-run schedule (hl_pipeline.h) for tests/test_pipeline_schedule.py:
+// deblocking (kind 0) or plane (kind 1) blocks of task (x, y) as X, Y pairs.
+extern "C" int emu_task_blocks(int kind, int x, int y, int mbw, int mbh, int* out)
+{
+    int b[kMaxTaskBlocks][2];
+    const int n = task_blocks(kind, x, y, mbw, mbh, b);
+    for (int i = 0; i < n; ++i) {
+        out[2 * i] = b[i][0];
+        out[2 * i + 1] = b[i][1];
+    }
+    return n;
+}
