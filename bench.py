@@ -67,7 +67,7 @@ def cpu_baseline(frames_host, n_frames):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--steps", type=int, default=28)  # warm-up IDR + P, then the 28 P pictures up to the next IDR
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-frames", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
