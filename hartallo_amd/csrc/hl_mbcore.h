@@ -741,6 +741,22 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                     S.be_w1[ci][k] = st.rest | (dist << 16);
                     S.be_w2[ci][k] = tok;
                     S.be_tcb[k][ci] = (uint8_t)st.tc;
+                    if (g.nblk == 1) {
+                        // a single-block partition: both nC neighbours lie outside it, so the
+                        // nC (and the candidate's cost) needs no other row (phase 2 skipped)
+                        int bits = 0;
+                        if (st.tc) {
+                            const int nC = nc_luma_of(S, blk_idx(g.px, g.py), [&](int ni) -> int { return S.tc[ni]; });
+                            bits = st.rest + ((tok >> (5 * (nC < 2 ? 0 : (nC < 4 ? 1 : (nC < 8 ? 2 : 3))))) & 31);
+                        }
+                        const CandSlot cs = S.wc[wave][ci];
+                        S.cd_cost[ci] = mv_cost(F, dist, bits, cs.mvx, cs.mvy, pmv);
+                        S.cd_bits[ci] = bits;
+                        S.cd_dist[ci] = dist;
+                        S.cd_single[ci] = st.tc ? st.sctr : 0;
+                        S.cd_cbp[ci] = st.tc ? 1 << blk_idx(g.px, g.py) : 0;
+                        S.cd_last[ci] = st.tc ? st.sctr : -1;
+                    }
                 }
             }
         }
@@ -752,7 +768,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
     // sees it at this point of the sequence (residual.c:640-755 with the live
     // TotalCoeffs of quirk 1), coeff_token, candidate sums, cost.  All LDS
     // reads are issued up front.
-    if (c.tid < (ncand << 4)) {
+    if (g.nblk > 1 && c.tid < (ncand << 4)) {
         const int wave = c.tid >> 6, ci = c.tid >> 4, k0 = c.tid & 15;
         const bool valid = k0 < g.nblk;
         const int k = valid ? k0 : 0;
@@ -811,7 +827,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
             S.cd_last[ci] = last ? (last & 15) : -1;
         }
     }
-    HL_SYNC();
+    if (g.nblk > 1) HL_SYNC();
     HL_PROF_ADD(c, 1, tp1);
     HL_PROF_T(tp2);
     // live TotalCoeffsLuma = last writer; the next reader is behind a barrier
