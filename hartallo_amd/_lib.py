@@ -33,6 +33,7 @@ EXPORTED_SYMBOLS = (
     "hl_amd_encode_device",
     "hl_amd_encode_batch",
     "hl_amd_set_pipeline",
+    "hl_amd_pipeline_occupancy",
     "hl_amd_get_recon",
     "hl_amd_set_timing",
     "hl_amd_get_timing",
@@ -93,6 +94,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_encode_batch.restype = i32
     lib.hl_amd_set_pipeline.argtypes = [vp, i32, i32, i32]
     lib.hl_amd_set_pipeline.restype = i32
+    lib.hl_amd_pipeline_occupancy.argtypes = []
+    lib.hl_amd_pipeline_occupancy.restype = i32
     lib.hl_amd_get_recon.argtypes = [vp, vp, vp, vp]
     lib.hl_amd_get_recon.restype = i32
     lib.hl_amd_set_timing.argtypes = [vp, i32]

@@ -80,19 +80,42 @@ __global__ __launch_bounds__(64) void k_deblock_diag(DeblockArgs D, int mbh, int
     }
 }
 
+// Deblocking and plane blocks of task (x, y) (hl_pipeline.h).
+__device__ void task_filters(const PipeFrame& PF, int x, int y, int mbw, int mbh, int tid)
+{
+    int blk[kMaxTaskBlocks][2];
+    const int nd = PF.deblock ? task_blocks(0, x, y, mbw, mbh, blk) : 0;
+    for (int i = 0; i < nd; ++i) {
+        const int a = blk[i][1] * mbw + blk[i][0];
+        for (int step = 0; step < 8; ++step) {
+            if (tid < 32) deblock_mb_step(PF.D, a, step, tid);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+    }
+    const int np = task_blocks(1, x, y, mbw, mbh, blk);
+    for (int i = 0; i < np; ++i)
+        plane_block(PF.F.cur[0], PF.F.W, PF.F.H, mbw, mbh, PF.pl_out, PF.F.pstride, PF.F.plsz, blk[i][0], blk[i][1], tid, kMbThreads);
+}
+
 // Pipelined run of P pictures (hl_pipeline.h): persistent workgroups, slot
 // = blockIdx % slots, tasks taken in wavefront order picture by picture.
 __global__ __launch_bounds__(kMbThreads) void k_pipeline(PipeArgs P, int mbw, int mbh)
 {
     __shared__ Shared S;
     __shared__ int32_t s_task;
-    const int tid = threadIdx.x, nmb = mbw * mbh;
+    const int nmb = mbw * mbh;
     const int slot = blockIdx.x % P.slots;
     int32_t* own = P.done + slot * nmb;
     for (;;) {
-        if (tid == 0) s_task = atomicAdd(&P.next[slot], 1);
+        if (threadIdx.x == 0) s_task = atomicAdd(&P.next[slot], 1);
         __syncthreads();
         const int t = __builtin_amdgcn_readfirstlane(s_task);
+        // opaque per task: keeps the compiler from hoisting encode_mb's
+        // lane-index arithmetic out of the task loop and holding it live
+        // across the whole body (160 spilled VGPRs without this)
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
         const int f = slot + P.slots * (t / nmb);
         if (f >= P.nframes) break;
         const PipeFrame& PF = P.fr[f];
@@ -119,19 +142,7 @@ __global__ __launch_bounds__(kMbThreads) void k_pipeline(PipeArgs P, int mbw, in
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         // deblocking, then quarter-pel planes, this decision completed
-        int blk[kMaxTaskBlocks][2];
-        const int nd = PF.deblock ? task_blocks(0, x, y, mbw, mbh, blk) : 0;
-        for (int i = 0; i < nd; ++i) {
-            const int a = blk[i][1] * mbw + blk[i][0];
-            for (int step = 0; step < 8; ++step) {
-                if (tid < 32) deblock_mb_step(PF.D, a, step, tid);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-            }
-        }
-        const int np = task_blocks(1, x, y, mbw, mbh, blk);
-        for (int i = 0; i < np; ++i)
-            plane_block(PF.F.cur[0], PF.F.W, PF.F.H, mbw, mbh, PF.pl_out, PF.F.pstride, PF.F.plsz, blk[i][0], blk[i][1], tid, kMbThreads);
+        task_filters(PF, x, y, mbw, mbh, tid);
         // publish (Guideline 16: every wave drained, barrier, release, flag)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -687,11 +698,19 @@ extern "C" int32_t hl_amd_encode_batch(hl_amd_encoder_t* e, int32_t n, const uin
 
 extern "C" int32_t hl_amd_set_pipeline(hl_amd_encoder_t* e, int32_t slots, int32_t wg_per_slot, int32_t reach)
 {
-    if (!e || slots < 1 || slots > 16 || wg_per_slot < 1 || slots * wg_per_slot > 256 || reach < 0) return HL_AMD_ERROR_INVALID_PARAMETER;
+    if (!e || slots < 1 || slots > 16 || wg_per_slot < 1 || slots * wg_per_slot > 1024 || reach < 0) return HL_AMD_ERROR_INVALID_PARAMETER;
     e->slots = slots;
     e->wg_per_slot = wg_per_slot;
     e->reach = reach;
     return HL_AMD_SUCCESS;
+}
+
+// Resident workgroups per CU of the pipelined kernel (HIP occupancy query).
+extern "C" int32_t hl_amd_pipeline_occupancy(void)
+{
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pipeline, kMbThreads, 0) != hipSuccess) return -1;
+    return n;
 }
 
 extern "C" int32_t hl_amd_encode_device(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t* u, const uint8_t* v, hl_amd_result_t* r)

@@ -104,6 +104,10 @@ int32_t hl_amd_encode_batch(hl_amd_encoder_t* encoder, int32_t n, const uint8_t*
  * at the start of every macroblock task; defaults 8 x 32, R = 2 */
 int32_t hl_amd_set_pipeline(hl_amd_encoder_t* encoder, int32_t slots, int32_t wg_per_slot, int32_t reach);
 
+/* resident workgroups per CU of the pipelined kernel (HIP occupancy query;
+ * geometry tuning), or -1 */
+int32_t hl_amd_pipeline_occupancy(void);
+
 /* reconstructed (deblocked) picture of the last encoded frame, i.e. the
  * reference picture the next frame predicts from (dpb.c:160-170) */
 int32_t hl_amd_get_recon(hl_amd_encoder_t* encoder, uint8_t* y, uint8_t* u, uint8_t* v);

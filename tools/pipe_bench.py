@@ -14,6 +14,10 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
+from hartallo_amd import _lib  # noqa: E402
+
+if os.environ.get("HL_LIB"):  # development: time a build variant (make variant-N)
+    _lib.load_library(os.path.abspath(os.environ["HL_LIB"]))
 from hartallo_amd import Encoder, synth  # noqa: E402
 
 
