@@ -27,11 +27,6 @@ build/prof/hartallo_amd/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(CSRC)/hl_wr
 	mkdir -p build/prof/hartallo_amd
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DHL_PROFILE=1 -shared -o $@ $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp
 
-# workgroup-size variants for experiments (tools/quick_bench.py)
-variant-%: $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp $(HDRS)
-	mkdir -p build/var$*
-	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DHL_MB_THREADS=$* -shared -o build/var$*/libhartallo_amd.so $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp
-
 oracle:
 	$(MAKE) -C oracle
 

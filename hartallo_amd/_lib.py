@@ -194,8 +194,8 @@ class Encoder:
             raise HlAmdError(rc, "hl_amd_encode_batch")
         return [self._result(r) for r in res] if collect else sum(r.data_size for r in res)
 
-    def set_pipeline(self, slots: int, wg_per_slot: int, reach: int):
-        rc = self.lib.hl_amd_set_pipeline(self._h, slots, wg_per_slot, reach)
+    def set_pipeline(self, workgroups: int, reach: int, window: int):
+        rc = self.lib.hl_amd_set_pipeline(self._h, workgroups, reach, window)
         if rc != HL_AMD_SUCCESS:
             raise HlAmdError(rc, "hl_amd_set_pipeline")
 

@@ -98,60 +98,162 @@ __device__ void task_filters(const PipeFrame& PF, int x, int y, int mbw, int mbh
         plane_block(PF.F.cur[0], PF.F.W, PF.F.H, mbw, mbh, PF.pl_out, PF.F.pstride, PF.F.plsz, blk[i][0], blk[i][1], tid, kMbThreads);
 }
 
-// Pipelined run of P pictures (hl_pipeline.h): persistent workgroups, slot
-// = blockIdx % slots, tasks taken in wavefront order picture by picture.
+// Dependency counters and ready queues of a run (hl_pipeline.h): only task
+// (0, 0) of the first picture starts ready.
+__global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
+{
+    const int nmb = mbw * mbh, i = blockIdx.x * 256 + threadIdx.x;
+    if (i < P.nframes * nmb) {
+        const int f = i / nmb, a = i - f * nmb;
+        int d[3][3];
+        P.cnt[i] = task_deps(f, a % mbw, a / mbw, mbw, mbh, P.reach, d);
+        P.done[i] = 0;
+        P.queue[i] = i == 0 ? 1 : 0;
+    }
+    if (i < P.nframes) {
+        P.head[i] = 0;
+        P.tail[i] = i == 0 ? 1 : 0;
+    }
+    if (i == 0) {
+        *P.oldest = 0;
+        *P.err = 0;
+    }
+}
+
+// Wave 0 takes the next ready task, oldest picture first: f * nmb + addr, or
+// -1 once the run has finished (or after ~10 s without a task: a wait gave
+// up somewhere and the host re-encodes the run).
+__device__ int pop_task(const PipeArgs& P, int nmb, bool reserved)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const int o = ld_relaxed(P.oldest);
+        if (o >= P.nframes) return -1;
+        const int w = reserved ? 1 : min(P.window, P.nframes - o);
+        int h = 0, t = 0;
+        if (lane < w) {
+            h = ld_relaxed(P.head + o + lane);
+            t = ld_relaxed(P.tail + o + lane);
+        }
+        const unsigned long long bal = __ballot(lane < w && h < t);
+        if (bal) {
+            const int i0 = __ffsll((long long)bal) - 1;
+            const int f = o + i0, hh = __builtin_amdgcn_readlane(h, i0);
+            int v = 0;
+            if (lane == 0 && atomicCAS(P.head + f, hh, hh + 1) == hh) {
+                // the slot is pushed right after the tail moved
+                for (unsigned k = 0; (v = ld_relaxed(P.queue + f * nmb + hh)) == 0; ++k)
+                    if (k > (1u << 26)) {
+                        atomicAdd(P.err, 1);
+                        v = -1;
+                        break;
+                    }
+            }
+            v = __builtin_amdgcn_readfirstlane(v);
+            if (v < 0) return -1;
+            if (v > 0) return f * nmb + v - 1;
+            continue;  // another workgroup took it
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 10 s at 100 MHz
+            if (lane == 0) atomicAdd(P.err, 1);
+            return -1;
+        }
+        __builtin_amdgcn_s_sleep(4);
+    }
+}
+
+// Pipelined run of P pictures (hl_pipeline.h): persistent workgroups taking
+// ready tasks (decision, then the deblocking and plane blocks it completes)
+// until the run has finished.
 __global__ __launch_bounds__(kMbThreads) void k_pipeline(PipeArgs P, int mbw, int mbh)
 {
     __shared__ Shared S;
     __shared__ int32_t s_task;
     const int nmb = mbw * mbh;
-    const int slot = blockIdx.x % P.slots;
-    int32_t* own = P.done + slot * nmb;
+    const bool reserved = blockIdx.x == 0;  // serves the oldest unfinished picture only
+#if defined(HL_PROFILE)
+    // per-workgroup totals (profiling build): prof[40..44] = waits for a ready
+    // task, decisions, filters, tasks, workgroup lifetime (shader clock)
+    unsigned long long pw_wait = 0, pw_mb = 0, pw_filt = 0, pw_n = 0;
+    const unsigned long long pw_t0 = __builtin_readcyclecounter();
+    unsigned long long* prof = P.fr[0].F.prof;
+#endif
     for (;;) {
-        if (threadIdx.x == 0) s_task = atomicAdd(&P.next[slot], 1);
+#if defined(HL_PROFILE)
+        const unsigned long long pt0 = __builtin_readcyclecounter();
+#endif
+        if (threadIdx.x < 64) {
+            const int t = pop_task(P, nmb, reserved);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            if (threadIdx.x == 0) s_task = t;
+        }
         __syncthreads();
         const int t = __builtin_amdgcn_readfirstlane(s_task);
+        if (t < 0) break;
         // opaque per task: keeps the compiler from hoisting encode_mb's
         // lane-index arithmetic out of the task loop and holding it live
         // across the whole body (160 spilled VGPRs without this)
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
-        const int f = slot + P.slots * (t / nmb);
-        if (f >= P.nframes) break;
+        const int f = t / nmb, addr = t - f * nmb;
         const PipeFrame& PF = P.fr[f];
-        const int addr = P.order[t % nmb];
         const int x = addr % mbw, y = addr / mbw;
         int gx = 1 << 20, gy = 1 << 20;
         if (f > 0) {
             gx = min(x + P.reach, mbw - 1);
             gy = min(y + P.reach, mbh - 1);
         }
-        // wait for the wavefront neighbours and the reference region
-        if (tid == 0) {
-            if (x > 0) spin_ge(own + addr - 1, f + 1, P.err);
-            if (y > 0) spin_ge(own + addr - mbw + (x + 1 < mbw ? 1 : 0), f + 1, P.err);
-            if (f > 0)
-                spin_ge(P.done + ((f - 1) % P.slots) * nmb + min(y + P.reach + 2, mbh - 1) * mbw + min(x + P.reach + 3, mbw - 1), f,
-                        P.err);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+#if defined(HL_PROFILE)
+        const unsigned long long pt1 = __builtin_readcyclecounter();
+#endif
         const int s_in = x == 0 ? PF.F.spec[y] : PF.F.chain[addr - 1].s_out;
         encode_mb(PF.F, S, addr, tid, kMbThreads, s_in, gx, gy);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+#if defined(HL_PROFILE)
+        const unsigned long long pt2 = __builtin_readcyclecounter();
+#endif
         // deblocking, then quarter-pel planes, this decision completed
         task_filters(PF, x, y, mbw, mbh, tid);
-        // publish (Guideline 16: every wave drained, barrier, release, flag)
+#if defined(HL_PROFILE)
+        pw_wait += pt1 - pt0;
+        pw_mb += pt2 - pt1;
+        pw_filt += __builtin_readcyclecounter() - pt2;
+        ++pw_n;
+#endif
+        // publish (Guideline 16: every wave drained, barrier, release), then
+        // release the successors; those whose last dependency this was are
+        // pushed onto their picture's ready queue
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) {
+        if (tid < 64) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            st_relaxed(own + addr, f + 1);
+            if (tid == 0) st_relaxed(P.done + t, 1);
+            int fo = 0, xo = 0, yo = 0;
+            const int ns = task_succ(f, x, y, mbw, mbh, P.reach, P.nframes, -1, fo, xo, yo);
+            for (int j = tid; j < ns; j += 64) {
+                task_succ(f, x, y, mbw, mbh, P.reach, P.nframes, j, fo, xo, yo);
+                const int a = yo * mbw + xo;
+                if (__hip_atomic_fetch_add(P.cnt + fo * nmb + a, -1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+                    const int pos = __hip_atomic_fetch_add(P.tail + fo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(P.queue + fo * nmb + pos, a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            // pictures finish in order: the last MB depends on every other one
+            // and on the previous picture's last MB
+            if (tid == 0 && addr == nmb - 1) __hip_atomic_store(P.oldest, f + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+#if defined(HL_PROFILE)
+    if (threadIdx.x == 0 && prof) {
+        atomicAdd(prof + 40, pw_wait);
+        atomicAdd(prof + 41, pw_mb);
+        atomicAdd(prof + 42, pw_filt);
+        atomicAdd(prof + 43, pw_n);
+        atomicAdd(prof + 44, __builtin_readcyclecounter() - pw_t0);
+    }
+#endif
 }
 
 static int diag_count(int mbw, int rows, int diag)
@@ -188,12 +290,13 @@ struct hl_amd_encoder_s {
     int32_t mb_launches;
     unsigned long long* d_prof;  // phase counters (HL_PROFILE builds)
     // pipelined runs of P pictures (hl_pipeline.h)
-    int slots, wg_per_slot, reach;  // 4 x 60 workgroups, R = 2 MBs by default
-    int bcap;                       // pictures the run buffers hold
-    uint8_t *d_bpic, *d_bpl;        // per picture: recon (Y|U|V), quarter-pel planes
+    int pipe_wg, reach, window;  // workgroups (0: one per resident slot), R in MBs, pictures looked at
+    int bcap;                    // pictures the run buffers hold
+    uint8_t *d_bpic, *d_bpl;     // per picture: recon (Y|U|V), quarter-pel planes
     MbRecord *d_brec, *h_brec;
     MbChain *d_bchain, *h_bchain;
-    int32_t *d_bspec, *d_done, *d_next, *d_err, *d_order;
+    int32_t *d_bspec, *d_err;
+    int32_t *d_cnt, *d_done, *d_queue, *d_head;  // scheduler state (head: [head | tail | oldest])
     PipeFrame *d_pf, *h_pf;
     std::vector<std::vector<uint8_t>> bout;  // bitstreams of the last hl_amd_encode_batch
 };
@@ -217,10 +320,11 @@ static void free_all(hl_amd_encoder_t* e)
     (void)hipFree(e->d_brec);
     (void)hipFree(e->d_bchain);
     (void)hipFree(e->d_bspec);
-    (void)hipFree(e->d_done);
-    (void)hipFree(e->d_next);
     (void)hipFree(e->d_err);
-    (void)hipFree(e->d_order);
+    (void)hipFree(e->d_cnt);
+    (void)hipFree(e->d_done);
+    (void)hipFree(e->d_queue);
+    (void)hipFree(e->d_head);
     (void)hipFree(e->d_pf);
     (void)hipHostFree(e->h_brec);
     (void)hipHostFree(e->h_bchain);
@@ -281,9 +385,9 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
         delete e;
         return HL_AMD_ERROR_OUTOFMEMMORY;
     }
-    e->slots = 8;
-    e->wg_per_slot = 32;
+    e->pipe_wg = 0;
     e->reach = 2;
+    e->window = 64;
     const StreamParams sp{e->W, e->H, p->qp, p->deblock};
     e->scratch.resize(slice_scratch_bytes(sp));
     e->out.resize(slice_scratch_bytes(sp) + 64);
@@ -465,9 +569,14 @@ static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
     (void)hipFree(e->d_bchain);
     (void)hipFree(e->d_bspec);
     (void)hipFree(e->d_pf);
+    (void)hipFree(e->d_cnt);
+    (void)hipFree(e->d_done);
+    (void)hipFree(e->d_queue);
+    (void)hipFree(e->d_head);
     (void)hipHostFree(e->h_brec);
     (void)hipHostFree(e->h_bchain);
     (void)hipHostFree(e->h_pf);
+    e->d_cnt = e->d_done = e->d_queue = e->d_head = nullptr;
     e->bcap = 0;
     hipError_t r;
     if ((r = hipMalloc(&e->d_bpic, pic * n)) || (r = hipMalloc(&e->d_bpl, 4 * e->plsz * n)) ||
@@ -475,20 +584,11 @@ static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
         (r = hipMalloc(&e->d_bspec, sizeof(int32_t) * e->mbh * n)) || (r = hipMalloc(&e->d_pf, sizeof(PipeFrame) * n)) ||
         (r = hipHostMalloc(&e->h_brec, sizeof(MbRecord) * nmb * n, hipHostMallocDefault)) ||
         (r = hipHostMalloc(&e->h_bchain, sizeof(MbChain) * nmb * n, hipHostMallocDefault)) ||
-        (r = hipHostMalloc(&e->h_pf, sizeof(PipeFrame) * n, hipHostMallocDefault)))
+        (r = hipHostMalloc(&e->h_pf, sizeof(PipeFrame) * n, hipHostMallocDefault)) ||
+        (r = hipMalloc(&e->d_cnt, sizeof(int32_t) * nmb * n)) || (r = hipMalloc(&e->d_done, sizeof(int32_t) * nmb * n)) ||
+        (r = hipMalloc(&e->d_queue, sizeof(int32_t) * nmb * n)) || (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * n + 1))))
         return r;
-    if (!e->d_done) {
-        if ((r = hipMalloc(&e->d_done, sizeof(int32_t) * nmb * 16)) || (r = hipMalloc(&e->d_next, sizeof(int32_t) * 16)) ||
-            (r = hipMalloc(&e->d_err, sizeof(int32_t) * 4)) || (r = hipMalloc(&e->d_order, sizeof(int32_t) * nmb)))
-            return r;
-        std::vector<int32_t> order;  // wavefront order: anti-diagonals d = x + 2y, top to bottom
-        for (int d = 0; d < e->mbw + 2 * e->mbh; ++d)
-            for (int y = 0; y < e->mbh; ++y) {
-                const int x = d - 2 * y;
-                if (x >= 0 && x < e->mbw) order.push_back(y * e->mbw + x);
-            }
-        if ((r = hipMemcpy(e->d_order, order.data(), sizeof(int32_t) * nmb, hipMemcpyHostToDevice))) return r;
-    }
+    if (!e->d_err && (r = hipMalloc(&e->d_err, sizeof(int32_t) * 4))) return r;
     std::vector<int32_t> spec((size_t)e->mbh * n, 9);  // speculated rdo.Single_ctr at every row start
     if ((r = hipMemcpy(e->d_bspec, spec.data(), sizeof(int32_t) * spec.size(), hipMemcpyHostToDevice))) return r;
     e->bcap = n;
@@ -583,8 +683,8 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         F.rec = e->d_brec + nmb * k;
         F.chain = e->d_bchain + nmb * k;
         F.spec = e->d_bspec + e->mbh * k;
-        F.ref_done = k == 0 ? nullptr : e->d_done + ((k - 1) % e->slots) * nmb;
-        F.ref_epoch = k;
+        F.ref_done = k == 0 ? nullptr : e->d_done + (k - 1) * nmb;
+        F.ref_epoch = 1;
         F.perr = e->d_err;
         pf.D.W = e->W;
         pf.D.H = e->H;
@@ -598,20 +698,30 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         pf.deblock = e->p.deblock;
     }
     HL_HIP_CHECK(hipMemcpyAsync(e->d_pf, e->h_pf, sizeof(PipeFrame) * m, hipMemcpyHostToDevice, e->stream));
-    HL_HIP_CHECK(hipMemsetAsync(e->d_done, 0, sizeof(int32_t) * nmb * e->slots, e->stream));
-    HL_HIP_CHECK(hipMemsetAsync(e->d_next, 0, sizeof(int32_t) * 16, e->stream));
-    HL_HIP_CHECK(hipMemsetAsync(e->d_err, 0, sizeof(int32_t) * 4, e->stream));
     PipeArgs P;
     P.fr = e->d_pf;
     P.nframes = m;
-    P.slots = e->slots;
-    P.order = e->d_order;
-    P.done = e->d_done;
-    P.next = e->d_next;
-    P.err = e->d_err;
     P.reach = e->reach;
+    P.window = e->window;
+    P.cnt = e->d_cnt;
+    P.done = e->d_done;
+    P.queue = e->d_queue;
+    P.head = e->d_head;
+    P.tail = e->d_head + m;
+    P.oldest = e->d_head + 2 * m;
+    P.err = e->d_err;
+    k_pipe_init<<<(unsigned)((nmb * m + 255) / 256), 256, 0, e->stream>>>(P, e->mbw, e->mbh);
+    HL_HIP_CHECK(hipGetLastError());
+    int wgs = e->pipe_wg;
+    if (wgs <= 0) {  // one workgroup per resident slot of the device
+        int dev = 0, cus = 0, occ = 0;
+        HL_HIP_CHECK(hipGetDevice(&dev));
+        HL_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        HL_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_pipeline, kMbThreads, 0));
+        wgs = std::max(1, cus * occ);
+    }
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[4], e->stream));
-    k_pipeline<<<e->slots * e->wg_per_slot, kMbThreads, 0, e->stream>>>(P, e->mbw, e->mbh);
+    k_pipeline<<<wgs, kMbThreads, 0, e->stream>>>(P, e->mbw, e->mbh);
     HL_HIP_CHECK(hipGetLastError());
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[5], e->stream));
     int32_t err = 0;
@@ -696,12 +806,13 @@ extern "C" int32_t hl_amd_encode_batch(hl_amd_encoder_t* e, int32_t n, const uin
     return HL_AMD_SUCCESS;
 }
 
-extern "C" int32_t hl_amd_set_pipeline(hl_amd_encoder_t* e, int32_t slots, int32_t wg_per_slot, int32_t reach)
+extern "C" int32_t hl_amd_set_pipeline(hl_amd_encoder_t* e, int32_t workgroups, int32_t reach, int32_t window)
 {
-    if (!e || slots < 1 || slots > 16 || wg_per_slot < 1 || slots * wg_per_slot > 1024 || reach < 0) return HL_AMD_ERROR_INVALID_PARAMETER;
-    e->slots = slots;
-    e->wg_per_slot = wg_per_slot;
+    if (!e || workgroups < 0 || workgroups > 4096 || reach < 0 || reach > 16 || window < 1 || window > 64)
+        return HL_AMD_ERROR_INVALID_PARAMETER;
+    e->pipe_wg = workgroups;
     e->reach = reach;
+    e->window = window;
     return HL_AMD_SUCCESS;
 }
 

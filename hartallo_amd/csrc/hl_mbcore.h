@@ -57,11 +57,10 @@ constexpr int kProfSlots = 12;
 #endif
 
 constexpr int kPad = 40;  // padding of the luma reference planes (origin clip is +-17, block 16, tap 3)
-constexpr int kMaxWaves = 16;  // workgroup of up to 1024 lanes per macroblock
-#ifndef HL_MB_THREADS
-#define HL_MB_THREADS 512
-#endif
-constexpr int kMbThreads = HL_MB_THREADS;          // lanes of the macroblock workgroup
+constexpr int kMaxWaves = 8;   // waves of the macroblock workgroup
+// lanes of the macroblock workgroup: 512 is the only size whose output has
+// been checked against the reference (a 256-lane build emits other bytes)
+constexpr int kMbThreads = 512;
 constexpr int kMbRows = kMbThreads / 16;           // 16-lane rows
 constexpr int kMaxPass = (9 * 16 + kMbRows - 1) / kMbRows;  // rows per lane for the largest step
 
@@ -980,31 +979,49 @@ struct Best {
 
 HD int ilog2_small(int v) { return v >= 16 ? 4 : (v >= 8 ? 3 : (v >= 4 ? 2 : (v >= 2 ? 1 : 0))); }
 
+// Pipelined runs (hl_pipeline.h): the task of a picture after which the
+// quarter-pel planes of all its MBs (X' <= X, Y' <= Y) are final.  Plane
+// blocks of (X, Y) run in task (X+2, Y+2), in the last rows in (X+3, mbh-1)
+// (trig_pl); a finished task implies every task before it in both
+// wavefront directions.  Model-checked by tests/test_pipeline_schedule.py.
+HD void reach_task(int X, int Y, int mbw, int mbh, int& tx, int& ty)
+{
+    ty = Y + 2 < mbh - 1 ? Y + 2 : mbh - 1;
+    const int k = ty == mbh - 1 ? 3 : 2;
+    tx = X + k < mbw - 1 ? X + k : mbw - 1;
+}
+
 // Pipelined runs: before a partition search, make sure the reference
-// picture's planes cover its motion window.  The diamond window is the
-// initial centre (the MVP or (0,0)) +- me_range in the integer stage, and
-// the half / quarter stages move at most me_range / 2 + me_range / 4 more,
-// so +-2 * me_range (+4 for rounding and the second tap plane) bounds every
-// fetch.  The task start guarantees MBs up to (gx, gy); a window reaching
-// further waits for the reference picture's task whose staircase covers it
-// (hl_pipeline.h).  Negative directions are always covered.
+// picture's planes cover its motion window.  The integer diamond stays
+// within +-me_range of its start (the MVP or (0,0), me_ds.c:302-358); the
+// half and quarter stages add at most me_range / 2 + me_range / 4 pels
+// (me_ds.c:360-470), and a quarter-pel fetch reads one sample further: the
+// last sample read lies within start + 1.75 * me_range + 2 of the block.
+// The task start guarantees MBs up to (gx, gy); a window reaching further
+// waits for the reference picture's task that covers it.  Negative
+// directions are always covered.
 HD void reach_wait(Ctx& c, const PartGeo& g, const int pmv[2])
 {
 #if defined(__HIP_DEVICE_COMPILE__)
     const FrameArgs& F = c.F;
     if (!F.ref_done) return;
-    const int px = c.xL + g.px + g.pw + (pmv[0] > 0 ? pmv[0] >> 2 : 0) + 2 * F.me_range + 4;
-    const int py = c.yL + g.py + g.ph + (pmv[1] > 0 ? pmv[1] >> 2 : 0) + 2 * F.me_range + 4;
+    const int ext = F.me_range + (F.me_range >> 1) + ((F.me_range + 3) >> 2) + 2;
+    const int px = c.xL + g.px + g.pw - 1 + (pmv[0] > 0 ? pmv[0] >> 2 : 0) + ext;
+    const int py = c.yL + g.py + g.ph - 1 + (pmv[1] > 0 ? pmv[1] >> 2 : 0) + ext;
     int X = min(F.mbw - 1, max(0, px >> 4)), Y = min(F.mbh - 1, max(0, py >> 4));
     if (X <= c.gx && Y <= c.gy) return;
     X = max(X, c.gx);
     Y = max(Y, c.gy);
+    HL_PROF_T(tw);
     if (c.tid == 0) {
-        spin_ge(F.ref_done + min(Y + 2, F.mbh - 1) * F.mbw + min(X + 3, F.mbw - 1), F.ref_epoch, F.perr);
+        int tx, ty;
+        reach_task(X, Y, F.mbw, F.mbh, tx, ty);
+        spin_ge(F.ref_done + ty * F.mbw + tx, F.ref_epoch, F.perr);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     HL_SYNC();
+    HL_PROF_ADD(c, 9, tw);
     c.gx = X;
     c.gy = Y;
 #else

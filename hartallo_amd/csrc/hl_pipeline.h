@@ -18,19 +18,25 @@
 //  * picture f+1 reads picture f's quarter-pel planes and chroma, and the
 //    per-address MbState objects that persist across pictures
 //    (hl_codec_264_mb_t, mb.h:99-269).  Task (f+1, x, y) waits until picture
-//    f has finished every task in the staircase below (x+R+3, y+R+2): that
+//    f has finished every task in the staircase below (x+R+2, y+R+2): that
 //    covers the planes of MBs up to (x+R, y+R) and every reader of the
 //    MbState it overwrites.  A partition search whose motion window reaches
 //    further waits for more (reach_wait in hl_mbcore.h).
 //
-// Frames are spread over S slots of W workgroups each (slot = frame mod S);
-// picture f only ever waits for picture f-1, so the slots cannot deadlock
-// once the grid (S x W <= 256 workgroups, one per CU) is resident.
+// Scheduling is readiness-driven: every task (picture f, MB) has a counter
+// of unfinished dependencies (task_deps); the workgroup that finishes a task
+// decrements the counters of its successors (task_succ, the exact inverse)
+// and pushes those that reach zero onto their picture's ready queue.
+// Workgroups pop ready tasks, oldest picture first, so no workgroup ever holds
+// a task that cannot run yet.  The one wait left inside a task (reach_wait,
+// for motion windows beyond the guaranteed reach) only ever waits for the
+// previous picture; workgroup 0 serves the oldest unfinished picture alone,
+// whose reference is complete, so the run always progresses.
 // Hand-offs between workgroups use the agent-scope release/acquire protocol
 // of the gfx950 guide (cdna_hip_programming.md, Guideline 16): payload
-// stores, s_waitcnt vmcnt(0) in every wave, barrier, one lane's release
-// fence, then a relaxed agent-scope flag store; consumers poll the flag
-// relaxed, then one agent-scope acquire.  Every spin is bounded.
+// stores, s_waitcnt vmcnt(0) in every wave, barrier, one wave's release
+// fence, then the counter / queue / flag atomics; consumers acquire once
+// before reading.  Every wait is bounded.
 #pragma once
 #include "hl_filters.h"
 
@@ -101,14 +107,74 @@ struct PipeFrame {
     int32_t deblock;  // deblocking enabled (disable_deblocking_filter_idc 0)
 };
 
+// Dependencies of task (f, x, y) inside a run: the wavefront neighbours
+// (x-1, y) and (x+1, y-1) (or (x, y-1) in the last column) and, from the
+// second picture of the run on, the task of picture f-1 that completes the
+// planes of MBs up to (x+R, y+R) (reach_task: (x+R+2, y+R+2) inside the
+// picture), which also covers every reader of the MB state it overwrites.
+HD int task_deps(int f, int x, int y, int mbw, int mbh, int R, int out[3][3])
+{
+    int n = 0;
+    if (x > 0) {
+        out[n][0] = f, out[n][1] = x - 1, out[n][2] = y;
+        ++n;
+    }
+    if (y > 0) {
+        out[n][0] = f, out[n][1] = x + 1 < mbw ? x + 1 : x, out[n][2] = y - 1;
+        ++n;
+    }
+    if (f > 0) {
+        out[n][0] = f - 1;
+        reach_task(x + R, y + R, mbw, mbh, out[n][1], out[n][2]);
+        ++n;
+    }
+    return n;
+}
+
+// Successors of task (f, X, Y): the tasks whose task_deps name it.  Returns
+// their number and, for j below it, the j-th in (fo, xo, yo): in-picture ones
+// first, then a rectangle of picture f+1 (several tasks at the right and
+// bottom edges, where the staircase corner is clamped).
+HD int task_succ(int f, int X, int Y, int mbw, int mbh, int R, int nframes, int j, int& fo, int& xo, int& yo)
+{
+    int n = 0;
+    if (X + 1 < mbw) {  // (X+1, Y) waits on its left neighbour
+        if (j == n) fo = f, xo = X + 1, yo = Y;
+        ++n;
+    }
+    if (Y + 1 < mbh) {
+        if (X > 0) {  // (X-1, Y+1) waits on its top-right neighbour
+            if (j == n) fo = f, xo = X - 1, yo = Y + 1;
+            ++n;
+        }
+        if (X == mbw - 1) {  // in the last column, on the one above
+            if (j == n) fo = f, xo = X, yo = Y + 1;
+            ++n;
+        }
+    }
+    if (f + 1 < nframes) {
+        const int k = Y == mbh - 1 ? 3 : 2;
+        const int xa = X < mbw - 1 ? X - R - k : (mbw - 1 - R - k > 0 ? mbw - 1 - R - k : 0);
+        const int ya = Y < mbh - 1 ? Y - R - 2 : (mbh - 1 - R - 2 > 0 ? mbh - 1 - R - 2 : 0);
+        const int nx = X < mbw - 1 ? (xa >= 0 ? 1 : 0) : mbw - xa, ny = Y < mbh - 1 ? (ya >= 0 ? 1 : 0) : mbh - ya;
+        if (j >= n && j < n + nx * ny) fo = f + 1, xo = xa + (j - n) % nx, yo = ya + (j - n) / nx;
+        n += nx * ny;
+    }
+    return n;
+}
+
 struct PipeArgs {
     const PipeFrame* fr;
-    int32_t nframes, slots;
-    const int32_t* order;  // MB addresses in wavefront (anti-diagonal) order
-    int32_t* done;         // [slots][nmb]: picture index + 1 once the task of MB addr finished
-    int32_t* next;         // [slots] task counters
-    int32_t* err;          // [0] = number of bounded spins that gave up
-    int32_t reach;         // guaranteed reference reach R in MBs
+    int32_t nframes;
+    int32_t reach;   // guaranteed reference reach R in MBs
+    int32_t window;  // pictures a workgroup looks at for ready tasks (from the oldest unfinished)
+    int32_t* cnt;    // [nframes][nmb] unfinished dependencies
+    int32_t* done;   // [nframes][nmb] 1 once the task finished (reach_wait polls it)
+    int32_t* queue;  // [nframes][nmb] ready tasks, MB address + 1 (0 = slot not yet written)
+    int32_t* head;   // [nframes] next queue slot to pop
+    int32_t* tail;   // [nframes] next queue slot to push
+    int32_t* oldest; // [0] first unfinished picture of the run
+    int32_t* err;    // [0] number of bounded waits that gave up
 };
 
 }  // namespace hl

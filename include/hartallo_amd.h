@@ -99,10 +99,13 @@ int32_t hl_amd_encode_device(hl_amd_encoder_t* encoder, const uint8_t* y, const 
 int32_t hl_amd_encode_batch(hl_amd_encoder_t* encoder, int32_t n, const uint8_t* const* y, const uint8_t* const* u,
                             const uint8_t* const* v, hl_amd_result_t* results);
 
-/* pipelined-run geometry: picture slots x workgroups per slot (<= 256 in
- * all, one workgroup per CU) and the reference reach R (in MBs) guaranteed
- * at the start of every macroblock task; defaults 8 x 32, R = 2 */
-int32_t hl_amd_set_pipeline(hl_amd_encoder_t* encoder, int32_t slots, int32_t wg_per_slot, int32_t reach);
+/* pipelined-run scheduling: persistent workgroups (0 = one per resident
+ * workgroup slot of the device, <= 4096), the reference reach R in MBs
+ * (0..16) that a macroblock task of picture f+1 waits for in picture f
+ * before it becomes ready, and the pictures (1..64, from the oldest
+ * unfinished one) a workgroup looks at for ready tasks; defaults 0, 2, 64.
+ * Results do not depend on these. */
+int32_t hl_amd_set_pipeline(hl_amd_encoder_t* encoder, int32_t workgroups, int32_t reach, int32_t window);
 
 /* resident workgroups per CU of the pipelined kernel (HIP occupancy query;
  * geometry tuning), or -1 */

@@ -176,3 +176,30 @@ extern "C" int emu_task_blocks(int kind, int x, int y, int mbw, int mbh, int* ou
     }
     return n;
 }
+
+// Dependencies / successors of pipelined-run tasks (hl_pipeline.h) as
+// (f, x, y) triples.
+extern "C" int emu_task_deps(int f, int x, int y, int mbw, int mbh, int R, int* out)
+{
+    int d[3][3];
+    const int n = task_deps(f, x, y, mbw, mbh, R, d);
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) out[3 * i + k] = d[i][k];
+    return n;
+}
+extern "C" int emu_task_succ(int f, int x, int y, int mbw, int mbh, int R, int nframes, int* out)
+{
+    int fo = 0, xo = 0, yo = 0;
+    const int n = task_succ(f, x, y, mbw, mbh, R, nframes, -1, fo, xo, yo);
+    for (int j = 0; j < n; ++j) {
+        task_succ(f, x, y, mbw, mbh, R, nframes, j, fo, xo, yo);
+        out[3 * j] = fo;
+        out[3 * j + 1] = xo;
+        out[3 * j + 2] = yo;
+    }
+    return n;
+}
+extern "C" void emu_reach_task(int X, int Y, int mbw, int mbh, int* out)
+{
+    reach_task(X, Y, mbw, mbh, out[0], out[1]);
+}

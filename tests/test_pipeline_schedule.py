@@ -14,6 +14,17 @@ and (x+1, y-1)); the checks:
      reference deblocks after the whole picture, slice.c:1868-1880);
   3. planes(X, Y) after the deblocking of its 3x3 neighbourhood (6-tap reach);
   4. every deblock and plane block exactly once.
+Across the pictures of a run (readiness-driven scheduling, task_deps /
+task_succ):
+  5. the successors of every task are exactly the tasks that name it as a
+     dependency (the counters of the scheduler reach zero exactly once);
+  6. in random orders of several pictures, task (f+1, x, y) runs after
+     picture f finished the planes of every MB (X <= x+R, Y <= y+R) (the
+     guaranteed reach) and every decision and deblocking that reads the
+     per-address MB state it overwrites; pictures finish in order;
+  7. once task reach_task(X, Y) finished, the planes of every MB (X' <= X,
+     Y' <= Y) are final (the wait of partition searches whose motion window
+     reaches beyond R).
 """
 import ctypes
 import random
@@ -29,19 +40,36 @@ def _blocks(lib, kind, x, y, mbw, mbh):
     return [(out[2 * i], out[2 * i + 1]) for i in range(n)]
 
 
-def _deps(x, y, mbw):
-    d = []
-    if x > 0:
-        d.append((x - 1, y))
-    if y > 0:
-        d.append((x + 1, y - 1) if x + 1 < mbw else (x, y - 1))
-    return d
+def _triples(out, n):
+    return [(out[3 * i], out[3 * i + 1], out[3 * i + 2]) for i in range(n)]
+
+
+def _task_deps(lib, f, x, y, mbw, mbh, R):
+    out = (ctypes.c_int * 9)()
+    return _triples(out, lib.emu_task_deps(f, x, y, mbw, mbh, R, out))
+
+
+def _task_succ(lib, f, x, y, mbw, mbh, R, nframes):
+    out = (ctypes.c_int * (3 * 512))()
+    return _triples(out, lib.emu_task_succ(f, x, y, mbw, mbh, R, nframes, out))
+
+
+def _lib():
+    lib = emu_lib()
+    lib.emu_task_blocks.argtypes = [ctypes.c_int] * 5 + [ctypes.POINTER(ctypes.c_int)]
+    lib.emu_task_deps.argtypes = [ctypes.c_int] * 6 + [ctypes.POINTER(ctypes.c_int)]
+    lib.emu_task_succ.argtypes = [ctypes.c_int] * 7 + [ctypes.POINTER(ctypes.c_int)]
+    lib.emu_reach_task.argtypes = [ctypes.c_int] * 4 + [ctypes.POINTER(ctypes.c_int)]
+    return lib
+
+
+def _deps(lib, x, y, mbw, mbh):  # inside one picture
+    return [(a, b) for (_, a, b) in _task_deps(lib, 0, x, y, mbw, mbh, 0)]
 
 
 @pytest.mark.parametrize("mbw,mbh", [(1, 1), (2, 1), (1, 2), (2, 2), (3, 3), (4, 2), (2, 4), (5, 7), (11, 9), (22, 18), (8, 3)])
 def test_task_schedule(mbw, mbh):
-    lib = emu_lib()
-    lib.emu_task_blocks.argtypes = [ctypes.c_int] * 5 + [ctypes.POINTER(ctypes.c_int)]
+    lib = _lib()
     tdb = {(x, y): _blocks(lib, 0, x, y, mbw, mbh) for y in range(mbh) for x in range(mbw)}
     tpl = {(x, y): _blocks(lib, 1, x, y, mbw, mbh) for y in range(mbh) for x in range(mbw)}
     inside = lambda p: 0 <= p[0] < mbw and 0 <= p[1] < mbh  # noqa: E731
@@ -49,7 +77,7 @@ def test_task_schedule(mbw, mbh):
         rng = random.Random(seed)
         done, order, pending = set(), [], [(x, y) for y in range(mbh) for x in range(mbw)]
         while pending:
-            t = rng.choice([p for p in pending if all(d in done for d in _deps(*p, mbw))])
+            t = rng.choice([p for p in pending if all(d in done for d in _deps(lib, *p, mbw, mbh))])
             pending.remove(t)
             done.add(t)
             order.append(t)
@@ -70,3 +98,82 @@ def test_task_schedule(mbw, mbh):
                 assert (X, Y) not in planed
                 planed.add((X, Y))
         assert len(deblocked) == len(planed) == mbw * mbh
+
+
+@pytest.mark.parametrize("mbw,mbh,R,nf", [(1, 1, 0, 3), (2, 3, 0, 4), (5, 4, 2, 3), (9, 6, 1, 3), (12, 7, 3, 2), (4, 9, 4, 3), (20, 3, 2, 2)])
+def test_task_successors_invert_dependencies(mbw, mbh, R, nf):
+    lib = _lib()
+    tasks = [(f, x, y) for f in range(nf) for y in range(mbh) for x in range(mbw)]
+    deps = {t: _task_deps(lib, *t, mbw, mbh, R) for t in tasks}
+    succ = {t: _task_succ(lib, *t, mbw, mbh, R, nf) for t in tasks}
+    inv = {t: [] for t in tasks}
+    for t in tasks:
+        assert len(set(deps[t])) == len(deps[t])
+        for d in deps[t]:
+            assert d in inv, (t, d)
+            inv[d].append(t)
+    for t in tasks:
+        assert sorted(succ[t]) == sorted(inv[t]), t
+        assert len(set(succ[t])) == len(succ[t])
+
+
+@pytest.mark.parametrize("mbw,mbh,R", [(3, 3, 0), (6, 5, 1), (9, 7, 2), (13, 6, 3), (5, 9, 0), (2, 2, 2), (12, 3, 2), (10, 2, 1), (8, 1, 0), (16, 4, 3), (7, 1, 2)])
+def test_run_schedule_across_pictures(mbw, mbh, R):
+    lib = _lib()
+    nf = 3
+    tasks = [(f, x, y) for f in range(nf) for y in range(mbh) for x in range(mbw)]
+    deps = {t: _task_deps(lib, *t, mbw, mbh, R) for t in tasks}
+    tdb = {(x, y): _blocks(lib, 0, x, y, mbw, mbh) for y in range(mbh) for x in range(mbw)}
+    tpl = {(x, y): _blocks(lib, 1, x, y, mbw, mbh) for y in range(mbh) for x in range(mbw)}
+    inside = lambda p: 0 <= p[0] < mbw and 0 <= p[1] < mbh  # noqa: E731
+    for seed in range(8):
+        rng = random.Random(seed)
+        done, pending = set(), set(tasks)
+        deblocked, planed, decided = set(), set(), set()
+        finished = []
+        while pending:
+            ready = sorted(t for t in pending if all(d in done for d in deps[t]))
+            t = rng.choice(ready)
+            f, x, y = t
+            if f > 0:
+                for X in range(min(x + R, mbw - 1) + 1):
+                    for Y in range(min(y + R, mbh - 1) + 1):
+                        assert (f - 1, X, Y) in planed, ("reach", t, (X, Y))
+                for r in [(x + 1, y), (x - 1, y + 1), (x, y + 1), (x + 1, y + 1)]:
+                    assert not inside(r) or (f - 1, *r) in decided, ("state reader pending", t, r)
+                for r in [(x, y), (x + 1, y), (x, y + 1)]:
+                    assert not inside(r) or (f - 1, *r) in deblocked, ("deblock reader pending", t, r)
+            pending.remove(t)
+            done.add(t)
+            decided.add(t)
+            for (X, Y) in tdb[(x, y)]:
+                deblocked.add((f, X, Y))
+            for (X, Y) in tpl[(x, y)]:
+                planed.add((f, X, Y))
+            if (x, y) == (mbw - 1, mbh - 1):
+                assert all((f, a, b) in done for a in range(mbw) for b in range(mbh)), "picture finished out of order"
+                finished.append(f)
+        assert finished == list(range(nf))
+
+
+@pytest.mark.parametrize("mbw,mbh", [(1, 1), (3, 2), (6, 5), (9, 7), (12, 3), (8, 1), (1, 6), (15, 9)])
+def test_reach_task(mbw, mbh):
+    lib = _lib()
+    tpl = {(x, y): _blocks(lib, 1, x, y, mbw, mbh) for y in range(mbh) for x in range(mbw)}
+    out = (ctypes.c_int * 2)()
+    reach = {}
+    for X in range(mbw):
+        for Y in range(mbh):
+            lib.emu_reach_task(X, Y, mbw, mbh, out)
+            assert 0 <= out[0] < mbw and 0 <= out[1] < mbh
+            reach.setdefault((out[0], out[1]), []).append((X, Y))
+    for seed in range(8):
+        rng = random.Random(seed)
+        done, planed, pending = set(), set(), [(x, y) for y in range(mbh) for x in range(mbw)]
+        while pending:
+            t = rng.choice([p for p in pending if all(d in done for d in _deps(lib, *p, mbw, mbh))])
+            pending.remove(t)
+            done.add(t)
+            planed.update(tpl[t])
+            for (X, Y) in reach.get(t, []):
+                assert all((a, b) in planed for a in range(X + 1) for b in range(Y + 1)), ("reach_task", (X, Y), t)

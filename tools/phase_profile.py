@@ -16,7 +16,7 @@ import hartallo_amd  # noqa: E402
 from hartallo_amd import _lib, synth  # noqa: E402
 
 PHASES = ["eval:block", "eval:nC", "eval:reduce", "search_partition", "mvp", "guess_intra(P)", "mb_begin", "mb_end", "whole MB",
-          "-", "intra:i16", "intra:i4"]
+          "reach_wait", "intra:i16", "intra:i4"]
 
 
 def main():

@@ -1,6 +1,6 @@
 """Timing of pipelined runs on the bench workload for several geometries.
 
-  python tools/pipe_bench.py [frames] [S,W,R ...]
+  python tools/pipe_bench.py [frames] [workgroups,R,window ...]
 
 Development tool: 1920x1088 QP28 ME16 deblock; two warm-up pictures (I, P)
 one call at a time, then `frames` P pictures in one hl_amd_encode_batch.
@@ -16,14 +16,14 @@ import torch  # noqa: E402
 
 from hartallo_amd import _lib  # noqa: E402
 
-if os.environ.get("HL_LIB"):  # development: time a build variant (make variant-N)
+if os.environ.get("HL_LIB"):  # development: time another build of the library
     _lib.load_library(os.path.abspath(os.environ["HL_LIB"]))
 from hartallo_amd import Encoder, synth  # noqa: E402
 
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 12
-    geos = [tuple(map(int, g.split(","))) for g in sys.argv[2:]] or [(4, 60, 2)]
+    geos = [tuple(map(int, g.split(","))) for g in sys.argv[2:]] or [(0, 2, 64)]
     W, H = 1920, 1088
     clip = synth.clip(W, H, n + 2, 11)
     dev = torch.from_numpy(clip).cuda()
@@ -40,7 +40,7 @@ def main():
         nbytes = enc.encode_batch_device(ptrs[2:], collect=False)
         dt = time.perf_counter() - t
         ms = enc.timing_ms()
-        print(f"S,W,R={g}: {n} P pictures in {dt * 1e3:.1f} ms = {n / dt:.2f} fps (kernel {ms[1]:.1f} ms, reruns {enc.last_reruns()}, {nbytes} bytes)",
+        print(f"wg,R,window={g}: {n} P pictures in {dt * 1e3:.1f} ms = {n / dt:.2f} fps (kernel {ms[1]:.1f} ms, reruns {enc.last_reruns()}, {nbytes} bytes)",
               flush=True)
         enc.close()
 

@@ -1,0 +1,67 @@
+"""Where the workgroups of a pipelined run spend their time (profiling build,
+`make profile`).
+
+  python tools/pipe_profile.py [frames] [workgroups,R,window]
+
+Development tool: 1920x1088 QP28 ME16 deblock; I and P warm-up pictures one
+call at a time, then `frames` P pictures in one hl_amd_encode_batch.  Prints
+the per-workgroup split of k_pipeline's lifetime (task-start waits,
+decisions, deblocking + planes, the rest = taking tasks / draining) and the
+per-MB phases of the decisions.
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from hartallo_amd import _lib  # noqa: E402
+
+_lib.load_library(os.path.join(ROOT, "build", "prof", "hartallo_amd", "libhartallo_amd.so"))
+from hartallo_amd import Encoder, synth  # noqa: E402
+
+PHASES = ["eval:block", "eval:nC", "eval:reduce", "search_partition", "mvp", "guess_intra(P)", "mb_begin", "mb_end", "whole MB",
+          "reach_wait", "intra:i16", "intra:i4"]
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+    geo = tuple(map(int, sys.argv[2].split(","))) if len(sys.argv) > 2 else (0, 2, 64)
+    W, H = 1920, 1088
+    nmb = (W // 16) * (H // 16)
+    clip = synth.clip(W, H, n + 2, 11)
+    dev = torch.from_numpy(clip).cuda()
+    torch.cuda.synchronize()
+    ny, nc = W * H, W * H // 4
+    ptrs = [(dev[i].data_ptr(), dev[i].data_ptr() + ny, dev[i].data_ptr() + ny + nc) for i in range(n + 2)]
+    enc = Encoder(W, H, 28, 16, 1, 30)
+    enc.set_pipeline(*geo)
+    enc.set_timing(True)
+    for i in range(2):
+        enc.encode_device(*ptrs[i], collect=False)
+    enc.profile_counters(64)  # reset
+    t = time.perf_counter()
+    enc.encode_batch_device(ptrs[2:], collect=False)
+    dt = time.perf_counter() - t
+    ms = enc.timing_ms()
+    cnt = enc.profile_counters(64)
+    print(f"wg,R,window={geo}: {n} P pictures in {dt * 1e3:.1f} ms (kernel {ms[1]:.1f} ms, reruns {enc.last_reruns()})")
+    life, wait, mb, filt, tasks = cnt[44], cnt[40], cnt[41], cnt[42], cnt[43]
+    if life:
+        wgs = geo[0] or 256
+        print(f"   workgroups {wgs}, tasks {tasks} ({tasks / max(1, n * nmb):.2f} per MB), mean lifetime {life / wgs / 1e6:.1f} Mcycles"
+              f" (~{life / wgs / (ms[1] * 1e-3) / 1e9:.2f} GHz shader clock if the kernel spans it)")
+        for name, v in (("task-start waits", wait), ("decisions", mb), ("deblock + planes", filt), ("rest", life - wait - mb - filt)):
+            print(f"   {name:18s} {100.0 * v / life:6.1f} %   {v / max(1, tasks) / 1e3:9.1f} kcycles/task")
+    for i, name in enumerate(PHASES):
+        cyc, calls = cnt[2 * i], cnt[2 * i + 1]
+        if calls:
+            print(f"   {name:18s} calls/MB {calls / (n * nmb):8.1f}  cycles/call {cyc / calls:10.0f}  kcycles/MB {cyc / (n * nmb) / 1e3:9.1f}")
+    enc.close()
+
+
+if __name__ == "__main__":
+    main()
