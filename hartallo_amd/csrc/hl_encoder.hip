@@ -11,9 +11,15 @@
 //   5. host CAVLC serialisation of the MB records (hl_writer.cpp)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/hartallo_amd.h"
@@ -242,7 +248,13 @@ __global__ __launch_bounds__(kMbThreads) void k_pipeline(PipeArgs P, int mbw, in
             }
             // pictures finish in order: the last MB depends on every other one
             // and on the previous picture's last MB
-            if (tid == 0 && addr == nmb - 1) __hip_atomic_store(P.oldest, f + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0 && addr == nmb - 1) {
+                __hip_atomic_store(P.oldest, f + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                // every record of picture f is in memory (the last MB's task
+                // transitively acquired all of them): tell the host, whose
+                // copy engine can fetch them while the run goes on
+                if (P.progress) __hip_atomic_store(P.progress, f + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
     }
 #if defined(HL_PROFILE)
@@ -299,6 +311,12 @@ struct hl_amd_encoder_s {
     int32_t *d_cnt, *d_done, *d_queue, *d_head;  // scheduler state (head: [head | tail | oldest])
     PipeFrame *d_pf, *h_pf;
     std::vector<std::vector<uint8_t>> bout;  // bitstreams of the last hl_amd_encode_batch
+    // host side of a run: pictures finished by k_pipeline (mapped host word),
+    // a copy stream for their records, slice writers working meanwhile
+    int32_t *h_prog, *d_prog;
+    hipStream_t cstream;
+    int nwriters;
+    std::vector<std::vector<uint8_t>> wscratch, wout;
 };
 
 static void free_all(hl_amd_encoder_t* e)
@@ -332,7 +350,9 @@ static void free_all(hl_amd_encoder_t* e)
     (void)hipHostFree(e->h_rec);
     (void)hipHostFree(e->h_chain);
     (void)hipHostFree(e->h_spec);
+    (void)hipHostFree(e->h_prog);
     if (e->stream) (void)hipStreamDestroy(e->stream);
+    if (e->cstream) (void)hipStreamDestroy(e->cstream);
     for (int i = 0; i < 6; ++i)
         if (e->ev[i]) (void)hipEventDestroy(e->ev[i]);
 }
@@ -357,7 +377,10 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
     e->qpc = kQpToQpc[p->qp];
     e->pstride = (e->W + 2 * kPad + 63) & ~63;
     const size_t pls = (size_t)e->pstride * (e->H + 2 * kPad);
-    bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess;
+    bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking) == hipSuccess &&
+              hipHostMalloc(&e->h_prog, sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+              hipHostGetDevicePointer((void**)&e->d_prog, e->h_prog, 0) == hipSuccess;
     for (int c = 0; c < 3 && ok; ++c) {
         const size_t sz = c ? (size_t)e->Wc * e->Hc : (size_t)e->W * e->H;
         ok = hipMalloc(&e->d_in[c], sz) == hipSuccess && hipMalloc(&e->d_pic[0][c], sz) == hipSuccess &&
@@ -384,6 +407,11 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
         free_all(e);
         delete e;
         return HL_AMD_ERROR_OUTOFMEMMORY;
+    }
+    {
+        const char* wt = getenv("HL_AMD_WRITER_THREADS");
+        const unsigned hc = std::thread::hardware_concurrency();
+        e->nwriters = wt ? std::max(1, atoi(wt)) : (int)std::max(1u, std::min(8u, hc));
     }
     e->pipe_wg = 0;
     e->reach = 2;
@@ -641,6 +669,70 @@ static void store_result(hl_amd_encoder_t* e, int i, const hl_amd_result_t& src,
     dst->data = e->bout[i].data();
 }
 
+// Slice writers of a pipelined run: pictures become writable in order (their
+// records copied to h_brec); worker threads serialise them meanwhile, each
+// with its own scratch buffers, into bout[base + k].
+struct RunWriters {
+    hl_amd_encoder_t* e;
+    int m, base;
+    std::mutex mu;
+    std::condition_variable cv;
+    int ready = 0, next = 0;
+    bool stop = false;
+    std::vector<size_t> size;  // bytes written per picture incl. the start code; 0 = too short
+    std::vector<std::thread> th;
+
+    RunWriters(hl_amd_encoder_t* enc, int m_, int base_) : e(enc), m(m_), base(base_), size(m_, 0)
+    {
+        const int n = std::max(1, std::min(m, e->nwriters));
+        const StreamParams sp{e->W, e->H, e->p.qp, e->p.deblock};
+        if ((int)e->wscratch.size() < n) {
+            e->wscratch.resize(n);
+            e->wout.resize(n);
+        }
+        for (int w = 0; w < n; ++w) {
+            e->wscratch[w].resize(slice_scratch_bytes(sp));
+            e->wout[w].resize(slice_scratch_bytes(sp) + 64);
+        }
+        for (int w = 0; w < n; ++w) th.emplace_back([this, w] { work(w); });
+    }
+    ~RunWriters() { finish(); }
+    void publish(int p)
+    {
+        std::lock_guard<std::mutex> l(mu);
+        ready = std::max(ready, p);
+        cv.notify_all();
+    }
+    void finish()
+    {
+        {
+            std::lock_guard<std::mutex> l(mu);
+            stop = true;
+            cv.notify_all();
+        }
+        for (auto& t : th) t.join();
+        th.clear();
+    }
+    void work(int w)
+    {
+        const StreamParams sp{e->W, e->H, e->p.qp, e->p.deblock};
+        for (;;) {
+            int k;
+            {
+                std::unique_lock<std::mutex> l(mu);
+                cv.wait(l, [this] { return next < ready || stop; });
+                if (next >= ready) return;
+                k = next++;
+            }
+            const SliceState ss{0, e->pict_count + k, e->idr_pic_id};
+            uint8_t* out = e->wout[w].data();
+            const size_t n = write_slice(sp, ss, e->h_brec + (size_t)e->nmb * k, e->wscratch[w].data(), out, e->wout[w].size());
+            size[k] = n;
+            if (n) e->bout[base + k].assign(out + 3, out + n);
+        }
+    }
+};
+
 // m consecutive P pictures in one pipelined launch; falls back to the
 // per-picture path when a row-start speculation turns out to matter.
 static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, const uint8_t* const* U, const uint8_t* const* V,
@@ -710,6 +802,7 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     P.tail = e->d_head + m;
     P.oldest = e->d_head + 2 * m;
     P.err = e->d_err;
+    P.progress = e->d_prog;
     k_pipe_init<<<(unsigned)((nmb * m + 255) / 256), 256, 0, e->stream>>>(P, e->mbw, e->mbh);
     HL_HIP_CHECK(hipGetLastError());
     int wgs = e->pipe_wg;
@@ -720,15 +813,48 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         HL_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_pipeline, kMbThreads, 0));
         wgs = std::max(1, cus * occ);
     }
+    __atomic_store_n(e->h_prog, 0, __ATOMIC_RELEASE);
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[4], e->stream));
     k_pipeline<<<wgs, kMbThreads, 0, e->stream>>>(P, e->mbw, e->mbh);
     HL_HIP_CHECK(hipGetLastError());
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[5], e->stream));
+    // While the run goes on, the records of every finished picture are copied
+    // on the copy stream and serialised by the writer threads.
+    RunWriters wr(e, m, base);
+    hipError_t q = hipSuccess;
+    int copied = 0;
+    for (;;) {
+        int p = __atomic_load_n(e->h_prog, __ATOMIC_ACQUIRE);
+        if (p <= copied) {
+            q = hipStreamQuery(e->stream);
+            if (q == hipErrorNotReady) {
+                std::this_thread::sleep_for(std::chrono::microseconds(100));
+                continue;
+            }
+            break;  // the run has ended (or failed); the rest is handled below
+        }
+        p = std::min(p, m);
+        q = hipMemcpyAsync(e->h_brec + nmb * copied, e->d_brec + nmb * copied, sizeof(MbRecord) * nmb * (p - copied), hipMemcpyDeviceToHost,
+                           e->cstream);
+        if (q == hipSuccess) q = hipStreamSynchronize(e->cstream);
+        if (q != hipSuccess) break;
+        copied = p;
+        wr.publish(copied);
+    }
+    if (q != hipSuccess && q != hipErrorNotReady) {
+        wr.finish();
+        HL_HIP_CHECK(q);
+    }
     int32_t err = 0;
-    HL_HIP_CHECK(hipMemcpyAsync(e->h_bchain, e->d_bchain, sizeof(MbChain) * nmb * m, hipMemcpyDeviceToHost, e->stream));
-    HL_HIP_CHECK(hipMemcpyAsync(e->h_brec, e->d_brec, sizeof(MbRecord) * nmb * m, hipMemcpyDeviceToHost, e->stream));
-    HL_HIP_CHECK(hipMemcpyAsync(&err, e->d_err, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
-    HL_HIP_CHECK(hipStreamSynchronize(e->stream));
+    hipError_t r = hipMemcpyAsync(e->h_bchain, e->d_bchain, sizeof(MbChain) * nmb * m, hipMemcpyDeviceToHost, e->stream);
+    if (r == hipSuccess) r = hipMemcpyAsync(&err, e->d_err, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream);
+    if (r == hipSuccess && copied < m)
+        r = hipMemcpyAsync(e->h_brec + nmb * copied, e->d_brec + nmb * copied, sizeof(MbRecord) * nmb * (m - copied), hipMemcpyDeviceToHost,
+                           e->stream);
+    if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+    if (r == hipSuccess && err == 0) wr.publish(m);
+    wr.finish();
+    HL_HIP_CHECK(r);
     if (e->timing) {
         (void)hipEventElapsedTime(&e->ms[0], e->ev[0], e->ev[1]);
         (void)hipEventElapsedTime(&e->ms[1], e->ev[4], e->ev[5]);
@@ -744,27 +870,23 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     if (!ok) {  // a speculated row start mattered (or a wait gave up): redo the run picture by picture
         HL_HIP_CHECK(hipMemcpyAsync(e->d_st, e->d_snap, sizeof(MbState) * nmb, hipMemcpyDeviceToDevice, e->stream));
         for (int k = 0; k < m; ++k) {
-            hl_amd_result_t r;
-            const int32_t rc = encode_frame(e, Y[k], U[k], V[k], &r);
+            hl_amd_result_t rr;
+            const int32_t rc = encode_frame(e, Y[k], U[k], V[k], &rr);
             if (rc) return rc;
-            store_result(e, base + k, r, &res[k]);
+            store_result(e, base + k, rr, &res[k]);
         }
         e->reruns = 1;
         return HL_AMD_SUCCESS;
     }
-    const StreamParams sp{e->W, e->H, e->p.qp, e->p.deblock};
     for (int k = 0; k < m; ++k) {
-        const SliceState ss{0, e->pict_count, e->idr_pic_id};
-        const size_t n = write_slice(sp, ss, e->h_brec + nmb * k, e->scratch.data(), e->out.data(), e->out.size());
-        if (!n) return HL_AMD_ERROR_TOOSHORT;
-        hl_amd_result_t r;
-        r.type = HL_AMD_RESULT_TYPE_DATA;
-        r.data = e->out.data() + 3;
-        r.data_size = n - 3;
-        r.hdr = e->hdr.data();
-        r.hdr_size = e->hdr.size();
-        if (e->frame_index == 0) r.type |= HL_AMD_RESULT_TYPE_HDR;
-        store_result(e, base + k, r, &res[k]);
+        if (!wr.size[k]) return HL_AMD_ERROR_TOOSHORT;
+        hl_amd_result_t& o = res[k];
+        o.type = HL_AMD_RESULT_TYPE_DATA;
+        o.data = e->bout[base + k].data();
+        o.data_size = e->bout[base + k].size();
+        o.hdr = e->hdr.data();
+        o.hdr_size = e->hdr.size();
+        if (e->frame_index == 0) o.type |= HL_AMD_RESULT_TYPE_HDR;
         ++e->pict_count;
         --e->gop_left;
         ++e->frame_index;
