@@ -192,6 +192,7 @@ __global__ __launch_bounds__(kMbThreads) void k_pipeline(PipeArgs P, int mbw, in
         if (threadIdx.x < 64) {
             const int t = pop_task(P, nmb, reserved);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
             if (threadIdx.x == 0) s_task = t;
         }
         __syncthreads();
@@ -228,13 +229,17 @@ __global__ __launch_bounds__(kMbThreads) void k_pipeline(PipeArgs P, int mbw, in
         pw_filt += __builtin_readcyclecounter() - pt2;
         ++pw_n;
 #endif
-        // publish (Guideline 16: every wave drained, barrier, release), then
-        // release the successors; those whose last dependency this was are
-        // pushed onto their picture's ready queue
+        // publish (Guideline 16: every wave drained, barrier, ONE release whose
+        // own wait is explicit), then release the successors with relaxed
+        // atomics: the L2 write-back of the release fence already covers the
+        // payload of this task, and every consumer acquires after its pop.
+        // Those whose last dependency this was are pushed onto their
+        // picture's ready queue.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid < 64) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (tid == 0) st_relaxed(P.done + t, 1);
             int fo = 0, xo = 0, yo = 0;
             const int ns = task_succ(f, x, y, mbw, mbh, P.reach, P.nframes, -1, fo, xo, yo);
