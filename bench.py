@@ -105,9 +105,8 @@ def main():
     elapsed = dist.max_over_ranks(time.perf_counter() - t0)
     ms = enc.timing_ms()
     mb_ms, mb_launches = ms[1], enc.last_mb_launches()  # the (last) pipelined launch
-    # frames of the last pipelined run: the timed frames after the last IDR picture in them
-    last_idr = max((i for i in range(args.warmup, n_frames) if i % GOP == 0), default=args.warmup - 1)
-    run_frames = n_frames - 1 - last_idr if mb_launches == 1 else 1
+    # pictures of the last pipelined launch: runs span GOPs, up to 64 pictures each
+    run_frames = (args.steps - 1) % 64 + 1 if mb_launches == 1 else 1
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -214,8 +214,11 @@ __global__ __launch_bounds__(kMbThreads) void k_pipeline(PipeArgs P, int mbw, in
 #if defined(HL_PROFILE)
         const unsigned long long pt1 = __builtin_readcyclecounter();
 #endif
-        const int s_in = x == 0 ? PF.F.spec[y] : PF.F.chain[addr - 1].s_out;
-        encode_mb(PF.F, S, addr, tid, kMbThreads, s_in, gx, gy);
+        // the left neighbour's chain record was written by another workgroup:
+        // vector loads behind the pop's acquire (never the scalar cache)
+        const int s_in = x == 0 ? PF.F.spec[y] : ld_relaxed(&PF.F.chain[addr - 1].s_out);
+        const int spec_in = x == 0 ? 1 : ld_relaxed(&PF.F.chain[addr - 1].spec);
+        encode_mb(PF.F, S, addr, tid, kMbThreads, s_in, gx, gy, spec_in);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
 #if defined(HL_PROFILE)
@@ -322,6 +325,7 @@ struct hl_amd_encoder_s {
     hipStream_t cstream;
     int nwriters;
     std::vector<std::vector<uint8_t>> wscratch, wout;
+    std::vector<int32_t> run_intra, run_idr_id;  // per picture of the run: IDR, idr_pic_id
 };
 
 static void free_all(hl_amd_encoder_t* e)
@@ -729,7 +733,7 @@ struct RunWriters {
                 if (next >= ready) return;
                 k = next++;
             }
-            const SliceState ss{0, e->pict_count + k, e->idr_pic_id};
+            const SliceState ss{e->run_intra[k], e->pict_count + k, e->run_idr_id[k]};
             uint8_t* out = e->wout[w].data();
             const size_t n = write_slice(sp, ss, e->h_brec + (size_t)e->nmb * k, e->wscratch[w].data(), out, e->wout[w].size());
             size[k] = n;
@@ -738,12 +742,27 @@ struct RunWriters {
     }
 };
 
-// m consecutive P pictures in one pipelined launch; falls back to the
-// per-picture path when a row-start speculation turns out to matter.
+constexpr int kMaxRun = 64;  // pictures per pipelined launch
+
+// m consecutive pictures (IDR and P, in GOP order) in one pipelined launch;
+// falls back to the per-picture path when a bounded wait gave up or a
+// row-start speculation turned out to matter (resolve_chain makes the latter
+// exact inside a run).
 static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, const uint8_t* const* U, const uint8_t* const* V,
                           hl_amd_result_t* res, int base)
 {
     HL_HIP_CHECK(ensure_batch(e, m));
+    // picture types and idr_pic_id of the run, as m encode_frame calls would set them
+    e->run_intra.resize(m);
+    e->run_idr_id.resize(m);
+    for (int k = 0, gl = e->gop_left, idr = e->idr_pic_id; k < m; ++k) {
+        const bool intra = gl <= 0;
+        if (intra) gl = e->p.gop_size;
+        e->run_intra[k] = intra;
+        e->run_idr_id[k] = idr;
+        idr += intra;
+        --gl;
+    }
     const size_t pic = (size_t)e->W * e->H * 3 / 2, nmb = e->nmb;
     uint8_t** ref0 = e->d_pic[e->cur ^ 1];
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[0], e->stream));
@@ -759,7 +778,7 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         PipeFrame& pf = e->h_pf[k];
         pf = PipeFrame{};
         FrameArgs& F = pf.F;
-        F = frame_args(e, false);
+        F = frame_args(e, e->run_intra[k] != 0);
         uint8_t* cur = e->d_bpic + pic * k;
         F.src[0] = Y[k];
         F.src[1] = U[k];
@@ -783,6 +802,10 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         F.ref_done = k == 0 ? nullptr : e->d_done + (k - 1) * nmb;
         F.ref_epoch = 1;
         F.perr = e->d_err;
+        F.run_done = e->d_done;
+        F.run_chain = e->d_bchain;
+        F.run_pos = k;
+        F.carry_in = e->chain_end;
         pf.D.W = e->W;
         pf.D.H = e->H;
         pf.D.Wc = e->Wc;
@@ -892,7 +915,9 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         o.hdr = e->hdr.data();
         o.hdr_size = e->hdr.size();
         if (e->frame_index == 0) o.type |= HL_AMD_RESULT_TYPE_HDR;
+        if (e->run_intra[k]) e->gop_left = e->p.gop_size;  // encode_frame's bookkeeping, picture by picture
         ++e->pict_count;
+        if (e->run_intra[k]) ++e->idr_pic_id;
         --e->gop_left;
         ++e->frame_index;
     }
@@ -917,7 +942,7 @@ extern "C" int32_t hl_amd_encode_batch(hl_amd_encoder_t* e, int32_t n, const uin
     e->bout.resize(n);
     int i = 0;
     while (i < n) {
-        if (e->gop_left <= 0 || n - i == 1) {  // IDR pictures (and a lone P picture) take the per-picture path
+        if (n - i == 1) {  // a lone picture takes the per-picture path
             hl_amd_result_t r;
             const int32_t rc = encode_frame(e, y[i], u[i], v[i], &r);
             if (rc) return rc;
@@ -925,7 +950,9 @@ extern "C" int32_t hl_amd_encode_batch(hl_amd_encoder_t* e, int32_t n, const uin
             ++i;
             continue;
         }
-        const int m = std::min(n - i, e->gop_left);
+        // runs span GOPs (IDR pictures included); kMaxRun bounds the run's
+        // buffers (~22 MB of HBM and 9 MB of pinned host memory per 1088p picture)
+        const int m = std::min(n - i, kMaxRun);
         const int32_t rc = encode_run(e, m, y + i, u + i, v + i, results + i, i);
         if (rc) return rc;
         i += m;

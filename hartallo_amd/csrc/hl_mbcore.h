@@ -92,6 +92,12 @@ struct FrameArgs {
     const int32_t* ref_done;  // task flags of the reference picture's slot
     int32_t ref_epoch;        // flag value once a task of the reference picture finished
     int32_t* perr;            // bounded-spin failures
+    // exact rdo.Single_ctr for stale reads of a speculated value (resolve_chain);
+    // run_done is null in the per-picture path (the host re-runs rows instead)
+    const int32_t* run_done;  // task flags of picture 0 of the run ([pos * mbw * mbh + addr])
+    const MbChain* run_chain; // chain records of picture 0 of the run (same layout)
+    int32_t run_pos;          // this picture's position in the run
+    int32_t carry_in;         // exact counter value entering picture 0 of the run
 };
 
 struct NbInfo {
@@ -159,6 +165,7 @@ struct Shared {
     int32_t dcY[16];             // I16x16: scaled DC per DC-matrix position
     int16_t i16_dcl[16];         // I16x16: DC levels of the current mode (scan order)
     int32_t dcrow[4];            // I16x16: DC block rate, TotalCoeff, single counter
+    int32_t chain_x;             // resolve_chain result
     int32_t predc[2][64];
     int32_t cres_dc[2][4], cres_cac[2][4], cres_cdc[2][4], cres_tc[2][4], cres_sctr[2][4];
     int32_t cdc_level[2][4];
@@ -178,6 +185,7 @@ struct Ctx {
     int chain, fresh, dep;  // rdo.Single_ctr emulation (uniform)
     LaneK K;                // per-lane constants of the 16-lane block pipeline (device)
     int gx, gy;             // reference planes known complete for MBs (X <= gx, Y <= gy) (pipelined runs)
+    int spec = 0;           // 1 = chain is still a row-start speculation (uniform)
 #if defined(HL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
     unsigned long long pacc[kProfSlots] = {};
     unsigned pcnt[kProfSlots] = {};
@@ -199,6 +207,7 @@ HD void chain_write(Ctx& c, int sctr)
 {
     c.chain = sctr;
     c.fresh = 1;
+    c.spec = 0;
 }
 
 // Luma 4x4 prediction from the padded quarter-pel planes for integer origin
@@ -1589,6 +1598,51 @@ HD void intra_chroma_pred(Ctx& c, int mode)
 // --------------------------------------------------------------------------
 // Intra 16x16 RDO (rdo.c:1526-1809)
 // --------------------------------------------------------------------------
+// Pipelined runs: the exact rdo.Single_ctr for a stale read (residual.c:881-897,
+// DESIGN.md §5) while this MB's value is still a row-start speculation.  It is
+// the value left by the last MB that wrote the counter: the end of the nearest
+// earlier row with a fresh write, walking back through this picture, then the
+// earlier pictures of the run, then the value entering the run.  Those rows
+// never wait on this task (they precede it in the wavefront and in picture
+// order), so the walk cannot deadlock; every wait is bounded.  Rare: about one
+// per 1088p I picture, none in the P pictures of the test content.
+HD void resolve_chain(Ctx& c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    const int nmb = F.mbw * F.mbh, lane = c.tid & 63;
+    if (c.tid < 64) {
+        int val = F.carry_in, pos = F.run_pos, y = c.mby - 1;
+        for (;;) {
+            if (y < 0) {
+                if (pos == 0) break;
+                --pos;
+                y = F.mbh - 1;
+            }
+            const int32_t* done = F.run_done + (size_t)pos * nmb + (size_t)y * F.mbw;
+            const MbChain* row = F.run_chain + (size_t)pos * nmb + (size_t)y * F.mbw;
+            if (lane == 0) spin_ge(done + F.mbw - 1, 1, F.perr);  // the row's last MB: the whole row is final
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bool fr = false;
+            for (int x = lane; x < F.mbw; x += 64) fr = fr || ld_relaxed(&row[x].fresh) != 0;
+            if (__ballot(fr)) {
+                val = ld_relaxed(&row[F.mbw - 1].s_out);
+                break;
+            }
+            --y;
+        }
+        if (c.tid == 0) S.chain_x = val;
+    }
+    HL_SYNC();
+    c.chain = uni(S.chain_x);
+    c.spec = 0;
+#else
+    (void)c;
+#endif
+}
+
 HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp)
 {
     const FrameArgs& F = c.F;
@@ -1654,7 +1708,10 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp)
             rate += uni(S.i16_bits[b]);
             bcbp |= 1 << b;
             if (uni(S.i16_tc[b]) > 0) chain_write(c, uni(S.i16_sctr[b]));
-            else if (!c.fresh) c.dep = 1;
+            else if (!c.fresh) {
+                if (c.spec && F.run_done) resolve_chain(c);  // pipelined run: read the exact value
+                else c.dep = 1;
+            }
             single += c.chain;
         }
         if (bcbp && single < 6) bcbp = 0;
@@ -2550,15 +2607,19 @@ HD void mb_end(Ctx& c)
         ch.s_out = c.chain;
         ch.dep = c.dep;
         ch.fresh = c.fresh;
+        ch.spec = c.spec;
     }
     HL_SYNC();
 }
 
-// One macroblock, start to end.  s_in = rdo.Single_ctr on entry; (gx, gy) =
-// reference region already known complete (pipelined runs; see reach_wait).
-HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, int s_in, int gx = 1 << 20, int gy = 1 << 20)
+// One macroblock, start to end.  s_in = rdo.Single_ctr on entry (spec_in = 1
+// while it is a row-start speculation); (gx, gy) = reference region already
+// known complete (pipelined runs; see reach_wait).
+HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, int s_in, int gx = 1 << 20, int gy = 1 << 20,
+               int spec_in = 1)
 {
     Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0, LaneK{}, gx, gy};
+    c.spec = spec_in;
 #if defined(__HIP_DEVICE_COMPILE__)
     c.K = make_lanek(tid, F.qp, F.qpc);
 #endif

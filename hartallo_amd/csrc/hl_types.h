@@ -68,6 +68,7 @@ struct MbChain {
     int32_t s_out;   // value left on exit
     int32_t dep;     // 1 = a stale read of the entry value happened before any fresh write
     int32_t fresh;   // 1 = the MB wrote the counter at least once
+    int32_t spec;    // 1 = s_out is still a row-start speculation (no fresh write or resolution since)
 };
 
 }  // namespace hl

@@ -106,3 +106,21 @@ def test_batch_1088p_equals_single_calls(gpu):
     for f in range(n):
         assert a[f] == b[f], f"frame {f}: first differing byte {first_diff(a[f], b[f])}"
     assert np.array_equal(ra, rb)
+
+
+def test_batch_1088p_spans_gops(gpu):
+    # runs span GOPs: IDR pictures inside one pipelined launch, whose row-start
+    # rdo.Single_ctr reads are resolved exactly in-kernel (no host re-run)
+    w, h, n = 1920, 1088, 7
+    clip = synth.clip(w, h, n, 13)
+    a, ra = _single(w, h, 28, 16, 1, 3, clip)
+    enc = Encoder(w, h, 28, 16, 1, 3)
+    dev, ptrs = _device_frames(clip, w, h)
+    b = [r.annexb() for r in enc.encode_batch_device(ptrs)]
+    reruns, launches = enc.last_reruns(), enc.last_mb_launches()
+    rb = np.concatenate(enc.recon())
+    enc.close()
+    for f in range(n):
+        assert a[f] == b[f], f"frame {f}: first differing byte {first_diff(a[f], b[f])}"
+    assert np.array_equal(ra, rb)
+    assert launches == 1 and reruns == 0, (launches, reruns)

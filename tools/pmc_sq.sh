@@ -6,7 +6,7 @@ i=0
 for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_INST_LEVEL_SMEM SQ_INSTS_LDS SQ_INST_LEVEL_LDS" \
            "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $set -d $GRAFT_REPO_ROOT/gpurun_out/sq$i -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/pipe_bench.py 12 8,32,2 > $GRAFT_REPO_ROOT/gpurun_out/sq$i.log 2>&1 || exit $?
+  timeout -s KILL 120 rocprofv3 --pmc $set -d $GRAFT_REPO_ROOT/gpurun_out/sq$i -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/pipe_bench.py 12 > $GRAFT_REPO_ROOT/gpurun_out/sq$i.log 2>&1 || exit $?
 done
 cd $GRAFT_REPO_ROOT
 python3 - <<'PY'

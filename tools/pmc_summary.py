@@ -25,7 +25,7 @@ def main():
     fetch = f[("k_pipeline", "FETCH_SIZE")]
     write = w[("k_pipeline", "WRITE_SIZE")]
     launches = fetch[1]
-    mbs = 12 * (1920 // 16) * (1088 // 16)  # bench: 12 pipelined pictures per launch
+    mbs = 12 * (1920 // 16) * (1088 // 16)  # bench --steps 12 --warmup 0: one launch of 12 pictures (IDR + 11 P)
     rd = 2.0 * fetch[0] * 1024 / launches
     wr = write[0] * 1024 / launches
     out = {"kernel": "k_pipeline", "launches": launches, "macroblocks_per_launch": mbs, "fetch_bytes_per_launch_x2": rd,
