@@ -6,8 +6,8 @@ Workload (BASELINE.json configs[2] as the reference can express it, SURVEY
 synthetic input (hartallo_amd.synth, seeded per rank).  A step is one frame
 through the whole encode path (quarter-pel planes, MB decisions, deblocking,
 CAVLC bitstream); inputs are resident in HBM before the timed region.
-The timed frames (by default the second GOP: one IDR picture and 29 P
-pictures) go through hl_amd_encode_batch: runs of P pictures are
+The timed frames (by default GOPs 2-5: four IDR pictures and 116 P
+pictures, after one warm-up GOP) go through hl_amd_encode_batch: runs of P pictures are
 frame-pipelined in one persistent launch (hl_pipeline.h), bit-identical to
 encoding them one call at a time (tests/test_gpu_pipeline.py).
 
@@ -35,6 +35,7 @@ BYTES_PER_MB = 2752  # compulsory HBM bytes per macroblock, DESIGN.md / SURVEY Â
 # HBM traffic of k_pipeline per macroblock, from rocprofv3 FETCH_SIZE / WRITE_SIZE
 # passes on this workload (tools/pmc_traffic.sh, corrected per MI355X_MICROARCH.md)
 PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_traffic_k_pipeline.json")
+MAX_RUN = 128  # pictures per pipelined launch (kMaxRun, hl_encoder.hip)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 
@@ -71,7 +72,7 @@ def cpu_baseline(frames_host, n_frames):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=GOP)  # one whole GOP: IDR + 29 P pictures
+    ap.add_argument("--steps", type=int, default=4 * GOP)  # four whole GOPs (IDR + 29 P pictures each), one pipelined launch
     ap.add_argument("--warmup", type=int, default=GOP)  # the first GOP (also warms the pipelined path)
     ap.add_argument("--cpu-frames", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -105,8 +106,8 @@ def main():
     elapsed = dist.max_over_ranks(time.perf_counter() - t0)
     ms = enc.timing_ms()
     mb_ms, mb_launches = ms[1], enc.last_mb_launches()  # the (last) pipelined launch
-    # pictures of the last pipelined launch: runs span GOPs, up to 64 pictures each
-    run_frames = (args.steps - 1) % 64 + 1 if mb_launches == 1 else 1
+    # pictures of the last pipelined launch: runs span GOPs, up to MAX_RUN pictures each
+    run_frames = (args.steps - 1) % MAX_RUN + 1 if mb_launches == 1 else 1
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -742,7 +742,7 @@ struct RunWriters {
     }
 };
 
-constexpr int kMaxRun = 64;  // pictures per pipelined launch
+constexpr int kMaxRun = 128;  // pictures per pipelined launch (bench.py MAX_RUN)
 
 // m consecutive pictures (IDR and P, in GOP order) in one pipelined launch;
 // falls back to the per-picture path when a bounded wait gave up or a

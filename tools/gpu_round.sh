@@ -10,7 +10,7 @@ tail -4 gpurun_out/gpu_tests.log
 timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1 || exit $?
 grep -v amdgpu.ids gpurun_out/bench.log
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 12 --warmup 2 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof_bench.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof_bench.log 2>&1 || exit $?
 cd $GRAFT_REPO_ROOT
 find gpurun_out/prof -name "*kernel_stats.csv" | head -3
 cat $(find gpurun_out/prof -name "*kernel_stats.csv" | head -1) | cut -c1-200
