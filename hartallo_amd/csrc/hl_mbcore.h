@@ -687,6 +687,9 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         const int pr = c.K.p >> 2, pc = c.K.p & 3;
         const uint8_t* base = F.pl[0];
         int pa[kMaxPass], pb[kMaxPass], sv[kMaxPass];
+        // single-block partitions: both nC neighbours lie outside the partition,
+        // so nC is fixed for its whole search (read here, beside the loads)
+        const int nc1 = g.nblk == 1 ? nc_luma_of(S, blk_idx(g.px, g.py), [&](int ni) -> int { return S.tc[ni]; }) : 0;
         // slots and source samples first (one LDS round trip), then all loads
         int o1[kMaxPass], o2[kMaxPass];
         HL_PROF_T(ta0);
@@ -731,11 +734,13 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                     dist = row_sum(iabs(res));
                 }
                 else {
+                    // reconstruction distortion first: independent of the CAVLC
+                    // chain, so the two DPP chains interleave in one basic block
+                    const int r = coop_idct(c.K, coop_dequant(q, c.K.ls, F.qp));
+                    dist = row_sum(iabs(sv[j] - clip255(pred + r)));
                     st = coop_cavlc(S.ct, q, c.K.s, S.lvs[grp]);
                     if (c.K.p == 0 && st.tc)  // coeff_token lengths for the four nC classes
                         tok = S.ct.tok[0][st.t1][st.tc] | (S.ct.tok[1][st.t1][st.tc] << 5) | (S.ct.tok[2][st.t1][st.tc] << 10) | (6 << 15);
-                    const int r = coop_idct(c.K, coop_dequant(q, c.K.ls, F.qp));
-                    dist = row_sum(iabs(sv[j] - clip255(pred + r)));
                 }
 #if defined(HL_STEP_PROF)
                 HL_PROF_ADD(c, 5, ta2);
@@ -753,10 +758,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                         // a single-block partition: both nC neighbours lie outside it, so the
                         // nC (and the candidate's cost) needs no other row (phase 2 skipped)
                         int bits = 0;
-                        if (st.tc) {
-                            const int nC = nc_luma_of(S, blk_idx(g.px, g.py), [&](int ni) -> int { return S.tc[ni]; });
-                            bits = st.rest + ((tok >> (5 * (nC < 2 ? 0 : (nC < 4 ? 1 : (nC < 8 ? 2 : 3))))) & 31);
-                        }
+                        if (st.tc) bits = st.rest + ((tok >> (5 * (nc1 < 2 ? 0 : (nc1 < 4 ? 1 : (nc1 < 8 ? 2 : 3))))) & 31);
                         const CandSlot cs = S.wc[wave][ci];
                         S.cd_cost[ci] = mv_cost(F, dist, bits, cs.mvx, cs.mvy, pmv);
                         S.cd_bits[ci] = bits;
