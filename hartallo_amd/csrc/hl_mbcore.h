@@ -1937,6 +1937,7 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4)
         }
         HL_SYNC();
         // nC is the same for all nine modes: they only rewrite this block
+        // (read after the barrier: the caller's last TotalCoeffs writes)
         const int nC = uni(nc_luma_of(S, blk, [&](int ni) -> int { return S.tc[ni]; }));
         if (row < 9) {
             const int m = row;
@@ -1948,10 +1949,11 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4)
                 const int res = sv - pred;
                 const bool exact = row_or(res != 0) == 0;
                 const int q = coop_quant(coop_fwd(c.K, res), c.K.mf, qbits, fq);
-                const CoopStat st = coop_cavlc(S.ct, q, c.K.s, S.lvs[row]);
+                // reconstruction before the CAVLC chain: the two interleave
                 const int r = coop_idct(c.K, coop_dequant(q, c.K.ls, F.qp));
                 const int rec = clip255(pred + r);
                 const int d = row_sum(iabs(sv - rec));
+                const CoopStat st = coop_cavlc(S.ct, q, c.K.s, S.lvs[row]);
                 S.i4_rec[m][c.K.p] = (uint8_t)rec;
                 S.i4_lv[m][c.K.s] = (int16_t)q;
                 if (c.K.p == 0) {
