@@ -65,7 +65,7 @@ __device__ __forceinline__ void diag_mb(int mbw, int mbh, int row0, int diag, in
     x = diag - 2 * yy;
 }
 
-__global__ __launch_bounds__(kMbThreads) void k_mb_diag(FrameArgs F, int diag, int row0)
+__global__ __launch_bounds__(kMbThreads, 2) void k_mb_diag(FrameArgs F, int diag, int row0)
 {
     __shared__ Shared S;
     int x, y;
@@ -172,7 +172,7 @@ __device__ int pop_task(const PipeArgs& P, int nmb, bool reserved)
 // Pipelined run of P pictures (hl_pipeline.h): persistent workgroups taking
 // ready tasks (decision, then the deblocking and plane blocks it completes)
 // until the run has finished.
-__global__ __launch_bounds__(kMbThreads) void k_pipeline(PipeArgs P, int mbw, int mbh)
+__global__ __launch_bounds__(kMbThreads, 2) void k_pipeline(PipeArgs P, int mbw, int mbh)
 {
     __shared__ Shared S;
     __shared__ int32_t s_task;
