@@ -1,0 +1,55 @@
+"""Repeats the GOP-spanning 1920x1088 pipelined run (tests/test_gpu_pipeline.py
+test_batch_1088p_spans_gops) in one process and reports every run whose
+stream differs from the same frames encoded one call at a time.
+
+  python tools/stress_spans_gops.py [repeats] [frames] [gop]
+
+Development tool for DESIGN.md §10 item 0 (a timing-dependent mismatch seen
+once under another device schedule).  Set HL_LIB to time another build.
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from hartallo_amd import _lib  # noqa: E402
+
+if os.environ.get("HL_LIB"):
+    _lib.load_library(os.path.abspath(os.environ["HL_LIB"]))
+from hartallo_amd import Encoder, synth  # noqa: E402
+from hl_testlib import first_diff  # noqa: E402
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 7
+    gop = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    w, h = 1920, 1088
+    clip = synth.clip(w, h, n, 13)
+    dev = torch.from_numpy(np.ascontiguousarray(clip)).cuda()
+    torch.cuda.synchronize()
+    ny = w * h
+    ptrs = [(dev[i].data_ptr(), dev[i].data_ptr() + ny, dev[i].data_ptr() + ny + ny // 4) for i in range(n)]
+    enc = Encoder(w, h, 28, 16, 1, gop)
+    ref = [enc.encode_device(*p).annexb() for p in ptrs]
+    enc.close()
+    bad = 0
+    for r in range(reps):
+        enc = Encoder(w, h, 28, 16, 1, gop)
+        out = [x.annexb() for x in enc.encode_batch_device(ptrs)]
+        reruns = enc.last_reruns()
+        enc.close()
+        diffs = [(f, first_diff(ref[f], out[f]), len(ref[f])) for f in range(n) if ref[f] != out[f]]
+        bad += bool(diffs)
+        print(f"run {r}: {'MISMATCH ' + str(diffs) if diffs else 'ok'} (reruns {reruns})", flush=True)
+    print(f"{bad} of {reps} runs differ", flush=True)
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()
