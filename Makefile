@@ -10,7 +10,7 @@ HDRS    := $(wildcard $(CSRC)/*.h) include/hartallo_amd.h
 # -ffp-contract=off: the RDO costs are IEEE double and must round exactly like the reference
 CXXFLAGS := -std=c++17 -O3 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-variable
 
-.PHONY: all product emu unit oracle profile clean
+.PHONY: all product emu unit oracle profile poison clean
 all: product emu unit oracle
 
 product: hartallo_amd/libhartallo_amd.so
@@ -31,6 +31,22 @@ profile: build/prof/hartallo_amd/libhartallo_amd.so
 build/prof/hartallo_amd/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp $(HDRS)
 	mkdir -p build/prof/hartallo_amd
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DHL_PROFILE=1 -shared -o $@ $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp
+
+# debug builds: LDS poisoned before every macroblock with two different salts
+# (tools/gpu_diag.sh); any output difference names a read of uninitialised LDS
+poison: build/poison1/libhartallo_amd.so build/poison2/libhartallo_amd.so
+build/poison%/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp $(HDRS)
+	mkdir -p build/poison$*
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DHL_POISON_LDS=$* -shared -o $@ $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp
+
+# memory-scope variants of the pipelined run's fences (diagnostics)
+scopes: build/acqsys/libhartallo_amd.so build/relacqsys/libhartallo_amd.so
+build/acqsys/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp $(HDRS)
+	mkdir -p build/acqsys
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) '-DHL_ACQ_SCOPE=""' -shared -o $@ $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp
+build/relacqsys/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp $(HDRS)
+	mkdir -p build/relacqsys
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) '-DHL_ACQ_SCOPE=""' '-DHL_REL_SCOPE=""' -shared -o $@ $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp
 
 oracle:
 	$(MAKE) -C oracle

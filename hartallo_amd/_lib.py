@@ -40,6 +40,8 @@ EXPORTED_SYMBOLS = (
     "hl_amd_last_reruns",
     "hl_amd_last_mb_launches",
     "hl_amd_profile_counters",
+    "hl_amd_debug_records",
+    "hl_amd_record_size",
     "hl_amd_version",
 )
 
@@ -63,6 +65,26 @@ class _Result(ctypes.Structure):
         ("data_size", ctypes.c_size_t),
     ]
 
+
+def _mb_record_dtype():
+    """numpy mirror of MbRecord (hartallo_amd/csrc/hl_types.h)."""
+    import numpy as np
+
+    return np.dtype([
+        ("e_type", "<i4"), ("mb_type", "<i4"), ("flags", "<i4"), ("pm0", "<i4"),
+        ("cbp", "<i4"), ("cbp_l", "<i4"), ("cbp_c", "<i4"), ("cbp_l4x4", "<i4"),
+        ("cbp_cdc", "<i4", 2), ("cbp_cac", "<i4", 2), ("num_part", "<i4"), ("num_sub", "<i4", 4), ("sub_mb_type", "<i4", 4),
+        ("chroma_mode", "<i4"), ("i16mode", "<i4"), ("mvd", "<i2", (4, 4, 2)), ("mv", "<i2", (4, 4, 2)),
+        ("prev_flag", "i1", 16), ("rem_mode", "i1", 16), ("i4mode", "i1", 16), ("nc_luma", "i1", 16), ("nc_cac", "i1", (2, 4)),
+        ("nc_dc", "i1"), ("pad0", "i1", 3), ("luma", "<i2", (16, 16)), ("i16dc", "<i2", 16), ("cdc", "<i2", (2, 4)),
+        ("cac", "<i2", (2, 4, 16)),
+    ])
+
+
+try:
+    MB_RECORD = _mb_record_dtype()
+except ImportError:  # numpy is optional for the plain ctypes binding
+    MB_RECORD = None
 
 _lib = None
 
@@ -108,6 +130,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_last_mb_launches.restype = i32
     lib.hl_amd_profile_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong), i32]
     lib.hl_amd_profile_counters.restype = i32
+    lib.hl_amd_debug_records.argtypes = [vp, i32, vp, ctypes.c_size_t]
+    lib.hl_amd_debug_records.restype = i32
+    lib.hl_amd_record_size.argtypes = []
+    lib.hl_amd_record_size.restype = i32
     lib.hl_amd_version.argtypes = []
     lib.hl_amd_version.restype = ctypes.c_char_p
     _lib = lib
@@ -225,6 +251,25 @@ class Encoder:
         a = (ctypes.c_ulonglong * n)()
         self.lib.hl_amd_profile_counters(self._h, a, n)
         return list(a)
+
+    def debug_records(self, k: int):
+        """MbRecord structs of picture k of the last encode call (numpy
+        structured array, one element per macroblock), or None when the
+        call did not keep them."""
+        import numpy as np
+
+        nmb = (self.width // 16) * (self.height // 16)
+        dt = MB_RECORD
+        if self.lib.hl_amd_record_size() == MB_RECORD.itemsize + 32:  # diagnostic build (HL_DIAG_INPUTS)
+            dt = np.dtype(MB_RECORD.descr + [("dbg", "<u4", 8)])
+        assert self.lib.hl_amd_record_size() == dt.itemsize
+        out = np.zeros(nmb, dt)
+        rc = self.lib.hl_amd_debug_records(self._h, k, out.ctypes.data, out.nbytes)
+        if rc == HL_AMD_ERROR_INVALID_STATE:
+            return None
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_debug_records")
+        return out
 
     def last_mb_launches(self) -> int:
         return self.lib.hl_amd_last_mb_launches(self._h)

@@ -16,9 +16,6 @@
 
 #include <algorithm>
 #include <atomic>
-#include <chrono>
-#include <condition_variable>
-#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -56,6 +53,35 @@ __global__ __launch_bounds__(256) void k_planes(const uint8_t* __restrict__ ref,
     pj[o] = qpel_plane_sample(ref, W, H, 3, x, y);
 }
 
+#if defined(HL_POISON_LDS)
+// Debug builds (-DHL_POISON_LDS=<salt>): the workgroup's LDS image (bytes
+// [HL_POISON_LO, HL_POISON_HI) of Shared, default all of it) is filled with a
+// pattern derived from the task before every macroblock, so that any read of
+// Shared before this macroblock wrote it changes the output.
+#ifndef HL_POISON_LO
+#define HL_POISON_LO 0
+#endif
+#ifndef HL_POISON_HI
+#define HL_POISON_HI sizeof(Shared)
+#endif
+__device__ void poison_lds(Shared& S, uint32_t seed)
+{
+    uint32_t* w = reinterpret_cast<uint32_t*>(&S);
+    const uint32_t lo = (uint32_t)(HL_POISON_LO) / 4, hi = ((uint32_t)(HL_POISON_HI) + 3) / 4;
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        uint32_t h = (i + 1u) * 2654435761u ^ (seed + (uint32_t)HL_POISON_LDS) * 0x9E3779B9u;
+        h ^= h >> 15;
+        h *= 0x2C1B3C6Du;
+        h ^= h >> 12;
+        w[i] = h;
+    }
+    __syncthreads();
+}
+#define HL_POISON(S, seed) poison_lds(S, seed)
+#else
+#define HL_POISON(S, seed) ((void)0)
+#endif
+
 // macroblocks (x, y) with x + 2 * (y - row0) == diag
 __device__ __forceinline__ void diag_mb(int mbw, int mbh, int row0, int diag, int k, int& x, int& y)
 {
@@ -72,6 +98,7 @@ __global__ __launch_bounds__(kMbThreads, 2) void k_mb_diag(FrameArgs F, int diag
     diag_mb(F.mbw, F.mbh, row0, diag, blockIdx.x, x, y);
     const int addr = y * F.mbw + x;
     const int s_in = x == 0 ? F.spec[y] : F.chain[addr - 1].s_out;
+    HL_POISON(S, (uint32_t)addr * 7919u + (uint32_t)diag);
     encode_mb(F, S, addr, threadIdx.x, kMbThreads, s_in);
 }
 
@@ -191,13 +218,16 @@ __global__ __launch_bounds__(kMbThreads, 2) void k_pipeline(PipeArgs P, int mbw,
 #endif
         if (threadIdx.x < 64) {
             const int t = pop_task(P, nmb, reserved);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
             if (threadIdx.x == 0) s_task = t;
         }
         __syncthreads();
         const int t = __builtin_amdgcn_readfirstlane(s_task);
         if (t < 0) break;
+#if defined(HL_DIAG) && HL_DIAG == 1
+        __syncthreads();
+#endif
         // opaque per task: keeps the compiler from hoisting encode_mb's
         // lane-index arithmetic out of the task loop and holding it live
         // across the whole body (160 spilled VGPRs without this)
@@ -218,6 +248,16 @@ __global__ __launch_bounds__(kMbThreads, 2) void k_pipeline(PipeArgs P, int mbw,
         // vector loads behind the pop's acquire (never the scalar cache)
         const int s_in = x == 0 ? PF.F.spec[y] : ld_relaxed(&PF.F.chain[addr - 1].s_out);
         const int spec_in = x == 0 ? 1 : ld_relaxed(&PF.F.chain[addr - 1].spec);
+        HL_POISON(S, (uint32_t)t * 7919u + blockIdx.x);
+#if defined(HL_DIAG) && HL_DIAG == 2
+        __syncthreads();
+#elif defined(HL_DIAG) && HL_DIAG == 3
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#elif defined(HL_DIAG) && HL_DIAG == 4
+        __builtin_amdgcn_s_sleep(20);
+#elif defined(HL_DIAG) && HL_DIAG == 6
+        if (threadIdx.x < 64) __builtin_amdgcn_s_sleep(20);
+#endif
         encode_mb(PF.F, S, addr, tid, kMbThreads, s_in, gx, gy, spec_in);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -241,7 +281,7 @@ __global__ __launch_bounds__(kMbThreads, 2) void k_pipeline(PipeArgs P, int mbw,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid < 64) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, HL_REL_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (tid == 0) st_relaxed(P.done + t, 1);
             int fo = 0, xo = 0, yo = 0;
@@ -256,13 +296,7 @@ __global__ __launch_bounds__(kMbThreads, 2) void k_pipeline(PipeArgs P, int mbw,
             }
             // pictures finish in order: the last MB depends on every other one
             // and on the previous picture's last MB
-            if (tid == 0 && addr == nmb - 1) {
-                __hip_atomic_store(P.oldest, f + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                // every record of picture f is in memory (the last MB's task
-                // transitively acquired all of them): tell the host, whose
-                // copy engine can fetch them while the run goes on
-                if (P.progress) __hip_atomic_store(P.progress, f + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
+            if (tid == 0 && addr == nmb - 1) __hip_atomic_store(P.oldest, f + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 #if defined(HL_PROFILE)
@@ -319,13 +353,10 @@ struct hl_amd_encoder_s {
     int32_t *d_cnt, *d_done, *d_queue, *d_head;  // scheduler state (head: [head | tail | oldest])
     PipeFrame *d_pf, *h_pf;
     std::vector<std::vector<uint8_t>> bout;  // bitstreams of the last hl_amd_encode_batch
-    // host side of a run: pictures finished by k_pipeline (mapped host word),
-    // a copy stream for their records, slice writers working meanwhile
-    int32_t *h_prog, *d_prog;
-    hipStream_t cstream;
-    int nwriters;
+    int nwriters;                            // host slice writer threads of a run
     std::vector<std::vector<uint8_t>> wscratch, wout;
     std::vector<int32_t> run_intra, run_idr_id;  // per picture of the run: IDR, idr_pic_id
+    std::vector<const MbRecord*> last_recs;      // host records per picture of the last encode call (diagnostics)
 };
 
 static void free_all(hl_amd_encoder_t* e)
@@ -359,9 +390,7 @@ static void free_all(hl_amd_encoder_t* e)
     (void)hipHostFree(e->h_rec);
     (void)hipHostFree(e->h_chain);
     (void)hipHostFree(e->h_spec);
-    (void)hipHostFree(e->h_prog);
     if (e->stream) (void)hipStreamDestroy(e->stream);
-    if (e->cstream) (void)hipStreamDestroy(e->cstream);
     for (int i = 0; i < 6; ++i)
         if (e->ev[i]) (void)hipEventDestroy(e->ev[i]);
 }
@@ -386,15 +415,15 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
     e->qpc = kQpToQpc[p->qp];
     e->pstride = (e->W + 2 * kPad + 63) & ~63;
     const size_t pls = (size_t)e->pstride * (e->H + 2 * kPad);
-    bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking) == hipSuccess &&
-              hipHostMalloc(&e->h_prog, sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
-              hipHostGetDevicePointer((void**)&e->d_prog, e->h_prog, 0) == hipSuccess;
+    // All work of an encoder runs on its own non-blocking stream, which does
+    // not order against the null stream: the initial state is written on
+    // that stream and synchronised before create returns.
+    bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess;
     for (int c = 0; c < 3 && ok; ++c) {
         const size_t sz = c ? (size_t)e->Wc * e->Hc : (size_t)e->W * e->H;
         ok = hipMalloc(&e->d_in[c], sz) == hipSuccess && hipMalloc(&e->d_pic[0][c], sz) == hipSuccess &&
-             hipMalloc(&e->d_pic[1][c], sz) == hipSuccess && hipMemset(e->d_pic[0][c], 0, sz) == hipSuccess &&
-             hipMemset(e->d_pic[1][c], 0, sz) == hipSuccess;
+             hipMalloc(&e->d_pic[1][c], sz) == hipSuccess && hipMemsetAsync(e->d_pic[0][c], 0, sz, e->stream) == hipSuccess &&
+             hipMemsetAsync(e->d_pic[1][c], 0, sz, e->stream) == hipSuccess;
     }
     e->plsz = pls;
     ok = ok && hipMalloc(&e->d_pl[0], 4 * pls) == hipSuccess;
@@ -405,12 +434,14 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
          hipHostMalloc(&e->h_rec, sizeof(MbRecord) * e->nmb, hipHostMallocDefault) == hipSuccess &&
          hipHostMalloc(&e->h_chain, sizeof(MbChain) * e->nmb, hipHostMallocDefault) == hipSuccess &&
          hipHostMalloc(&e->h_spec, sizeof(int32_t) * e->mbh, hipHostMallocDefault) == hipSuccess;
-    ok = ok && hipMemset(e->d_st, 0, sizeof(MbState) * e->nmb) == hipSuccess;
+    // the per-address MB objects start zeroed (calloc'd by the reference, mb.c)
+    ok = ok && hipMemsetAsync(e->d_st, 0, sizeof(MbState) * e->nmb, e->stream) == hipSuccess;
 #if defined(HL_PROFILE)
     // 64 phase counters, then the cycles of every macroblock of the last frame
     ok = ok && hipMalloc(&e->d_prof, (64 + e->nmb) * sizeof(unsigned long long)) == hipSuccess &&
-         hipMemset(e->d_prof, 0, (64 + e->nmb) * sizeof(unsigned long long)) == hipSuccess;
+         hipMemsetAsync(e->d_prof, 0, (64 + e->nmb) * sizeof(unsigned long long), e->stream) == hipSuccess;
 #endif
+    ok = ok && hipStreamSynchronize(e->stream) == hipSuccess;
     for (int i = 0; i < 6 && ok; ++i) ok = hipEventCreate(&e->ev[i]) == hipSuccess;
     if (!ok) {
         free_all(e);
@@ -600,20 +631,29 @@ static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
 {
     if (n <= e->bcap) return hipSuccess;
     const size_t pic = (size_t)e->W * e->H * 3 / 2, nmb = e->nmb;
-    (void)hipFree(e->d_bpic);
-    (void)hipFree(e->d_bpl);
-    (void)hipFree(e->d_brec);
-    (void)hipFree(e->d_bchain);
-    (void)hipFree(e->d_bspec);
-    (void)hipFree(e->d_pf);
-    (void)hipFree(e->d_cnt);
-    (void)hipFree(e->d_done);
-    (void)hipFree(e->d_queue);
-    (void)hipFree(e->d_head);
-    (void)hipHostFree(e->h_brec);
-    (void)hipHostFree(e->h_bchain);
-    (void)hipHostFree(e->h_pf);
-    e->d_cnt = e->d_done = e->d_queue = e->d_head = nullptr;
+    // free and forget every run buffer first, so that a failed allocation
+    // below never leaves a dangling pointer for free_all or a later retry
+    auto dfree = [](auto*& p) {
+        (void)hipFree(p);
+        p = nullptr;
+    };
+    auto hfree = [](auto*& p) {
+        (void)hipHostFree(p);
+        p = nullptr;
+    };
+    dfree(e->d_bpic);
+    dfree(e->d_bpl);
+    dfree(e->d_brec);
+    dfree(e->d_bchain);
+    dfree(e->d_bspec);
+    dfree(e->d_pf);
+    dfree(e->d_cnt);
+    dfree(e->d_done);
+    dfree(e->d_queue);
+    dfree(e->d_head);
+    hfree(e->h_brec);
+    hfree(e->h_bchain);
+    hfree(e->h_pf);
     e->bcap = 0;
     hipError_t r;
     if ((r = hipMalloc(&e->d_bpic, pic * n)) || (r = hipMalloc(&e->d_bpl, 4 * e->plsz * n)) ||
@@ -626,8 +666,15 @@ static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
         (r = hipMalloc(&e->d_queue, sizeof(int32_t) * nmb * n)) || (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * n + 1))))
         return r;
     if (!e->d_err && (r = hipMalloc(&e->d_err, sizeof(int32_t) * 4))) return r;
+    // defined contents from the start (nothing reads a run buffer before the
+    // run writes it; this keeps any such read deterministic)
+    if ((r = hipMemsetAsync(e->d_bpic, 0, pic * n, e->stream)) || (r = hipMemsetAsync(e->d_bpl, 0, 4 * e->plsz * n, e->stream)) ||
+        (r = hipMemsetAsync(e->d_brec, 0, sizeof(MbRecord) * nmb * n, e->stream)) ||
+        (r = hipMemsetAsync(e->d_bchain, 0, sizeof(MbChain) * nmb * n, e->stream)))
+        return r;
     std::vector<int32_t> spec((size_t)e->mbh * n, 9);  // speculated rdo.Single_ctr at every row start
-    if ((r = hipMemcpy(e->d_bspec, spec.data(), sizeof(int32_t) * spec.size(), hipMemcpyHostToDevice))) return r;
+    if ((r = hipMemcpyAsync(e->d_bspec, spec.data(), sizeof(int32_t) * spec.size(), hipMemcpyHostToDevice, e->stream))) return r;
+    if ((r = hipStreamSynchronize(e->stream))) return r;
     e->bcap = n;
     return hipSuccess;
 }
@@ -678,69 +725,39 @@ static void store_result(hl_amd_encoder_t* e, int i, const hl_amd_result_t& src,
     dst->data = e->bout[i].data();
 }
 
-// Slice writers of a pipelined run: pictures become writable in order (their
-// records copied to h_brec); worker threads serialise them meanwhile, each
-// with its own scratch buffers, into bout[base + k].
-struct RunWriters {
-    hl_amd_encoder_t* e;
-    int m, base;
-    std::mutex mu;
-    std::condition_variable cv;
-    int ready = 0, next = 0;
-    bool stop = false;
-    std::vector<size_t> size;  // bytes written per picture incl. the start code; 0 = too short
-    std::vector<std::thread> th;
-
-    RunWriters(hl_amd_encoder_t* enc, int m_, int base_) : e(enc), m(m_), base(base_), size(m_, 0)
-    {
-        const int n = std::max(1, std::min(m, e->nwriters));
-        const StreamParams sp{e->W, e->H, e->p.qp, e->p.deblock};
-        if ((int)e->wscratch.size() < n) {
-            e->wscratch.resize(n);
-            e->wout.resize(n);
-        }
-        for (int w = 0; w < n; ++w) {
-            e->wscratch[w].resize(slice_scratch_bytes(sp));
-            e->wout[w].resize(slice_scratch_bytes(sp) + 64);
-        }
-        for (int w = 0; w < n; ++w) th.emplace_back([this, w] { work(w); });
+// Slice writers of a pipelined run: the run's records are in h_brec; worker
+// threads serialise its pictures in parallel, each with its own scratch
+// buffers, into bout[base + k].  Returns the bytes written per picture
+// (start code included; 0 = output buffer too short).
+static std::vector<size_t> write_run(hl_amd_encoder_t* e, int m, int base)
+{
+    const int n = std::max(1, std::min(m, e->nwriters));
+    const StreamParams sp{e->W, e->H, e->p.qp, e->p.deblock};
+    if ((int)e->wscratch.size() < n) {
+        e->wscratch.resize(n);
+        e->wout.resize(n);
     }
-    ~RunWriters() { finish(); }
-    void publish(int p)
-    {
-        std::lock_guard<std::mutex> l(mu);
-        ready = std::max(ready, p);
-        cv.notify_all();
+    for (int w = 0; w < n; ++w) {
+        e->wscratch[w].resize(slice_scratch_bytes(sp));
+        e->wout[w].resize(slice_scratch_bytes(sp) + 64);
     }
-    void finish()
-    {
-        {
-            std::lock_guard<std::mutex> l(mu);
-            stop = true;
-            cv.notify_all();
-        }
-        for (auto& t : th) t.join();
-        th.clear();
-    }
-    void work(int w)
-    {
-        const StreamParams sp{e->W, e->H, e->p.qp, e->p.deblock};
-        for (;;) {
-            int k;
-            {
-                std::unique_lock<std::mutex> l(mu);
-                cv.wait(l, [this] { return next < ready || stop; });
-                if (next >= ready) return;
-                k = next++;
-            }
+    std::vector<size_t> size(m, 0);
+    std::atomic<int> next{0};
+    auto work = [&](int w) {
+        for (int k; (k = next.fetch_add(1)) < m;) {
             const SliceState ss{e->run_intra[k], e->pict_count + k, e->run_idr_id[k]};
             uint8_t* out = e->wout[w].data();
-            const size_t n = write_slice(sp, ss, e->h_brec + (size_t)e->nmb * k, e->wscratch[w].data(), out, e->wout[w].size());
-            size[k] = n;
-            if (n) e->bout[base + k].assign(out + 3, out + n);
+            const size_t nb = write_slice(sp, ss, e->h_brec + (size_t)e->nmb * k, e->wscratch[w].data(), out, e->wout[w].size());
+            size[k] = nb;
+            if (nb) e->bout[base + k].assign(out + 3, out + nb);
         }
-    }
-};
+    };
+    std::vector<std::thread> th;
+    for (int w = 1; w < n; ++w) th.emplace_back(work, w);
+    work(0);
+    for (auto& t : th) t.join();
+    return size;
+}
 
 constexpr int kMaxRun = 128;  // pictures per pipelined launch (bench.py MAX_RUN)
 
@@ -830,7 +847,6 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     P.tail = e->d_head + m;
     P.oldest = e->d_head + 2 * m;
     P.err = e->d_err;
-    P.progress = e->d_prog;
     k_pipe_init<<<(unsigned)((nmb * m + 255) / 256), 256, 0, e->stream>>>(P, e->mbw, e->mbh);
     HL_HIP_CHECK(hipGetLastError());
     int wgs = e->pipe_wg;
@@ -841,48 +857,19 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         HL_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_pipeline, kMbThreads, 0));
         wgs = std::max(1, cus * occ);
     }
-    __atomic_store_n(e->h_prog, 0, __ATOMIC_RELEASE);
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[4], e->stream));
     k_pipeline<<<wgs, kMbThreads, 0, e->stream>>>(P, e->mbw, e->mbh);
     HL_HIP_CHECK(hipGetLastError());
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[5], e->stream));
-    // While the run goes on, the records of every finished picture are copied
-    // on the copy stream and serialised by the writer threads.
-    RunWriters wr(e, m, base);
-    hipError_t q = hipSuccess;
-    int copied = 0;
-    for (;;) {
-        int p = __atomic_load_n(e->h_prog, __ATOMIC_ACQUIRE);
-        if (p <= copied) {
-            q = hipStreamQuery(e->stream);
-            if (q == hipErrorNotReady) {
-                std::this_thread::sleep_for(std::chrono::microseconds(100));
-                continue;
-            }
-            break;  // the run has ended (or failed); the rest is handled below
-        }
-        p = std::min(p, m);
-        q = hipMemcpyAsync(e->h_brec + nmb * copied, e->d_brec + nmb * copied, sizeof(MbRecord) * nmb * (p - copied), hipMemcpyDeviceToHost,
-                           e->cstream);
-        if (q == hipSuccess) q = hipStreamSynchronize(e->cstream);
-        if (q != hipSuccess) break;
-        copied = p;
-        wr.publish(copied);
-    }
-    if (q != hipSuccess && q != hipErrorNotReady) {
-        wr.finish();
-        HL_HIP_CHECK(q);
-    }
+    // The records, chain records and give-up counter come back stream-ordered
+    // after the run (the persistent kernel holds every CU, so copies issued
+    // while it runs could not start anyway); writer threads then serialise
+    // the pictures in parallel.
     int32_t err = 0;
-    hipError_t r = hipMemcpyAsync(e->h_bchain, e->d_bchain, sizeof(MbChain) * nmb * m, hipMemcpyDeviceToHost, e->stream);
-    if (r == hipSuccess) r = hipMemcpyAsync(&err, e->d_err, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream);
-    if (r == hipSuccess && copied < m)
-        r = hipMemcpyAsync(e->h_brec + nmb * copied, e->d_brec + nmb * copied, sizeof(MbRecord) * nmb * (m - copied), hipMemcpyDeviceToHost,
-                           e->stream);
-    if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
-    if (r == hipSuccess && err == 0) wr.publish(m);
-    wr.finish();
-    HL_HIP_CHECK(r);
+    HL_HIP_CHECK(hipMemcpyAsync(e->h_bchain, e->d_bchain, sizeof(MbChain) * nmb * m, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(&err, e->d_err, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(e->h_brec, e->d_brec, sizeof(MbRecord) * nmb * m, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipStreamSynchronize(e->stream));
     if (e->timing) {
         (void)hipEventElapsedTime(&e->ms[0], e->ev[0], e->ev[1]);
         (void)hipEventElapsedTime(&e->ms[1], e->ev[4], e->ev[5]);
@@ -906,8 +893,10 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         e->reruns = 1;
         return HL_AMD_SUCCESS;
     }
+    const std::vector<size_t> wsize = write_run(e, m, base);
+    for (int k = 0; k < m; ++k) e->last_recs[base + k] = e->h_brec + nmb * k;
     for (int k = 0; k < m; ++k) {
-        if (!wr.size[k]) return HL_AMD_ERROR_TOOSHORT;
+        if (!wsize[k]) return HL_AMD_ERROR_TOOSHORT;
         hl_amd_result_t& o = res[k];
         o.type = HL_AMD_RESULT_TYPE_DATA;
         o.data = e->bout[base + k].data();
@@ -940,6 +929,7 @@ extern "C" int32_t hl_amd_encode_batch(hl_amd_encoder_t* e, int32_t n, const uin
     for (int i = 0; i < n; ++i)
         if (!y[i] || !u[i] || !v[i]) return HL_AMD_ERROR_INVALID_PARAMETER;
     e->bout.resize(n);
+    e->last_recs.assign(n, nullptr);
     int i = 0;
     while (i < n) {
         if (n - i == 1) {  // a lone picture takes the per-picture path
@@ -947,6 +937,7 @@ extern "C" int32_t hl_amd_encode_batch(hl_amd_encoder_t* e, int32_t n, const uin
             const int32_t rc = encode_frame(e, y[i], u[i], v[i], &r);
             if (rc) return rc;
             store_result(e, i, r, &results[i]);
+            e->last_recs[i] = e->h_rec;
             ++i;
             continue;
         }
@@ -981,6 +972,7 @@ extern "C" int32_t hl_amd_pipeline_occupancy(void)
 extern "C" int32_t hl_amd_encode_device(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t* u, const uint8_t* v, hl_amd_result_t* r)
 {
     if (!e || !y || !u || !v || !r) return HL_AMD_ERROR_INVALID_PARAMETER;
+    e->last_recs.assign(1, e->h_rec);
     return encode_frame(e, y, u, v, r);
 }
 
@@ -990,6 +982,7 @@ extern "C" int32_t hl_amd_encode(hl_amd_encoder_t* e, const uint8_t* y, const ui
     HL_HIP_CHECK(hipMemcpyAsync(e->d_in[0], y, (size_t)e->W * e->H, hipMemcpyHostToDevice, e->stream));
     HL_HIP_CHECK(hipMemcpyAsync(e->d_in[1], u, (size_t)e->Wc * e->Hc, hipMemcpyHostToDevice, e->stream));
     HL_HIP_CHECK(hipMemcpyAsync(e->d_in[2], v, (size_t)e->Wc * e->Hc, hipMemcpyHostToDevice, e->stream));
+    e->last_recs.assign(1, e->h_rec);
     return encode_frame(e, e->d_in[0], e->d_in[1], e->d_in[2], r);
 }
 
@@ -1033,5 +1026,16 @@ extern "C" int32_t hl_amd_profile_counters(hl_amd_encoder_t* e, unsigned long lo
     HL_HIP_CHECK(hipMemset(e->d_prof, 0, sizeof(unsigned long long) * 64));
     return HL_AMD_SUCCESS;
 }
+
+extern "C" int32_t hl_amd_debug_records(hl_amd_encoder_t* e, int32_t k, void* out, size_t bytes)
+{
+    if (!e || !out || k < 0) return HL_AMD_ERROR_INVALID_PARAMETER;
+    if (k >= (int)e->last_recs.size() || !e->last_recs[k]) return HL_AMD_ERROR_INVALID_STATE;
+    if (bytes != sizeof(MbRecord) * (size_t)e->nmb) return HL_AMD_ERROR_INVALID_PARAMETER;
+    memcpy(out, e->last_recs[k], bytes);
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_record_size(void) { return (int32_t)sizeof(MbRecord); }
 
 extern "C" const char* hl_amd_version(void) { return "hartallo_amd 0.1 (gfx950)"; }

@@ -593,6 +593,31 @@ HD void mb_begin(Ctx& c)
         S.mb_type = 0;
     }
     HL_SYNC();
+#if defined(HL_DIAG_INPUTS)
+    // diagnostic builds: digests of everything the decision reads from other
+    // macroblocks, so that a parity failure names the input that differed
+    if (tid == 0) {
+        auto fnv = [](const void* p, int n, uint32_t h) {
+            const uint8_t* b = (const uint8_t*)p;
+            for (int i = 0; i < n; ++i) h = (h ^ b[i]) * 16777619u;
+            return h;
+        };
+        uint32_t* d = F.rec[a].dbg;
+        d[0] = fnv(S.top, sizeof(S.top), 2166136261u);
+        d[1] = fnv(S.left, sizeof(S.left), 2166136261u);
+        d[2] = fnv(S.cleft, sizeof(S.cleft), fnv(S.ctop, sizeof(S.ctop), 2166136261u));
+        uint32_t h = 2166136261u;
+        for (int w = 1; w < 5; ++w) {
+            h = fnv(&S.nb[w].avail, 4, h);
+            if (S.nb[w].avail) h = fnv(&S.nb[w], sizeof(NbInfo), h);
+        }
+        d[3] = fnv(S.mvs, sizeof(S.mvs), fnv(S.mvg, sizeof(S.mvg), h));
+        d[4] = fnv(S.extCB, 4, fnv(S.extCA, 4, fnv(S.extB, 16, fnv(S.extA, 16, fnv(S.nb_i4, sizeof(S.nb_i4), fnv(S.nb_pm0, 12, 2166136261u))))));
+        d[5] = fnv(&S.cbp_c, 4, fnv(&S.cbp_l, 4, fnv(S.tcc, 8, fnv(S.tc, 16, 2166136261u))));
+        d[6] = fnv(S.cac, sizeof(S.cac), fnv(S.src, 256, 2166136261u));
+        d[7] = (uint32_t)(c.chain & 0xFF) | ((uint32_t)c.spec << 8);
+    }
+#endif
 }
 
 // --------------------------------------------------------------------------
@@ -1030,7 +1055,7 @@ HD void reach_wait(Ctx& c, const PartGeo& g, const int pmv[2])
         int tx, ty;
         reach_task(X, Y, F.mbw, F.mbh, tx, ty);
         spin_ge(F.ref_done + ty * F.mbw + tx, F.ref_epoch, F.perr);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     HL_SYNC();
@@ -1627,7 +1652,7 @@ HD void resolve_chain(Ctx& c)
             const int32_t* done = F.run_done + (size_t)pos * nmb + (size_t)y * F.mbw;
             const MbChain* row = F.run_chain + (size_t)pos * nmb + (size_t)y * F.mbw;
             if (lane == 0) spin_ge(done + F.mbw - 1, 1, F.perr);  // the row's last MB: the whole row is final
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             bool fr = false;
             for (int x = lane; x < F.mbw; x += 64) fr = fr || ld_relaxed(&row[x].fresh) != 0;

@@ -175,7 +175,6 @@ struct PipeArgs {
     int32_t* tail;   // [nframes] next queue slot to push
     int32_t* oldest; // [0] first unfinished picture of the run
     int32_t* err;    // [0] number of bounded waits that gave up
-    int32_t* progress;  // host-mapped: pictures finished so far (the host writes their bitstreams meanwhile), or null
 };
 
 }  // namespace hl

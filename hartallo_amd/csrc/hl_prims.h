@@ -387,6 +387,16 @@ HD void unscan(const T* list, int* m)
 // Inter-workgroup flags (agent scope, see hl_pipeline.h)
 typedef __attribute__((address_space(1))) int32_t gi32;
 
+// Scopes of the inter-workgroup release / acquire fences of pipelined runs
+// (hl_pipeline.h).  Agent scope is the documented gfx950 form
+// (cdna_hip_programming.md, Guideline 16); diagnostic builds may override.
+#ifndef HL_ACQ_SCOPE
+#define HL_ACQ_SCOPE "agent"
+#endif
+#ifndef HL_REL_SCOPE
+#define HL_REL_SCOPE "agent"
+#endif
+
 __device__ __forceinline__ int32_t ld_relaxed(const int32_t* p)
 {
     return __hip_atomic_load((gi32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -59,6 +59,9 @@ struct MbRecord {
     int16_t i16dc[16];
     int16_t cdc[2][4];
     int16_t cac[2][4][16];      // ChromaACLevel as written (15 used)
+#if defined(HL_DIAG_INPUTS)
+    uint32_t dbg[8];            // diagnostic builds: digests of the MB's inputs (hl_mbcore.h mb_begin)
+#endif
 };
 
 // Per-MB record of the rdo.Single_ctr chain (the reference keeps one

@@ -136,6 +136,13 @@ int32_t hl_amd_last_mb_launches(hl_amd_encoder_t* encoder);
  * frame (n <= 64 + macroblocks).  The phase counters are cleared by the call. */
 int32_t hl_amd_profile_counters(hl_amd_encoder_t* encoder, unsigned long long* out, int32_t n);
 
+/* diagnostics: the macroblock records (syntax handed to the slice writer,
+ * hartallo_amd/csrc/hl_types.h MbRecord) of picture k of the last encode
+ * call, bytes = macroblocks * hl_amd_record_size(); INVALID_STATE when the
+ * call did not keep them (a run re-encoded picture by picture) */
+int32_t hl_amd_debug_records(hl_amd_encoder_t* encoder, int32_t k, void* out, size_t bytes);
+int32_t hl_amd_record_size(void);
+
 const char* hl_amd_version(void);
 
 #ifdef __cplusplus

@@ -11,7 +11,11 @@
  * The dumps are read back through the reference's own structures
  * (hl_codec_264_t / hl_codec_264_layer_t / hl_codec_264_mb_t).
  *
- * usage: ref_enc W H N qp me_range deblock gop early_term in.yuv out_prefix [quiet]
+ * and <prefix>.idx, the byte offset in <prefix>.264 where each frame's
+ * output ends (one decimal number per line).
+ *
+ * usage: ref_enc W H N qp me_range deblock gop early_term in.yuv out_prefix [quiet|rec]
+ *   quiet: no .rec.yuv / .mbs dumps (timing runs); rec: .rec.yuv but no .mbs
  */
 #include <hartallo/hl_api.h>
 #include <hartallo/hl_frame.h>
@@ -90,7 +94,8 @@ int main(int argc, char** argv)
     int mer = atoi(argv[5]), db = atoi(argv[6]), gop = atoi(argv[7]), et = atoi(argv[8]);
     const char* in = argv[9];
     const char* pre = argv[10];
-    int quiet = argc > 11;
+    int quiet = argc > 11 && strcmp(argv[11], "rec") != 0;
+    int no_mbs = argc > 11;
     char path[1024];
 
     hl_debug_set_level(HL_DEBUG_LEVEL_ERROR);
@@ -124,9 +129,13 @@ int main(int argc, char** argv)
     if (!quiet) {
         snprintf(path, sizeof(path), "%s.rec.yuv", pre);
         frec = fopen(path, "wb");
+    }
+    if (!no_mbs) {
         snprintf(path, sizeof(path), "%s.mbs", pre);
         fmb = fopen(path, "wb");
     }
+    snprintf(path, sizeof(path), "%s.idx", pre);
+    FILE* fidx = fopen(path, "wb");
     static const uint8_t scp[3] = { 0, 0, 1 };
     int32_t rec[MBR_STRIDE];
     int n = 0;
@@ -144,6 +153,7 @@ int main(int argc, char** argv)
         if (n > 0) tp += dt;
         if (r->type & HL_CODEC_RESULT_TYPE_HDR) fwrite(c->hdr_bytes, 1, c->hdr_bytes_count, fo);
         if (r->type & HL_CODEC_RESULT_TYPE_DATA) { fwrite(scp, 1, 3, fo); fwrite(r->data_ptr, 1, r->data_size, fo); }
+        if (fidx) fprintf(fidx, "%ld\n", ftell(fo));
         if (!quiet) {
             hl_codec_264_t* p264 = (hl_codec_264_t*)c;
             hl_codec_264_layer_t* L = p264->layers.pc_active;
@@ -151,7 +161,7 @@ int main(int argc, char** argv)
             fwrite(pict->pc_data_y, 1, (size_t)W * H, frec);
             fwrite(pict->pc_data_u, 1, (size_t)W * H / 4, frec);
             fwrite(pict->pc_data_v, 1, (size_t)W * H / 4, frec);
-            for (size_t a = 0; a < L->u_list_macroblocks_count; ++a) {
+            for (size_t a = 0; fmb && a < L->u_list_macroblocks_count; ++a) {
                 dump_mb(L->pp_list_macroblocks[a], rec);
                 fwrite(rec, sizeof(int32_t), MBR_STRIDE, fmb);
             }
@@ -161,6 +171,7 @@ int main(int argc, char** argv)
     fclose(fo);
     if (frec) fclose(frec);
     if (fmb) fclose(fmb);
+    if (fidx) fclose(fidx);
     printf("{\"frames\": %d, \"seconds\": %.6f, \"fps\": %.4f, \"mb_per_s\": %.1f, \"p_seconds\": %.6f, \"p_fps\": %.4f}\n",
            n, tot, n / tot, (double)n * (W / 16) * (H / 16) / tot, tp, n > 1 ? (n - 1) / tp : 0.0);
     return 0;

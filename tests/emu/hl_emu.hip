@@ -111,7 +111,22 @@ extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, co
     F.spec = e->spec.data();
     F.prof = nullptr;
     int chain = e->chain_end;
+    // HL_EMU_POISON=<seed>: fill the workgroup's LDS image with pseudo-random
+    // bytes before every macroblock (a GPU workgroup finds whatever the
+    // previous task or kernel left there); any read-before-write of Shared
+    // that matters then changes the output.
+    static const char* poison = getenv("HL_EMU_POISON");
+    static uint64_t prng = poison ? strtoull(poison, nullptr, 10) * 0x9E3779B97F4A7C15ull + 1 : 0;
     for (int a = 0; a < e->nmb; ++a) {
+        if (poison) {
+            uint8_t* s = (uint8_t*)e->S;
+            for (size_t i = 0; i < sizeof(Shared); ++i) {
+                prng ^= prng << 13;
+                prng ^= prng >> 7;
+                prng ^= prng << 17;
+                s[i] = (uint8_t)prng;
+            }
+        }
         encode_mb(F, *e->S, a, 0, 1, chain);
         chain = e->chain[a].s_out;
     }

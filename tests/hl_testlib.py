@@ -149,6 +149,65 @@ class GpuEncoder:
         return np.concatenate(self.enc.recon())
 
 
+def significant_records(r: np.ndarray) -> np.ndarray:
+    """Copy of an MbRecord array with the fields the slice writer does not
+    read for that macroblock zeroed (they hold LDS scratch of the search,
+    which is not part of the result): mv of intra MBs, levels of uncoded
+    blocks, I16 / I4 / chroma syntax of MBs without it, padding."""
+    r = r.copy()
+    if "dbg" in r.dtype.names:
+        r["dbg"] = 0
+    intra = (r["flags"] & 1) != 0
+    skip = (r["flags"] & 4) != 0
+    r["pad0"] = 0
+    r["mv"][intra] = 0
+    for f in ("num_sub", "sub_mb_type", "mvd"):
+        r[f][intra | skip] = 0
+    r["i16dc"][r["pm0"] != 3] = 0
+    r["nc_dc"][r["pm0"] != 3] = 0
+    for f in ("i4mode", "prev_flag", "rem_mode"):
+        r[f][r["pm0"] != 2] = 0
+    for f in ("chroma_mode", "i16mode"):
+        r[f][~intra] = 0
+    coded8 = (r["cbp_l"][:, None] >> (np.arange(16)[None, :] >> 2)) & 1
+    r["luma"][coded8 == 0] = 0
+    r["nc_luma"][coded8 == 0] = 0
+    r["cdc"][(r["cbp_c"] & 3) == 0] = 0
+    r["cac"][(r["cbp_c"] & 2) == 0] = 0
+    r["nc_cac"][(r["cbp_c"] & 2) == 0] = 0
+    return r
+
+
+def first_record_diff(recs_a, recs_b, mbw: int) -> str:
+    """First (picture, MB, field) where two lists of per-picture MbRecord
+    arrays (Encoder.debug_records) differ in a field the writer reads, as a
+    message for a failing parity assertion."""
+    for f, (a, b) in enumerate(zip(recs_a, recs_b)):
+        if a is None or b is None:
+            return f"picture {f}: records not kept"
+        if "dbg" in a.dtype.names:  # diagnostic build: the first MB whose inputs differ, in decision order
+            order = sorted(range(len(a)), key=lambda m: ((m % mbw) + 2 * (m // mbw), m // mbw))
+            for m in order:
+                if not np.array_equal(a[m]["dbg"], b[m]["dbg"]):
+                    k = int(np.nonzero(a[m]["dbg"] != b[m]["dbg"])[0][0])
+                    names = ["top", "left", "chroma nb", "nb state/motion", "nC/ext", "live tc/cbp", "cac/src", "chain"]
+                    print(f"  picture {f}: first input difference at MB {m} ({m % mbw},{m // mbw}) in {names[k]}: "
+                          f"{a[m]['dbg'].tolist()} vs {b[m]['dbg'].tolist()}", flush=True)
+                    break
+        a, b = significant_records(a), significant_records(b)
+        if a.tobytes() == b.tobytes():
+            continue
+        for m in range(len(a)):
+            if a[m].tobytes() != b[m].tobytes():
+                for name in a.dtype.names:
+                    if not np.array_equal(a[m][name], b[m][name]):
+                        va, vb = np.asarray(a[m][name]).ravel(), np.asarray(b[m][name]).ravel()
+                        i = int(np.nonzero(va != vb)[0][0])
+                        return (f"picture {f} MB {m} ({m % mbw},{m // mbw}) e_type {a[m]['e_type']}/{b[m]['e_type']} field {name}[{i}:]: "
+                                f"{va[i:i + 16].tolist()} vs {vb[i:i + 16].tolist()}")
+    return "records equal (difference after the decisions: writer or deblocking)"
+
+
 def md5(b) -> str:
     return hashlib.md5(bytes(b)).hexdigest()
 

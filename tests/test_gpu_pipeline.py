@@ -17,7 +17,7 @@ import pytest
 import torch
 
 from hartallo_amd import Encoder, synth
-from hl_testlib import GOLDEN, GOLDEN_CONFIGS, OracleEncoder, first_diff, golden_input, md5
+from hl_testlib import GOLDEN, GOLDEN_CONFIGS, OracleEncoder, first_diff, first_record_diff, golden_input, md5
 
 pytestmark = pytest.mark.gpu
 
@@ -31,7 +31,7 @@ def _device_frames(clip, w, h):
     return dev, [(dev[i].data_ptr(), dev[i].data_ptr() + n, dev[i].data_ptr() + n + n // 4) for i in range(len(clip))]
 
 
-def _batch(w, h, qp, mer, db, gop, clip, geometry=None, split=None):
+def _batch(w, h, qp, mer, db, gop, clip, geometry=None, split=None, records=None):
     enc = Encoder(w, h, qp, mer, db, gop)
     if geometry:
         enc.set_pipeline(*geometry)
@@ -40,28 +40,45 @@ def _batch(w, h, qp, mer, db, gop, clip, geometry=None, split=None):
     i = 0
     for n in bounds:
         out += enc.encode_batch_device(ptrs[i:i + n])
+        if records is not None:
+            records += [enc.debug_records(k) for k in range(n)]
         i += n
     rec = np.concatenate(enc.recon())
     enc.close()
     return [r.annexb() for r in out], rec
 
 
-def _single(w, h, qp, mer, db, gop, clip):
+def _single(w, h, qp, mer, db, gop, clip, records=None):
     enc = Encoder(w, h, qp, mer, db, gop)
     dev, ptrs = _device_frames(clip, w, h)
-    out = [enc.encode_device(*p).annexb() for p in ptrs]
+    out = []
+    for p in ptrs:
+        out.append(enc.encode_device(*p).annexb())
+        if records is not None:
+            records.append(enc.debug_records(0))
     rec = np.concatenate(enc.recon())
     enc.close()
     return out, rec
+
+
+def _diagnose(w, h, qp, mer, db, gop, clip, geometry=None, split=None):
+    """On a mismatch: the first (picture, MB, field) where the pipelined
+    run's decisions differ from one-call-per-picture encoding."""
+    ra, rb = [], []
+    _single(w, h, qp, mer, db, gop, clip, ra)
+    _batch(w, h, qp, mer, db, gop, clip, geometry, split, rb)
+    return first_record_diff(ra, rb, w // 16)
 
 
 @pytest.mark.parametrize("cfg", [c for c in GOLDEN_CONFIGS if c[3] >= 3], ids=[c[0] for c in GOLDEN_CONFIGS if c[3] >= 3])
 def test_batch_golden_streams(gpu, cfg):
     name, w, h, n, qp, mer, db, gop, seed = cfg
     ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()
-    out, rec = _batch(w, h, qp, mer, db, gop, golden_input(cfg))
+    clip = golden_input(cfg)
+    out, rec = _batch(w, h, qp, mer, db, gop, clip)
     got = b"".join(out)
-    assert got == ref, f"{name}: first differing byte {first_diff(got, ref)}"
+    if got != ref:
+        pytest.fail(f"{name}: first differing byte {first_diff(got, ref)}; {_diagnose(w, h, qp, mer, db, gop, clip)}")
     assert md5(rec) == GOLD[name]["recon_md5"][n - 1]
 
 
@@ -72,7 +89,9 @@ def test_batch_equals_single_calls(gpu, geometry):
     a, ra = _single(w, h, 26, 16, 1, 30, clip)
     b, rb = _batch(w, h, 26, 16, 1, 30, clip, geometry, split=[1, 5, 3])
     for f in range(n):
-        assert a[f] == b[f], f"frame {f}: first differing byte {first_diff(a[f], b[f])}"
+        if a[f] != b[f]:
+            pytest.fail(f"frame {f}: first differing byte {first_diff(a[f], b[f])}; "
+                        f"{_diagnose(w, h, 26, 16, 1, 30, clip, geometry, [1, 5, 3])}")
     assert np.array_equal(ra, rb)
 
 
@@ -104,7 +123,8 @@ def test_batch_1088p_equals_single_calls(gpu):
     a, ra = _single(w, h, 28, 16, 1, 30, clip)
     b, rb = _batch(w, h, 28, 16, 1, 30, clip)
     for f in range(n):
-        assert a[f] == b[f], f"frame {f}: first differing byte {first_diff(a[f], b[f])}"
+        if a[f] != b[f]:
+            pytest.fail(f"frame {f}: first differing byte {first_diff(a[f], b[f])}; {_diagnose(w, h, 28, 16, 1, 30, clip)}")
     assert np.array_equal(ra, rb)
 
 
@@ -121,6 +141,7 @@ def test_batch_1088p_spans_gops(gpu):
     rb = np.concatenate(enc.recon())
     enc.close()
     for f in range(n):
-        assert a[f] == b[f], f"frame {f}: first differing byte {first_diff(a[f], b[f])}"
+        if a[f] != b[f]:
+            pytest.fail(f"frame {f}: first differing byte {first_diff(a[f], b[f])}; {_diagnose(w, h, 28, 16, 1, 3, clip)}")
     assert np.array_equal(ra, rb)
     assert launches == 1 and reruns == 0, (launches, reruns)

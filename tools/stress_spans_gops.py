@@ -4,8 +4,9 @@ stream differs from the same frames encoded one call at a time.
 
   python tools/stress_spans_gops.py [repeats] [frames] [gop]
 
-Development tool for DESIGN.md §10 item 0 (a timing-dependent mismatch seen
-once under another device schedule).  Set HL_LIB to time another build.
+Development tool for the pipelined-run parity defect.  Set HL_LIB
+to run another build of the library, HL_PIPE=workgroups,reach,window to set
+the pipeline geometry.
 """
 import os
 import sys
@@ -22,7 +23,7 @@ from hartallo_amd import _lib  # noqa: E402
 if os.environ.get("HL_LIB"):
     _lib.load_library(os.path.abspath(os.environ["HL_LIB"]))
 from hartallo_amd import Encoder, synth  # noqa: E402
-from hl_testlib import first_diff  # noqa: E402
+from hl_testlib import first_diff, first_record_diff  # noqa: E402
 
 
 def main():
@@ -36,17 +37,33 @@ def main():
     ny = w * h
     ptrs = [(dev[i].data_ptr(), dev[i].data_ptr() + ny, dev[i].data_ptr() + ny + ny // 4) for i in range(n)]
     enc = Encoder(w, h, 28, 16, 1, gop)
-    ref = [enc.encode_device(*p).annexb() for p in ptrs]
+    ref, ref_recs = [], []
+    for p in ptrs:
+        ref.append(enc.encode_device(*p).annexb())
+        ref_recs.append(enc.debug_records(0))
+    ref_rec = np.concatenate(enc.recon())
     enc.close()
+    geometry = tuple(int(v) for v in os.environ["HL_PIPE"].split(",")) if os.environ.get("HL_PIPE") else None
     bad = 0
     for r in range(reps):
         enc = Encoder(w, h, 28, 16, 1, gop)
-        out = [x.annexb() for x in enc.encode_batch_device(ptrs)]
+        if geometry:
+            enc.set_pipeline(*geometry)
+        if os.environ.get("HL_STRESS_SINGLE"):  # the per-picture path instead of pipelined runs
+            out, recs = [], []
+            for p in ptrs:
+                out.append(enc.encode_device(*p).annexb())
+                recs.append(enc.debug_records(0))
+        else:
+            out = [x.annexb() for x in enc.encode_batch_device(ptrs)]
+            recs = [enc.debug_records(k) for k in range(n)]
         reruns = enc.last_reruns()
+        recon_ok = np.array_equal(np.concatenate(enc.recon()), ref_rec)
         enc.close()
         diffs = [(f, first_diff(ref[f], out[f]), len(ref[f])) for f in range(n) if ref[f] != out[f]]
-        bad += bool(diffs)
-        print(f"run {r}: {'MISMATCH ' + str(diffs) if diffs else 'ok'} (reruns {reruns})", flush=True)
+        bad += bool(diffs) or not recon_ok
+        msg = "ok" if not diffs else f"MISMATCH {diffs}; {first_record_diff(ref_recs, recs, w // 16)}"
+        print(f"run {r}: {msg} (recon {'equal' if recon_ok else 'DIFFERS'}, reruns {reruns})", flush=True)
     print(f"{bad} of {reps} runs differ", flush=True)
     sys.exit(1 if bad else 0)
 
