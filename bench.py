@@ -36,6 +36,13 @@ BYTES_PER_MB = 2752  # compulsory HBM bytes per macroblock, DESIGN.md / SURVEY Â
 # passes on this workload (tools/pmc_traffic.sh, corrected per MI355X_MICROARCH.md)
 PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_traffic_k_pipeline.json")
 MAX_RUN = 128  # pictures per pipelined launch (kMaxRun, hl_encoder.hip)
+# The synthetic stream is always generated for BENCH_CLIP_FRAMES frames (its
+# texture depends on the clip length) and its first warmup + steps frames are
+# encoded; tests/golden/bench_golden.json holds the reference encoder's
+# per-frame output MD5s for it (tests/golden/make_bench_golden.py), checked
+# after the timed region.
+BENCH_CLIP_FRAMES = 150
+BENCH_GOLDEN = os.path.join(ROOT, "tests", "golden", "bench_golden.json")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 
@@ -69,6 +76,21 @@ def cpu_baseline(frames_host, n_frames):
     }
 
 
+def check_bitexact(outputs, seed):
+    """True / False when every frame's Annex-B output matches the reference
+    encoder's MD5 for this stream (tests/golden/bench_golden.json), None when
+    no reference MD5s cover it."""
+    import hashlib
+
+    key = f"bench_1088p_s{seed}"
+    if not os.path.exists(BENCH_GOLDEN):
+        return None
+    gold = json.load(open(BENCH_GOLDEN)).get(key)
+    if not gold or len(outputs) > len(gold["frame_md5"]) or gold["width"] != W or gold["height"] != H or gold["qp"] != QP:
+        return None
+    return all(hashlib.md5(o).hexdigest() == g for o, g in zip(outputs, gold["frame_md5"]))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -86,7 +108,8 @@ def main():
     torch.cuda.set_device(local)
 
     n_frames = args.warmup + args.steps
-    frames_host = synth.clip(W, H, n_frames, dist.stream_seed(rank))
+    seed = dist.stream_seed(rank)
+    frames_host = synth.clip(W, H, max(n_frames, BENCH_CLIP_FRAMES), seed)[:n_frames]
     # inputs resident in HBM before timing
     dev = torch.from_numpy(frames_host).to(f"cuda:{local}")
     torch.cuda.synchronize()
@@ -94,8 +117,9 @@ def main():
     ptrs = [(dev[i].data_ptr(), dev[i].data_ptr() + ny, dev[i].data_ptr() + ny + nc) for i in range(n_frames)]
 
     enc = Encoder(W, H, QP, ME_RANGE, DEBLOCK, GOP, 0, local)
+    outputs = []
     if args.warmup:  # same entry point as the timed frames (warms the pipelined path and its buffers)
-        enc.encode_batch_device(ptrs[:args.warmup], collect=False)
+        outputs += [r.annexb() for r in enc.encode_batch_device(ptrs[:args.warmup])]
     enc.set_timing(True)
     dist.barrier()
     torch.cuda.synchronize()
@@ -106,6 +130,10 @@ def main():
     elapsed = dist.max_over_ranks(time.perf_counter() - t0)
     ms = enc.timing_ms()
     mb_ms, mb_launches = ms[1], enc.last_mb_launches()  # the (last) pipelined launch
+    # bit-exactness of everything this rank encoded, outside the timed region
+    outputs += [r.annexb() for r in enc.last_batch_results()]
+    bitexact = check_bitexact(outputs, seed)
+    bitexact_all = dist.min_over_ranks(1 if bitexact else 0) if bitexact is not None else None
     # pictures of the last pipelined launch: runs span GOPs, up to MAX_RUN pictures each
     run_frames = (args.steps - 1) % MAX_RUN + 1 if mb_launches == 1 else 1
 
@@ -141,6 +169,9 @@ def main():
             "config": {"workload": "1920x1088 YUV420 IPPP GOP30 QP28 ME16 deblock, one stream per GPU, frame-pipelined", "width": W, "height": H,
                        "qp": QP, "me_range": ME_RANGE, "deblock": DEBLOCK, "gop": GOP, "parallelism": f"streams{world}"},
             "mb_per_s_per_gpu": round(fps / world * nmb, 1),
+            "bitexact": bitexact_all if bitexact_all is None else bool(bitexact_all),
+            "bitexact_check": "every frame of every rank (warm-up and timed) vs the reference encoder's per-frame MD5s "
+                              "(tests/golden/bench_golden.json, oracle/_ref/ref_enc on the same synthetic stream)",
             "bitstream_bytes_per_frame": round(out_bytes / args.steps, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -42,6 +42,8 @@ EXPORTED_SYMBOLS = (
     "hl_amd_profile_counters",
     "hl_amd_debug_records",
     "hl_amd_record_size",
+    "hl_amd_debug_chain",
+    "hl_amd_debug_recon",
     "hl_amd_version",
 )
 
@@ -130,10 +132,12 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_last_mb_launches.restype = i32
     lib.hl_amd_profile_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong), i32]
     lib.hl_amd_profile_counters.restype = i32
-    lib.hl_amd_debug_records.argtypes = [vp, i32, vp, ctypes.c_size_t]
-    lib.hl_amd_debug_records.restype = i32
-    lib.hl_amd_record_size.argtypes = []
-    lib.hl_amd_record_size.restype = i32
+    # diagnostics entry points (absent from older builds loaded through HL_LIB)
+    for name, args in (("hl_amd_debug_records", [vp, i32, vp, ctypes.c_size_t]), ("hl_amd_debug_chain", [vp, i32, vp, ctypes.c_size_t]),
+                       ("hl_amd_debug_recon", [vp, i32, vp, vp, vp]), ("hl_amd_record_size", [])):
+        if hasattr(lib, name):
+            getattr(lib, name).argtypes = args
+            getattr(lib, name).restype = i32
     lib.hl_amd_version.argtypes = []
     lib.hl_amd_version.restype = ctypes.c_char_p
     _lib = lib
@@ -218,7 +222,13 @@ class Encoder:
         rc = self.lib.hl_amd_encode_batch(self._h, n, arr[0], arr[1], arr[2], res)
         if rc != HL_AMD_SUCCESS:
             raise HlAmdError(rc, "hl_amd_encode_batch")
+        self._last_batch = res  # the results stay valid until the next encode call
         return [self._result(r) for r in res] if collect else sum(r.data_size for r in res)
+
+    def last_batch_results(self):
+        """The results of the last encode_batch_device call (also after
+        collect=False), valid until the next encode call."""
+        return [self._result(r) for r in self._last_batch]
 
     def set_pipeline(self, workgroups: int, reach: int, window: int):
         rc = self.lib.hl_amd_set_pipeline(self._h, workgroups, reach, window)
@@ -258,6 +268,8 @@ class Encoder:
         call did not keep them."""
         import numpy as np
 
+        if not hasattr(self.lib, "hl_amd_debug_records"):
+            return None
         nmb = (self.width // 16) * (self.height // 16)
         dt = MB_RECORD
         if self.lib.hl_amd_record_size() == MB_RECORD.itemsize + 32:  # diagnostic build (HL_DIAG_INPUTS)
@@ -269,6 +281,38 @@ class Encoder:
             return None
         if rc != HL_AMD_SUCCESS:
             raise HlAmdError(rc, "hl_amd_debug_records")
+        return out
+
+    def debug_chain(self, k: int):
+        """MbChain records (s_in, s_out, dep, fresh, spec per macroblock) of
+        picture k of the last encode call, as an (nmb, 5) int32 array."""
+        import numpy as np
+
+        if not hasattr(self.lib, "hl_amd_debug_chain"):
+            return None
+        nmb = (self.width // 16) * (self.height // 16)
+        out = np.zeros((nmb, 5), np.int32)
+        rc = self.lib.hl_amd_debug_chain(self._h, k, out.ctypes.data, out.nbytes)
+        if rc == HL_AMD_ERROR_INVALID_STATE:
+            return None
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_debug_chain")
+        return out
+
+    def debug_recon(self, k: int):
+        """Reconstructed planes of picture k of the last encode call,
+        concatenated Y|U|V (None when not kept)."""
+        import numpy as np
+
+        if not hasattr(self.lib, "hl_amd_debug_recon"):
+            return None
+        n = self.width * self.height
+        out = np.zeros(n * 3 // 2, np.uint8)
+        rc = self.lib.hl_amd_debug_recon(self._h, k, out.ctypes.data, out.ctypes.data + n, out.ctypes.data + n + n // 4)
+        if rc == HL_AMD_ERROR_INVALID_STATE:
+            return None
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_debug_recon")
         return out
 
     def last_mb_launches(self) -> int:

@@ -357,6 +357,8 @@ struct hl_amd_encoder_s {
     std::vector<std::vector<uint8_t>> wscratch, wout;
     std::vector<int32_t> run_intra, run_idr_id;  // per picture of the run: IDR, idr_pic_id
     std::vector<const MbRecord*> last_recs;      // host records per picture of the last encode call (diagnostics)
+    std::vector<const MbChain*> last_chain;      // host chain records, same
+    std::vector<const uint8_t*> last_pic;        // device recon (Y|U|V planes contiguous) or null = the current reference
 };
 
 static void free_all(hl_amd_encoder_t* e)
@@ -401,7 +403,9 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
     *out = nullptr;
     if (p->width <= 0 || p->height <= 0 || (p->width & 15) || (p->height & 15)) return HL_AMD_ERROR_INVALID_FORMAT;
     if (p->qp < 0 || p->qp > 51) return HL_AMD_ERROR_INVALID_PARAMETER;
-    if (p->me_early_term) return HL_AMD_ERROR_NOT_IMPLEMENTED;
+    // early termination reads the source one sample around the MB quadrants
+    // (rdo.c:895-896): the picture needs two MB rows and columns
+    if (p->me_early_term && (p->width < 32 || p->height < 32)) return HL_AMD_ERROR_INVALID_FORMAT;
     HL_HIP_CHECK(hipSetDevice(p->device));
     hl_amd_encoder_t* e = new hl_amd_encoder_s();
     e->p = *p;
@@ -528,6 +532,7 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
     F.qpc = e->qpc;
     F.is_intra = intra;
     F.me_range = std::min(64, std::max(1, e->p.me_range));
+    F.early_term = e->p.me_early_term != 0;
     F.lambda = 0.852 * (double)(1 << ((e->p.qp - 12) / 3));
     F.src[0] = y;
     F.src[1] = u;
@@ -710,6 +715,7 @@ static FrameArgs frame_args(hl_amd_encoder_t* e, bool intra)
     F.qpc = e->qpc;
     F.is_intra = intra;
     F.me_range = std::min(64, std::max(1, e->p.me_range));
+    F.early_term = e->p.me_early_term != 0;
     F.lambda = 0.852 * (double)(1 << ((e->p.qp - 12) / 3));
     F.pstride = e->pstride;
     F.plsz = (int32_t)e->plsz;
@@ -894,7 +900,11 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         return HL_AMD_SUCCESS;
     }
     const std::vector<size_t> wsize = write_run(e, m, base);
-    for (int k = 0; k < m; ++k) e->last_recs[base + k] = e->h_brec + nmb * k;
+    for (int k = 0; k < m; ++k) {
+        e->last_recs[base + k] = e->h_brec + nmb * k;
+        e->last_chain[base + k] = e->h_bchain + nmb * k;
+        e->last_pic[base + k] = e->d_bpic + pic * k;
+    }
     for (int k = 0; k < m; ++k) {
         if (!wsize[k]) return HL_AMD_ERROR_TOOSHORT;
         hl_amd_result_t& o = res[k];
@@ -930,6 +940,8 @@ extern "C" int32_t hl_amd_encode_batch(hl_amd_encoder_t* e, int32_t n, const uin
         if (!y[i] || !u[i] || !v[i]) return HL_AMD_ERROR_INVALID_PARAMETER;
     e->bout.resize(n);
     e->last_recs.assign(n, nullptr);
+    e->last_chain.assign(n, nullptr);
+    e->last_pic.assign(n, nullptr);
     int i = 0;
     while (i < n) {
         if (n - i == 1) {  // a lone picture takes the per-picture path
@@ -938,6 +950,7 @@ extern "C" int32_t hl_amd_encode_batch(hl_amd_encoder_t* e, int32_t n, const uin
             if (rc) return rc;
             store_result(e, i, r, &results[i]);
             e->last_recs[i] = e->h_rec;
+            e->last_chain[i] = e->h_chain;
             ++i;
             continue;
         }
@@ -973,6 +986,8 @@ extern "C" int32_t hl_amd_encode_device(hl_amd_encoder_t* e, const uint8_t* y, c
 {
     if (!e || !y || !u || !v || !r) return HL_AMD_ERROR_INVALID_PARAMETER;
     e->last_recs.assign(1, e->h_rec);
+    e->last_chain.assign(1, e->h_chain);
+    e->last_pic.assign(1, nullptr);
     return encode_frame(e, y, u, v, r);
 }
 
@@ -983,6 +998,8 @@ extern "C" int32_t hl_amd_encode(hl_amd_encoder_t* e, const uint8_t* y, const ui
     HL_HIP_CHECK(hipMemcpyAsync(e->d_in[1], u, (size_t)e->Wc * e->Hc, hipMemcpyHostToDevice, e->stream));
     HL_HIP_CHECK(hipMemcpyAsync(e->d_in[2], v, (size_t)e->Wc * e->Hc, hipMemcpyHostToDevice, e->stream));
     e->last_recs.assign(1, e->h_rec);
+    e->last_chain.assign(1, e->h_chain);
+    e->last_pic.assign(1, nullptr);
     return encode_frame(e, e->d_in[0], e->d_in[1], e->d_in[2], r);
 }
 
@@ -1037,5 +1054,31 @@ extern "C" int32_t hl_amd_debug_records(hl_amd_encoder_t* e, int32_t k, void* ou
 }
 
 extern "C" int32_t hl_amd_record_size(void) { return (int32_t)sizeof(MbRecord); }
+
+extern "C" int32_t hl_amd_debug_chain(hl_amd_encoder_t* e, int32_t k, void* out, size_t bytes)
+{
+    if (!e || !out || k < 0) return HL_AMD_ERROR_INVALID_PARAMETER;
+    if (k >= (int)e->last_chain.size() || !e->last_chain[k]) return HL_AMD_ERROR_INVALID_STATE;
+    if (bytes != sizeof(MbChain) * (size_t)e->nmb) return HL_AMD_ERROR_INVALID_PARAMETER;
+    memcpy(out, e->last_chain[k], bytes);
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_debug_recon(hl_amd_encoder_t* e, int32_t k, uint8_t* y, uint8_t* u, uint8_t* v)
+{
+    if (!e || !y || !u || !v || k < 0) return HL_AMD_ERROR_INVALID_PARAMETER;
+    if (k >= (int)e->last_pic.size()) return HL_AMD_ERROR_INVALID_STATE;
+    const uint8_t* p = e->last_pic[k];
+    if (!p) {
+        if (k != (int)e->last_pic.size() - 1) return HL_AMD_ERROR_INVALID_STATE;
+        return hl_amd_get_recon(e, y, u, v);
+    }
+    const size_t ny = (size_t)e->W * e->H, nc = (size_t)e->Wc * e->Hc;
+    HL_HIP_CHECK(hipMemcpyAsync(y, p, ny, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(u, p + ny, nc, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(v, p + ny + nc, nc, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipStreamSynchronize(e->stream));
+    return HL_AMD_SUCCESS;
+}
 
 extern "C" const char* hl_amd_version(void) { return "hartallo_amd 0.1 (gfx950)"; }

@@ -78,6 +78,7 @@ constexpr int kNA = -1;   // not-available sample marker
 struct FrameArgs {
     int32_t W, H, Wc, Hc, mbw, mbh;
     int32_t qp, qpc, is_intra, me_range;
+    int32_t early_term;     // hl_codec_t.me_early_term_flag (rdo.c:888-931)
     double lambda;
     const uint8_t* src[3];
     uint8_t* cur[3];
@@ -140,12 +141,19 @@ struct Shared {
     CandSlot wc[kMaxWaves][9];  // candidates of the step, one copy per wave (each wave writes its own)
     int32_t be_nz[9][16], be_tc[9][16], be_t1[9][16], be_sctr[9][16], be_bits[9][16], be_dist[9][16];
     int32_t be_w0[9][16], be_w1[9][16], be_w2[9][16];    // packed block statistics (device path)
-    alignas(16) uint8_t be_tcb[16][16];                  // TotalCoeff [block][candidate]
+    // Per-step results are double-buffered by step parity (Ctx::par): after a
+    // step's last barrier, waves still read its results (the candidate scan,
+    // the live TotalCoeffs update, the Single_ctr chain) while faster waves
+    // already write the next step's -- a step only reuses the buffer of the
+    // step before the previous one, whose readers all passed a barrier since.
+    alignas(16) uint8_t be_tcb[2][16][16];               // TotalCoeff [parity][block][candidate]
     alignas(16) int32_t lvs[kMaxWaves * 4][16];          // per-row level scratch of coop_cavlc
     CoopTables ct;
     uint32_t qtab[16];                                   // packed quarter-pel phase table
-    double cd_cost[9];
-    int32_t cd_bits[9], cd_dist[9], cd_single[9], cd_cbp[9], cd_last[9];
+    struct CandRes {
+        double cost[9];
+        int32_t bits[9], dist[9], single[9], cbp[9], last[9];
+    } cd[2];  // per candidate of a step [parity]
     // --- per (sub)partition search results
     double bcost[4][4];
     int32_t bdist[4][4], bsingle[4][4], bcbp[4][4];
@@ -168,6 +176,7 @@ struct Shared {
     int16_t i16_dcl[16];         // I16x16: DC levels of the current mode (scan order)
     int32_t dcrow[4];            // I16x16: DC block rate, TotalCoeff, single counter
     int32_t chain_x;             // resolve_chain result
+    int32_t homo[4];             // early termination: homogeneity of the four 8x8 source quadrants
     int32_t predc[2][64];
     int32_t cres_dc[2][4], cres_cac[2][4], cres_cdc[2][4], cres_tc[2][4], cres_sctr[2][4];
     int32_t cdc_level[2][4];
@@ -188,6 +197,7 @@ struct Ctx {
     LaneK K;                // per-lane constants of the 16-lane block pipeline (device)
     int gx, gy;             // reference planes known complete for MBs (X <= gx, Y <= gy) (pipelined runs)
     int spec = 0;           // 1 = chain is still a row-start speculation (uniform)
+    int par = 0;            // buffer parity of the last candidate step (Shared::cd, be_tcb)
 #if defined(HL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
     unsigned long long pacc[kProfSlots] = {};
     unsigned pcnt[kProfSlots] = {};
@@ -703,6 +713,9 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
 #endif
     const FrameArgs& F = c.F;
     Shared& S = c.S;
+    c.par ^= 1;
+    Shared::CandRes& R = S.cd[c.par];
+    uint8_t(&tcb)[16][16] = S.be_tcb[c.par];
     HL_PROF_T(tp0);
 #if defined(__HIP_DEVICE_COMPILE__)
     // phase 1: one 16-lane row per (candidate, 4x4 block); every row of the
@@ -780,19 +793,19 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                     S.be_w0[ci][k] = st.tc | (st.t1 << 5) | ((st.sctr + 1) << 8);
                     S.be_w1[ci][k] = st.rest | (dist << 16);
                     S.be_w2[ci][k] = tok;
-                    S.be_tcb[k][ci] = (uint8_t)st.tc;
+                    tcb[k][ci] = (uint8_t)st.tc;
                     if (g.nblk == 1) {
                         // a single-block partition: both nC neighbours lie outside it, so the
                         // nC (and the candidate's cost) needs no other row (phase 2 skipped)
                         int bits = 0;
                         if (st.tc) bits = st.rest + ((tok >> (5 * (nc1 < 2 ? 0 : (nc1 < 4 ? 1 : (nc1 < 8 ? 2 : 3))))) & 31);
                         const CandSlot cs = S.wc[wave][ci];
-                        S.cd_cost[ci] = mv_cost(F, dist, bits, cs.mvx, cs.mvy, pmv);
-                        S.cd_bits[ci] = bits;
-                        S.cd_dist[ci] = dist;
-                        S.cd_single[ci] = st.tc ? st.sctr : 0;
-                        S.cd_cbp[ci] = st.tc ? 1 << blk_idx(g.px, g.py) : 0;
-                        S.cd_last[ci] = st.tc ? st.sctr : -1;
+                        R.cost[ci] = mv_cost(F, dist, bits, cs.mvx, cs.mvy, pmv);
+                        R.bits[ci] = bits;
+                        R.dist[ci] = dist;
+                        R.single[ci] = st.tc ? st.sctr : 0;
+                        R.cbp[ci] = st.tc ? 1 << blk_idx(g.px, g.py) : 0;
+                        R.last[ci] = st.tc ? st.sctr : -1;
                     }
                 }
             }
@@ -817,7 +830,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         const int kkA = inA ? ((hy << g.lbw) + hx - 1) : 0, kkB = inB ? (((hy - 1) << g.lbw) + hx) : 0;
         const int w0 = S.be_w0[ci][k], w1 = S.be_w1[ci][k], w2 = S.be_w2[ci][k];
         const int eA = S.extA[bi], eB = S.extB[bi], cbp = S.cbp_l, tA = S.tc[niA], tB = S.tc[niB];
-        const uint4 rA = *reinterpret_cast<const uint4*>(S.be_tcb[kkA]), rB = *reinterpret_cast<const uint4*>(S.be_tcb[kkB]);
+        const uint4 rA = *reinterpret_cast<const uint4*>(tcb[kkA]), rB = *reinterpret_cast<const uint4*>(tcb[kkB]);
         const CandSlot cs = S.wc[wave][ci];
         int bits = 0, dist = 0, cs_sum = 0, last = 0;
         const int tc = w0 & 31;
@@ -856,12 +869,12 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         cs_sum = row_sum(cs_sum);
         last = row_max(last);
         if (k0 == 0) {
-            S.cd_cost[ci] = mv_cost(F, dist, bits, cs.mvx, cs.mvy, pmv);
-            S.cd_bits[ci] = bits;
-            S.cd_dist[ci] = dist;
-            S.cd_single[ci] = cs_sum >> 16;
-            S.cd_cbp[ci] = cs_sum & 0xFFFF;
-            S.cd_last[ci] = last ? (last & 15) : -1;
+            R.cost[ci] = mv_cost(F, dist, bits, cs.mvx, cs.mvy, pmv);
+            R.bits[ci] = bits;
+            R.dist[ci] = dist;
+            R.single[ci] = cs_sum >> 16;
+            R.cbp[ci] = cs_sum & 0xFFFF;
+            R.last[ci] = last ? (last & 15) : -1;
         }
     }
     if (g.nblk > 1) HL_SYNC();
@@ -870,7 +883,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
     // live TotalCoeffsLuma = last writer; the next reader is behind a barrier
     if (c.tid < g.nblk) {
         const int k = c.tid;
-        const int v = tcb_last(*reinterpret_cast<const uint4*>(S.be_tcb[k]), (1u << ncand) - 1u);
+        const int v = tcb_last(*reinterpret_cast<const uint4*>(tcb[k]), (1u << ncand) - 1u);
         if (v >= 0) S.tc[blk_idx(g.px + ((k & (g.nbw - 1)) << 2), g.py + ((k >> g.lbw) << 2))] = (int8_t)v;
     }
 #else
@@ -951,12 +964,12 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                 last = S.be_sctr[t][k];
             }
         }
-        S.cd_cost[t] = mv_cost(F, dist, bits, S.wc[0][t].mvx, S.wc[0][t].mvy, pmv);
-        S.cd_bits[t] = bits;
-        S.cd_dist[t] = dist;
-        S.cd_single[t] = single;
-        S.cd_cbp[t] = cbp;
-        S.cd_last[t] = last;
+        R.cost[t] = mv_cost(F, dist, bits, S.wc[0][t].mvx, S.wc[0][t].mvy, pmv);
+        R.bits[t] = bits;
+        R.dist[t] = dist;
+        R.single[t] = single;
+        R.cbp[t] = cbp;
+        R.last[t] = last;
     }
     for (int k = 0; k < g.nblk; ++k) {
         const int hx = k % g.nbw, hy = k / g.nbw;
@@ -972,14 +985,14 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
 #if defined(__HIP_DEVICE_COMPILE__)
     {  // last candidate that wrote the counter (vectorised over the step)
         const int l = c.tid & 15;
-        const int v = l < ncand ? S.cd_last[l] : -1;
+        const int v = l < ncand ? R.last[l] : -1;
         const unsigned long long bal = __ballot(v >= 0) & 0xFFFFull;
         if (bal) chain_write(c, __builtin_amdgcn_readlane(v, 63 - __clzll((long long)bal)));
     }
 #else
     for (int ci = ncand - 1; ci >= 0; --ci)
-        if (S.cd_last[ci] >= 0) {
-            chain_write(c, S.cd_last[ci]);
+        if (R.last[ci] >= 0) {
+            chain_write(c, R.last[ci]);
             break;
         }
 #endif
@@ -992,17 +1005,17 @@ HD int pick_first_min(const Ctx& c, int ncand, double& m)
     const Shared& S = c.S;
 #if defined(__HIP_DEVICE_COMPILE__)
     const int l = c.tid & 15;
-    const double v = l < ncand ? S.cd_cost[l] : 1.7976931348623157e308;
+    const double v = l < ncand ? S.cd[c.par].cost[l] : 1.7976931348623157e308;
     const double mn = row_min_f64(v);
     const unsigned long long bal = __ballot(l < ncand && v == mn) & 0xFFFFull;
     m = uni(mn);
     return uni(__ffsll((long long)bal) - 1);
 #else
     int bi = 0;
-    m = S.cd_cost[0];
+    m = S.cd[c.par].cost[0];
     for (int ci = 1; ci < ncand; ++ci)
-        if (S.cd_cost[ci] < m) {
-            m = S.cd_cost[ci];
+        if (S.cd[c.par].cost[ci] < m) {
+            m = S.cd[c.par].cost[ci];
             bi = ci;
         }
     return bi;
@@ -1115,12 +1128,12 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         if (pmv[0] == smv[0] && pmv[1] == smv[1]) {
             put_cand(c, g.px, g.py, 0, pmv[0], pmv[1], 0, (c.tid & 63) == 0);
             eval_candidates(c, g, 1, pmv);
-            if (uni(S.cd_bits[0]) == 0 || uni(S.cd_single[0]) < 6) {
+            if (uni(S.cd[c.par].bits[0]) == 0 || uni(S.cd[c.par].single[0]) < 6) {
                 probably = true;
                 b.cost = 0.0;
-                b.single = uni(S.cd_single[0]);
-                b.dist = uni(S.cd_dist[0]);
-                b.cbp = uni(S.cd_cbp[0]);
+                b.single = uni(S.cd[c.par].single[0]);
+                b.dist = uni(S.cd[c.par].dist[0]);
+                b.cbp = uni(S.cd[c.par].cbp[0]);
                 b.mv[0] = pmv[0];
                 b.mv[1] = pmv[1];
             }
@@ -1136,9 +1149,9 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         const int bi = pick_first_min(c, nc0, m);
         if (m < b.cost) {
             b.cost = m;
-            b.single = uni(S.cd_single[bi]);
-            b.dist = uni(S.cd_dist[bi]);
-            b.cbp = uni(S.cd_cbp[bi]);
+            b.single = uni(S.cd[c.par].single[bi]);
+            b.dist = uni(S.cd[c.par].dist[bi]);
+            b.cbp = uni(S.cd[c.par].cbp[bi]);
             b.mv[0] = bi ? 0 : pmv[0];
             b.mv[1] = bi ? 0 : pmv[1];
         }
@@ -1217,9 +1230,9 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
             if (m < b.cost) {
                 best = uni(S.wc[c.tid >> 6][bi].pad);
                 b.cost = m;
-                b.single = uni(S.cd_single[bi]);
-                b.dist = uni(S.cd_dist[bi]);
-                b.cbp = uni(S.cd_cbp[bi]);
+                b.single = uni(S.cd[c.par].single[bi]);
+                b.dist = uni(S.cd[c.par].dist[bi]);
+                b.cbp = uni(S.cd[c.par].cbp[bi]);
                 b.mv[0] = uni((int)S.wc[c.tid >> 6][bi].mvx);
                 b.mv[1] = uni((int)S.wc[c.tid >> 6][bi].mvy);
             }
@@ -2338,6 +2351,54 @@ HD void reconstruct_inter_luma(Ctx& c, int single_luma)
 }
 
 // --------------------------------------------------------------------------
+// Early termination (me_early_term_flag), rdo.c:888-931 (JVT-O079
+// 2.1.3.4.3.1): after the 16x16 search only the partition modes the source
+// MB's homogeneity allows are searched.  Homogeneity of an 8x8 quadrant is
+// the Sobel-like edge energy of hl_math_homogeneousity8x8_u8_cpp
+// (hl_math.c:470-486); the quadrants of border MBs are shifted one sample
+// inwards (rdo.c:895-896).  Returns the mode mask, bit j + 1 = kParts[j].
+// One wave per quadrant, one lane per sample.
+// --------------------------------------------------------------------------
+constexpr int kHomoTh16x16 = 20000, kHomoTh8x8 = 5000, kHomoTh8x4 = 7500;  // hl_codec_264_defs.h:61-63
+
+HD int homo_sample(const FrameArgs& F, int x, int y)  // |dx| + |dy| at source sample (x, y), eq. 2-35
+{
+    const uint8_t* u = F.src[0] + y * F.W + x;
+    const uint8_t *um = u - F.W, *up = u + F.W;
+    const int dx = up[-1] + (up[0] << 1) + up[1] - um[-1] - (um[0] << 1) - um[1];
+    const int dy = um[1] + (u[1] << 1) + up[1] - um[-1] - (u[-1] << 1) - up[-1];
+    return iabs(dx) + iabs(dy);
+}
+
+HD int early_term_modes(Ctx& c)
+{
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    const int xs = c.xL == 0 ? 1 : (c.xL == F.W - 16 ? F.W - 17 : c.xL);
+    const int ys = c.yL == 0 ? 1 : (c.yL == F.H - 16 ? F.H - 17 : c.yL);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int q = c.tid >> 6, i = c.tid & 63;
+    if (q < 4) {
+        int v = homo_sample(F, xs + (q & 1) * 8 + (i & 7), ys + (q >> 1) * 8 + (i >> 3));
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (i == 0) S.homo[q] = v;
+    }
+#else
+    for (int q = 0; q < 4; ++q) {
+        int v = 0;
+        for (int i = 0; i < 64; ++i) v += homo_sample(F, xs + (q & 1) * 8 + (i & 7), ys + (q >> 1) * 8 + (i >> 3));
+        S.homo[q] = v;
+    }
+#endif
+    HL_SYNC();
+    const int h0 = uni(S.homo[0]), h1 = uni(S.homo[1]), h2 = uni(S.homo[2]), h3 = uni(S.homo[3]);
+    if (h0 < kHomoTh8x8 && h1 < kHomoTh8x8 && h2 < kHomoTh8x8 && h3 < kHomoTh8x8) return 1 << 1;
+    if (h0 + h1 + h2 + h3 < kHomoTh16x16) return (h0 < kHomoTh8x8 && h1 < kHomoTh8x8) ? (1 << 1) | (1 << 2) : (1 << 1) | (1 << 3);
+    if (h0 < kHomoTh8x4 && h1 < kHomoTh8x4 && h2 < kHomoTh8x4 && h3 < kHomoTh8x4) return 0x7E;  // all but the 4x4 sub-partitions
+    return 0xFFFF;
+}
+
+// --------------------------------------------------------------------------
 // P macroblock decision, rdo.c:678-1271
 // --------------------------------------------------------------------------
 HD void guess_inter(Ctx& c)
@@ -2349,11 +2410,16 @@ HD void guess_inter(Ctx& c)
     double best_cost = 1.7976931348623157e308;
     int best_single = 9, best_part = -1, best_fam = -1;
     bool best_found = false, pskip = false;
+    // b_probably_pskip is function-scoped in the reference (rdo.c:691): a mode
+    // skipped by early termination leaves the last searched mode's value
+    bool probably = false;
+    int mode_flags = 0xFFFF;  // rdo.c:874
     if (c.tid == 0) S.flags = FL_INTER;
     for (int fam = 0; fam < 4 && !best_found; ++fam) {
-        bool probably = false;
         for (int j = fam_first(fam); j < fam_first(fam + 1); ++j) {
             const PartDef& pd = kParts[j];
+            if (!((1 << (j + 1)) & mode_flags)) continue;
+            if (F.early_term && j == 0) mode_flags = early_term_modes(c);
             HL_SYNC();
             if (c.tid == 0) {
                 S.e_type = fam_type(fam);

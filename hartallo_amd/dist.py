@@ -39,6 +39,17 @@ def max_over_ranks(value: float) -> float:
     return float(t.item())
 
 
+def min_over_ranks(value: float) -> float:
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        return value
+    t = torch.tensor([value], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return float(t.item())
+
+
 def stream_seed(rank: int, base: int = 11) -> int:
     """Each rank encodes its own synthetic stream (weak scaling)."""
     return base + rank

@@ -143,6 +143,12 @@ int32_t hl_amd_profile_counters(hl_amd_encoder_t* encoder, unsigned long long* o
 int32_t hl_amd_debug_records(hl_amd_encoder_t* encoder, int32_t k, void* out, size_t bytes);
 int32_t hl_amd_record_size(void);
 
+/* diagnostics: the rdo.Single_ctr chain records (hl_types.h MbChain, 20 bytes
+ * per macroblock) and the reconstructed (deblocked) planes of picture k of
+ * the last encode call */
+int32_t hl_amd_debug_chain(hl_amd_encoder_t* encoder, int32_t k, void* out, size_t bytes);
+int32_t hl_amd_debug_recon(hl_amd_encoder_t* encoder, int32_t k, uint8_t* y, uint8_t* u, uint8_t* v);
+
 const char* hl_amd_version(void);
 
 #ifdef __cplusplus

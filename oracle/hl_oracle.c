@@ -1834,6 +1834,49 @@ static void reconstruct_inter(hlo_enc_t* e, mb_t* m, int32_t single_luma) /* rdo
     reconstruct_chroma(e, m, predCb, predCr);
 }
 
+/* hl_math_homogeneousity8x8_u8_cpp, hl_math.c:470-486 (JVT-O079 eq. 2-35):
+ * Sobel-like edge energy of the 8x8 block at p (p must not lie on the picture
+ * border: the taps reach one sample beyond the block on every side). */
+static int32_t homogeneity8x8(const uint8_t* p, int stride)
+{
+    int32_t i, j, ret = 0;
+    for (j = 0; j < 8; ++j) {
+        const uint8_t* u = p + stride * j;
+        const uint8_t* um = u - stride;
+        const uint8_t* up = u + stride;
+        for (i = 0; i < 8; ++i) {
+            const int32_t dx = up[i - 1] + (up[i] << 1) + up[i + 1] - um[i - 1] - (um[i] << 1) - um[i + 1];
+            const int32_t dy = um[i + 1] + (u[i + 1] << 1) + up[i + 1] - um[i - 1] - (u[i - 1] << 1) - up[i - 1];
+            ret += (dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy);
+        }
+    }
+    return ret;
+}
+
+/* Early termination (me_early_term_flag), rdo.c:888-931: the partition
+ * modes left enabled after the 16x16 search, from the homogeneity of the
+ * four 8x8 quadrants of the source MB (JVT-O079 2.1.3.4.3.1).  Bit k+1 =
+ * MODE_ k (reference numbering HL_CODEC_264_MODE_16X16 = 1 ...). */
+#define HOMO_TH16X16 20000 /* HL_CODEC_264_RDO_HOMOGENEOUSITY_TH16X16, defs.h:61 */
+#define HOMO_TH8X8 5000    /* defs.h:62 */
+#define HOMO_TH8X4 7500    /* defs.h:63 */
+static int early_term_modes(const hlo_enc_t* e, const mb_t* m)
+{
+    const int W = e->W, H = e->H;
+    const int xs = m->xL == 0 ? 1 : (m->xL == W - 16 ? W - 17 : m->xL);
+    const int ys = m->yL == 0 ? 1 : (m->yL == H - 16 ? H - 17 : m->yL);
+    int32_t h[4];
+    int k;
+    for (k = 0; k < 4; ++k) h[k] = homogeneity8x8(e->src[0] + (xs + (k & 1) * 8) + (ys + (k >> 1) * 8) * W, W);
+    if (h[0] < HOMO_TH8X8 && h[1] < HOMO_TH8X8 && h[2] < HOMO_TH8X8 && h[3] < HOMO_TH8X8) return 1 << 1;
+    if (h[0] + h[1] + h[2] + h[3] < HOMO_TH16X16) {
+        if (h[0] < HOMO_TH8X8 && h[1] < HOMO_TH8X8) return (1 << 1) | (1 << 2);
+        return (1 << 1) | (1 << 3);
+    }
+    if (h[0] < HOMO_TH8X4 && h[1] < HOMO_TH8X4 && h[2] < HOMO_TH8X4 && h[3] < HOMO_TH8X4) return 0x7E; /* every mode but the 4x4 sub-partitions */
+    return 0xFFFF;
+}
+
 /* hl_codec_264_rdo_mb_guess_best_inter_pred_avc, rdo.c:678-1271 */
 static void guess_inter(hlo_enc_t* e, mb_t* m)
 {
@@ -1846,6 +1889,7 @@ static void guess_inter(hlo_enc_t* e, mb_t* m)
     const part_t* bestPart = NULL;
     const pdef_t* bestDef = NULL;
     int best_found = 0, pskip = 0, probably = 0, i, j, pi, spi;
+    int mode_flags = 0xFFFF; /* rdo.c:874 (one reference picture) */
 
     me->me_range = CLIP3(1, 64, e->p.me_range);
     m->flags = FL_INTER_P;
@@ -1856,6 +1900,10 @@ static void guess_inter(hlo_enc_t* e, mb_t* m)
             const part_t* part = &def->parts[j];
             double cost_sum = 0;
             int32_t dist_sum = 0, single_sum = 0;
+            /* modes disabled by early termination are skipped; `probably`
+             * then keeps the value of the last mode searched (rdo.c:883-885) */
+            if (!((1 << (part->Mode + 1)) & mode_flags)) continue;
+            if (e->p.early_term && part->Mode == MODE_16x16) mode_flags = early_term_modes(e, m);
             find_best_cost(e, m, part);
             probably = me->probably_pskip;
             for (pi = 0; pi < m->NumMbPart; ++pi)
@@ -2287,7 +2335,7 @@ hlo_enc_t* hlo_create(const hlo_params_t* p)
 {
     hlo_enc_t* e;
     int c, m, i, j;
-    if (!p || p->width <= 0 || p->height <= 0 || (p->width & 15) || (p->height & 15) || p->early_term) return NULL;
+    if (!p || p->width <= 0 || p->height <= 0 || (p->width & 15) || (p->height & 15)) return NULL;
     init_level_table();
     e = (hlo_enc_t*)calloc(1, sizeof(*e));
     e->p = *p;

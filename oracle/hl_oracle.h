@@ -29,7 +29,7 @@ typedef struct hlo_params_s {
     int32_t me_range;     /* hl_codec_t.me_range (clipped to [1,64])         */
     int32_t deblock;      /* hl_codec_t.deblock_flag                         */
     int32_t gop_size;     /* hl_codec_t.gop_size                             */
-    int32_t early_term;   /* hl_codec_t.me_early_term_flag (must be 0)       */
+    int32_t early_term;   /* hl_codec_t.me_early_term_flag (rdo.c:888-931)   */
 } hlo_params_t;
 
 typedef struct hlo_enc_s hlo_enc_t;

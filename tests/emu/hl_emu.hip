@@ -16,7 +16,7 @@
 using namespace hl;
 
 struct EmuEnc {
-    int W, H, Wc, Hc, mbw, mbh, nmb, qp, qpc, me_range, deblock, gop;
+    int W, H, Wc, Hc, mbw, mbh, nmb, qp, qpc, me_range, deblock, gop, early_term;
     int pstride;
     std::vector<uint8_t> pic[2][3];
     std::vector<uint8_t> pl[4];
@@ -29,7 +29,7 @@ struct EmuEnc {
     Shared* S;
 };
 
-extern "C" void* emu_create(int W, int H, int qp, int me_range, int deblock, int gop)
+extern "C" void* emu_create(int W, int H, int qp, int me_range, int deblock, int gop, int early_term)
 {
     if (W <= 0 || H <= 0 || (W & 15) || (H & 15)) return nullptr;
     EmuEnc* e = new EmuEnc();
@@ -45,6 +45,7 @@ extern "C" void* emu_create(int W, int H, int qp, int me_range, int deblock, int
     e->me_range = me_range < 1 ? 1 : (me_range > 64 ? 64 : me_range);
     e->deblock = deblock;
     e->gop = gop;
+    e->early_term = early_term;
     e->pstride = W + 2 * kPad;
     for (int k = 0; k < 2; ++k)
         for (int c = 0; c < 3; ++c) e->pic[k][c].assign(c ? (size_t)e->Wc * e->Hc : (size_t)W * H, 0);
@@ -95,6 +96,7 @@ extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, co
     F.qpc = e->qpc;
     F.is_intra = intra;
     F.me_range = e->me_range;
+    F.early_term = e->early_term;
     F.lambda = 0.852 * (double)(1 << ((e->qp - 12) / 3));
     F.src[0] = y;
     F.src[1] = u;

@@ -1,6 +1,7 @@
 """Regenerates tests/golden/ from the reference encoder itself.
 
-Each configuration in tests/hl_testlib.GOLDEN_CONFIGS is synthesised with
+Each configuration in tests/hl_testlib.GOLDEN_CONFIGS (and GOLDEN_ET_CONFIGS,
+encoded with me_early_term_flag = 1) is synthesised with
 hartallo_amd.synth (seeded), encoded by oracle/_ref/ref_enc (the reference's
 own C sources compiled by oracle/Makefile, driven through hl_codec_encode as
 source/test_encoder.c does), and stored as:
@@ -21,7 +22,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 
 import numpy as np  # noqa: E402
 
-from hl_testlib import GOLDEN_CONFIGS, REF_ENC, golden_input, md5  # noqa: E402
+from hl_testlib import GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, REF_ENC, golden_input, md5  # noqa: E402
 
 
 def main():
@@ -29,20 +30,22 @@ def main():
         sys.exit(f"{REF_ENC} missing: run `make -C oracle ref` where /root/reference exists")
     table = {}
     with tempfile.TemporaryDirectory() as td:
-        for cfg in GOLDEN_CONFIGS:
+        for cfg in GOLDEN_CONFIGS + GOLDEN_ET_CONFIGS:
             name, w, h, n, qp, mer, db, gop, seed = cfg
+            et = 1 if cfg in GOLDEN_ET_CONFIGS else 0
             clip = golden_input(cfg)
             inp = os.path.join(td, name + ".yuv")
             clip.tofile(inp)
             pre = os.path.join(td, name)
-            subprocess.run([REF_ENC, str(w), str(h), str(n), str(qp), str(mer), str(db), str(gop), "0", inp, pre], check=True,
-                           stdout=subprocess.DEVNULL)
+            subprocess.run([REF_ENC, str(w), str(h), str(n), str(qp), str(mer), str(db), str(gop), str(et), inp, pre, "rec"],
+                           check=True, stdout=subprocess.DEVNULL)
             stream = open(pre + ".264", "rb").read()
             rec = np.fromfile(pre + ".rec.yuv", dtype=np.uint8).reshape(n, -1)
             with open(os.path.join(HERE, name + ".264"), "wb") as f:
                 f.write(stream)
             table[name] = {
                 "width": w, "height": h, "frames": n, "qp": qp, "me_range": mer, "deblock": db, "gop": gop, "seed": seed,
+                "early_term": et,
                 "stream_md5": md5(stream), "stream_bytes": len(stream),
                 "recon_md5": [md5(r) for r in rec],
             }

@@ -54,7 +54,7 @@ def emu_lib():
     if _emu is None:
         lib = ctypes.CDLL(EMU_LIB)
         lib.emu_create.restype = ctypes.c_void_p
-        lib.emu_create.argtypes = [ctypes.c_int] * 6
+        lib.emu_create.argtypes = [ctypes.c_int] * 7
         lib.emu_destroy.argtypes = [ctypes.c_void_p]
         lib.emu_encode_frame.restype = ctypes.c_long
         lib.emu_encode_frame.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_long]
@@ -80,10 +80,10 @@ def _recon(ptr_fn, w: int, h: int) -> np.ndarray:
 class OracleEncoder:
     """CPU restatement of the reference encoder (oracle/hl_oracle.c)."""
 
-    def __init__(self, w, h, qp=28, me_range=16, deblock=1, gop=30):
+    def __init__(self, w, h, qp=28, me_range=16, deblock=1, gop=30, early_term=0):
         self.lib = oracle_lib()
         self.w, self.h = w, h
-        p = _OParams(w, h, qp, me_range, deblock, gop, 0)
+        p = _OParams(w, h, qp, me_range, deblock, gop, early_term)
         self.h_ = self.lib.hlo_create(ctypes.byref(p))
         if not self.h_:
             raise ValueError("oracle rejected parameters")
@@ -111,10 +111,10 @@ class OracleEncoder:
 class EmuEncoder:
     """Host build of the gfx950 kernel logic (tests/emu/hl_emu.hip)."""
 
-    def __init__(self, w, h, qp=28, me_range=16, deblock=1, gop=30):
+    def __init__(self, w, h, qp=28, me_range=16, deblock=1, gop=30, early_term=0):
         self.lib = emu_lib()
         self.w, self.h = w, h
-        self.h_ = self.lib.emu_create(w, h, qp, me_range, deblock, gop)
+        self.h_ = self.lib.emu_create(w, h, qp, me_range, deblock, gop, early_term)
         self.out = np.zeros(w * h * 4 + (1 << 20), np.uint8)
 
     def encode(self, frame: np.ndarray) -> bytes:
@@ -135,10 +135,10 @@ class EmuEncoder:
 class GpuEncoder:
     """The product (libhartallo_amd.so) with the same encode() shape."""
 
-    def __init__(self, w, h, qp=28, me_range=16, deblock=1, gop=30):
+    def __init__(self, w, h, qp=28, me_range=16, deblock=1, gop=30, early_term=0):
         from hartallo_amd import Encoder
 
-        self.enc = Encoder(w, h, qp, me_range, deblock, gop)
+        self.enc = Encoder(w, h, qp, me_range, deblock, gop, early_term)
         self.w, self.h = w, h
 
     def encode(self, frame: np.ndarray) -> bytes:
@@ -160,7 +160,13 @@ def significant_records(r: np.ndarray) -> np.ndarray:
     intra = (r["flags"] & 1) != 0
     skip = (r["flags"] & 4) != 0
     r["pad0"] = 0
-    r["mv"][intra] = 0
+    # motion of the partitions the MB has (P_Skip: [0][0]); none for intra
+    pi = np.arange(4)[None, :, None]
+    spi = np.arange(4)[None, None, :]
+    num_part = np.where(intra, 0, np.maximum(r["num_part"], 1))[:, None, None]
+    num_sub = np.where(r["flags"][:, None] & 4, 1, np.maximum(r["num_sub"], 1))[:, :, None]
+    keep = (pi < num_part) & (spi < num_sub)
+    r["mv"][~keep] = 0
     for f in ("num_sub", "sub_mb_type", "mvd"):
         r[f][intra | skip] = 0
     r["i16dc"][r["pm0"] != 3] = 0
@@ -232,6 +238,19 @@ GOLDEN_CONFIGS = [
     ("tiny_32x16_qp26", 32, 16, 6, 26, 8, 1, 2, 8),
     ("qcif_qp0_me1", 176, 144, 3, 0, 1, 1, 400, 9),
     ("w480_h272_qp28_me16", 480, 272, 4, 28, 16, 1, 30, 10),
+]
+
+
+# Early-termination goldens (me_early_term_flag = 1, the hl_codec_create
+# default, hl_types.h:67): same layout, encoded by make_golden.py with
+# early_term 1.  Early termination needs W, H >= 32 (rdo.c:895-896 read one
+# sample around the MB quadrants).
+GOLDEN_ET_CONFIGS = [
+    ("et_qcif_ippp_qp28", 176, 144, 6, 28, 16, 1, 30, 41),
+    ("et_cif_qp31_me8", 352, 288, 5, 31, 8, 0, 400, 42),
+    ("et_w480_qp20_gop3", 480, 272, 5, 20, 16, 1, 3, 43),
+    ("et_w64_h32_qp36", 64, 32, 6, 36, 4, 1, 4, 44),
+    ("et_qcif_qp12_me2", 176, 144, 4, 12, 2, 1, 400, 45),
 ]
 
 

@@ -62,5 +62,5 @@ def test_parameter_validation_before_device():
         p = _Params(bad[0], bad[1], bad[2], 16, 1, 30, 0, 0)
         rc = lib.hl_amd_encoder_create(ctypes.byref(p), ctypes.byref(h))
         assert rc in (1, 4), bad
-    p = _Params(352, 288, 28, 16, 1, 30, 1, 0)  # early termination is not part of the path
-    assert lib.hl_amd_encoder_create(ctypes.byref(p), ctypes.byref(h)) == 7
+    p = _Params(32, 16, 28, 16, 1, 30, 1, 0)  # early termination needs W, H >= 32 (rdo.c:895-896)
+    assert lib.hl_amd_encoder_create(ctypes.byref(p), ctypes.byref(h)) == 4

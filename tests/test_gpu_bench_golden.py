@@ -1,0 +1,131 @@
+"""Parity at the BASELINE sizes against the reference encoder itself.
+
+tests/golden/bench_golden.json holds, per frame, the MD5 of the reference
+encoder's Annex-B output and of its reconstructed picture for
+  * bench.py's stream (1920x1088, QP28, ME 16, deblocking, GOP 30,
+    synth.clip(1920, 1088, 150, 11)), and
+  * BASELINE config 2 as the reference expresses it (1280x720 IPPP GOP 30,
+    QP28, ME 16, 31 frames across the second IDR),
+produced by oracle/_ref/ref_enc (tests/golden/make_bench_golden.py).  The
+pipelined path (one launch spanning GOPs), the way bench.py and the driver
+call it, and the per-picture path must reproduce them.  Tolerance: none.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from hartallo_amd import Encoder, synth
+from hl_testlib import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+BENCH = json.load(open(os.path.join(GOLDEN, "bench_golden.json")))
+_CLIPS = {}
+
+
+def _clip(name):
+    if name not in _CLIPS:
+        g = BENCH[name]
+        _CLIPS[name] = synth.clip(g["width"], g["height"], g["frames"], g["seed"])
+    return _CLIPS[name]
+
+
+def _ptrs(dev, w, h):
+    n = w * h
+    return [(dev[i].data_ptr(), dev[i].data_ptr() + n, dev[i].data_ptr() + n + n // 4) for i in range(dev.shape[0])]
+
+
+def _md5(b):
+    return hashlib.md5(bytes(b)).hexdigest()
+
+
+def _check(name, first, outs, recons):
+    g = BENCH[name]
+    for i, o in enumerate(outs):
+        f = first + i
+        assert _md5(o) == g["frame_md5"][f], f"{name} frame {f}: output differs from the reference ({len(o)} vs {g['frame_bytes'][f]} bytes)"
+    for i, r in enumerate(recons):
+        if r is not None:
+            assert _md5(r) == g["recon_md5"][first + i], f"{name} frame {first + i}: reconstruction differs from the reference"
+
+
+def _batch(name, calls, geometry=None):
+    """Encodes the stream's first sum(calls) frames with one
+    encode_batch_device call per entry of `calls`."""
+    g = BENCH[name]
+    w, h = g["width"], g["height"]
+    n = sum(calls)
+    dev = torch.from_numpy(np.ascontiguousarray(_clip(name)[:n])).cuda()
+    torch.cuda.synchronize()
+    ptrs = _ptrs(dev, w, h)
+    enc = Encoder(w, h, g["qp"], g["me_range"], g["deblock"], g["gop"])
+    if geometry:
+        enc.set_pipeline(*geometry)
+    outs, recons, i = [], [], 0
+    for m in calls:
+        outs += [r.annexb() for r in enc.encode_batch_device(ptrs[i:i + m])]
+        recons += [enc.debug_recon(k) for k in range(m)]
+        i += m
+    enc.close()
+    return outs, recons
+
+
+def test_bench_stream_driver_calls(gpu):
+    # the driver's `bench.py --steps 20 --warmup 5`: a 5-frame warm-up call, then 20 frames
+    outs, recons = _batch("bench_1088p_s11", [5, 20])
+    _check("bench_1088p_s11", 0, outs, recons)
+
+
+def test_bench_stream_one_launch_across_gops(gpu):
+    # one pipelined launch over 40 pictures: the IDR at frame 30 sits inside the run
+    outs, recons = _batch("bench_1088p_s11", [40])
+    _check("bench_1088p_s11", 0, outs, recons)
+
+
+def test_bench_stream_default_run(gpu):
+    # bench.py's default: warm-up GOP, then four GOPs in one launch (150 frames)
+    outs, recons = _batch("bench_1088p_s11", [30, 120])
+    _check("bench_1088p_s11", 0, outs, recons)
+
+
+def test_bench_stream_other_rank(gpu):
+    # rank 3 of a multi-GPU bench encodes seed 14
+    outs, recons = _batch("bench_1088p_s14", [5, 20])
+    _check("bench_1088p_s14", 0, outs, recons)
+
+
+def test_bench_stream_per_picture(gpu):
+    g = BENCH["bench_1088p_s11"]
+    w, h = g["width"], g["height"]
+    dev = torch.from_numpy(np.ascontiguousarray(_clip("bench_1088p_s11")[:4])).cuda()
+    torch.cuda.synchronize()
+    enc = Encoder(w, h, g["qp"], g["me_range"], g["deblock"], g["gop"])
+    outs, recons = [], []
+    for p in _ptrs(dev, w, h):
+        outs.append(enc.encode_device(*p).annexb())
+        recons.append(np.concatenate(enc.recon()))
+    enc.close()
+    _check("bench_1088p_s11", 0, outs, recons)
+
+
+def test_config2_720p_pipelined(gpu):
+    outs, recons = _batch("c2_720p_s7", [31])
+    _check("c2_720p_s7", 0, outs, recons)
+
+
+def test_config2_720p_per_picture(gpu):
+    g = BENCH["c2_720p_s7"]
+    w, h = g["width"], g["height"]
+    dev = torch.from_numpy(np.ascontiguousarray(_clip("c2_720p_s7"))).cuda()
+    torch.cuda.synchronize()
+    enc = Encoder(w, h, g["qp"], g["me_range"], g["deblock"], g["gop"])
+    outs, recons = [], []
+    for p in _ptrs(dev, w, h):
+        outs.append(enc.encode_device(*p).annexb())
+        recons.append(np.concatenate(enc.recon()))
+    enc.close()
+    _check("c2_720p_s7", 0, outs, recons)

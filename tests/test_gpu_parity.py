@@ -16,19 +16,22 @@ import os
 import numpy as np
 import pytest
 
-from hl_testlib import GOLDEN, GOLDEN_CONFIGS, GpuEncoder, OracleEncoder, first_diff, golden_input, md5
+from hl_testlib import GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, GpuEncoder, OracleEncoder, first_diff, golden_input, md5
 
 pytestmark = pytest.mark.gpu
 
 GOLD = json.load(open(os.path.join(GOLDEN, "golden.json")))
 
 
-@pytest.mark.parametrize("cfg", GOLDEN_CONFIGS, ids=[c[0] for c in GOLDEN_CONFIGS])
+ALL = GOLDEN_CONFIGS + GOLDEN_ET_CONFIGS
+
+
+@pytest.mark.parametrize("cfg", ALL, ids=[c[0] for c in ALL])
 def test_golden_streams(gpu, cfg):
     name, w, h, n, qp, mer, db, gop, seed = cfg
     clip = golden_input(cfg)
     ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()
-    enc = GpuEncoder(w, h, qp, mer, db, gop)
+    enc = GpuEncoder(w, h, qp, mer, db, gop, GOLD[name].get("early_term", 0))
     out = b""
     for f in range(n):
         out += enc.encode(clip[f])
@@ -67,5 +70,17 @@ def test_rejects_bad_format(gpu):
         Encoder(1920, 1080)
     assert e.value.code == 4  # HL_ERROR_INVALID_FORMAT, hl_codec_264.c:437-438
     with pytest.raises(HlAmdError) as e:
-        Encoder(352, 288, me_early_term=1)
-    assert e.value.code == 7
+        Encoder(32, 16, me_early_term=1)  # early termination reads one sample around the MB quadrants
+    assert e.value.code == 4
+
+
+def test_early_term_720p_vs_oracle(gpu):
+    # me_early_term_flag = 1 is the hl_codec_create default (hl_types.h:67)
+    w, h, n = 1280, 720, 3
+    clip = __import__("hartallo_amd.synth", fromlist=["clip"]).clip(w, h, n, 7)
+    g = GpuEncoder(w, h, 28, 16, 1, 30, 1)
+    o = OracleEncoder(w, h, 28, 16, 1, 30, 1)
+    for f in range(n):
+        a, b = g.encode(clip[f]), o.encode(clip[f])
+        assert a == b, f"frame {f}: first differing byte {first_diff(a, b)}"
+        assert np.array_equal(g.recon(), o.recon()), f"frame {f}: recon differs"

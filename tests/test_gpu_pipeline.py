@@ -17,7 +17,7 @@ import pytest
 import torch
 
 from hartallo_amd import Encoder, synth
-from hl_testlib import GOLDEN, GOLDEN_CONFIGS, OracleEncoder, first_diff, first_record_diff, golden_input, md5
+from hl_testlib import GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, OracleEncoder, first_diff, first_record_diff, golden_input, md5
 
 pytestmark = pytest.mark.gpu
 
@@ -31,8 +31,8 @@ def _device_frames(clip, w, h):
     return dev, [(dev[i].data_ptr(), dev[i].data_ptr() + n, dev[i].data_ptr() + n + n // 4) for i in range(len(clip))]
 
 
-def _batch(w, h, qp, mer, db, gop, clip, geometry=None, split=None, records=None):
-    enc = Encoder(w, h, qp, mer, db, gop)
+def _batch(w, h, qp, mer, db, gop, clip, geometry=None, split=None, records=None, et=0):
+    enc = Encoder(w, h, qp, mer, db, gop, et)
     if geometry:
         enc.set_pipeline(*geometry)
     dev, ptrs = _device_frames(clip, w, h)
@@ -48,8 +48,8 @@ def _batch(w, h, qp, mer, db, gop, clip, geometry=None, split=None, records=None
     return [r.annexb() for r in out], rec
 
 
-def _single(w, h, qp, mer, db, gop, clip, records=None):
-    enc = Encoder(w, h, qp, mer, db, gop)
+def _single(w, h, qp, mer, db, gop, clip, records=None, et=0):
+    enc = Encoder(w, h, qp, mer, db, gop, et)
     dev, ptrs = _device_frames(clip, w, h)
     out = []
     for p in ptrs:
@@ -61,24 +61,28 @@ def _single(w, h, qp, mer, db, gop, clip, records=None):
     return out, rec
 
 
-def _diagnose(w, h, qp, mer, db, gop, clip, geometry=None, split=None):
+def _diagnose(w, h, qp, mer, db, gop, clip, geometry=None, split=None, et=0):
     """On a mismatch: the first (picture, MB, field) where the pipelined
     run's decisions differ from one-call-per-picture encoding."""
     ra, rb = [], []
-    _single(w, h, qp, mer, db, gop, clip, ra)
-    _batch(w, h, qp, mer, db, gop, clip, geometry, split, rb)
+    _single(w, h, qp, mer, db, gop, clip, ra, et)
+    _batch(w, h, qp, mer, db, gop, clip, geometry, split, rb, et)
     return first_record_diff(ra, rb, w // 16)
 
 
-@pytest.mark.parametrize("cfg", [c for c in GOLDEN_CONFIGS if c[3] >= 3], ids=[c[0] for c in GOLDEN_CONFIGS if c[3] >= 3])
+BATCH_GOLDEN = [c for c in GOLDEN_CONFIGS + GOLDEN_ET_CONFIGS if c[3] >= 3]
+
+
+@pytest.mark.parametrize("cfg", BATCH_GOLDEN, ids=[c[0] for c in BATCH_GOLDEN])
 def test_batch_golden_streams(gpu, cfg):
     name, w, h, n, qp, mer, db, gop, seed = cfg
+    et = GOLD[name].get("early_term", 0)
     ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()
     clip = golden_input(cfg)
-    out, rec = _batch(w, h, qp, mer, db, gop, clip)
+    out, rec = _batch(w, h, qp, mer, db, gop, clip, et=et)
     got = b"".join(out)
     if got != ref:
-        pytest.fail(f"{name}: first differing byte {first_diff(got, ref)}; {_diagnose(w, h, qp, mer, db, gop, clip)}")
+        pytest.fail(f"{name}: first differing byte {first_diff(got, ref)}; {_diagnose(w, h, qp, mer, db, gop, clip, et=et)}")
     assert md5(rec) == GOLD[name]["recon_md5"][n - 1]
 
 

@@ -1,24 +1,27 @@
 """The CPU oracle (oracle/hl_oracle.c) is pinned to the reference: it must
 reproduce every golden stream (produced by the reference encoder itself,
-tests/golden/make_golden.py) byte for byte, and its reconstructed pictures
+tests/golden/make_golden.py; early termination on for the et_* ones) byte for byte, and its reconstructed pictures
 must match the reference's per-frame MD5s."""
 import json
 import os
 
 import pytest
 
-from hl_testlib import GOLDEN, GOLDEN_CONFIGS, OracleEncoder, first_diff, golden_input, md5
+from hl_testlib import GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, OracleEncoder, first_diff, golden_input, md5
 
 GOLD = json.load(open(os.path.join(GOLDEN, "golden.json")))
 
 
-@pytest.mark.parametrize("cfg", GOLDEN_CONFIGS, ids=[c[0] for c in GOLDEN_CONFIGS])
+ALL = GOLDEN_CONFIGS + GOLDEN_ET_CONFIGS
+
+
+@pytest.mark.parametrize("cfg", ALL, ids=[c[0] for c in ALL])
 def test_oracle_matches_reference(cfg):
     name, w, h, n, qp, mer, db, gop, seed = cfg
     clip = golden_input(cfg)
     ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()
     assert md5(ref) == GOLD[name]["stream_md5"]
-    enc = OracleEncoder(w, h, qp, mer, db, gop)
+    enc = OracleEncoder(w, h, qp, mer, db, gop, GOLD[name].get("early_term", 0))
     out = b""
     for f in range(n):
         out += enc.encode(clip[f])
@@ -30,3 +33,22 @@ def test_oracle_matches_reference(cfg):
 def test_oracle_rejects_unsupported():
     with pytest.raises(ValueError):
         OracleEncoder(1920, 1080)  # height not a multiple of 16 (hl_codec_264.c:437)
+
+
+def test_oracle_matches_bench_goldens():
+    """The reference MD5s of the BASELINE-size workloads
+    (tests/golden/bench_golden.json) agree with the oracle on the first
+    frames (the GPU tests check every frame)."""
+    import hashlib
+
+    from hartallo_amd import synth
+
+    bench = json.load(open(os.path.join(GOLDEN, "bench_golden.json")))
+    for name, n in (("bench_1088p_s11", 2), ("c2_720p_s7", 2)):
+        g = bench[name]
+        clip = synth.clip(g["width"], g["height"], g["frames"], g["seed"])
+        enc = OracleEncoder(g["width"], g["height"], g["qp"], g["me_range"], g["deblock"], g["gop"])
+        for f in range(n):
+            out = enc.encode(clip[f])
+            assert hashlib.md5(out).hexdigest() == g["frame_md5"][f], f"{name} frame {f}"
+            assert md5(enc.recon()) == g["recon_md5"][f], f"{name} recon {f}"

@@ -1,8 +1,7 @@
 #!/bin/bash
-# Diagnosis of the pipelined-run mismatch, run on the GPU box
-# from the repo root: the GOP-spanning stress run on the input-digest build
-# (HL_DIAG_INPUTS: each record carries digests of the MB's inputs, so a
-# mismatch names the first input that differed).
+# Diagnosis of the pipelined-run mismatch on the GPU box: the
+# GOP-spanning stress run on the round-1 build (build/old) and on the same
+# build with the per-step candidate results double-buffered (build/oldC).
 set -o pipefail
 mkdir -p gpurun_out
 run() {  # name, seconds, command...
@@ -16,4 +15,7 @@ run() {  # name, seconds, command...
     return 0
 }
 S="python -u tools/stress_spans_gops.py"
-HL_LIB=build/dinp/libhartallo_amd.so run stress_dinp 300 $S 10
+for v in old oldC old oldC old oldC; do
+    HL_LIB=build/$v/libhartallo_amd.so run stress_$v 200 $S 8
+done
+run stress_new 200 $S 8

@@ -37,12 +37,30 @@ def main():
     ny = w * h
     ptrs = [(dev[i].data_ptr(), dev[i].data_ptr() + ny, dev[i].data_ptr() + ny + ny // 4) for i in range(n)]
     enc = Encoder(w, h, 28, 16, 1, gop)
-    ref, ref_recs = [], []
+    ref, ref_recs, ref_chain, ref_pics = [], [], [], []
     for p in ptrs:
         ref.append(enc.encode_device(*p).annexb())
         ref_recs.append(enc.debug_records(0))
+        ref_chain.append(enc.debug_chain(0))
+        ref_pics.append(enc.debug_recon(0))
     ref_rec = np.concatenate(enc.recon())
     enc.close()
+    mbw, mbh = w // 16, h // 16
+    wave = sorted(range(mbw * mbh), key=lambda m: ((m % mbw) + 2 * (m // mbw), m // mbw))
+
+    def first_mb(diff_mask):  # first MB in wavefront order with a difference
+        for m in wave:
+            if diff_mask[m]:
+                return f"({m % mbw},{m // mbw})"
+        return None
+
+    def pic_diff(a, b):
+        n = w * h
+        ya, yb = a[:n].reshape(h, w), b[:n].reshape(h, w)
+        mb = (ya != yb).reshape(mbh, 16, mbw, 16).any(axis=(1, 3)).ravel()
+        ca = a[n:].reshape(2, h // 2, w // 2) != b[n:].reshape(2, h // 2, w // 2)
+        mbc = ca.reshape(2, mbh, 8, mbw, 8).any(axis=(0, 2, 4)).ravel()
+        return first_mb(mb), first_mb(mbc)
     geometry = tuple(int(v) for v in os.environ["HL_PIPE"].split(",")) if os.environ.get("HL_PIPE") else None
     bad = 0
     for r in range(reps):
@@ -50,13 +68,17 @@ def main():
         if geometry:
             enc.set_pipeline(*geometry)
         if os.environ.get("HL_STRESS_SINGLE"):  # the per-picture path instead of pipelined runs
-            out, recs = [], []
+            out, recs, chains, pics = [], [], [], []
             for p in ptrs:
                 out.append(enc.encode_device(*p).annexb())
                 recs.append(enc.debug_records(0))
+                chains.append(enc.debug_chain(0))
+                pics.append(enc.debug_recon(0))
         else:
             out = [x.annexb() for x in enc.encode_batch_device(ptrs)]
             recs = [enc.debug_records(k) for k in range(n)]
+        chains = [enc.debug_chain(k) for k in range(n)]
+        pics = [enc.debug_recon(k) for k in range(n)]
         reruns = enc.last_reruns()
         recon_ok = np.array_equal(np.concatenate(enc.recon()), ref_rec)
         enc.close()
@@ -64,6 +86,12 @@ def main():
         bad += bool(diffs) or not recon_ok
         msg = "ok" if not diffs else f"MISMATCH {diffs}; {first_record_diff(ref_recs, recs, w // 16)}"
         print(f"run {r}: {msg} (recon {'equal' if recon_ok else 'DIFFERS'}, reruns {reruns})", flush=True)
+        for f in range(n) if (diffs or not recon_ok) and chains[0] is not None else []:
+            ch = first_mb((chains[f] != ref_chain[f]).any(axis=1))
+            ly, lc = pic_diff(ref_pics[f], pics[f])
+            if ch or ly or lc:
+                print(f"   picture {f}: first MB (wavefront order) with a different chain record {ch}, luma recon {ly}, chroma recon {lc}",
+                      flush=True)
     print(f"{bad} of {reps} runs differ", flush=True)
     sys.exit(1 if bad else 0)
 
