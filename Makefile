@@ -48,7 +48,7 @@ build/relacqsys/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp
 	mkdir -p build/relacqsys
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) '-DHL_ACQ_SCOPE=""' '-DHL_REL_SCOPE=""' -shared -o $@ $(CSRC)/hl_encoder.hip $(CSRC)/hl_writer.cpp
 
-oracle:
+oracle: product  # oracle/_ref/drop_in_enc links the product library
 	$(MAKE) -C oracle
 
 clean:

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -875,12 +876,13 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     HL_HIP_CHECK(hipMemcpyAsync(e->h_bchain, e->d_bchain, sizeof(MbChain) * nmb * m, hipMemcpyDeviceToHost, e->stream));
     HL_HIP_CHECK(hipMemcpyAsync(&err, e->d_err, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
     HL_HIP_CHECK(hipMemcpyAsync(e->h_brec, e->d_brec, sizeof(MbRecord) * nmb * m, hipMemcpyDeviceToHost, e->stream));
+    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[2], e->stream));
     HL_HIP_CHECK(hipStreamSynchronize(e->stream));
     if (e->timing) {
         (void)hipEventElapsedTime(&e->ms[0], e->ev[0], e->ev[1]);
         (void)hipEventElapsedTime(&e->ms[1], e->ev[4], e->ev[5]);
-        e->ms[2] = 0.f;
-        (void)hipEventElapsedTime(&e->ms[3], e->ev[0], e->ev[5]);
+        (void)hipEventElapsedTime(&e->ms[2], e->ev[5], e->ev[2]);
+        e->ms[3] = 0.f;
     }
     e->mb_launches = 1;
     e->reruns = 0;
@@ -899,7 +901,9 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         e->reruns = 1;
         return HL_AMD_SUCCESS;
     }
+    const auto tw0 = std::chrono::steady_clock::now();
     const std::vector<size_t> wsize = write_run(e, m, base);
+    if (e->timing) e->ms[3] = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - tw0).count();
     for (int k = 0; k < m; ++k) {
         e->last_recs[base + k] = e->h_brec + nmb * k;
         e->last_chain[base + k] = e->h_bchain + nmb * k;

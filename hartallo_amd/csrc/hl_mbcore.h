@@ -62,7 +62,10 @@ constexpr int kMaxWaves = 8;   // waves of the macroblock workgroup
 // been checked against the reference.  A 256-lane build (two workgroups per
 // CU, 512 macroblocks in flight) measured only +4 % on the pipelined bench and
 // its 720p output differs from the oracle, so it is not pursued.
-constexpr int kMbThreads = 512;
+#ifndef HL_MB_THREADS
+#define HL_MB_THREADS 512
+#endif
+constexpr int kMbThreads = HL_MB_THREADS;
 constexpr int kMbRows = kMbThreads / 16;           // 16-lane rows
 constexpr int kMaxPass = (9 * 16 + kMbRows - 1) / kMbRows;  // rows per lane for the largest step
 

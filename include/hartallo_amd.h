@@ -115,11 +115,15 @@ int32_t hl_amd_pipeline_occupancy(void);
  * reference picture the next frame predicts from (dpb.c:160-170) */
 int32_t hl_amd_get_recon(hl_amd_encoder_t* encoder, uint8_t* y, uint8_t* u, uint8_t* v);
 
-/* GPU time of the last encode call, in milliseconds, split by stage:
- * [0] quarter-pel planes kernel, [1] macroblock-decision kernels (sum over
- * the wavefront launches, re-runs included), [2] deblocking kernels,
- * [3] the frame's device timeline from planes to deblock end (host
- * validation gaps included).  Filled only when timing is on. */
+/* Time of the last encode call, in milliseconds, split by stage.
+ * Per-picture calls: [0] quarter-pel planes kernel, [1] macroblock-decision
+ * kernels (sum over the wavefront launches, re-runs included), [2]
+ * deblocking kernels, [3] the frame's device timeline from planes to
+ * deblock end (host validation gaps included).
+ * Pipelined runs (hl_amd_encode_batch): [0] planes of the picture before
+ * the run, [1] the pipelined kernel, [2] the copy of the run's records to
+ * the host, [3] host slice writing (wall time).  Filled only when timing is
+ * on. */
 int32_t hl_amd_set_timing(hl_amd_encoder_t* encoder, int32_t enable);
 int32_t hl_amd_get_timing(hl_amd_encoder_t* encoder, float* ms4);
 

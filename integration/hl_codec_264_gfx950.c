@@ -1,0 +1,121 @@
+/*
+ * hl_codec_264_gfx950.c -- the hartallo-side plugin that drops the MI355X
+ * (gfx950) encode path in behind hartallo's codec API.  This is the file a
+ * maintainer adds to hartallo (source/h264/); it is compiled here against
+ * the reference's own headers and linked with the reference's own library
+ * by oracle/Makefile (oracle/_ref/drop_in_enc, tests/test_drop_in.py), so
+ * the drop-in is exercised through hl_codec_encode exactly as
+ * source/test_encoder.c:135-146 calls it.
+ *
+ * The plugin ABI is hl_codec_plugin_def_t (include/hartallo/hl_codec.h:
+ * 173-184); its encode slot is called by hl_codec_encode (source/hl_codec.c:
+ * 152-159), which refuses a plugin whose decode slot is NULL (:154).  The
+ * codec object must start with hl_codec_t (HL_DECLARE_CODEC, hl_codec.h:171)
+ * because the API reads and writes its fields directly.
+ */
+#include <hartallo/hl_codec.h>
+#include <hartallo/hl_frame.h>
+#include <hartallo/hl_object.h>
+#include <stdarg.h>
+
+#include "hartallo_amd.h" /* include/hartallo_amd.h of the gfx950 library */
+
+extern const hl_codec_plugin_def_t* hl_codec_264_plugin_def_t; /* the stock plugin (hl_codec_264.c:1186) */
+
+typedef struct hl_codec_264_gfx950_s {
+    HL_DECLARE_CODEC; /* first member (hl_codec.h:171) */
+    hl_amd_encoder_t* enc;
+    hl_size_t width, height;
+} hl_codec_264_gfx950_t;
+
+static hl_object_t* gfx950_ctor(hl_object_t* self, va_list* app)
+{
+    (void)app;
+    return self;
+}
+
+static hl_object_t* gfx950_dtor(hl_object_t* self)
+{
+    hl_codec_264_gfx950_t* p = (hl_codec_264_gfx950_t*)self;
+    if (p && p->enc) {
+        hl_amd_encoder_destroy(p->enc);
+        p->enc = NULL;
+    }
+    return self;
+}
+
+static int gfx950_cmp(const hl_object_t* a, const hl_object_t* b) { return (int)((const char*)a - (const char*)b); }
+
+static const hl_object_def_t gfx950_def_s = {sizeof(hl_codec_264_gfx950_t), gfx950_ctor, gfx950_dtor, gfx950_cmp, HL_TRUE};
+
+/* plugin encode(): one planar YUV420 frame in host memory -> headers + one
+ * slice NAL, as the stock plugin's _hl_codec_264_encode (hl_codec_264.c:
+ * 404-1038) returns them */
+static HL_ERROR_T gfx950_encode(hl_codec_t* base, const hl_frame_t* frame, hl_codec_result_t* result)
+{
+    hl_codec_264_gfx950_t* self = (hl_codec_264_gfx950_t*)base;
+    const hl_frame_video_t* f = (const hl_frame_video_t*)frame;
+    hl_amd_result_t r;
+    int32_t err;
+    if (!self || !f || !result) return HL_ERROR_INVALID_PARAMETER;
+    if (!self->enc || f->data_width[0] != self->width || f->data_height[0] != self->height) {
+        hl_amd_params_t p;
+        if (self->enc) {
+            hl_amd_encoder_destroy(self->enc);
+            self->enc = NULL;
+        }
+        p.width = (int32_t)f->data_width[0];
+        p.height = (int32_t)f->data_height[0];
+        p.qp = base->qp;
+        p.me_range = base->me_range;
+        p.deblock = base->deblock_flag;
+        p.gop_size = base->gop_size;
+        p.me_early_term = base->me_early_term_flag;
+        p.device = 0; /* one process per GPU (HIP_VISIBLE_DEVICES) */
+        if ((err = hl_amd_encoder_create(&p, &self->enc))) return (HL_ERROR_T)err; /* HL_ERROR_T values (hl_types.h:101-122) */
+        self->width = f->data_width[0];
+        self->height = f->data_height[0];
+    }
+    if ((err = hl_amd_encode(self->enc, f->data_ptr[0], f->data_ptr[1], f->data_ptr[2], &r)))
+        return (HL_ERROR_T)err;
+    result->type = HL_CODEC_RESULT_TYPE_NONE;
+    if (r.type & HL_AMD_RESULT_TYPE_HDR) { /* hl_codec_264.c:675-686 */
+        base->hdr_bytes = r.hdr;
+        base->hdr_bytes_count = r.hdr_size;
+        result->type |= HL_CODEC_RESULT_TYPE_HDR;
+    }
+    result->type |= HL_CODEC_RESULT_TYPE_DATA; /* hl_codec_264.c:1000-1006 */
+    result->data_ptr = r.data; /* owned by the encoder, valid until the next call */
+    result->data_size = r.data_size;
+    result->width = self->width;
+    result->height = self->height;
+    return HL_ERROR_SUCCESS;
+}
+
+static HL_ERROR_T gfx950_set_option(hl_codec_t* base, const struct hl_option_s* opt)
+{
+    return hl_codec_264_plugin_def_t->set_option(base, opt);
+}
+
+static HL_ERROR_T gfx950_decode(hl_codec_t* base, const void* data, hl_size_t size, hl_codec_result_t* result)
+{
+    (void)base;
+    (void)data;
+    (void)size;
+    (void)result;
+    return HL_ERROR_NOT_IMPLEMENTED; /* non-NULL: hl_codec_encode checks plugin->decode (hl_codec.c:154) */
+}
+
+const hl_codec_plugin_def_t hl_codec_264_gfx950_plugin_def_s = {
+    &gfx950_def_s, HL_CODEC_TYPE_H264, HL_MEDIA_TYPE_VIDEO, "H.264 AVC encoder (MI355X gfx950)", gfx950_set_option, gfx950_decode, gfx950_encode,
+};
+
+/* After hl_engine_init(): make this the plugin hl_codec_plugin_find(H264)
+ * returns (hl_codec.c:161-229: register adds at the first free slot, find
+ * returns the first match). */
+HL_ERROR_T hl_codec_264_gfx950_install(void)
+{
+    HL_ERROR_T err = hl_codec_plugin_unregister(hl_codec_264_plugin_def_t);
+    if (err) return err;
+    return hl_codec_plugin_register(&hl_codec_264_gfx950_plugin_def_s);
+}

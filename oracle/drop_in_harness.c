@@ -1,0 +1,81 @@
+/*
+ * drop_in_harness.c -- TEST INFRASTRUCTURE.  Drives the reference's own
+ * codec API (allweax/hartallo, oracle/_ref/libhl.a) with the gfx950 plugin
+ * (integration/hl_codec_264_gfx950.c) installed in place of the stock H.264
+ * plugin: hl_engine_init, hl_codec_264_gfx950_install (unregister +
+ * register, hl_codec.c:161-212), hl_codec_plugin_find, hl_codec_create and
+ * hl_codec_encode with the settings of source/test_encoder.c:135-146.  Every
+ * frame is encoded by libhartallo_amd.so on the GPU; the output is written
+ * as test_encoder.c:220-236 writes it.
+ *
+ * usage: drop_in_enc W H N qp me_range deblock gop early_term in.yuv out.264
+ *   early_term -1 keeps the hl_codec_create default (hl_types.h:67)
+ */
+#include <hartallo/hl_api.h>
+#include <hartallo/hl_codec.h>
+#include <hartallo/hl_debug.h>
+#include <hartallo/hl_frame.h>
+#include <hartallo/hl_object.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+extern const hl_codec_plugin_def_t hl_codec_264_gfx950_plugin_def_s;
+HL_ERROR_T hl_codec_264_gfx950_install(void);
+
+int main(int argc, char** argv)
+{
+    if (argc < 11) {
+        fprintf(stderr, "usage: %s W H N qp me_range deblock gop early_term in.yuv out.264\n", argv[0]);
+        return 1;
+    }
+    int W = atoi(argv[1]), H = atoi(argv[2]), N = atoi(argv[3]), qp = atoi(argv[4]);
+    int mer = atoi(argv[5]), db = atoi(argv[6]), gop = atoi(argv[7]), et = atoi(argv[8]);
+    hl_debug_set_level(HL_DEBUG_LEVEL_ERROR);
+    if (hl_engine_init()) return 2;
+    if (hl_codec_264_gfx950_install()) return 3;
+    const struct hl_codec_plugin_def_s* pl = 0;
+    struct hl_codec_s* c = 0;
+    struct hl_codec_result_s* r = 0;
+    hl_frame_video_t* f = 0;
+    if (hl_codec_plugin_find(HL_CODEC_TYPE_H264, &pl) || pl != &hl_codec_264_gfx950_plugin_def_s) {
+        fprintf(stderr, "the gfx950 plugin is not the one hl_codec_plugin_find returns\n");
+        return 4;
+    }
+    hl_codec_create(pl, &c);
+    hl_codec_result_create(&r);
+    hl_frame_video_create(&f);
+    c->gop_size = gop; c->me_range = mer; c->qp = qp; c->fps.num = 1; c->fps.den = 15;
+    c->rc_bitrate = -1; c->deblock_flag = db; c->threads_count = 1; c->max_ref_frame = 1;
+    c->distortion_mesure_type = HL_VIDEO_DISTORTION_MESURE_TYPE_SAD;
+    if (et >= 0) c->me_early_term_flag = et;
+    size_t fs = (size_t)W * H * 3 / 2;
+    uint8_t* buf = (uint8_t*)malloc(fs);
+    FILE* fi = fopen(argv[9], "rb");
+    FILE* fo = fopen(argv[10], "wb");
+    if (!fi || !fo) return 5;
+    static const uint8_t scp[3] = {0, 0, 1};
+    int n = 0;
+    while (n < N && fread(buf, 1, fs, fi) == fs) {
+        hl_frame_video_fill(f, HL_VIDEO_CHROMA_YUV420, W, H, buf, fs);
+        f->encoding = HL_VIDEO_ENCODING_TYPE_AUTO;
+        int e = hl_codec_encode(c, (hl_frame_t*)f, r);
+        if (e) {
+            fprintf(stderr, "encode err %d at frame %d\n", e, n);
+            return 6;
+        }
+        if (r->type & HL_CODEC_RESULT_TYPE_HDR) fwrite(c->hdr_bytes, 1, c->hdr_bytes_count, fo);
+        if (r->type & HL_CODEC_RESULT_TYPE_DATA) {
+            fwrite(scp, 1, 3, fo);
+            fwrite(r->data_ptr, 1, r->data_size, fo);
+        }
+        ++n;
+    }
+    fclose(fo);
+    fclose(fi);
+    hl_object_unref(r);
+    hl_object_unref(c);
+    hl_object_unref(f);
+    printf("{\"frames\": %d}\n", n);
+    return 0;
+}

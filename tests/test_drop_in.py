@@ -1,0 +1,66 @@
+"""The drop-in boundary exercised through the reference itself.
+
+integration/hl_codec_264_gfx950.c is the plugin a maintainer adds to
+hartallo: it registers in place of the stock H.264 plugin and forwards the
+encode slot (hl_codec.h:173-184) to libhartallo_amd.so.  oracle/Makefile
+compiles it against the reference's own headers and links it with the
+reference's own library (oracle/_ref/libhl.a) into oracle/_ref/drop_in_enc,
+which encodes through hl_codec_encode exactly as source/test_encoder.c does
+(oracle/drop_in_harness.c).  On the GPU its streams must equal the streams
+the stock reference encoder produced (tests/golden), byte for byte --
+including the early-termination goldens encoded with the hl_codec_create
+default me_early_term_flag = 1 left untouched.
+"""
+import json
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+from hl_testlib import GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, ROOT, first_diff, golden_input
+
+DROP_IN = os.path.join(ROOT, "oracle", "_ref", "drop_in_enc")
+PLUGIN = os.path.join(ROOT, "integration", "hl_codec_264_gfx950.c")
+REF = "/root/reference"
+GOLD = json.load(open(os.path.join(GOLDEN, "golden.json")))
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "include")), reason="reference sources are only in the build container")
+def test_plugin_compiles_against_reference_headers():
+    prelude = os.path.join(ROOT, "oracle", "_ref", "prelude.h")
+    cmd = ["gcc", "-fsyntax-only", "-Wall", "-Wextra", "-Werror=incompatible-pointer-types", "-Werror=int-conversion",
+           "-Werror=implicit-function-declaration", "-D_GNU_SOURCE", "-include", "limits.h", "-include", prelude,
+           "-I" + os.path.join(REF, "include"), "-I" + os.path.join(ROOT, "include"), PLUGIN]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert "hl_codec_264_gfx950" not in r.stderr, r.stderr  # no warning from the plugin itself
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "include")), reason="reference sources are only in the build container")
+def test_drop_in_driver_is_built():
+    assert os.path.exists(DROP_IN), "make -C oracle ref builds oracle/_ref/drop_in_enc"
+    syms = subprocess.run(["nm", DROP_IN], capture_output=True, text=True).stdout
+    for s in ("hl_codec_264_gfx950_install", "hl_codec_encode", "hl_codec_264_plugin_def_t"):
+        assert s in syms, s
+
+
+CASES = [c for c in GOLDEN_CONFIGS if c[0] in ("cif_ippp_qp31_me8", "qcif_gop3_qp20_me4", "w480_h272_qp28_me16")] + GOLDEN_ET_CONFIGS[:3]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", CASES, ids=[c[0] for c in CASES])
+def test_drop_in_through_hl_codec_encode(gpu, cfg):
+    if not os.path.exists(DROP_IN):
+        pytest.fail("oracle/_ref/drop_in_enc missing (built in the build container by make -C oracle ref)")
+    name, w, h, n, qp, mer, db, gop, seed = cfg
+    et = -1 if GOLD[name].get("early_term", 0) else 0  # -1: leave the hl_codec_create default (1)
+    with tempfile.TemporaryDirectory() as td:
+        inp, out = os.path.join(td, "in.yuv"), os.path.join(td, "out.264")
+        golden_input(cfg).tofile(inp)
+        r = subprocess.run([DROP_IN, str(w), str(h), str(n), str(qp), str(mer), str(db), str(gop), str(et), inp, out],
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr
+        got = open(out, "rb").read()
+    ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()
+    assert got == ref, f"{name}: first differing byte {first_diff(got, ref)}"

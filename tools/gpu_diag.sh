@@ -1,7 +1,6 @@
 #!/bin/bash
-# Diagnosis of the pipelined-run mismatch on the GPU box: the
-# GOP-spanning stress run on the round-1 build (build/old) and on the same
-# build with the per-step candidate results double-buffered (build/oldC).
+# A/B of library variants on the GPU box (tools/ab_bench.py) after a parity
+# pass of the variant (pipeline goldens + bench goldens).
 set -o pipefail
 mkdir -p gpurun_out
 run() {  # name, seconds, command...
@@ -10,12 +9,13 @@ run() {  # name, seconds, command...
     echo "== $name"
     timeout -k 10 "$secs" "$@" > "gpurun_out/diag_$name.log" 2>&1
     local rc=$?
-    echo "== $name rc=$rc $(tail -1 gpurun_out/diag_$name.log)"
+    grep -v amdgpu.ids "gpurun_out/diag_$name.log" | tail -${TAILN:-3}
+    echo "== $name rc=$rc"
     case $rc in 124|134|137|139) exit $rc ;; esac
     return 0
 }
-S="python -u tools/stress_spans_gops.py"
-for v in old oldC old oldC old oldC; do
-    HL_LIB=build/$v/libhartallo_amd.so run stress_$v 200 $S 8
+T="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+for v in "$@"; do
+    HL_LIB=build/$v/libhartallo_amd.so run parity_$v 400 $T tests/test_gpu_pipeline.py tests/test_gpu_parity.py tests/test_gpu_bench_golden.py -k "golden or driver or 720p"
 done
-run stress_new 200 $S 8
+TAILN=20 run ab 900 python -u tools/ab_bench.py hartallo_amd/libhartallo_amd.so $(for v in "$@"; do echo build/$v/libhartallo_amd.so; done)
