@@ -46,15 +46,28 @@ BENCH_GOLDEN = os.path.join(ROOT, "tests", "golden", "bench_golden.json")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(frames_host, n_frames):
-    """Times the reference encoder (oracle/_ref/ref_enc, built from the
-    reference's own sources) -- or, without it, the bit-exact C restatement --
-    on the first n_frames of this rank's workload, single thread."""
-    ref = os.path.join(ROOT, "oracle", "_ref", "ref_enc")
-    orc = os.path.join(ROOT, "oracle", "_build", "hlenc_oracle")
-    exe, kind = (ref, "reference") if os.path.exists(ref) else (orc, "port")
-    if not os.path.exists(exe):
+    """Times the reference encoder on the first n_frames of this rank's
+    workload, single thread: its x86-intrinsic build (oracle/_ref/ref_enc_sse,
+    the encoder BASELINE.json's north star names), else its pure-C build
+    (oracle/_ref/ref_enc), else the bit-exact C restatement (oracle/)."""
+    cands = [(os.path.join(ROOT, "oracle", "_ref", "ref_enc_sse"), "reference", "x86-intrinsic (SSE2-SSE4.2) build of the reference sources"),
+             (os.path.join(ROOT, "oracle", "_ref", "ref_enc"), "reference", "pure-C build of the reference sources"),
+             (os.path.join(ROOT, "oracle", "_build", "hlenc_oracle"), "port", "bit-exact C restatement (oracle/hl_oracle.c)")]
+    found = [c for c in cands if os.path.exists(c[0])]
+    if not found:
         return None
+    exe, kind, what = found[0]
     with tempfile.TemporaryDirectory() as td:
         inp = os.path.join(td, "in.yuv")
         frames_host[:n_frames].tofile(inp)
@@ -71,8 +84,9 @@ def cpu_baseline(frames_host, n_frames):
         "unit": "frames/s",
         "cores": 1,
         "kind": kind,
-        "sample": f"first {n_frames} frames (1 I + {n_frames - 1} P) of the same 1920x1088 QP{QP} stream, encode time only, 1 thread: "
-                  f"I picture {t_i:.2f} s, P pictures {t_p:.2f} s each, rate of a GOP{GOP} (1 I + {GOP - 1} P) from these",
+        "sample": f"{what}, first {n_frames} frames (1 I + {n_frames - 1} P) of the same 1920x1088 QP{QP} stream, encode time only, "
+                  f"1 thread on {cpu_model()}: I picture {t_i:.2f} s, P pictures {t_p:.2f} s each, rate of a GOP{GOP} "
+                  f"(1 I + {GOP - 1} P) from these (--cpu-frames {GOP} times a whole GOP)",
     }
 
 
@@ -96,7 +110,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=4 * GOP)  # four whole GOPs (IDR + 29 P pictures each), one pipelined launch
     ap.add_argument("--warmup", type=int, default=GOP)  # the first GOP (also warms the pipelined path)
-    ap.add_argument("--cpu-frames", type=int, default=3)
+    ap.add_argument("--cpu-frames", type=int, default=6)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 

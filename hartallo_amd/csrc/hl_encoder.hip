@@ -39,20 +39,7 @@ using namespace hl;
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
-// Quarter-pel planes: one lane per padded sample, all four planes.
-__global__ __launch_bounds__(256) void k_planes(const uint8_t* __restrict__ ref, int W, int H, uint8_t* pf, uint8_t* pb,
-                                                uint8_t* ph, uint8_t* pj, int pstride)
-{
-    const int PW = W + 2 * kPad, PH = H + 2 * kPad;
-    const int px = blockIdx.x * 64 + (threadIdx.x & 63), py = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (px >= PW || py >= PH) return;
-    const int x = px - kPad, y = py - kPad;
-    const size_t o = (size_t)py * pstride + px;
-    pf[o] = qpel_plane_sample(ref, W, H, 0, x, y);
-    pb[o] = qpel_plane_sample(ref, W, H, 1, x, y);
-    ph[o] = qpel_plane_sample(ref, W, H, 2, x, y);
-    pj[o] = qpel_plane_sample(ref, W, H, 3, x, y);
-}
+static void launch_planes(hl_amd_encoder_t* e, const uint8_t* ref_y);
 
 #if defined(HL_POISON_LDS)
 // Debug builds (-DHL_POISON_LDS=<salt>): the workgroup's LDS image (bytes
@@ -456,7 +443,7 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
     {
         const char* wt = getenv("HL_AMD_WRITER_THREADS");
         const unsigned hc = std::thread::hardware_concurrency();
-        e->nwriters = wt ? std::max(1, atoi(wt)) : (int)std::max(1u, std::min(8u, hc));
+        e->nwriters = wt ? std::max(1, atoi(wt)) : (int)std::max(1u, std::min(16u, hc));
     }
     e->pipe_wg = 0;
     e->reach = 2;
@@ -476,6 +463,12 @@ extern "C" void hl_amd_encoder_destroy(hl_amd_encoder_t* e)
     (void)hipStreamSynchronize(e->stream);
     free_all(e);
     delete e;
+}
+
+static void launch_planes(hl_amd_encoder_t* e, const uint8_t* ref_y)
+{
+    const dim3 grid((e->W + 2 * kPad + kPlTileW - 1) / kPlTileW, (e->H + 2 * kPad + kPlTileH - 1) / kPlTileH);
+    k_planes<<<grid, 256, 0, e->stream>>>(ref_y, e->W, e->H, e->d_pl[0], e->pstride, (int)e->plsz);
 }
 
 // Launches the MB wavefront for rows [row0, mbh).
@@ -553,8 +546,7 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
 
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[0], e->stream));
     if (!intra) {
-        dim3 grid((e->W + 2 * kPad + 63) / 64, (e->H + 2 * kPad + 3) / 4);
-        k_planes<<<grid, 256, 0, e->stream>>>(ref[0], e->W, e->H, e->d_pl[0], e->d_pl[1], e->d_pl[2], e->d_pl[3], e->pstride);
+        launch_planes(e, ref[0]);
         HL_HIP_CHECK(hipGetLastError());
     }
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[1], e->stream));
@@ -633,10 +625,17 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
 // ---------------------------------------------------------------------------
 // pipelined runs of P pictures
 // ---------------------------------------------------------------------------
+constexpr int kMaxRun = 128;  // pictures per pipelined launch (bench.py MAX_RUN)
+
 static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
 {
     if (n <= e->bcap) return hipSuccess;
     const size_t pic = (size_t)e->W * e->H * 3 / 2, nmb = e->nmb;
+    // Sized for a whole run of kMaxRun pictures at the first batch when that
+    // fits in 4 GB of HBM (about 22 MB per 1088p picture, 2.8 GB at 1088p),
+    // so that later, longer batches never reallocate between runs.
+    const size_t per_pic = pic + 4 * e->plsz + (sizeof(MbRecord) + sizeof(MbChain) + 3 * sizeof(int32_t)) * nmb;
+    if (per_pic * kMaxRun <= (4ull << 30)) n = std::max(n, kMaxRun);
     // free and forget every run buffer first, so that a failed allocation
     // below never leaves a dangling pointer for free_all or a later retry
     auto dfree = [](auto*& p) {
@@ -766,8 +765,6 @@ static std::vector<size_t> write_run(hl_amd_encoder_t* e, int m, int base)
     return size;
 }
 
-constexpr int kMaxRun = 128;  // pictures per pipelined launch (bench.py MAX_RUN)
-
 // m consecutive pictures (IDR and P, in GOP order) in one pipelined launch;
 // falls back to the per-picture path when a bounded wait gave up or a
 // row-start speculation turned out to matter (resolve_chain makes the latter
@@ -791,8 +788,7 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     uint8_t** ref0 = e->d_pic[e->cur ^ 1];
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[0], e->stream));
     {  // quarter-pel planes of the picture before the run
-        dim3 grid((e->W + 2 * kPad + 63) / 64, (e->H + 2 * kPad + 3) / 4);
-        k_planes<<<grid, 256, 0, e->stream>>>(ref0[0], e->W, e->H, e->d_pl[0], e->d_pl[1], e->d_pl[2], e->d_pl[3], e->pstride);
+        launch_planes(e, ref0[0]);
         HL_HIP_CHECK(hipGetLastError());
     }
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[1], e->stream));

@@ -25,6 +25,66 @@ HD uint8_t qpel_plane_sample(const uint8_t* ref, int W, int H, int plane, int x,
     }
 }
 
+#if defined(__HIPCC__)
+// Quarter-pel planes (full, b, h, j) of a reference picture, padded by kPad
+// (qpel_plane_sample, hl_filters.h: every tap coordinate clamped to the
+// picture independently, interpol.c:74-225).  One workgroup per 128x16 tile
+// of the padded planes: the clamped source tile with its 6-tap apron is
+// staged in LDS once, the vertical 6-tap sums (h1, |h1| < 2^14) once more,
+// and every lane writes 8 consecutive samples of each plane as one 8-byte
+// store.  HBM-bound: 1 B/px read (cached), 4 B/px written.
+constexpr int kPlTileW = 128, kPlTileH = 16;
+__global__ __launch_bounds__(256) void k_planes(const uint8_t* __restrict__ ref, int W, int H, uint8_t* __restrict__ pl0, int pstride,
+                                                int plsz)
+{
+    constexpr int TW = kPlTileW + 6, TR = kPlTileH + 5;
+    __shared__ uint8_t T[TR][TW + 2];
+    __shared__ int16_t V[kPlTileH][TW + 2];
+    const int PW = W + 2 * kPad, PH = H + 2 * kPad;
+    const int tx = blockIdx.x * kPlTileW, ty = blockIdx.y * kPlTileH;  // tile origin, padded coordinates
+    const int x0 = tx - kPad - 2, y0 = ty - kPad - 2;                   // picture coordinates of T[0][0]
+    for (int i = threadIdx.x; i < TR * TW; i += 256) {
+        const int r = i / TW, c = i - r * TW;
+        T[r][c] = ref[clip3(0, H - 1, y0 + r) * W + clip3(0, W - 1, x0 + c)];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kPlTileH * TW; i += 256) {
+        const int r = i / TW, c = i - r * TW;
+        V[r][c] = (int16_t)tap6(T[r][c], T[r + 1][c], T[r + 2][c], T[r + 3][c], T[r + 4][c], T[r + 5][c]);
+    }
+    __syncthreads();
+    const int row = threadIdx.x >> 4, xs = (threadIdx.x & 15) * 8;
+    const int py = ty + row, px = tx + xs;
+    if (py >= PH || px >= PW) return;  // PW is a multiple of 16: an 8-sample group never straddles it
+    uint64_t f = 0, b = 0, h = 0, j = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int c = xs + k + 2;
+        const uint8_t* t = T[row + 2];
+        const int16_t* v = V[row];
+        const uint64_t sf = t[c];
+        int vb = (tap6(t[c - 2], t[c - 1], t[c], t[c + 1], t[c + 2], t[c + 3]) + 16) >> 5;
+        int vh = (v[c] + 16) >> 5;
+        int vj = (tap6(v[c - 2], v[c - 1], v[c], v[c + 1], v[c + 2], v[c + 3]) + 512) >> 10;
+        // opaque: keeps hipcc (ROCm 7.2) from fusing shift + clamp + byte
+        // packing into v_ashr_pk_u8_i32, whose result's upper half it then
+        // ORs as if zero -- wrong bytes 2 and 3 of every packed pair on gfx950
+        // (tests/test_gpu_unit.py::test_planes_kernel)
+        asm volatile("" : "+v"(vb), "+v"(vh), "+v"(vj));
+        const uint64_t sb = (uint64_t)clip255(vb), sh = (uint64_t)clip255(vh), sj = (uint64_t)clip255(vj);
+        f |= sf << (8 * k);
+        b |= sb << (8 * k);
+        h |= sh << (8 * k);
+        j |= sj << (8 * k);
+    }
+    const size_t o = (size_t)py * pstride + px;
+    *reinterpret_cast<uint64_t*>(pl0 + o) = f;
+    *reinterpret_cast<uint64_t*>(pl0 + plsz + o) = b;
+    *reinterpret_cast<uint64_t*>(pl0 + 2 * (size_t)plsz + o) = h;
+    *reinterpret_cast<uint64_t*>(pl0 + 3 * (size_t)plsz + o) = j;
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // Deblocking
 // ---------------------------------------------------------------------------

@@ -3,8 +3,10 @@
 // against the scalar primitives (hl_prims.h) on the same random blocks, so a
 // parity failure of the full encoder can be narrowed to one primitive.
 #include <hip/hip_runtime.h>
+#include <string.h>
 
 #include "../../hartallo_amd/csrc/hl_coop.h"
+#include "../../hartallo_amd/csrc/hl_filters.h"
 
 using namespace hl;
 
@@ -101,3 +103,26 @@ extern "C" int unit_run(const uint8_t* h_src, const uint8_t* h_pred, int n, int 
 }
 
 extern "C" int unit_sizeof_out() { return (int)sizeof(UnitOut); }
+
+// The product's quarter-pel plane kernel (k_planes, hl_filters.h) and the
+// per-sample definition it implements (qpel_plane_sample, run on the host)
+// on the same picture: out_gpu / out_host hold the four padded planes, each
+// pstride x (H + 2 kPad) with pstride = (W + 2 kPad + 63) & ~63.
+extern "C" int unit_planes(const uint8_t* h_ref, int W, int H, uint8_t* out_gpu, uint8_t* out_host)
+{
+    const int pstride = (W + 2 * kPad + 63) & ~63, ph = H + 2 * kPad;
+    const size_t plsz = (size_t)pstride * ph;
+    uint8_t *d_ref = nullptr, *d_pl = nullptr;
+    if (hipMalloc(&d_ref, (size_t)W * H) || hipMalloc(&d_pl, 4 * plsz)) return 1;
+    if (hipMemcpy(d_ref, h_ref, (size_t)W * H, hipMemcpyHostToDevice) || hipMemset(d_pl, 0, 4 * plsz)) return 2;
+    const dim3 grid((W + 2 * kPad + kPlTileW - 1) / kPlTileW, (H + 2 * kPad + kPlTileH - 1) / kPlTileH);
+    k_planes<<<grid, 256>>>(d_ref, W, H, d_pl, pstride, (int)plsz);
+    if (hipDeviceSynchronize() || hipMemcpy(out_gpu, d_pl, 4 * plsz, hipMemcpyDeviceToHost)) return 3;
+    (void)hipFree(d_ref);
+    (void)hipFree(d_pl);
+    memset(out_host, 0, 4 * plsz);
+    for (int p = 0; p < 4; ++p)
+        for (int y = 0; y < ph; ++y)
+            for (int x = 0; x < W + 2 * kPad; ++x) out_host[p * plsz + (size_t)y * pstride + x] = qpel_plane_sample(h_ref, W, H, p, x - kPad, y - kPad);
+    return 0;
+}

@@ -43,3 +43,18 @@ def test_coop_block_pipeline(gpu, qp, mode):
         outs.append(o)
     bad = np.nonzero((outs[0] != outs[1]).any(axis=1))[0]
     assert bad.size == 0, f"{bad.size} blocks differ; first {bad[0]}: scalar {outs[0][bad[0]][:5]} coop {outs[1][bad[0]][:5]}"
+
+
+@pytest.mark.parametrize("w,h", [(32, 16), (176, 144), (352, 288), (1920, 1088)])
+def test_planes_kernel(gpu, w, h):
+    """k_planes (hl_filters.h) against the per-sample definition
+    qpel_plane_sample (interpol.c:74-225 edge semantics) on a random picture."""
+    lib = ctypes.CDLL(LIB)
+    rng = np.random.default_rng(w + h)
+    ref = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    pstride = (w + 80 + 63) & ~63
+    size = 4 * pstride * (h + 80)
+    a, b = np.zeros(size, np.uint8), np.zeros(size, np.uint8)
+    assert lib.unit_planes(ref.ctypes.data_as(ctypes.c_void_p), w, h, a.ctypes.data_as(ctypes.c_void_p), b.ctypes.data_as(ctypes.c_void_p)) == 0
+    bad = np.nonzero(a != b)[0]
+    assert bad.size == 0, f"{bad.size} samples differ; first at plane {bad[0] // (size // 4)}"

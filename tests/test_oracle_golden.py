@@ -52,3 +52,24 @@ def test_oracle_matches_bench_goldens():
             out = enc.encode(clip[f])
             assert hashlib.md5(out).hexdigest() == g["frame_md5"][f], f"{name} frame {f}"
             assert md5(enc.recon()) == g["recon_md5"][f], f"{name} recon {f}"
+
+
+REF_ENC_SSE = os.path.join(os.path.dirname(GOLDEN), "..", "oracle", "_ref", "ref_enc_sse")
+
+
+@pytest.mark.skipif(not os.path.exists(REF_ENC_SSE), reason="oracle/_ref/ref_enc_sse is built where the reference sources are")
+@pytest.mark.parametrize("name", ["cif_ippp_qp31_me8", "qcif_gop3_qp20_me4", "et_qcif_ippp_qp28"])
+def test_sse_reference_build_matches_goldens(name, tmp_path):
+    """The x86-intrinsic build of the reference (bench.py's CPU baseline)
+    produces the pure-C build's streams."""
+    import subprocess
+
+    from hl_testlib import GOLDEN_ET_CONFIGS
+
+    cfg = next(c for c in GOLDEN_CONFIGS + GOLDEN_ET_CONFIGS if c[0] == name)
+    _, w, h, n, qp, mer, db, gop, seed = cfg
+    inp = tmp_path / "in.yuv"
+    golden_input(cfg).tofile(inp)
+    subprocess.run([REF_ENC_SSE, str(w), str(h), str(n), str(qp), str(mer), str(db), str(gop), str(GOLD[name].get("early_term", 0)),
+                    str(inp), str(tmp_path / "o"), "quiet"], check=True, capture_output=True)
+    assert (tmp_path / "o.264").read_bytes() == open(os.path.join(GOLDEN, name + ".264"), "rb").read()
