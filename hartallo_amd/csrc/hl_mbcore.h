@@ -50,7 +50,7 @@ namespace hl {
         (c).pacc[slot] += __builtin_readcyclecounter() - (t0);   \
         (c).pcnt[slot] += 1;                                     \
     } while (0)
-constexpr int kProfSlots = 12;
+constexpr int kProfSlots = 18;  // prof[2 * slot], prof[2 * slot + 1] (< 40: the pipelined kernel uses 40-44)
 #else
 #define HL_PROF_T(v) const unsigned long long v = 0
 #define HL_PROF_ADD(c, slot, t0) ((void)(t0))
@@ -756,7 +756,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         }
 #if defined(HL_STEP_PROF)
         sv[0] += pa[0] * 0;  // wait for the loads here (profiling only)
-        HL_PROF_ADD(c, 3, ta0);
+        HL_PROF_ADD(c, 12, ta0);
         HL_PROF_T(ta1);
 #endif
 #pragma unroll
@@ -768,7 +768,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                 const int res = sv[j] - pred;
                 const int q = coop_quant(coop_fwd(c.K, res), c.K.mf, qbits, f);
 #if defined(HL_STEP_PROF)
-                HL_PROF_ADD(c, 4, ta1);
+                HL_PROF_ADD(c, 13, ta1);
                 HL_PROF_T(ta2);
 #endif
                 CoopStat st{0, 0, 0, -1};
@@ -786,11 +786,11 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                         tok = S.ct.tok[0][st.t1][st.tc] | (S.ct.tok[1][st.t1][st.tc] << 5) | (S.ct.tok[2][st.t1][st.tc] << 10) | (6 << 15);
                 }
 #if defined(HL_STEP_PROF)
-                HL_PROF_ADD(c, 5, ta2);
+                HL_PROF_ADD(c, 14, ta2);
                 HL_PROF_T(ta3);
 #endif
 #if defined(HL_STEP_PROF)
-                HL_PROF_ADD(c, 6, ta3);
+                HL_PROF_ADD(c, 15, ta3);
 #endif
                 if (c.K.p == 0) {
                     S.be_w0[ci][k] = st.tc | (st.t1 << 5) | ((st.sctr + 1) << 8);
@@ -1203,6 +1203,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     int cx = b.mv[0] >> 2, cy = b.mv[1] >> 2;
     int left = cx - range, right = cx + range, top = cy - range, bottom = cy + range;
     for (;;) {
+        HL_PROF_T(tgap);
         int ncand = 0;
         const uint32_t pkx = shift == 2 ? pIntX : (shift == 1 ? pHalfX : pQuarX);
         const uint32_t pky = shift == 2 ? pIntY : (shift == 1 ? pHalfY : pQuarY);
@@ -1227,7 +1228,9 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
 #endif
         int best = -1;
         if (ncand) {
+            HL_PROF_ADD(c, 16, tgap);
             eval_candidates(c, g, ncand, pmv);
+            HL_PROF_T(tsel);
             double m;
             const int bi = pick_first_min(c, ncand, m);
             if (m < b.cost) {
@@ -1239,6 +1242,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
                 b.mv[0] = uni((int)S.wc[c.tid >> 6][bi].mvx);
                 b.mv[1] = uni((int)S.wc[c.tid >> 6][bi].mvy);
             }
+            HL_PROF_ADD(c, 17, tsel);
         }
         flags = 0xFFFFFF;
         if (shift == 2 && best == -1) {

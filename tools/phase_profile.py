@@ -16,12 +16,13 @@ import hartallo_amd  # noqa: E402
 from hartallo_amd import _lib, synth  # noqa: E402
 
 PHASES = ["eval:block", "eval:nC", "eval:reduce", "search_partition", "mvp", "guess_intra(P)", "mb_begin", "mb_end", "whole MB",
-          "reach_wait", "intra:i16", "intra:i4"]
+          "reach_wait", "intra:i16", "intra:i4", "step:slots+loads", "step:fwd+quant", "step:idct+cavlc", "step:-", "step:candidates",
+          "step:selection"]
 
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-    _lib.load_library(os.path.join(ROOT, "build", "prof", "hartallo_amd", "libhartallo_amd.so"))
+    _lib.load_library(os.environ.get("HL_LIB") or os.path.join(ROOT, "build", "prof", "hartallo_amd", "libhartallo_amd.so"))
     W, H = 1920, 1088
     clip = synth.clip(W, H, n, 11)
     enc = hartallo_amd.Encoder(W, H, 28, 16, 1, 30)
