@@ -38,6 +38,7 @@ EXPORTED_SYMBOLS = (
     "hl_amd_set_timing",
     "hl_amd_get_timing",
     "hl_amd_last_reruns",
+    "hl_amd_last_chain_walks",
     "hl_amd_last_mb_launches",
     "hl_amd_profile_counters",
     "hl_amd_debug_records",
@@ -128,6 +129,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_get_timing.restype = i32
     lib.hl_amd_last_reruns.argtypes = [vp]
     lib.hl_amd_last_reruns.restype = i32
+    lib.hl_amd_last_chain_walks.argtypes = [vp]
+    lib.hl_amd_last_chain_walks.restype = i32
     lib.hl_amd_last_mb_launches.argtypes = [vp]
     lib.hl_amd_last_mb_launches.restype = i32
     lib.hl_amd_profile_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong), i32]
@@ -256,6 +259,10 @@ class Encoder:
 
     def last_reruns(self) -> int:
         return self.lib.hl_amd_last_reruns(self._h)
+
+    def last_chain_walks(self) -> int:
+        """resolve_chain walks of the last pipelined run (diagnostics)"""
+        return self.lib.hl_amd_last_chain_walks(self._h)
 
     def profile_counters(self, n: int = 32):
         a = (ctypes.c_ulonglong * n)()

@@ -130,6 +130,7 @@ __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
         P.cnt[i] = task_deps(f, a % mbw, a / mbw, mbw, mbh, P.reach, d);
         P.done[i] = 0;
         P.queue[i] = i == 0 ? 1 : 0;
+        P.claim[i] = 0;
     }
     if (i < P.nframes) {
         P.head[i] = 0;
@@ -137,21 +138,24 @@ __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
     }
     if (i == 0) {
         *P.oldest = 0;
-        *P.err = 0;
+        P.err[0] = 0;
+        P.err[1] = 0;
     }
 }
 
-// Wave 0 takes the next ready task, oldest picture first: f * nmb + addr, or
-// -1 once the run has finished (or after ~10 s without a task: a wait gave
-// up somewhere and the host re-encodes the run).
-__device__ int pop_task(const PipeArgs& P, int nmb, bool reserved)
+// Wave 0 takes the next ready task, oldest picture first, and claims it:
+// f * nmb + addr, or -1 once the run has finished (or after ~10 s without a
+// task: a wait gave up somewhere and the host re-encodes the run).  A queue
+// entry whose claim fails was taken by workgroup 0 (claim_next) and is
+// skipped.
+__device__ int pop_task(const PipeArgs& P, int nmb)
 {
     const int lane = threadIdx.x & 63;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         const int o = ld_relaxed(P.oldest);
         if (o >= P.nframes) return -1;
-        const int w = reserved ? 1 : min(P.window, P.nframes - o);
+        const int w = min(P.window, P.nframes - o);
         int h = 0, t = 0;
         if (lane < w) {
             h = ld_relaxed(P.head + o + lane);
@@ -170,6 +174,7 @@ __device__ int pop_task(const PipeArgs& P, int nmb, bool reserved)
                         v = -1;
                         break;
                     }
+                if (v > 0 && atomicCAS(P.claim + f * nmb + v - 1, 0, 1) != 0) v = 0;
             }
             v = __builtin_amdgcn_readfirstlane(v);
             if (v < 0) return -1;
@@ -184,6 +189,33 @@ __device__ int pop_task(const PipeArgs& P, int nmb, bool reserved)
     }
 }
 
+// Workgroup 0 claims tasks in run order (picture, then raster address)
+// instead of popping ready ones, and waits for the claimed task's
+// dependencies.  Every wait inside a task (reach_wait, resolve_chain) and
+// every dependency targets a task earlier in run order, and every earlier
+// task is claimed, i.e. held by a running workgroup or done; so the earliest
+// unfinished task never waits, and the run completes with any number of
+// workgroups (one included) -- no geometry can deadlock.
+__device__ int claim_next(const PipeArgs& P, int nmb, int& cursor)
+{
+    const int lane = threadIdx.x & 63, total = P.nframes * nmb;
+    for (;; ++cursor) {
+        if (cursor >= total) return -1;
+        int c = 0;
+        if (lane == 0) c = atomicCAS(P.claim + cursor, 0, 1);
+        if (__builtin_amdgcn_readfirstlane(c) == 0) break;
+    }
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (ld_relaxed(P.cnt + cursor) != 0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 10 s at 100 MHz
+            if (lane == 0) atomicAdd(P.err, 1);
+            return -1;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return cursor++;
+}
+
 // Pipelined run of P pictures (hl_pipeline.h): persistent workgroups taking
 // ready tasks (decision, then the deblocking and plane blocks it completes)
 // until the run has finished.
@@ -192,7 +224,8 @@ __global__ __launch_bounds__(kMbThreads, 2) void k_pipeline(PipeArgs P, int mbw,
     __shared__ Shared S;
     __shared__ int32_t s_task;
     const int nmb = mbw * mbh;
-    const bool reserved = blockIdx.x == 0;  // serves the oldest unfinished picture only
+    const bool in_order = blockIdx.x == 0;  // claims tasks in run order (claim_next)
+    int cursor = 0;
 #if defined(HL_PROFILE)
     // per-workgroup totals (profiling build): prof[40..44] = waits for a ready
     // task, decisions, filters, tasks, workgroup lifetime (shader clock)
@@ -205,7 +238,7 @@ __global__ __launch_bounds__(kMbThreads, 2) void k_pipeline(PipeArgs P, int mbw,
         const unsigned long long pt0 = __builtin_readcyclecounter();
 #endif
         if (threadIdx.x < 64) {
-            const int t = pop_task(P, nmb, reserved);
+            const int t = in_order ? claim_next(P, nmb, cursor) : pop_task(P, nmb);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
             if (threadIdx.x == 0) s_task = t;
@@ -326,6 +359,7 @@ struct hl_amd_encoder_s {
     int32_t* h_spec;
     std::vector<uint8_t> hdr, out, scratch;
     int32_t frame_index, gop_left, pict_count, idr_pic_id, chain_end, reruns;
+    int32_t chain_walks;  // resolve_chain walks of the last pipelined run
     bool timing;
     hipEvent_t ev[6];
     float ms[4];
@@ -338,7 +372,7 @@ struct hl_amd_encoder_s {
     MbRecord *d_brec, *h_brec;
     MbChain *d_bchain, *h_bchain;
     int32_t *d_bspec, *d_err;
-    int32_t *d_cnt, *d_done, *d_queue, *d_head;  // scheduler state (head: [head | tail | oldest])
+    int32_t *d_cnt, *d_done, *d_queue, *d_head;  // scheduler state (cnt: [cnt | claim], head: [head | tail | oldest])
     PipeFrame *d_pf, *h_pf;
     std::vector<std::vector<uint8_t>> bout;  // bitstreams of the last hl_amd_encode_batch
     int nwriters;                            // host slice writer threads of a run
@@ -667,7 +701,7 @@ static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
         (r = hipHostMalloc(&e->h_brec, sizeof(MbRecord) * nmb * n, hipHostMallocDefault)) ||
         (r = hipHostMalloc(&e->h_bchain, sizeof(MbChain) * nmb * n, hipHostMallocDefault)) ||
         (r = hipHostMalloc(&e->h_pf, sizeof(PipeFrame) * n, hipHostMallocDefault)) ||
-        (r = hipMalloc(&e->d_cnt, sizeof(int32_t) * nmb * n)) || (r = hipMalloc(&e->d_done, sizeof(int32_t) * nmb * n)) ||
+        (r = hipMalloc(&e->d_cnt, sizeof(int32_t) * 2 * nmb * n)) || (r = hipMalloc(&e->d_done, sizeof(int32_t) * nmb * n)) ||
         (r = hipMalloc(&e->d_queue, sizeof(int32_t) * nmb * n)) || (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * n + 1))))
         return r;
     if (!e->d_err && (r = hipMalloc(&e->d_err, sizeof(int32_t) * 4))) return r;
@@ -844,6 +878,7 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     P.reach = e->reach;
     P.window = e->window;
     P.cnt = e->d_cnt;
+    P.claim = e->d_cnt + nmb * m;
     P.done = e->d_done;
     P.queue = e->d_queue;
     P.head = e->d_head;
@@ -868,9 +903,9 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     // after the run (the persistent kernel holds every CU, so copies issued
     // while it runs could not start anyway); writer threads then serialise
     // the pictures in parallel.
-    int32_t err = 0;
+    int32_t errw[2] = {0, 0};  // bounded waits that gave up, resolve_chain walks
     HL_HIP_CHECK(hipMemcpyAsync(e->h_bchain, e->d_bchain, sizeof(MbChain) * nmb * m, hipMemcpyDeviceToHost, e->stream));
-    HL_HIP_CHECK(hipMemcpyAsync(&err, e->d_err, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(errw, e->d_err, sizeof(errw), hipMemcpyDeviceToHost, e->stream));
     HL_HIP_CHECK(hipMemcpyAsync(e->h_brec, e->d_brec, sizeof(MbRecord) * nmb * m, hipMemcpyDeviceToHost, e->stream));
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[2], e->stream));
     HL_HIP_CHECK(hipStreamSynchronize(e->stream));
@@ -880,6 +915,8 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         (void)hipEventElapsedTime(&e->ms[2], e->ev[5], e->ev[2]);
         e->ms[3] = 0.f;
     }
+    const int32_t err = errw[0];
+    e->chain_walks = errw[1];
     e->mb_launches = 1;
     e->reruns = 0;
     if (err) fprintf(stderr, "hartallo_amd: pipelined run: %d bounded waits gave up; re-encoding the run picture by picture\n", err);
@@ -1029,6 +1066,7 @@ extern "C" int32_t hl_amd_get_timing(hl_amd_encoder_t* e, float* ms4)
 }
 
 extern "C" int32_t hl_amd_last_reruns(hl_amd_encoder_t* e) { return e ? e->reruns : -1; }
+extern "C" int32_t hl_amd_last_chain_walks(hl_amd_encoder_t* e) { return e ? e->chain_walks : -1; }
 
 extern "C" int32_t hl_amd_last_mb_launches(hl_amd_encoder_t* e) { return e ? e->mb_launches : -1; }
 

@@ -97,7 +97,7 @@ struct FrameArgs {
     // pipelined runs (hl_pipeline.h); ref_done is null in the per-picture path
     const int32_t* ref_done;  // task flags of the reference picture's slot
     int32_t ref_epoch;        // flag value once a task of the reference picture finished
-    int32_t* perr;            // bounded-spin failures
+    int32_t* perr;            // [0] bounded-spin failures, [1] resolve_chain walks
     // exact rdo.Single_ctr for stale reads of a speculated value (resolve_chain);
     // run_done is null in the per-picture path (the host re-runs rows instead)
     const int32_t* run_done;  // task flags of picture 0 of the run ([pos * mbw * mbh + addr])
@@ -1662,6 +1662,7 @@ HD void resolve_chain(Ctx& c)
     Shared& S = c.S;
     const int nmb = F.mbw * F.mbh, lane = c.tid & 63;
     if (c.tid < 64) {
+        if (c.tid == 0) atomicAdd(F.perr + 1, 1);  // walk counter (diagnostics, hl_amd_last_chain_walks)
         int val = F.carry_in, pos = F.run_pos, y = c.mby - 1;
         for (;;) {
             if (y < 0) {

@@ -27,11 +27,14 @@
 // of unfinished dependencies (task_deps); the workgroup that finishes a task
 // decrements the counters of its successors (task_succ, the exact inverse)
 // and pushes those that reach zero onto their picture's ready queue.
-// Workgroups pop ready tasks, oldest picture first, so no workgroup ever holds
-// a task that cannot run yet.  The one wait left inside a task (reach_wait,
-// for motion windows beyond the guaranteed reach) only ever waits for the
-// previous picture; workgroup 0 serves the oldest unfinished picture alone,
-// whose reference is complete, so the run always progresses.
+// Workgroups pop ready tasks, oldest picture first, so they never hold a task
+// that cannot run yet.  The waits left inside a task (reach_wait, for motion
+// windows beyond the guaranteed reach; resolve_chain, for an exact
+// rdo.Single_ctr at a row start) only ever wait for tasks earlier in run
+// order (picture, then raster address).  Workgroup 0 claims tasks in exactly
+// that order instead of popping, so the earliest unfinished task is always
+// held by a running workgroup that does not wait: the run progresses with
+// any number of workgroups.
 // Hand-offs between workgroups use the agent-scope release/acquire protocol
 // of the gfx950 guide (cdna_hip_programming.md, Guideline 16): payload
 // stores, s_waitcnt vmcnt(0) in every wave, barrier, one wave's release
@@ -169,6 +172,7 @@ struct PipeArgs {
     int32_t reach;   // guaranteed reference reach R in MBs
     int32_t window;  // pictures a workgroup looks at for ready tasks (from the oldest unfinished)
     int32_t* cnt;    // [nframes][nmb] unfinished dependencies
+    int32_t* claim;  // [nframes][nmb] 1 once a workgroup holds the task
     int32_t* done;   // [nframes][nmb] 1 once the task finished (reach_wait polls it)
     int32_t* queue;  // [nframes][nmb] ready tasks, MB address + 1 (0 = slot not yet written)
     int32_t* head;   // [nframes] next queue slot to pop

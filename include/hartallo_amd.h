@@ -61,7 +61,8 @@ typedef struct hl_amd_params_s {
     int32_t me_range;       /* hl_codec_t.me_range, clipped to [1,64] (rdo.c:847) */
     int32_t deblock;        /* hl_codec_t.deblock_flag */
     int32_t gop_size;       /* hl_codec_t.gop_size */
-    int32_t me_early_term;  /* hl_codec_t.me_early_term_flag; only 0 is supported */
+    int32_t me_early_term;  /* hl_codec_t.me_early_term_flag (homogeneity mode masks,
+                               rdo.c:888-931); 1 needs width and height >= 32 */
     int32_t device;         /* HIP device ordinal */
 } hl_amd_params_t;
 
@@ -130,6 +131,11 @@ int32_t hl_amd_get_timing(hl_amd_encoder_t* encoder, float* ms4);
 /* number of row-start re-runs the last frame needed (rdo.Single_ctr
  * speculation) -- diagnostics */
 int32_t hl_amd_last_reruns(hl_amd_encoder_t* encoder);
+
+/* number of in-kernel rdo.Single_ctr walks (resolve_chain: a row start
+ * read the counter while its value was still speculated) in the last
+ * pipelined run -- diagnostics */
+int32_t hl_amd_last_chain_walks(hl_amd_encoder_t* encoder);
 
 /* number of macroblock-decision kernel launches of the last frame */
 int32_t hl_amd_last_mb_launches(hl_amd_encoder_t* encoder);

@@ -4,9 +4,9 @@ A batch must produce exactly the bitstream and reconstruction of the same
 frames encoded one call at a time -- which test_gpu_parity.py pins to the
 reference -- and of the golden streams the reference itself produced.  The
 pipeline geometry is varied so that the cross-picture waits are exercised
-with few workgroups (down to the one reserved for the oldest picture), narrow
-and wide windows and no guaranteed reach (every partition
-search then waits on the reference picture's progress).
+with few workgroups (down to the single one that claims tasks in run order),
+narrow and wide windows and no guaranteed reach (every partition search then
+waits on the reference picture's progress).
 Tolerance: none.
 """
 import json
@@ -149,3 +149,26 @@ def test_batch_1088p_spans_gops(gpu):
             pytest.fail(f"frame {f}: first differing byte {first_diff(a[f], b[f])}; {_diagnose(w, h, 28, 16, 1, 3, clip)}")
     assert np.array_equal(ra, rb)
     assert launches == 1 and reruns == 0, (launches, reruns)
+
+
+@pytest.mark.parametrize("geometry", [(1, 0, 8), (2, 2, 4)], ids=lambda g: "x".join(map(str, g)))
+def test_batch_idr_in_run_few_workgroups(gpu, geometry):
+    # 1088p, GOP 3, 4 pictures in one launch (I P P I): the I pictures' exact
+    # row-start rdo.Single_ctr walks (resolve_chain) wait mid-task on the end
+    # of an earlier row.  With one or two workgroups that row must be held by
+    # a running workgroup (claim_next), or the run stalls until a bounded wait
+    # gives up and the host re-encodes it.
+    w, h, n = 1920, 1088, 4
+    clip = synth.clip(w, h, n, 13)
+    a, ra = _single(w, h, 28, 16, 1, 3, clip)
+    enc = Encoder(w, h, 28, 16, 1, 3)
+    enc.set_pipeline(*geometry)
+    dev, ptrs = _device_frames(clip, w, h)
+    b = [r.annexb() for r in enc.encode_batch_device(ptrs)]
+    reruns, launches, walks = enc.last_reruns(), enc.last_mb_launches(), enc.last_chain_walks()
+    rb = np.concatenate(enc.recon())
+    enc.close()
+    assert a == b
+    assert np.array_equal(ra, rb)
+    assert launches == 1 and reruns == 0, (launches, reruns)
+    assert walks > 0  # the case this test is about did occur

@@ -177,3 +177,113 @@ def test_reach_task(mbw, mbh):
             planed.update(tpl[t])
             for (X, Y) in reach.get(t, []):
                 assert all((a, b) in planed for a in range(X + 1) for b in range(Y + 1)), ("reach_task", (X, Y), t)
+
+
+def _run_order_key(t):
+    f, x, y = t
+    return (f, y, x)
+
+
+@pytest.mark.parametrize("mbw,mbh,R", [(6, 5, 0), (9, 4, 2), (5, 7, 1), (12, 3, 0), (1, 4, 0), (4, 1, 1)])
+def test_waits_target_earlier_tasks(mbw, mbh, R):
+    """The premise of k_pipeline's progress argument (hl_encoder.hip
+    claim_next): every dependency (task_deps) and every wait inside a task --
+    reach_wait on reach_task of the previous picture, resolve_chain on the last
+    MB of an earlier row -- names a task earlier in run order (picture, then
+    raster address)."""
+    lib = _lib()
+    out = (ctypes.c_int * 2)()
+    for f in range(3):
+        for y in range(mbh):
+            for x in range(mbw):
+                t = (f, x, y)
+                for d in _task_deps(lib, *t, mbw, mbh, R):
+                    assert _run_order_key(d) < _run_order_key(t), (t, d)
+                if f > 0:
+                    for X in range(x, mbw):
+                        for Y in range(y, mbh):
+                            lib.emu_reach_task(X, Y, mbw, mbh, out)
+                            assert _run_order_key((f - 1, out[0], out[1])) < _run_order_key(t)
+                for yy in range(y):
+                    assert _run_order_key((f, mbw - 1, yy)) < _run_order_key(t)
+
+
+def _simulate(lib, mbw, mbh, R, nf, workers, seed, window=64, in_order=True):
+    """Discrete-event model of k_pipeline's scheduler: worker 0 claims tasks
+    in run order and waits for their dependencies (claim_next), the others pop
+    ready tasks from per-picture FIFO queues, oldest picture first, skipping
+    claimed ones (pop_task).  A random subset of tasks blocks inside the task
+    on an earlier task (resolve_chain's row end, reach_wait's reference task)
+    before it can finish.  Returns True when the run completes."""
+    rng = random.Random(seed)
+    tasks = [(f, x, y) for f in range(nf) for y in range(mbh) for x in range(mbw)]
+    order = sorted(tasks, key=_run_order_key)
+    deps = {t: _task_deps(lib, *t, mbw, mbh, R) for t in tasks}
+    succ = {t: _task_succ(lib, *t, mbw, mbh, R, nf) for t in tasks}
+    cnt = {t: len(deps[t]) for t in tasks}
+    wait = {}
+    for t in tasks:
+        f, x, y = t
+        if y > 0 and rng.random() < 0.3:
+            wait[t] = (f, mbw - 1, rng.randrange(y))          # resolve_chain: an earlier row's end
+        elif f > 0 and rng.random() < 0.3:
+            wait[t] = (f - 1, rng.randrange(mbw), rng.randrange(mbh))  # reach_wait: the reference picture
+    queues = [[] for _ in range(nf)]
+    queues[0].append((0, 0, 0))
+    claimed, done = set(), set()
+    cursor = 0
+    held = [None] * workers
+    while len(done) < len(tasks):
+        progress = False
+        for w in rng.sample(range(workers), workers):
+            t = held[w]
+            if t is None:
+                if w == 0 and in_order:
+                    while cursor < len(order) and order[cursor] in claimed:
+                        cursor += 1
+                    if cursor < len(order):
+                        t = order[cursor]
+                        claimed.add(t)
+                        held[w] = t
+                        progress = True
+                elif len(done) < len(tasks):
+                    oldest = min(f for f in range(nf) if any((f, x, y) not in done for x in range(mbw) for y in range(mbh)))
+                    for f in range(oldest, min(nf, oldest + window)):
+                        while queues[f] and queues[f][0] in claimed:
+                            queues[f].pop(0)
+                            progress = True
+                        if queues[f]:
+                            t = queues[f].pop(0)
+                            claimed.add(t)
+                            held[w] = t
+                            progress = True
+                            break
+                continue
+            if cnt[t] or (t in wait and wait[t] not in done):
+                continue  # claimed before ready (worker 0), or blocked inside the task
+            done.add(t)
+            held[w] = None
+            progress = True
+            for s in succ[t]:
+                cnt[s] -= 1
+                if cnt[s] == 0:
+                    queues[s[0]].append(s)
+        if not progress:
+            return False
+    return True
+
+
+@pytest.mark.parametrize("workers", [1, 2, 3, 6])
+@pytest.mark.parametrize("mbw,mbh,R", [(6, 5, 0), (8, 3, 2), (3, 6, 1)])
+def test_scheduler_progresses_with_few_workgroups(mbw, mbh, R, workers):
+    lib = _lib()
+    for seed in range(6):
+        assert _simulate(lib, mbw, mbh, R, 3, workers, seed), (mbw, mbh, R, workers, seed)
+
+
+def test_scheduler_model_finds_deadlocks():
+    # without the in-order workgroup, a single workgroup popping ready tasks
+    # gets stuck inside a task that waits on a task nobody holds: the model
+    # above does detect that
+    lib = _lib()
+    assert not all(_simulate(lib, 6, 5, 0, 3, 1, seed, in_order=False) for seed in range(6))
