@@ -33,6 +33,8 @@ EXPORTED_SYMBOLS = (
     "hl_amd_encode_device",
     "hl_amd_encode_batch",
     "hl_amd_set_pipeline",
+    "hl_amd_set_rate_control",
+    "hl_amd_last_qp",
     "hl_amd_pipeline_occupancy",
     "hl_amd_get_recon",
     "hl_amd_set_timing",
@@ -80,7 +82,7 @@ def _mb_record_dtype():
         ("chroma_mode", "<i4"), ("i16mode", "<i4"), ("mvd", "<i2", (4, 4, 2)), ("mv", "<i2", (4, 4, 2)),
         ("prev_flag", "i1", 16), ("rem_mode", "i1", 16), ("i4mode", "i1", 16), ("nc_luma", "i1", 16), ("nc_cac", "i1", (2, 4)),
         ("nc_dc", "i1"), ("pad0", "i1", 3), ("luma", "<i2", (16, 16)), ("i16dc", "<i2", 16), ("cdc", "<i2", (2, 4)),
-        ("cac", "<i2", (2, 4, 16)),
+        ("cac", "<i2", (2, 4, 16)), ("mad", "<i4"), ("pad1", "<i4"),
     ])
 
 
@@ -119,6 +121,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_encode_batch.restype = i32
     lib.hl_amd_set_pipeline.argtypes = [vp, i32, i32, i32]
     lib.hl_amd_set_pipeline.restype = i32
+    lib.hl_amd_set_rate_control.argtypes = [vp, ctypes.c_int64, i32, i32, i32, i32, i32]
+    lib.hl_amd_set_rate_control.restype = i32
+    lib.hl_amd_last_qp.argtypes = [vp]
+    lib.hl_amd_last_qp.restype = i32
     lib.hl_amd_pipeline_occupancy.argtypes = []
     lib.hl_amd_pipeline_occupancy.restype = i32
     lib.hl_amd_get_recon.argtypes = [vp, vp, vp, vp]
@@ -232,6 +238,18 @@ class Encoder:
         """The results of the last encode_batch_device call (also after
         collect=False), valid until the next encode call."""
         return [self._result(r) for r in self._last_batch]
+
+    def set_rate_control(self, bitrate: int, fps_num: int = 1, fps_den: int = 15, basicunit: int = -1, qp_min: int = -1,
+                         qp_max: int = -1):
+        """Rate control (hl_codec_t.rc_bitrate > 0 and its companions; call
+        before the first frame; bitrate <= 0 turns it off)."""
+        rc = self.lib.hl_amd_set_rate_control(self._h, bitrate, fps_num, fps_den, basicunit, qp_min, qp_max)
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_set_rate_control")
+
+    def last_qp(self) -> int:
+        """SliceQPY of the last encoded picture."""
+        return self.lib.hl_amd_last_qp(self._h)
 
     def set_pipeline(self, workgroups: int, reach: int, window: int):
         rc = self.lib.hl_amd_set_pipeline(self._h, workgroups, reach, window)

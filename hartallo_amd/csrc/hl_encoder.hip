@@ -17,10 +17,12 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <memory>
 #include <thread>
 #include <vector>
 
 #include "../../include/hartallo_amd.h"
+#include "hl_rc.h"
 #include "hl_pipeline.h"
 #include "hl_writer.h"
 
@@ -282,6 +284,14 @@ __global__ __launch_bounds__(kMbThreads, 2) void k_pipeline(PipeArgs P, int mbw,
         encode_mb(PF.F, S, addr, tid, kMbThreads, s_in, gx, gy, spec_in);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (PF.hrec) {  // the record to host memory in 16-byte words; the publish fence below is system scope
+            static_assert(sizeof(MbRecord) % 16 == 0, "MbRecord copies in 16-byte words");
+            const int32_t* src = reinterpret_cast<const int32_t*>(PF.F.rec + addr);
+            uint4* dst = reinterpret_cast<uint4*>(PF.hrec + addr);
+            for (int i = tid; i < (int)(sizeof(MbRecord) / 16); i += kMbThreads)
+                dst[i] = make_uint4(ld_relaxed(src + 4 * i), ld_relaxed(src + 4 * i + 1), ld_relaxed(src + 4 * i + 2),
+                                    ld_relaxed(src + 4 * i + 3));
+        }
 #if defined(HL_PROFILE)
         const unsigned long long pt2 = __builtin_readcyclecounter();
 #endif
@@ -302,7 +312,8 @@ __global__ __launch_bounds__(kMbThreads, 2) void k_pipeline(PipeArgs P, int mbw,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid < 64) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, HL_REL_SCOPE);
+            if (P.progress) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // host-visible records (system scope)
+            else __builtin_amdgcn_fence(__ATOMIC_RELEASE, HL_REL_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (tid == 0) st_relaxed(P.done + t, 1);
             int fo = 0, xo = 0, yo = 0;
@@ -317,7 +328,12 @@ __global__ __launch_bounds__(kMbThreads, 2) void k_pipeline(PipeArgs P, int mbw,
             }
             // pictures finish in order: the last MB depends on every other one
             // and on the previous picture's last MB
-            if (tid == 0 && addr == nmb - 1) __hip_atomic_store(P.oldest, f + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0 && addr == nmb - 1) {
+                __hip_atomic_store(P.oldest, f + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                // every record of picture f is in host memory (each task released at system scope)
+                if (P.progress) __hip_atomic_store(P.progress, f + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (P.pub_clock) P.pub_clock[f] = wall_clock64();
+            }
         }
     }
 #if defined(HL_PROFILE)
@@ -369,7 +385,9 @@ struct hl_amd_encoder_s {
     int pipe_wg, reach, window;  // workgroups (0: one per resident slot), R in MBs, pictures looked at
     int bcap;                    // pictures the run buffers hold
     uint8_t *d_bpic, *d_bpl;     // per picture: recon (Y|U|V), quarter-pel planes
-    MbRecord *d_brec, *h_brec;
+    MbRecord *d_brec, *h_brec, *dh_brec;  // dh_brec: device address of the pinned h_brec (the run writes it)
+    int32_t* h_progress;                  // pinned: pictures of the running run whose records are in h_brec
+    std::chrono::steady_clock::time_point run_t0;  // launch time of the running run (writer tracing)
     MbChain *d_bchain, *h_bchain;
     int32_t *d_bspec, *d_err;
     int32_t *d_cnt, *d_done, *d_queue, *d_head;  // scheduler state (cnt: [cnt | claim], head: [head | tail | oldest])
@@ -381,6 +399,9 @@ struct hl_amd_encoder_s {
     std::vector<const MbRecord*> last_recs;      // host records per picture of the last encode call (diagnostics)
     std::vector<const MbChain*> last_chain;      // host chain records, same
     std::vector<const uint8_t*> last_pic;        // device recon (Y|U|V planes contiguous) or null = the current reference
+    std::unique_ptr<hl::RateControl> rc;         // rate control (rc_bitrate > 0), hl_rc.h
+    hl::RcConfig rc_cfg;
+    int32_t last_qp;                             // SliceQPY of the last encoded picture
 };
 
 static void free_all(hl_amd_encoder_t* e)
@@ -414,6 +435,7 @@ static void free_all(hl_amd_encoder_t* e)
     (void)hipHostFree(e->h_rec);
     (void)hipHostFree(e->h_chain);
     (void)hipHostFree(e->h_spec);
+    (void)hipHostFree(e->h_progress);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     for (int i = 0; i < 6; ++i)
         if (e->ev[i]) (void)hipEventDestroy(e->ev[i]);
@@ -459,7 +481,8 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
          hipMalloc(&e->d_spec, sizeof(int32_t) * e->mbh) == hipSuccess &&
          hipHostMalloc(&e->h_rec, sizeof(MbRecord) * e->nmb, hipHostMallocDefault) == hipSuccess &&
          hipHostMalloc(&e->h_chain, sizeof(MbChain) * e->nmb, hipHostMallocDefault) == hipSuccess &&
-         hipHostMalloc(&e->h_spec, sizeof(int32_t) * e->mbh, hipHostMallocDefault) == hipSuccess;
+         hipHostMalloc(&e->h_spec, sizeof(int32_t) * e->mbh, hipHostMallocDefault) == hipSuccess &&
+         hipHostMalloc(&e->h_progress, 64, hipHostMallocCoherent) == hipSuccess;
     // the per-address MB objects start zeroed (calloc'd by the reference, mb.c)
     ok = ok && hipMemsetAsync(e->d_st, 0, sizeof(MbState) * e->nmb, e->stream) == hipSuccess;
 #if defined(HL_PROFILE)
@@ -547,6 +570,9 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
 {
     const bool intra = e->gop_left <= 0;
     if (intra) e->gop_left = e->p.gop_size;
+    // rate control picks the picture's QP before it is coded (hl_codec_264.c:719-742)
+    const int qp = e->rc ? e->rc->begin_picture(intra) : e->p.qp;
+    const int qpc = kQpToQpc[qp];
     uint8_t** cur = e->d_pic[e->cur];
     uint8_t** ref = e->d_pic[e->cur ^ 1];
     FrameArgs F{};  // ref_done = null: the per-picture path needs no reference waits
@@ -556,12 +582,12 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
     F.Hc = e->Hc;
     F.mbw = e->mbw;
     F.mbh = e->mbh;
-    F.qp = e->p.qp;
-    F.qpc = e->qpc;
+    F.qp = qp;
+    F.qpc = qpc;
     F.is_intra = intra;
     F.me_range = std::min(64, std::max(1, e->p.me_range));
     F.early_term = e->p.me_early_term != 0;
-    F.lambda = 0.852 * (double)(1 << ((e->p.qp - 12) / 3));
+    F.lambda = 0.852 * (double)(1 << ((qp - 12) / 3));  // slice.c:1766
     F.src[0] = y;
     F.src[1] = u;
     F.src[2] = v;
@@ -618,8 +644,8 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
         D.H = e->H;
         D.Wc = e->Wc;
         D.mbw = e->mbw;
-        D.qp = e->p.qp;
-        D.qpc = e->qpc;
+        D.qp = qp;
+        D.qpc = qpc;
         for (int c = 0; c < 3; ++c) D.pic[c] = cur[c];
         D.st = e->d_st;
         const int ndiag = (e->mbw - 1) + 2 * (e->mbh - 1) + 1;
@@ -638,9 +664,19 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
         (void)hipEventElapsedTime(&e->ms[3], e->ev[0], e->ev[3]);
     }
     const StreamParams sp{e->W, e->H, e->p.qp, e->p.deblock};
-    const SliceState ss{intra ? 1 : 0, e->pict_count, e->idr_pic_id};
-    const size_t n = write_slice(sp, ss, e->h_rec, e->scratch.data(), e->out.data(), e->out.size());
+    const SliceState ss{intra ? 1 : 0, e->pict_count, e->idr_pic_id, qp};
+    SliceBits sb{};
+    const size_t n = write_slice(sp, ss, e->h_rec, e->scratch.data(), e->out.data(), e->out.size(), &sb);
     if (!n) return HL_AMD_ERROR_TOOSHORT;
+    if (e->rc) {  // hl_codec_264_rc_end_frame / _end_gop, hl_codec_264.c:1018-1031
+        RcPictureStats st{};
+        for (int a = 0; a < e->nmb; ++a) st.mad_sum += e->h_rec[a].mad;
+        st.header_bits = sb.header_bits;
+        st.texture_bits = sb.texture_bits;
+        st.nbits = (int32_t)((n - 3) * 8);
+        e->rc->end_picture(intra, st, e->gop_left - 1 <= 0);
+    }
+    e->last_qp = qp;
     r->type = HL_AMD_RESULT_TYPE_DATA;
     r->data = e->out.data() + 3;
     r->data_size = n - 3;
@@ -702,7 +738,8 @@ static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
         (r = hipHostMalloc(&e->h_bchain, sizeof(MbChain) * nmb * n, hipHostMallocDefault)) ||
         (r = hipHostMalloc(&e->h_pf, sizeof(PipeFrame) * n, hipHostMallocDefault)) ||
         (r = hipMalloc(&e->d_cnt, sizeof(int32_t) * 2 * nmb * n)) || (r = hipMalloc(&e->d_done, sizeof(int32_t) * nmb * n)) ||
-        (r = hipMalloc(&e->d_queue, sizeof(int32_t) * nmb * n)) || (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * n + 1))))
+        (r = hipMalloc(&e->d_queue, sizeof(int32_t) * nmb * n)) || (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * n + 1))) ||
+        (r = hipHostGetDevicePointer((void**)&e->dh_brec, e->h_brec, 0)))
         return r;
     if (!e->d_err && (r = hipMalloc(&e->d_err, sizeof(int32_t) * 4))) return r;
     // defined contents from the start (nothing reads a run buffer before the
@@ -769,7 +806,7 @@ static void store_result(hl_amd_encoder_t* e, int i, const hl_amd_result_t& src,
 // threads serialise its pictures in parallel, each with its own scratch
 // buffers, into bout[base + k].  Returns the bytes written per picture
 // (start code included; 0 = output buffer too short).
-static std::vector<size_t> write_run(hl_amd_encoder_t* e, int m, int base)
+static std::vector<size_t> write_run(hl_amd_encoder_t* e, int m, int base, const std::atomic<bool>* abort = nullptr)
 {
     const int n = std::max(1, std::min(m, e->nwriters));
     const StreamParams sp{e->W, e->H, e->p.qp, e->p.deblock};
@@ -785,9 +822,20 @@ static std::vector<size_t> write_run(hl_amd_encoder_t* e, int m, int base)
     std::atomic<int> next{0};
     auto work = [&](int w) {
         for (int k; (k = next.fetch_add(1)) < m;) {
-            const SliceState ss{e->run_intra[k], e->pict_count + k, e->run_idr_id[k]};
+            // during a run: wait until the kernel has put picture k's records in host memory
+            while (abort && __atomic_load_n(e->h_progress, __ATOMIC_ACQUIRE) <= k) {
+                if (abort->load()) return;
+                std::this_thread::sleep_for(std::chrono::microseconds(50));
+            }
+            const SliceState ss{e->run_intra[k], e->pict_count + k, e->run_idr_id[k], e->p.qp};
             uint8_t* out = e->wout[w].data();
+            static const bool trace = getenv("HL_AMD_TRACE_WRITERS") != nullptr;
+            const auto tk = std::chrono::steady_clock::now();
             const size_t nb = write_slice(sp, ss, e->h_brec + (size_t)e->nmb * k, e->wscratch[w].data(), out, e->wout[w].size());
+            if (trace)
+                fprintf(stderr, "writer %d picture %d: start %.2f ms, write %.2f ms\n", w, k,
+                        std::chrono::duration<double, std::milli>(tk - e->run_t0).count(),
+                        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tk).count());
             size[k] = nb;
             if (nb) e->bout[base + k].assign(out + 3, out + nb);
         }
@@ -870,6 +918,7 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         pf.D.st = e->d_st;
         pf.pl_out = e->d_bpl + 4 * e->plsz * k;
         pf.deblock = e->p.deblock;
+        pf.hrec = e->dh_brec + nmb * k;
     }
     HL_HIP_CHECK(hipMemcpyAsync(e->d_pf, e->h_pf, sizeof(PipeFrame) * m, hipMemcpyHostToDevice, e->stream));
     PipeArgs P;
@@ -885,6 +934,17 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     P.tail = e->d_head + m;
     P.oldest = e->d_head + 2 * m;
     P.err = e->d_err;
+    int32_t* d_progress = nullptr;
+    HL_HIP_CHECK(hipHostGetDevicePointer((void**)&d_progress, e->h_progress, 0));
+    __atomic_store_n(e->h_progress, 0, __ATOMIC_RELEASE);
+    P.progress = d_progress;
+    static const bool trace = getenv("HL_AMD_TRACE_WRITERS") != nullptr;
+    static unsigned long long* h_clock = nullptr;
+    P.pub_clock = nullptr;
+    if (trace) {
+        if (!h_clock) HL_HIP_CHECK(hipHostMalloc((void**)&h_clock, sizeof(unsigned long long) * 1024, hipHostMallocCoherent));
+        HL_HIP_CHECK(hipHostGetDevicePointer((void**)&P.pub_clock, h_clock, 0));
+    }
     k_pipe_init<<<(unsigned)((nmb * m + 255) / 256), 256, 0, e->stream>>>(P, e->mbw, e->mbh);
     HL_HIP_CHECK(hipGetLastError());
     int wgs = e->pipe_wg;
@@ -896,24 +956,40 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         wgs = std::max(1, cus * occ);
     }
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[4], e->stream));
+    e->run_t0 = std::chrono::steady_clock::now();
     k_pipeline<<<wgs, kMbThreads, 0, e->stream>>>(P, e->mbw, e->mbh);
     HL_HIP_CHECK(hipGetLastError());
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[5], e->stream));
-    // The records, chain records and give-up counter come back stream-ordered
-    // after the run (the persistent kernel holds every CU, so copies issued
-    // while it runs could not start anyway); writer threads then serialise
-    // the pictures in parallel.
-    int32_t errw[2] = {0, 0};  // bounded waits that gave up, resolve_chain walks
+    // The kernel stores every finished MB's record into pinned host memory and
+    // counts finished pictures in a host-mapped word: writer threads serialise
+    // each picture's slice as soon as it is complete, while the run goes on.
+    // The chain records and the give-up counter come back after the run.
+    // bounded waits that gave up, resolve_chain walks: pinned, so that the
+    // copy is asynchronous (a copy into pageable memory blocks the host
+    // until the kernel ends, and with it the writers)
+    int32_t* errw = e->h_progress + 4;
     HL_HIP_CHECK(hipMemcpyAsync(e->h_bchain, e->d_bchain, sizeof(MbChain) * nmb * m, hipMemcpyDeviceToHost, e->stream));
-    HL_HIP_CHECK(hipMemcpyAsync(errw, e->d_err, sizeof(errw), hipMemcpyDeviceToHost, e->stream));
-    HL_HIP_CHECK(hipMemcpyAsync(e->h_brec, e->d_brec, sizeof(MbRecord) * nmb * m, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(errw, e->d_err, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[2], e->stream));
-    HL_HIP_CHECK(hipStreamSynchronize(e->stream));
+    std::atomic<bool> abort{false};
+    std::vector<size_t> wsize;
+    std::thread writers([&] { wsize = write_run(e, m, base, &abort); });
+    const hipError_t serr = hipStreamSynchronize(e->stream);
+    const auto tw0 = std::chrono::steady_clock::now();
+    if (serr != hipSuccess || __atomic_load_n(e->h_progress, __ATOMIC_ACQUIRE) < m) abort = true;
+    writers.join();
+    if (e->timing) e->ms[3] = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - tw0).count();
+    if (trace)
+        for (int k = 0; k < m; ++k) fprintf(stderr, "picture %d published at device clock +%.2f ms\n", k, (h_clock[k] - h_clock[0]) * 1e-5);
+    HL_HIP_CHECK(serr);
+    if (abort) {
+        fprintf(stderr, "hartallo_amd: pipelined run ended with %d of %d pictures published\n", __atomic_load_n(e->h_progress, __ATOMIC_ACQUIRE), m);
+        return HL_AMD_ERROR_SYSTEM;
+    }
     if (e->timing) {
         (void)hipEventElapsedTime(&e->ms[0], e->ev[0], e->ev[1]);
         (void)hipEventElapsedTime(&e->ms[1], e->ev[4], e->ev[5]);
         (void)hipEventElapsedTime(&e->ms[2], e->ev[5], e->ev[2]);
-        e->ms[3] = 0.f;
     }
     const int32_t err = errw[0];
     e->chain_walks = errw[1];
@@ -934,9 +1010,6 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         e->reruns = 1;
         return HL_AMD_SUCCESS;
     }
-    const auto tw0 = std::chrono::steady_clock::now();
-    const std::vector<size_t> wsize = write_run(e, m, base);
-    if (e->timing) e->ms[3] = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - tw0).count();
     for (int k = 0; k < m; ++k) {
         e->last_recs[base + k] = e->h_brec + nmb * k;
         e->last_chain[base + k] = e->h_bchain + nmb * k;
@@ -981,7 +1054,9 @@ extern "C" int32_t hl_amd_encode_batch(hl_amd_encoder_t* e, int32_t n, const uin
     e->last_pic.assign(n, nullptr);
     int i = 0;
     while (i < n) {
-        if (n - i == 1) {  // a lone picture takes the per-picture path
+        // a lone picture, and every picture under rate control (its QP needs
+        // the previous picture's bits), takes the per-picture path
+        if (n - i == 1 || e->rc) {
             hl_amd_result_t r;
             const int32_t rc = encode_frame(e, y[i], u[i], v[i], &r);
             if (rc) return rc;
@@ -1000,6 +1075,23 @@ extern "C" int32_t hl_amd_encode_batch(hl_amd_encoder_t* e, int32_t n, const uin
     }
     return HL_AMD_SUCCESS;
 }
+
+extern "C" int32_t hl_amd_set_rate_control(hl_amd_encoder_t* e, int64_t bitrate, int32_t fps_num, int32_t fps_den,
+                                           int32_t basicunit, int32_t qp_min, int32_t qp_max)
+{
+    if (!e) return HL_AMD_ERROR_INVALID_PARAMETER;
+    if (e->frame_index != 0) return HL_AMD_ERROR_INVALID_STATE;  // the model starts with the first GOP
+    if (bitrate <= 0) {
+        e->rc.reset();
+        return HL_AMD_SUCCESS;
+    }
+    if (fps_num <= 0 || fps_den <= 0 || fps_den / fps_num <= 0) return HL_AMD_ERROR_INVALID_PARAMETER;
+    e->rc_cfg = hl::RcConfig{bitrate, fps_num, fps_den, basicunit, qp_min, qp_max, e->p.gop_size, e->W, e->H};
+    e->rc.reset(new hl::RateControl(e->rc_cfg));
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_last_qp(hl_amd_encoder_t* e) { return e ? e->last_qp : -1; }
 
 extern "C" int32_t hl_amd_set_pipeline(hl_amd_encoder_t* e, int32_t workgroups, int32_t reach, int32_t window)
 {

@@ -67,7 +67,13 @@ constexpr int kMaxWaves = 8;   // waves of the macroblock workgroup
 #endif
 constexpr int kMbThreads = HL_MB_THREADS;
 constexpr int kMbRows = kMbThreads / 16;           // 16-lane rows
+// Candidates of one evaluation: a diamond step (<= 9 points), optionally
+// followed by the next stage's first step evaluated speculatively (<= 9 + 5
+// points, partitions of up to 8 blocks; see search_partition).
+constexpr int kMaxCand = 16;
+constexpr int kSpecMaxBlocks = 8;
 constexpr int kMaxPass = (9 * 16 + kMbRows - 1) / kMbRows;  // rows per lane for the largest step
+static_assert(14 * kSpecMaxBlocks <= kMaxPass * kMbRows, "a speculative step fits the pass budget");
 
 // One candidate of a step: plane offsets of its quarter-pel prediction
 // (second plane = first when the phase needs no average) and its MV.
@@ -141,9 +147,10 @@ struct Shared {
     int16_t cac[2][4][16];// live ChromaACLevel
     int32_t cbp_l, cbp_c; // live CodedBlockPattern{Luma,Chroma}
     // --- candidate step scratch
-    CandSlot wc[kMaxWaves][9];  // candidates of the step, one copy per wave (each wave writes its own)
-    int32_t be_nz[9][16], be_tc[9][16], be_t1[9][16], be_sctr[9][16], be_bits[9][16], be_dist[9][16];
-    int32_t be_w0[9][16], be_w1[9][16], be_w2[9][16];    // packed block statistics (device path)
+    CandSlot wc[kMaxWaves][kMaxCand];  // candidates of the step, one copy per wave (each wave writes its own)
+    int32_t be_nz[kMaxCand][16], be_tc[kMaxCand][16], be_t1[kMaxCand][16], be_sctr[kMaxCand][16], be_bits[kMaxCand][16],
+        be_dist[kMaxCand][16];
+    int32_t be_w0[kMaxCand][16], be_w1[kMaxCand][16], be_w2[kMaxCand][16];  // packed block statistics (device path)
     // Per-step results are double-buffered by step parity (Ctx::par): after a
     // step's last barrier, waves still read its results (the candidate scan,
     // the live TotalCoeffs update, the Single_ctr chain) while faster waves
@@ -154,8 +161,8 @@ struct Shared {
     CoopTables ct;
     uint32_t qtab[16];                                   // packed quarter-pel phase table
     struct CandRes {
-        double cost[9];
-        int32_t bits[9], dist[9], single[9], cbp[9], last[9];
+        double cost[kMaxCand];
+        int32_t bits[kMaxCand], dist[kMaxCand], single[kMaxCand], cbp[kMaxCand], last[kMaxCand];
     } cd[2];  // per candidate of a step [parity]
     // --- per (sub)partition search results
     double bcost[4][4];
@@ -189,6 +196,7 @@ struct Shared {
     int8_t i4mode[16], prev_flag[16], rem_mode[16];
     int16_t mvd[4][4][2];
     int8_t nc_luma[16], nc_cac[2][4], nc_dc;
+    int32_t mad;  // distortion of the chosen mode (rate control MAD, rdo.c:211-228, 1266-1268)
 };
 
 struct Ctx {
@@ -882,13 +890,6 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
     }
     if (g.nblk > 1) HL_SYNC();
     HL_PROF_ADD(c, 1, tp1);
-    HL_PROF_T(tp2);
-    // live TotalCoeffsLuma = last writer; the next reader is behind a barrier
-    if (c.tid < g.nblk) {
-        const int k = c.tid;
-        const int v = tcb_last(*reinterpret_cast<const uint4*>(tcb[k]), (1u << ncand) - 1u);
-        if (v >= 0) S.tc[blk_idx(g.px + ((k & (g.nbw - 1)) << 2), g.py + ((k >> g.lbw) << 2))] = (int8_t)v;
-    }
 #else
     HL_PROF_T(tp2);
     const int n = ncand * g.nblk;
@@ -954,7 +955,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         });
         S.be_bits[ci][k] += token_len(nC, S.be_tc[ci][k], S.be_t1[ci][k]);
     }
-    // phase 3: per-candidate sums; live TotalCoeffsLuma = last writer
+    // phase 3: per-candidate sums
     for (int t = 0; t < ncand; ++t) {
         int bits = 0, dist = 0, single = 0, cbp = 0, last = -1;
         for (int k = 0; k < g.nblk; ++k) {
@@ -974,49 +975,68 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         R.cbp[t] = cbp;
         R.last[t] = last;
     }
+#endif
+}
+
+// The live state left by the first n candidates of the last evaluation, in
+// order (the reference's sequence of trial CAVLC writes): TotalCoeffsLuma of
+// every block = its last writer (residual.c:796-806); rdo.Single_ctr = the
+// last candidate that wrote it (residual.c:881-897).  The next reader of
+// S.tc is behind a barrier.
+HD void commit_candidates(Ctx& c, const PartGeo& g, int n)
+{
+    Shared& S = c.S;
+    const Shared::CandRes& R = S.cd[c.par];
+    HL_PROF_T(tp2);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint8_t(&tcb)[16][16] = S.be_tcb[c.par];
+    if (c.tid < g.nblk) {
+        const int k = c.tid;
+        const int v = tcb_last(*reinterpret_cast<const uint4*>(tcb[k]), (1u << n) - 1u);
+        if (v >= 0) S.tc[blk_idx(g.px + ((k & (g.nbw - 1)) << 2), g.py + ((k >> g.lbw) << 2))] = (int8_t)v;
+    }
+    {  // last candidate that wrote the counter (vectorised over the step)
+        const int l = c.tid & 15;
+        const int v = l < n ? R.last[l] : -1;
+        const unsigned long long bal = __ballot(v >= 0) & 0xFFFFull;
+        if (bal) chain_write(c, __builtin_amdgcn_readlane(v, 63 - __clzll((long long)bal)));
+    }
+#else
     for (int k = 0; k < g.nblk; ++k) {
         const int hx = k % g.nbw, hy = k / g.nbw;
         const int bi = blk_idx(g.px + (hx << 2), g.py + (hy << 2));
-        for (int cj = ncand - 1; cj >= 0; --cj)
+        for (int cj = n - 1; cj >= 0; --cj)
             if (S.be_nz[cj][k]) {
                 S.tc[bi] = (int8_t)S.be_tc[cj][k];
                 break;
             }
     }
-#endif
-    HL_PROF_ADD(c, 2, tp2);
-#if defined(__HIP_DEVICE_COMPILE__)
-    {  // last candidate that wrote the counter (vectorised over the step)
-        const int l = c.tid & 15;
-        const int v = l < ncand ? R.last[l] : -1;
-        const unsigned long long bal = __ballot(v >= 0) & 0xFFFFull;
-        if (bal) chain_write(c, __builtin_amdgcn_readlane(v, 63 - __clzll((long long)bal)));
-    }
-#else
-    for (int ci = ncand - 1; ci >= 0; --ci)
+    for (int ci = n - 1; ci >= 0; --ci)
         if (R.last[ci] >= 0) {
             chain_write(c, R.last[ci]);
             break;
         }
 #endif
+    HL_PROF_ADD(c, 2, tp2);
 }
 
 // The sequential strict-< scan of one step's candidates (me_ds.c:339-347):
 // index of the first candidate with the smallest cost, and that cost.
-HD int pick_first_min(const Ctx& c, int ncand, double& m)
+HD int pick_first_min(const Ctx& c, int lo, int hi, double& m)  // candidates [lo, hi), hi > lo
 {
     const Shared& S = c.S;
 #if defined(__HIP_DEVICE_COMPILE__)
     const int l = c.tid & 15;
-    const double v = l < ncand ? S.cd[c.par].cost[l] : 1.7976931348623157e308;
+    const bool in = l >= lo && l < hi;
+    const double v = in ? S.cd[c.par].cost[l] : 1.7976931348623157e308;
     const double mn = row_min_f64(v);
-    const unsigned long long bal = __ballot(l < ncand && v == mn) & 0xFFFFull;
+    const unsigned long long bal = __ballot(in && v == mn) & 0xFFFFull;
     m = uni(mn);
     return uni(__ffsll((long long)bal) - 1);
 #else
-    int bi = 0;
-    m = S.cd[c.par].cost[0];
-    for (int ci = 1; ci < ncand; ++ci)
+    int bi = lo;
+    m = S.cd[c.par].cost[lo];
+    for (int ci = lo + 1; ci < hi; ++ci)
         if (S.cd[c.par].cost[ci] < m) {
             m = S.cd[c.par].cost[ci];
             bi = ci;
@@ -1131,6 +1151,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         if (pmv[0] == smv[0] && pmv[1] == smv[1]) {
             put_cand(c, g.px, g.py, 0, pmv[0], pmv[1], 0, (c.tid & 63) == 0);
             eval_candidates(c, g, 1, pmv);
+            commit_candidates(c, g, 1);
             if (uni(S.cd[c.par].bits[0]) == 0 || uni(S.cd[c.par].single[0]) < 6) {
                 probably = true;
                 b.cost = 0.0;
@@ -1147,9 +1168,10 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     put_cand(c, g.px, g.py, 0, pmv[0], pmv[1], 0, (c.tid & 63) == 0);
     put_cand(c, g.px, g.py, 1, 0, 0, 0, (c.tid & 63) == 0);
     eval_candidates(c, g, nc0, pmv);
+    commit_candidates(c, g, nc0);
     {
         double m;
-        const int bi = pick_first_min(c, nc0, m);
+        const int bi = pick_first_min(c, 0, nc0, m);
         if (m < b.cost) {
             b.cost = m;
             b.single = uni(S.cd[c.par].single[bi]);
@@ -1198,78 +1220,138 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         }
         return (int)((w >> (9 * k)) & 0x1FF);
     };
+    // Each step evaluates its diamond points (segment A).  A step that finds
+    // no better point ends its stage, and the next stage's first step is
+    // then fully determined (its centre follows from the unchanged best MV),
+    // so partitions of up to kSpecMaxBlocks blocks evaluate that step
+    // speculatively behind segment A in the same pass (segment B, <= 5 half
+    // or 9 quarter points).  Candidate order inside the pass is the
+    // reference's evaluation order, so every nC (quirk 1) and cost of B is
+    // exact when A fails; when A improves, B is dropped and only A's trial
+    // writes are committed to the live state.
     const int range = c.F.me_range;
+    const bool spec_ok = g.nblk <= kSpecMaxBlocks;
     int shift = 2, count = 9, flags = 0xFFFFFF;
     int cx = b.mv[0] >> 2, cy = b.mv[1] >> 2;
     int left = cx - range, right = cx + range, top = cy - range, bottom = cy + range;
-    for (;;) {
-        HL_PROF_T(tgap);
-        int ncand = 0;
-        const uint32_t pkx = shift == 2 ? pIntX : (shift == 1 ? pHalfX : pQuarX);
-        const uint32_t pky = shift == 2 ? pIntY : (shift == 1 ? pHalfY : pQuarY);
-#if defined(__HIP_DEVICE_COMPILE__)
-        {  // lane i of every wave checks diamond point i; enabled points are compacted in order
-            const int i = c.tid & 63, ii = min(i, 8);
-            const int mx = cx + (int)((pkx >> (3 * ii)) & 7) - 2, my = cy + (int)((pky >> (3 * ii)) & 7) - 2;
-            const bool en = i < count && ((flags >> i) & 1) && mx >= left && mx <= right && my >= top && my <= bottom;
-            const unsigned long long bal = __ballot(en);
-            ncand = __popcll(bal);
-            if (en) put_cand(c, g.px, g.py, __popcll(bal & ((1ull << i) - 1ull)), mx << shift, my << shift, i, true);
-        }
-#else
-        for (int i = 0; i < count; ++i) {
-            if (!(flags & (1 << i))) continue;
-            const int dx = (int)((pkx >> (3 * i)) & 7) - 2, dy = (int)((pky >> (3 * i)) & 7) - 2;
-            const int mx = cx + dx, my = cy + dy;
-            if (mx < left || mx > right || my < top || my > bottom) continue;
-            put_cand(c, g.px, g.py, ncand, mx << shift, my << shift, i, true);
-            ++ncand;
-        }
-#endif
-        int best = -1;
-        if (ncand) {
-            HL_PROF_ADD(c, 16, tgap);
-            eval_candidates(c, g, ncand, pmv);
-            HL_PROF_T(tsel);
-            double m;
-            const int bi = pick_first_min(c, ncand, m);
-            if (m < b.cost) {
-                best = uni(S.wc[c.tid >> 6][bi].pad);
-                b.cost = m;
-                b.single = uni(S.cd[c.par].single[bi]);
-                b.dist = uni(S.cd[c.par].dist[bi]);
-                b.cbp = uni(S.cd[c.par].cbp[bi]);
-                b.mv[0] = uni((int)S.wc[c.tid >> 6][bi].mvx);
-                b.mv[1] = uni((int)S.wc[c.tid >> 6][bi].mvy);
-            }
-            HL_PROF_ADD(c, 17, tsel);
-        }
+    auto next_stage = [&]() {  // me_ds.c:360-375: window re-centred, every point enabled
         flags = 0xFFFFFF;
-        if (shift == 2 && best == -1) {
+        if (shift == 2) {
             shift = 1;
             count = 5;
             cx = b.mv[0] >> 2;  // integer-pel value used as the half-pel centre (me_ds.c:360)
             cy = b.mv[1] >> 2;
         }
-        else if (shift == 1 && best == -1) {
+        else {
             shift = 0;
             count = 9;
             cx = b.mv[0];
             cy = b.mv[1];
         }
-        else if (shift == 0 && best == -1) {
-            break;
-        }
-        else {
-            cx = b.mv[0] >> shift;
-            cy = b.mv[1] >> shift;
-            flags &= mask_of(shift, best) | ~0x1FF;
-            continue;
-        }
         left = cx - range;
         right = cx + range;
         top = cy - range;
         bottom = cy + range;
+    };
+    auto take = [&](int bi, double m) {
+        b.cost = m;
+        b.single = uni(S.cd[c.par].single[bi]);
+        b.dist = uni(S.cd[c.par].dist[bi]);
+        b.cbp = uni(S.cd[c.par].cbp[bi]);
+        b.mv[0] = uni((int)S.wc[c.tid >> 6][bi].mvx);
+        b.mv[1] = uni((int)S.wc[c.tid >> 6][bi].mvy);
+        return uni(S.wc[c.tid >> 6][bi].pad);
+    };
+    for (;;) {
+        HL_PROF_T(tgap);
+        const bool spec = spec_ok && shift > 0;
+        // segment B: the next stage's first step as next_stage() would set it up
+        const int sB = shift - 1, cntB = spec ? (sB == 1 ? 5 : 9) : 0;
+        const int bx = sB == 1 ? b.mv[0] >> 2 : b.mv[0], by = sB == 1 ? b.mv[1] >> 2 : b.mv[1];
+        int nA = 0, nB = 0;
+        const uint32_t pkx = shift == 2 ? pIntX : (shift == 1 ? pHalfX : pQuarX);
+        const uint32_t pky = shift == 2 ? pIntY : (shift == 1 ? pHalfY : pQuarY);
+        const uint32_t pkxB = sB == 1 ? pHalfX : pQuarX, pkyB = sB == 1 ? pHalfY : pQuarY;
+#if defined(__HIP_DEVICE_COMPILE__)
+        {  // lane i < 9 of every wave checks point i of A, lane 16 + i point i of B;
+           // enabled points are compacted in that order
+            const int i = c.tid & 63, ia = min(i, 8), ib = min(max(i - 16, 0), 8);
+            bool en;
+            int mx, my, sh, pt;
+            if (i < 16) {
+                mx = cx + (int)((pkx >> (3 * ia)) & 7) - 2;
+                my = cy + (int)((pky >> (3 * ia)) & 7) - 2;
+                en = i < count && ((flags >> i) & 1) && mx >= left && mx <= right && my >= top && my <= bottom;
+                sh = shift;
+                pt = i;
+            }
+            else {
+                mx = bx + (int)((pkxB >> (3 * ib)) & 7) - 2;
+                my = by + (int)((pkyB >> (3 * ib)) & 7) - 2;
+                en = i - 16 < cntB && mx >= bx - range && mx <= bx + range && my >= by - range && my <= by + range;
+                sh = sB;
+                pt = i - 16;
+            }
+            const unsigned long long bal = __ballot(en);
+            nA = __popcll(bal & 0xFFFFull);
+            nB = __popcll(bal & 0xFFFF0000ull);
+            if (en) put_cand(c, g.px, g.py, __popcll(bal & ((1ull << i) - 1ull)), mx << sh, my << sh, pt, true);
+        }
+#else
+        for (int i = 0; i < count; ++i) {
+            if (!(flags & (1 << i))) continue;
+            const int mx = cx + (int)((pkx >> (3 * i)) & 7) - 2, my = cy + (int)((pky >> (3 * i)) & 7) - 2;
+            if (mx < left || mx > right || my < top || my > bottom) continue;
+            put_cand(c, g.px, g.py, nA++, mx << shift, my << shift, i, true);
+        }
+        for (int i = 0; i < cntB; ++i) {
+            const int mx = bx + (int)((pkxB >> (3 * i)) & 7) - 2, my = by + (int)((pkyB >> (3 * i)) & 7) - 2;
+            if (mx < bx - range || mx > bx + range || my < by - range || my > by + range) continue;
+            put_cand(c, g.px, g.py, nA + nB++, mx << sB, my << sB, i, true);
+        }
+#endif
+        if (nA + nB) {
+            HL_PROF_ADD(c, 16, tgap);
+            eval_candidates(c, g, nA + nB, pmv);
+        }
+        HL_PROF_T(tsel);
+        int best = -1;
+        if (nA) {
+            double m;
+            const int bi = pick_first_min(c, 0, nA, m);
+            if (m < b.cost) best = take(bi, m);
+        }
+        if (best >= 0) {  // A moved the centre: B is dropped, the stage goes on (window kept, me_ds.c:309)
+            commit_candidates(c, g, nA);
+            HL_PROF_ADD(c, 17, tsel);
+            cx = b.mv[0] >> shift;
+            cy = b.mv[1] >> shift;
+            flags = 0xFFFFFF & (mask_of(shift, best) | ~0x1FF);
+            continue;
+        }
+        if (shift == 0 || !spec) {  // no B: commit A, then the next stage (or the end)
+            if (nA) commit_candidates(c, g, nA);
+            HL_PROF_ADD(c, 17, tsel);
+            if (shift == 0) break;
+            next_stage();
+            continue;
+        }
+        next_stage();  // A found nothing: B is the new stage's first step, already evaluated
+        if (nB) {
+            double m;
+            const int bi = pick_first_min(c, nA, nA + nB, m);
+            if (m < b.cost) best = take(bi, m);
+        }
+        if (nA + nB) commit_candidates(c, g, nA + nB);
+        HL_PROF_ADD(c, 17, tsel);
+        if (best >= 0) {
+            cx = b.mv[0] >> shift;
+            cy = b.mv[1] >> shift;
+            flags = 0xFFFFFF & (mask_of(shift, best) | ~0x1FF);
+            continue;
+        }
+        if (shift == 0) break;
+        next_stage();
     }
     HL_SYNC();
     if (c.tid == 0) {
@@ -1693,8 +1775,9 @@ HD void resolve_chain(Ctx& c)
 #endif
 }
 
-HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp)
+HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp, int& best_dist)
 {
+    best_dist = 0;
     const FrameArgs& F = c.F;
     Shared& S = c.S;
     best_cost = 1.7976931348623157e308;
@@ -1801,6 +1884,7 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp)
         const double cost = dadd((double)dist, dmul(F.lambda, (double)rate));
         if (cost < best_cost) {
             best_cost = cost;
+            best_dist = dist;
             best_cbp = bcbp;
             if (c.tid == 0) S.i16mode = mode;
             if (c.tid < 16) S.i16_best_dc[c.tid] = bcbp ? S.i16_dcl[c.tid] : 0;
@@ -1943,6 +2027,7 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp)
         const double cost = dadd((double)dist, dmul(F.lambda, (double)rate));
         if (cost < best_cost) {
             best_cost = cost;
+            best_dist = dist;
             best_cbp = bcbp;
             if (c.tid == 0) {
                 S.i16mode = mode;
@@ -1961,8 +2046,9 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp)
 // --------------------------------------------------------------------------
 // Intra 4x4 RDO (rdo.c:1813-2098)
 // --------------------------------------------------------------------------
-HD void guess_i4(Ctx& c, double& best_cost, int& cbp4)
+HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
 {
+    best_dist = 0;
     const FrameArgs& F = c.F;
     Shared& S = c.S;
     best_cost = 0.0;
@@ -2047,6 +2133,7 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4)
             }
         }
         best_cost = dadd(best_cost, dmin);
+        best_dist += uni(S.i4_dist[best]);  // d_min_dist4x4 (rdo.c:2011, 2023); 0 for an exact mode
         if (!best_zero) cbp4 |= 1 << blk;
         if (c.tid < 16) {
             S.rec[(yO + (c.tid >> 2)) * 16 + xO + (c.tid & 3)] = S.i4_rec[best][c.tid];
@@ -2144,6 +2231,7 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4)
         }
         if (lastw >= 0) chain_write(c, S.i4_sctr[lastw]);
         best_cost = dadd(best_cost, dmin);
+        best_dist += S.i4_dist[best];
         if (!best_zero) cbp4 |= 1 << blk;
         for (int t = c.tid; t < 16; t += c.nthr) {
             S.rec[(yO + (t >> 2)) * 16 + xO + (t & 3)] = S.i4_rec[best][t];
@@ -2204,13 +2292,13 @@ HD double guess_intra(Ctx& c)
     const FrameArgs& F = c.F;
     Shared& S = c.S;
     double c16, c4;
-    int cbp16, cbp4 = 0;
+    int cbp16, cbp4 = 0, d16 = 0, d4 = 0;
     HL_PROF_T(t16);
-    guess_i16(c, c16, cbp16);
+    guess_i16(c, c16, cbp16, d16);
     HL_PROF_ADD(c, 10, t16);
     HL_PROF_T(t4);
     if (c16 == 0.0) c4 = 1.7976931348623157e308;
-    else guess_i4(c, c4, cbp4);
+    else guess_i4(c, c4, cbp4, d4);
     HL_PROF_ADD(c, 11, t4);
     HL_SYNC();
     const int i16mode = S.i16mode;
@@ -2235,6 +2323,7 @@ HD double guess_intra(Ctx& c)
     HL_SYNC();
     if (c.tid == 0) {
         S.chroma_mode = cmode;
+        S.mad = is_i16 ? d16 : d4;
         if (is_i16) {
             S.mb_type = 1;
             S.e_type = ET_I16;
@@ -2416,7 +2505,7 @@ HD void guess_inter(Ctx& c)
     auto fam_first = [](int f) -> int { return f < 4 ? f : 7; };  // {0, 1, 2, 3, 7}
     auto fam_type = [](int f) -> int32_t { return f < 3 ? ET_P16x16 + f : ET_P8x8REF0; };
     double best_cost = 1.7976931348623157e308;
-    int best_single = 9, best_part = -1, best_fam = -1;
+    int best_single = 9, best_part = -1, best_fam = -1, best_dist = 0;
     bool best_found = false, pskip = false;
     // b_probably_pskip is function-scoped in the reference (rdo.c:691): a mode
     // skipped by early termination leaves the last searched mode's value
@@ -2449,11 +2538,12 @@ HD void guess_inter(Ctx& c)
                 }
             probably = prob;
             double cost_sum = 0.0;
-            int single_sum = 0;
+            int single_sum = 0, dist_sum = 0;
             for (int pi = 0; pi < pd.num_part; ++pi)
                 for (int spi = 0; spi < pd.num_sub; ++spi) {
                     cost_sum = dadd(cost_sum, uni(S.bcost[pi][spi]));
                     single_sum += uni(S.bsingle[pi][spi]);
+                    dist_sum += uni(S.bdist[pi][spi]);
                 }
             if (!probably && cost_sum != 0.0 && single_sum < 6 && fam == 0) {
                 int smv[2];
@@ -2465,6 +2555,7 @@ HD void guess_inter(Ctx& c)
             if (cost_sum < best_cost) {
                 best_cost = cost_sum;
                 best_single = single_sum;
+                best_dist = dist_sum;
                 best_part = j;
                 best_fam = fam;
                 HL_SYNC();
@@ -2504,6 +2595,7 @@ HD void guess_inter(Ctx& c)
     const PartDef& bp = kParts[best_part];
     HL_SYNC();
     if (c.tid == 0) {
+        S.mad = best_dist;
         S.flags = FL_INTER;
         S.pm0 = PM_L0;
         S.e_type = fam_type(best_fam);
@@ -2708,6 +2800,7 @@ HD void mb_end(Ctx& c)
             R.cdc[i >> 2][i & 3] = (int16_t)S.cdc_level[i >> 2][i & 3];
         }
         R.nc_dc = S.nc_dc;
+        R.mad = S.mad;
         MbChain& ch = F.chain[c.addr];
         ch.s_out = c.chain;
         ch.dep = c.dep;

@@ -108,6 +108,7 @@ struct PipeFrame {
     DeblockArgs D;
     uint8_t* pl_out;  // this picture's quarter-pel planes (plane p at pl_out + p * F.plsz)
     int32_t deblock;  // deblocking enabled (disable_deblocking_filter_idc 0)
+    MbRecord* hrec;   // host-mapped copy of the picture's records (the slice writers read it during the run), or null
 };
 
 // Dependencies of task (f, x, y) inside a run: the wavefront neighbours
@@ -179,6 +180,8 @@ struct PipeArgs {
     int32_t* tail;   // [nframes] next queue slot to push
     int32_t* oldest; // [0] first unfinished picture of the run
     int32_t* err;    // [0] number of bounded waits that gave up
+    int32_t* progress;  // host-mapped: pictures whose records are all in host memory (system scope), or null
+    unsigned long long* pub_clock;  // diagnostics: device wall clock at each picture's publication, or null
 };
 
 }  // namespace hl

@@ -59,6 +59,8 @@ struct MbRecord {
     int16_t i16dc[16];
     int16_t cdc[2][4];
     int16_t cac[2][4][16];      // ChromaACLevel as written (15 used)
+    int32_t mad;                // distortion of the chosen mode (rate control, rdo.c:211-228, 1266-1268)
+    int32_t pad1;               // 1120 bytes: whole 16-byte words (the pipelined run copies records to the host)
 #if defined(HL_DIAG_INPUTS)
     uint32_t dbg[8];            // diagnostic builds: digests of the MB's inputs (hl_mbcore.h mb_begin)
 #endif

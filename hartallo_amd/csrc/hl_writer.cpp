@@ -262,7 +262,8 @@ size_t slice_scratch_bytes(const StreamParams& p)
     return (size_t)p.width * p.height * 3 / 2 + 4096 + (nmb << 8);
 }
 
-size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap)
+size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap,
+                   SliceBits* bits)
 {
     static const int16_t kZeros[16] = {0};
     const size_t scap = slice_scratch_bytes(p);
@@ -291,7 +292,7 @@ size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* r
         bw.u1(0);            // no_output_of_prior_pics_flag
         bw.u1(0);            // long_term_reference_flag
     }
-    bw.se(0);                // slice_qp_delta
+    bw.se(s.qp - p.qp);      // slice_qp_delta (encode.c:257, 274)
     bw.ue(p.deblock ? 0 : 1);
     if (p.deblock) {
         bw.se(0);
@@ -299,6 +300,7 @@ size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* r
     }
     // slice_data, mb.c:543-892
     int skip_run = 0;
+    int64_t texture = 0;
     for (int a = 0; a < nmb; ++a) {
         const MbRecord& m = recs[a];
         if (!s.idr) {
@@ -337,6 +339,7 @@ size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* r
         if (m.pm0 != PM_I16) bw.ue(kCbpCode[m.cbp][m.pm0 == PM_I4 ? 0 : 1]);
         if (m.cbp_l > 0 || m.cbp_c > 0 || m.pm0 == PM_I16) {
             bw.se(0);  // mb_qp_delta
+            const int64_t t0 = bw.bits();
             if (m.pm0 == PM_I16) write_block(bw, m.i16dc, 15, 16, m.nc_dc);
             for (int i8 = 0; i8 < 4; ++i8)
                 for (int i4 = 0; i4 < 4; ++i4)
@@ -350,7 +353,12 @@ size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* r
             for (int c = 0; c < 2; ++c)
                 for (int i4 = 0; i4 < 4; ++i4)
                     if (m.cbp_c & 2) write_block(bw, (m.cbp_cac[c] & (1 << i4)) ? m.cac[c][i4] : kZeros, 14, 15, m.nc_cac[c][i4]);
+            texture += bw.bits() - t0;
         }
+    }
+    if (bits) {
+        bits->texture_bits = (int32_t)texture;
+        bits->header_bits = (int32_t)(bw.bits() - texture);
     }
     bw.trailing();
     size_t n = bw.bytes();

@@ -44,6 +44,14 @@ size_t write_stream_headers(const StreamParams& p, uint8_t* out, size_t cap);
 
 struct SliceState {
     int32_t idr, frame_num, idr_pic_id;
+    int32_t qp;  // SliceQPY (rate control may move it off the PPS value; slice_qp_delta = qp - p.qp)
+};
+
+// Bit counts of a written slice as the reference's rate control takes them
+// (slice.c:994-995, mb.c:580-886): header = slice header (NAL header byte
+// included) + every macroblock's header syntax, texture = residual().
+struct SliceBits {
+    int32_t header_bits, texture_bits;
 };
 
 // Writes "00 00 01" + one escaped slice NAL for the frame's MB records.
@@ -56,6 +64,7 @@ size_t slice_scratch_bytes(const StreamParams& p);
 // writer serialises with; the GPU bit counter (hl_prims.h level_code_len)
 // must agree with it for every (suffixLength, levelCode).
 int level_code_bits(int suffix_length, int level_code);
-size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap);
+size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap,
+                   SliceBits* bits = nullptr);
 
 }  // namespace hl

@@ -67,7 +67,13 @@ class hl_codec_t:  # noqa: N801
     gop_size: int = 25
     me_range: int = 16
     deblock_flag: int = 1
-    me_early_term_flag: int = 1  # reference default (hl_types.h:67); the GPU path needs 0
+    me_early_term_flag: int = 1  # reference default (hl_types.h:67)
+    fps_num: int = 1             # fps (hl_codec.c:37-38): 1/15
+    fps_den: int = 15
+    rc_bitrate: int = -1         # rate control when > 0 (hl_types.h:59-64 defaults)
+    rc_basicunit: int = -1
+    rc_qp_min: int = -1
+    rc_qp_max: int = -1
     threads_count: int = 1
     max_ref_frame: int = 1
     device: int = 0
@@ -129,6 +135,9 @@ def hl_codec_encode(codec: hl_codec_t, frame: hl_frame_video_t, result: hl_codec
         try:
             codec._enc = Encoder(frame.width, frame.height, codec.qp, codec.me_range, codec.deblock_flag, codec.gop_size,
                                  codec.me_early_term_flag, codec.device)
+            if codec.rc_bitrate > 0:  # hl_codec_264.c:719-742
+                codec._enc.set_rate_control(codec.rc_bitrate, codec.fps_num, codec.fps_den, codec.rc_basicunit, codec.rc_qp_min,
+                                            codec.rc_qp_max)
         except HlAmdError as e:
             return e.code
         codec.width, codec.height = frame.width, frame.height

@@ -100,6 +100,18 @@ int32_t hl_amd_encode_device(hl_amd_encoder_t* encoder, const uint8_t* y, const 
 int32_t hl_amd_encode_batch(hl_amd_encoder_t* encoder, int32_t n, const uint8_t* const* y, const uint8_t* const* u,
                             const uint8_t* const* v, hl_amd_result_t* results);
 
+/* rate control (hl_codec_t.rc_bitrate > 0; hl_codec_264.c:719-742, 1018-1031,
+ * model hl_codec_264_rc.c): bitrate in bits/s, frame rate fps_den / fps_num
+ * (hl_codec_t.fps, integer quotient), rc_basicunit (<= 0: the picture),
+ * rc_qp_min / rc_qp_max (-1: 0 / 51).  Call before the first frame;
+ * bitrate <= 0 turns it off.  Each picture's QP then follows the previous
+ * pictures' bits, so hl_amd_encode_batch codes the pictures one by one. */
+int32_t hl_amd_set_rate_control(hl_amd_encoder_t* encoder, int64_t bitrate, int32_t fps_num, int32_t fps_den,
+                                int32_t basicunit, int32_t qp_min, int32_t qp_max);
+
+/* SliceQPY of the last encoded picture (the rate-controlled QP), or -1 */
+int32_t hl_amd_last_qp(hl_amd_encoder_t* encoder);
+
 /* pipelined-run scheduling: persistent workgroups (0 = one per resident
  * workgroup slot of the device, <= 4096), the reference reach R in MBs
  * (0..16) that a macroblock task of picture f+1 waits for in picture f

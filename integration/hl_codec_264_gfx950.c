@@ -73,6 +73,11 @@ static HL_ERROR_T gfx950_encode(hl_codec_t* base, const hl_frame_t* frame, hl_co
         p.me_early_term = base->me_early_term_flag;
         p.device = 0; /* one process per GPU (HIP_VISIBLE_DEVICES) */
         if ((err = hl_amd_encoder_create(&p, &self->enc))) return (HL_ERROR_T)err; /* HL_ERROR_T values (hl_types.h:101-122) */
+        /* rate control: the hl_codec_t fields hl_codec_264.c:719-742 reads */
+        if (base->rc_bitrate > 0 &&
+            (err = hl_amd_set_rate_control(self->enc, base->rc_bitrate, base->fps.num, base->fps.den, base->rc_basicunit,
+                                           base->rc_qp_min, base->rc_qp_max)))
+            return (HL_ERROR_T)err;
         self->width = f->data_width[0];
         self->height = f->data_height[0];
     }

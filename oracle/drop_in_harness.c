@@ -49,6 +49,11 @@ int main(int argc, char** argv)
     c->rc_bitrate = -1; c->deblock_flag = db; c->threads_count = 1; c->max_ref_frame = 1;
     c->distortion_mesure_type = HL_VIDEO_DISTORTION_MESURE_TYPE_SAD;
     if (et >= 0) c->me_early_term_flag = et;
+    /* rate control set on the hl_codec_t as a hartallo caller would */
+    if (getenv("HL_REF_RC_BITRATE")) c->rc_bitrate = atoi(getenv("HL_REF_RC_BITRATE"));
+    if (getenv("HL_REF_RC_BASICUNIT")) c->rc_basicunit = atoi(getenv("HL_REF_RC_BASICUNIT"));
+    if (getenv("HL_REF_RC_QP_MIN")) c->rc_qp_min = atoi(getenv("HL_REF_RC_QP_MIN"));
+    if (getenv("HL_REF_RC_QP_MAX")) c->rc_qp_max = atoi(getenv("HL_REF_RC_QP_MAX"));
     size_t fs = (size_t)W * H * 3 / 2;
     uint8_t* buf = (uint8_t*)malloc(fs);
     FILE* fi = fopen(argv[9], "rb");

@@ -15,6 +15,8 @@
  * output ends (one decimal number per line).
  *
  * usage: ref_enc W H N qp me_range deblock gop early_term in.yuv out_prefix [quiet|rec]
+ * rate control (rc_bitrate > 0, hl_codec_264.c:719-742) from the environment:
+ *   HL_REF_RC_BITRATE, HL_REF_RC_BASICUNIT, HL_REF_RC_QP_MIN, HL_REF_RC_QP_MAX
  *   quiet: no .rec.yuv / .mbs dumps (timing runs); rec: .rec.yuv but no .mbs
  */
 #include <hartallo/hl_api.h>
@@ -117,6 +119,11 @@ int main(int argc, char** argv)
     c->me_part_types = HL_VIDEO_ME_PART_TYPE_ALL;
     c->me_subpart_types = HL_VIDEO_ME_SUBPART_TYPE_ALL;
     c->me_early_term_flag = et;
+    /* rate control (hl_codec_264.c:719-742): HL_REF_RC_BITRATE=<bits/s> turns it on */
+    if (getenv("HL_REF_RC_BITRATE")) c->rc_bitrate = atoi(getenv("HL_REF_RC_BITRATE"));
+    if (getenv("HL_REF_RC_BASICUNIT")) c->rc_basicunit = atoi(getenv("HL_REF_RC_BASICUNIT"));
+    if (getenv("HL_REF_RC_QP_MIN")) c->rc_qp_min = atoi(getenv("HL_REF_RC_QP_MIN"));
+    if (getenv("HL_REF_RC_QP_MAX")) c->rc_qp_max = atoi(getenv("HL_REF_RC_QP_MAX"));
 
     size_t fs = (size_t)W * H * 3 / 2;
     uint8_t* buf = (uint8_t*)malloc(fs);

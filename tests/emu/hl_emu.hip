@@ -5,12 +5,15 @@
 // oracle without a GPU.  The product library never links this file; it
 // fails loudly without a GPU instead of falling back to it.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <memory>
 #include <vector>
 
 #include "../../hartallo_amd/csrc/hl_pipeline.h"
+#include "../../hartallo_amd/csrc/hl_rc.h"
 #include "../../hartallo_amd/csrc/hl_writer.h"
 
 using namespace hl;
@@ -27,6 +30,8 @@ struct EmuEnc {
     std::vector<uint8_t> scratch, out, hdr;
     int cur, frame_index, gop_left, pict_count, idr_pic_id, chain_end;
     Shared* S;
+    std::unique_ptr<RateControl> rc;  // rate control (hl_rc.h), as in the product
+    int last_qp;
 };
 
 extern "C" void* emu_create(int W, int H, int qp, int me_range, int deblock, int gop, int early_term)
@@ -73,11 +78,28 @@ extern "C" void emu_destroy(void* h)
 }
 
 // Writes hdr (first frame) + 00 00 01 + slice into out; returns bytes or -1.
+// rate control of the product path (hl_amd_set_rate_control)
+extern "C" int emu_set_rc(void* h, long long bitrate, int fps_num, int fps_den, int basicunit, int qp_min, int qp_max)
+{
+    EmuEnc* e = (EmuEnc*)h;
+    if (bitrate <= 0) {
+        e->rc.reset();
+        return 0;
+    }
+    if (fps_num <= 0 || fps_den / fps_num <= 0) return 1;
+    e->rc.reset(new RateControl(RcConfig{bitrate, fps_num, fps_den, basicunit, qp_min, qp_max, e->gop, e->W, e->H}));
+    return 0;
+}
+
+extern "C" int emu_last_qp(void* h) { return ((EmuEnc*)h)->last_qp; }
+
 extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, const uint8_t* v, uint8_t* out, long cap)
 {
     EmuEnc* e = (EmuEnc*)h;
     const bool intra = e->gop_left <= 0;
     if (intra) e->gop_left = e->gop;
+    const int qp = e->rc ? e->rc->begin_picture(intra) : e->qp;
+    const int qpc = kQpToQpc[qp];
     auto& cur = e->pic[e->cur];
     auto& ref = e->pic[e->cur ^ 1];
     if (!intra)
@@ -92,12 +114,12 @@ extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, co
     F.Hc = e->Hc;
     F.mbw = e->mbw;
     F.mbh = e->mbh;
-    F.qp = e->qp;
-    F.qpc = e->qpc;
+    F.qp = qp;
+    F.qpc = qpc;
     F.is_intra = intra;
     F.me_range = e->me_range;
     F.early_term = e->early_term;
-    F.lambda = 0.852 * (double)(1 << ((e->qp - 12) / 3));
+    F.lambda = 0.852 * (double)(1 << ((qp - 12) / 3));
     F.src[0] = y;
     F.src[1] = u;
     F.src[2] = v;
@@ -139,8 +161,8 @@ extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, co
         D.H = e->H;
         D.Wc = e->Wc;
         D.mbw = e->mbw;
-        D.qp = e->qp;
-        D.qpc = e->qpc;
+        D.qp = qp;
+        D.qpc = qpc;
         for (int c = 0; c < 3; ++c) D.pic[c] = cur[c].data();
         D.st = e->st.data();
         for (int a = 0; a < e->nmb; ++a)
@@ -148,15 +170,28 @@ extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, co
                 for (int lane = 0; lane < 32; ++lane) deblock_mb_step(D, a, step, lane);
     }
     const StreamParams sp{e->W, e->H, e->qp, e->deblock};
-    const SliceState ss{intra ? 1 : 0, e->pict_count, e->idr_pic_id};
+    const SliceState ss{intra ? 1 : 0, e->pict_count, e->idr_pic_id, qp};
     size_t n = 0;
     if (e->frame_index == 0) {
         if ((long)e->hdr.size() > cap) return -1;
         memcpy(out, e->hdr.data(), e->hdr.size());
         n = e->hdr.size();
     }
-    const size_t m = write_slice(sp, ss, e->rec.data(), e->scratch.data(), out + n, (size_t)cap - n);
+    SliceBits sb{};
+    const size_t m = write_slice(sp, ss, e->rec.data(), e->scratch.data(), out + n, (size_t)cap - n, &sb);
     if (!m) return -1;
+    if (e->rc) {
+        RcPictureStats st{};
+        for (int a = 0; a < e->nmb; ++a) st.mad_sum += e->rec[a].mad;
+        st.header_bits = sb.header_bits;
+        st.texture_bits = sb.texture_bits;
+        st.nbits = (int32_t)((m - 3) * 8);
+        e->rc->end_picture(intra, st, e->gop_left - 1 <= 0);
+        if (getenv("HL_EMU_RC_DEBUG"))
+            fprintf(stderr, "%d qp %d hdr %d tex %d mad %lld nbytes %d\n", e->frame_index, qp, st.header_bits, st.texture_bits,
+                    (long long)st.mad_sum, st.nbits / 8);
+    }
+    e->last_qp = qp;
     n += m;
     e->cur ^= 1;
     ++e->pict_count;

@@ -22,7 +22,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 
 import numpy as np  # noqa: E402
 
-from hl_testlib import GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, REF_ENC, golden_input, md5  # noqa: E402
+from hl_testlib import GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, GOLDEN_RC_CONFIGS, REF_ENC, golden_input, md5, slice_qps  # noqa: E402
 
 
 def main():
@@ -30,15 +30,21 @@ def main():
         sys.exit(f"{REF_ENC} missing: run `make -C oracle ref` where /root/reference exists")
     table = {}
     with tempfile.TemporaryDirectory() as td:
-        for cfg in GOLDEN_CONFIGS + GOLDEN_ET_CONFIGS:
-            name, w, h, n, qp, mer, db, gop, seed = cfg
+        for cfg in GOLDEN_CONFIGS + GOLDEN_ET_CONFIGS + GOLDEN_RC_CONFIGS:
+            name, w, h, n, qp, mer, db, gop, seed = cfg[:9]
             et = 1 if cfg in GOLDEN_ET_CONFIGS else 0
+            env = dict(os.environ)
+            for k in ("HL_REF_RC_BITRATE", "HL_REF_RC_BASICUNIT", "HL_REF_RC_QP_MIN", "HL_REF_RC_QP_MAX"):
+                env.pop(k, None)
+            if cfg in GOLDEN_RC_CONFIGS:  # rate control: bitrate, basic unit, QP range (ref_harness.c)
+                env.update(HL_REF_RC_BITRATE=str(cfg[9]), HL_REF_RC_BASICUNIT=str(cfg[10]), HL_REF_RC_QP_MIN=str(cfg[11]),
+                           HL_REF_RC_QP_MAX=str(cfg[12]))
             clip = golden_input(cfg)
             inp = os.path.join(td, name + ".yuv")
             clip.tofile(inp)
             pre = os.path.join(td, name)
             subprocess.run([REF_ENC, str(w), str(h), str(n), str(qp), str(mer), str(db), str(gop), str(et), inp, pre, "rec"],
-                           check=True, stdout=subprocess.DEVNULL)
+                           check=True, stdout=subprocess.DEVNULL, env=env)
             stream = open(pre + ".264", "rb").read()
             rec = np.fromfile(pre + ".rec.yuv", dtype=np.uint8).reshape(n, -1)
             with open(os.path.join(HERE, name + ".264"), "wb") as f:
@@ -46,7 +52,9 @@ def main():
             table[name] = {
                 "width": w, "height": h, "frames": n, "qp": qp, "me_range": mer, "deblock": db, "gop": gop, "seed": seed,
                 "early_term": et,
-                "stream_md5": md5(stream), "stream_bytes": len(stream),
+                **({"rc_bitrate": cfg[9], "rc_basicunit": cfg[10], "rc_qp_min": cfg[11], "rc_qp_max": cfg[12],
+                    "fps_num": 1, "fps_den": 15} if cfg in GOLDEN_RC_CONFIGS else {}),
+                "stream_md5": md5(stream), "stream_bytes": len(stream), "slice_qp": slice_qps(stream, qp),
                 "recon_md5": [md5(r) for r in rec],
             }
             print(f"{name}: {len(stream)} bytes")

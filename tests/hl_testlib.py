@@ -60,6 +60,8 @@ def emu_lib():
         lib.emu_encode_frame.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_long]
         lib.emu_recon.restype = ctypes.c_void_p
         lib.emu_recon.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        lib.emu_set_rc.argtypes = [ctypes.c_void_p, ctypes.c_longlong] + [ctypes.c_int] * 5
+        lib.emu_last_qp.argtypes = [ctypes.c_void_p]
         _emu = lib
     return _emu
 
@@ -117,6 +119,12 @@ class EmuEncoder:
         self.h_ = self.lib.emu_create(w, h, qp, me_range, deblock, gop, early_term)
         self.out = np.zeros(w * h * 4 + (1 << 20), np.uint8)
 
+    def set_rate_control(self, bitrate, fps_num=1, fps_den=15, basicunit=-1, qp_min=-1, qp_max=-1):
+        assert self.lib.emu_set_rc(ctypes.c_void_p(self.h_), bitrate, fps_num, fps_den, basicunit, qp_min, qp_max) == 0
+
+    def last_qp(self) -> int:
+        return self.lib.emu_last_qp(ctypes.c_void_p(self.h_))
+
     def encode(self, frame: np.ndarray) -> bytes:
         y, u, v = _planes(frame, self.w, self.h)
         n = self.lib.emu_encode_frame(ctypes.c_void_p(self.h_), y.ctypes.data, u.ctypes.data, v.ctypes.data, self.out.ctypes.data,
@@ -147,6 +155,12 @@ class GpuEncoder:
 
     def recon(self) -> np.ndarray:
         return np.concatenate(self.enc.recon())
+
+    def set_rate_control(self, *a, **k):
+        self.enc.set_rate_control(*a, **k)
+
+    def last_qp(self) -> int:
+        return self.enc.last_qp()
 
 
 def significant_records(r: np.ndarray) -> np.ndarray:
@@ -254,6 +268,58 @@ GOLDEN_ET_CONFIGS = [
 ]
 
 
+# Rate-control goldens (hl_codec_t.rc_bitrate > 0, hl_codec_264.c:719-742):
+# (name, W, H, frames, qp, me_range, deblock, gop, seed, bitrate, basicunit,
+# qp_min, qp_max), fps 1/15 as test_encoder.c sets it.  Several GOPs each, so
+# the model's GOP-to-GOP QP carry (rc.c:844-882) is exercised; bu11 runs the
+# basic-unit bookkeeping.
+GOLDEN_RC_CONFIGS = [
+    ("rc_qcif_100k_gop5", 176, 144, 16, 28, 8, 1, 5, 51, 100000, -1, -1, -1),
+    ("rc_qcif_30k_gop6", 176, 144, 14, 28, 8, 1, 6, 52, 30000, -1, -1, -1),
+    ("rc_qcif_bu11_gop6", 176, 144, 13, 28, 8, 1, 6, 53, 100000, 11, -1, -1),
+    ("rc_cif_200k_gop4_nodb", 352, 288, 9, 28, 8, 0, 4, 54, 200000, -1, -1, -1),
+    ("rc_qcif_1m5_gop6", 176, 144, 13, 28, 16, 1, 6, 55, 1500000, -1, -1, -1),
+    ("rc_qcif_60k_qp20_36", 176, 144, 12, 28, 8, 1, 5, 56, 60000, -1, 20, 36),
+]
+
+
+def slice_qps(stream: bytes, pic_init_qp: int) -> list:
+    """SliceQPY of every slice NAL of an Annex-B stream (slice_qp_delta of the
+    Baseline slice header this encoder writes, slice.c:660-900)."""
+    out, i = [], 0
+    while True:
+        j = stream.find(b"\x00\x00\x01", i)
+        if j < 0:
+            return out
+        i = j + 3
+        t = stream[i] & 31
+        if t not in (1, 5):
+            continue
+        bits = "".join(f"{b:08b}" for b in stream[i + 1:i + 24])
+        pos = [0]
+
+        def u(n):
+            v = int(bits[pos[0]:pos[0] + n], 2)
+            pos[0] += n
+            return v
+
+        def ue():
+            z = 0
+            while bits[pos[0]] == "0":
+                z += 1
+                pos[0] += 1
+            pos[0] += 1
+            return (1 << z) - 1 + (u(z) if z else 0)
+
+        ue(), ue(), ue(), u(8)          # first_mb, slice_type, pps id, frame_num
+        if t == 5:
+            ue(), u(1), u(1)            # idr_pic_id, dec_ref_pic_marking
+        else:
+            u(1), ue(), u(1), u(1)      # override, num_ref_idx, modification, marking
+        k = ue()
+        out.append(pic_init_qp + ((k + 1) // 2 if k & 1 else -(k // 2)))
+
+
 def golden_input(cfg) -> np.ndarray:
-    _, w, h, n, _, _, _, _, seed = cfg
+    _, w, h, n, _, _, _, _, seed = cfg[:9]
     return synth.clip(w, h, n, seed)

@@ -18,7 +18,7 @@ import tempfile
 
 import pytest
 
-from hl_testlib import GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, ROOT, first_diff, golden_input
+from hl_testlib import GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, GOLDEN_RC_CONFIGS, ROOT, first_diff, golden_input
 
 DROP_IN = os.path.join(ROOT, "oracle", "_ref", "drop_in_enc")
 PLUGIN = os.path.join(ROOT, "integration", "hl_codec_264_gfx950.c")
@@ -45,7 +45,8 @@ def test_drop_in_driver_is_built():
         assert s in syms, s
 
 
-CASES = [c for c in GOLDEN_CONFIGS if c[0] in ("cif_ippp_qp31_me8", "qcif_gop3_qp20_me4", "w480_h272_qp28_me16")] + GOLDEN_ET_CONFIGS[:3]
+CASES = ([c for c in GOLDEN_CONFIGS if c[0] in ("cif_ippp_qp31_me8", "qcif_gop3_qp20_me4", "w480_h272_qp28_me16")] + GOLDEN_ET_CONFIGS[:3] +
+         [c for c in GOLDEN_RC_CONFIGS if c[0] in ("rc_qcif_100k_gop5", "rc_qcif_bu11_gop6", "rc_qcif_60k_qp20_36")])
 
 
 @pytest.mark.gpu
@@ -53,13 +54,17 @@ CASES = [c for c in GOLDEN_CONFIGS if c[0] in ("cif_ippp_qp31_me8", "qcif_gop3_q
 def test_drop_in_through_hl_codec_encode(gpu, cfg):
     if not os.path.exists(DROP_IN):
         pytest.fail("oracle/_ref/drop_in_enc missing (built in the build container by make -C oracle ref)")
-    name, w, h, n, qp, mer, db, gop, seed = cfg
+    name, w, h, n, qp, mer, db, gop, seed = cfg[:9]
     et = -1 if GOLD[name].get("early_term", 0) else 0  # -1: leave the hl_codec_create default (1)
+    env = dict(os.environ)
+    if cfg in GOLDEN_RC_CONFIGS:  # rc_bitrate etc. on the hl_codec_t (oracle/drop_in_harness.c)
+        env.update(HL_REF_RC_BITRATE=str(cfg[9]), HL_REF_RC_BASICUNIT=str(cfg[10]), HL_REF_RC_QP_MIN=str(cfg[11]),
+                   HL_REF_RC_QP_MAX=str(cfg[12]))
     with tempfile.TemporaryDirectory() as td:
         inp, out = os.path.join(td, "in.yuv"), os.path.join(td, "out.264")
         golden_input(cfg).tofile(inp)
         r = subprocess.run([DROP_IN, str(w), str(h), str(n), str(qp), str(mer), str(db), str(gop), str(et), inp, out],
-                           capture_output=True, text=True, timeout=240)
+                           capture_output=True, text=True, timeout=240, env=env)
         assert r.returncode == 0, r.stderr
         got = open(out, "rb").read()
     ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()

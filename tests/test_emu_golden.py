@@ -9,7 +9,8 @@ import os
 
 import pytest
 
-from hl_testlib import EMU_LIB, GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, EmuEncoder, OracleEncoder, first_diff, golden_input, md5
+from hl_testlib import (EMU_LIB, GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, GOLDEN_RC_CONFIGS, EmuEncoder, OracleEncoder, first_diff,
+                        golden_input, md5)
 from hartallo_amd import synth
 
 GOLD = json.load(open(os.path.join(GOLDEN, "golden.json")))
@@ -28,6 +29,25 @@ def test_kernel_logic_matches_reference(cfg):
     for f in range(n):
         out += enc.encode(clip[f])
         assert md5(enc.recon()) == GOLD[name]["recon_md5"][f], f"{name}: recon of frame {f}"
+    assert out == ref, f"{name}: first differing byte {first_diff(out, ref)}"
+
+
+@pytest.mark.parametrize("cfg", GOLDEN_RC_CONFIGS, ids=[c[0] for c in GOLDEN_RC_CONFIGS])
+def test_rate_control_matches_reference(cfg):
+    """The product's rate control (hartallo_amd/csrc/hl_rc.cpp) driving the
+    kernel logic reproduces the reference's rate-controlled streams: every
+    picture's QP (hl_codec_264_rc.c model), stream and recon."""
+    name, w, h, n, qp, mer, db, gop, seed, br, bu, qmin, qmax = cfg
+    clip = golden_input(cfg)
+    ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()
+    g = GOLD[name]
+    enc = EmuEncoder(w, h, qp, mer, db, gop)
+    enc.set_rate_control(br, g["fps_num"], g["fps_den"], bu, qmin, qmax)
+    out = b""
+    for f in range(n):
+        out += enc.encode(clip[f])
+        assert enc.last_qp() == g["slice_qp"][f], f"{name}: QP of frame {f}"
+        assert md5(enc.recon()) == g["recon_md5"][f], f"{name}: recon of frame {f}"
     assert out == ref, f"{name}: first differing byte {first_diff(out, ref)}"
 
 

@@ -16,7 +16,7 @@ import os
 import numpy as np
 import pytest
 
-from hl_testlib import GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, GpuEncoder, OracleEncoder, first_diff, golden_input, md5
+from hl_testlib import GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, GOLDEN_RC_CONFIGS, GpuEncoder, OracleEncoder, first_diff, golden_input, md5
 
 pytestmark = pytest.mark.gpu
 
@@ -37,6 +37,45 @@ def test_golden_streams(gpu, cfg):
         out += enc.encode(clip[f])
         assert md5(enc.recon()) == GOLD[name]["recon_md5"][f], f"{name}: recon of frame {f} differs"
     assert out == ref, f"{name}: first differing byte {first_diff(out, ref)}"
+
+
+@pytest.mark.parametrize("cfg", GOLDEN_RC_CONFIGS, ids=[c[0] for c in GOLDEN_RC_CONFIGS])
+def test_rate_control_golden_streams(gpu, cfg):
+    """rc_bitrate > 0 (hl_codec_264.c:719-742): per-picture QPs from the rate
+    controller, streams and recon identical to the reference's."""
+    name, w, h, n, qp, mer, db, gop, seed, br, bu, qmin, qmax = cfg
+    clip = golden_input(cfg)
+    ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()
+    g = GOLD[name]
+    enc = GpuEncoder(w, h, qp, mer, db, gop)
+    enc.set_rate_control(br, g["fps_num"], g["fps_den"], bu, qmin, qmax)
+    out = b""
+    for f in range(n):
+        out += enc.encode(clip[f])
+        assert enc.last_qp() == g["slice_qp"][f], f"{name}: QP of frame {f}"
+        assert md5(enc.recon()) == g["recon_md5"][f], f"{name}: recon of frame {f} differs"
+    assert out == ref, f"{name}: first differing byte {first_diff(out, ref)}"
+
+
+def test_rate_control_batch_equals_calls(gpu):
+    """Under rate control hl_amd_encode_batch codes picture by picture and
+    returns the same stream as one call per frame."""
+    import torch
+
+    from hartallo_amd import Encoder
+
+    cfg = GOLDEN_RC_CONFIGS[0]
+    name, w, h, n, qp, mer, db, gop, seed, br, bu, qmin, qmax = cfg
+    clip = golden_input(cfg)
+    ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()
+    dev = torch.from_numpy(clip).cuda()
+    ny = w * h
+    ptrs = [(dev[i].data_ptr(), dev[i].data_ptr() + ny, dev[i].data_ptr() + ny + ny // 4) for i in range(n)]
+    enc = Encoder(w, h, qp, mer, db, gop)
+    enc.set_rate_control(br, 1, 15, bu, qmin, qmax)
+    out = b"".join(r.annexb() for r in enc.encode_batch_device(ptrs))
+    enc.close()
+    assert out == ref, f"first differing byte {first_diff(out, ref)}"
 
 
 def _vs_oracle(w, h, n, qp, mer, db, gop, seed):

@@ -35,6 +35,8 @@ def child(lib):
     ptrs = [(dev[i].data_ptr(), dev[i].data_ptr() + ny, dev[i].data_ptr() + ny + ny // 4) for i in range(150)]
     for warm, steps in ((5, 20), (30, 120)):
         enc = Encoder(W, H, 28, 16, 1, 30)
+        if os.environ.get("HL_AB_GEOM"):  # "workgroups,reach,window" (hl_amd_set_pipeline)
+            enc.set_pipeline(*[int(v) for v in os.environ["HL_AB_GEOM"].split(",")])
         enc.set_timing(True)
         outs = [r.annexb() for r in enc.encode_batch_device(ptrs[:warm])]
         torch.cuda.synchronize()
@@ -47,7 +49,7 @@ def child(lib):
         outs += [r.annexb() for r in enc.last_batch_results()]
         exact = all(hashlib.md5(o).hexdigest() == m for o, m in zip(outs, g["frame_md5"]))
         enc.close()
-        print(f"{os.path.relpath(lib, ROOT)} warmup {warm} steps {steps}: {steps / dt:.2f} fps ({dt * 1e3:.1f} ms, kernel {kernel_ms:.1f} ms, "
+        print(f"{os.path.relpath(lib, ROOT)} geom {os.environ.get('HL_AB_GEOM', 'default')} warmup {warm} steps {steps}: {steps / dt:.2f} fps ({dt * 1e3:.1f} ms, kernel {kernel_ms:.1f} ms, "
               f"records copy {tm[2]:.1f} ms, slice writing {tm[3]:.1f} ms) "
               f"bitexact {exact}", flush=True)
 
