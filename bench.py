@@ -34,7 +34,10 @@ QP, ME_RANGE, DEBLOCK, GOP = 28, 16, 1, 30
 BYTES_PER_MB = 2752  # compulsory HBM bytes per macroblock, DESIGN.md / SURVEY §8(d)
 # HBM traffic of k_pipeline per macroblock, from rocprofv3 FETCH_SIZE / WRITE_SIZE
 # passes on this workload (tools/pmc_traffic.sh, corrected per MI355X_MICROARCH.md)
-PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_traffic_k_pipeline.json")
+# (kept under tools/pmc/, which travels to the GPU box; copies in profiles/)
+PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "pmc", "r02_pmc_traffic_k_pipeline.json")
+# SQ issue / wait counters of the same kernel (tools/pmc_sq.sh): what bounds it
+PMC_SQ = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "pmc", "r02_pmc_sq_k_pipeline.txt")
 MAX_RUN = 128  # pictures per pipelined launch (kMaxRun, hl_encoder.hip)
 # The synthetic stream is always generated for BENCH_CLIP_FRAMES frames (its
 # texture depends on the clip length) and its first warmup + steps frames are
@@ -167,6 +170,12 @@ def main():
         traffic = None
         if mb_launches == 1 and os.path.exists(PMC_TRAFFIC):
             traffic = round(json.load(open(PMC_TRAFFIC))["traffic_bytes_per_mb"] * nmb * run_frames)
+        sq = {}
+        if os.path.exists(PMC_SQ):
+            for ln in open(PMC_SQ):
+                f = ln.split()
+                if len(f) == 2 and f[0].startswith("SQ_"):
+                    sq[f[0]] = float(f[1])
         line = {
             "metric": "1080p encoded frames/sec (bit-exact) at 1/2/4/8 MI355X; macroblocks/sec/GPU",
             "value": round(fps, 4),
@@ -191,7 +200,11 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_pipeline", "avg_launch_us": round(avg_launch_s * 1e6, 2),
                          "frames_per_launch": run_frames,
-                         "note": "latency-bound MB wavefront, frames pipelined; achieved = 2752 B/MB x MBs per launch / launch time"},
+                         "note": "latency-bound MB wavefront, frames pipelined; achieved = 2752 B/MB x MBs per launch / launch time",
+                         # what bounds it instead (rocprofv3 SQ counters, tools/pmc/r02_pmc_sq_k_pipeline.txt)
+                         "sq_wait_frac": round(sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"], 3) if sq else None,
+                         "sq_issue_frac": round(sq["SQ_ACTIVE_INST_ANY"] / sq["SQ_WAVE_CYCLES"], 3) if sq else None,
+                         "valu_insts_per_mb": round(sq["SQ_INSTS_VALU"] / (12 * nmb)) if sq else None},
             "cpu_baseline": base,
         }
         print(json.dumps(line), flush=True)
