@@ -67,13 +67,13 @@ constexpr int kMaxWaves = 8;   // waves of the macroblock workgroup
 #endif
 constexpr int kMbThreads = HL_MB_THREADS;
 constexpr int kMbRows = kMbThreads / 16;           // 16-lane rows
-// Candidates of one evaluation: a diamond step (<= 9 points), optionally
-// followed by the next stage's first step evaluated speculatively (<= 9 + 5
-// points, partitions of up to 8 blocks; see search_partition).
-constexpr int kMaxCand = 16;
+// Candidates of one evaluation pass: a chain of up to four search steps
+// (MVP/(0,0), then the first integer, half and quarter steps), the later ones
+// speculative (see search_partition); at most kMaxPass rows per lane.
+constexpr int kMaxCand = 32;
+constexpr int kMaxSeg = 4;
 constexpr int kSpecMaxBlocks = 8;
 constexpr int kMaxPass = (9 * 16 + kMbRows - 1) / kMbRows;  // rows per lane for the largest step
-static_assert(14 * kSpecMaxBlocks <= kMaxPass * kMbRows, "a speculative step fits the pass budget");
 
 // One candidate of a step: plane offsets of its quarter-pel prediction
 // (second plane = first when the phase needs no average) and its MV.
@@ -156,7 +156,7 @@ struct Shared {
     // the live TotalCoeffs update, the Single_ctr chain) while faster waves
     // already write the next step's -- a step only reuses the buffer of the
     // step before the previous one, whose readers all passed a barrier since.
-    alignas(16) uint8_t be_tcb[2][16][16];               // TotalCoeff [parity][block][candidate]
+    alignas(16) uint8_t be_tcb[2][16][kMaxCand];         // TotalCoeff [parity][block][candidate]
     alignas(16) int32_t lvs[kMaxWaves * 4][16];          // per-row level scratch of coop_cavlc
     CoopTables ct;
     uint32_t qtab[16];                                   // packed quarter-pel phase table
@@ -699,15 +699,20 @@ __device__ __forceinline__ uint32_t nz_bytes(uint32_t w)
     const uint32_t t = ((w | ((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu)) >> 7) & 0x01010101u;
     return (t * 0x01020408u) >> 24;
 }
-// Last candidate (bit set in `allow`) whose TotalCoeff in the block row r is
-// non-zero: returns its TotalCoeff, or -1.
-__device__ __forceinline__ int tcb_last(const uint4& r, uint32_t allow)
+// Last candidate (bit set in `allow`) whose TotalCoeff in the block row
+// (32 candidates, two 16-byte words) is non-zero: its TotalCoeff, or -1.
+__device__ __forceinline__ int tcb_last(const uint8_t* row, uint32_t allow)
 {
-    const uint32_t m = (nz_bytes(r.x) | (nz_bytes(r.y) << 4) | (nz_bytes(r.z) << 8) | (nz_bytes(r.w) << 12)) & allow;
+    const uint4 a = *reinterpret_cast<const uint4*>(row), b = *reinterpret_cast<const uint4*>(row + 16);
+    const uint32_t m = (nz_bytes(a.x) | (nz_bytes(a.y) << 4) | (nz_bytes(a.z) << 8) | (nz_bytes(a.w) << 12) | (nz_bytes(b.x) << 16) |
+                        (nz_bytes(b.y) << 20) | (nz_bytes(b.z) << 24) | (nz_bytes(b.w) << 28)) &
+                       allow;
     if (!m) return -1;
     const int j = 31 - __clz(m);
-    const uint32_t w = j < 4 ? r.x : (j < 8 ? r.y : (j < 12 ? r.z : r.w));
-    return (int)((w >> ((j & 3) * 8)) & 0xFF);
+    const uint4 q = j < 16 ? a : b;
+    const int jj = j & 15;
+    const uint32_t w = jj < 4 ? q.x : (jj < 8 ? q.y : (jj < 12 ? q.z : q.w));
+    return (int)((w >> ((jj & 3) * 8)) & 0xFF);
 }
 #endif
 
@@ -726,7 +731,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
     Shared& S = c.S;
     c.par ^= 1;
     Shared::CandRes& R = S.cd[c.par];
-    uint8_t(&tcb)[16][16] = S.be_tcb[c.par];
+    uint8_t(&tcb)[16][kMaxCand] = S.be_tcb[c.par];
     HL_PROF_T(tp0);
 #if defined(__HIP_DEVICE_COMPILE__)
     // phase 1: one 16-lane row per (candidate, 4x4 block); every row of the
@@ -841,14 +846,14 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         const int kkA = inA ? ((hy << g.lbw) + hx - 1) : 0, kkB = inB ? (((hy - 1) << g.lbw) + hx) : 0;
         const int w0 = S.be_w0[ci][k], w1 = S.be_w1[ci][k], w2 = S.be_w2[ci][k];
         const int eA = S.extA[bi], eB = S.extB[bi], cbp = S.cbp_l, tA = S.tc[niA], tB = S.tc[niB];
-        const uint4 rA = *reinterpret_cast<const uint4*>(tcb[kkA]), rB = *reinterpret_cast<const uint4*>(tcb[kkB]);
+        const uint8_t *rA = tcb[kkA], *rB = tcb[kkB];
         const CandSlot cs = S.wc[wave][ci];
         int bits = 0, dist = 0, cs_sum = 0, last = 0;
         const int tc = w0 & 31;
         if (valid) {
             dist = w1 >> 16;
             if (tc) {
-                const uint32_t allow = (2u << ci) - 1u;  // candidates 0..ci
+                const uint32_t allow = ci == 31 ? ~0u : (2u << ci) - 1u;  // candidates 0..ci
                 int nA = 0, nB = 0;
                 bool aA = true, aB = true;
                 if (bx == 0) {
@@ -989,16 +994,16 @@ HD void commit_candidates(Ctx& c, const PartGeo& g, int n)
     const Shared::CandRes& R = S.cd[c.par];
     HL_PROF_T(tp2);
 #if defined(__HIP_DEVICE_COMPILE__)
-    const uint8_t(&tcb)[16][16] = S.be_tcb[c.par];
+    const uint8_t(&tcb)[16][kMaxCand] = S.be_tcb[c.par];
     if (c.tid < g.nblk) {
         const int k = c.tid;
-        const int v = tcb_last(*reinterpret_cast<const uint4*>(tcb[k]), (1u << n) - 1u);
+        const int v = tcb_last(tcb[k], n >= 32 ? ~0u : (1u << n) - 1u);
         if (v >= 0) S.tc[blk_idx(g.px + ((k & (g.nbw - 1)) << 2), g.py + ((k >> g.lbw) << 2))] = (int8_t)v;
     }
-    {  // last candidate that wrote the counter (vectorised over the step)
-        const int l = c.tid & 15;
+    {  // last candidate that wrote the counter (vectorised over the pass)
+        const int l = c.tid & 31;
         const int v = l < n ? R.last[l] : -1;
-        const unsigned long long bal = __ballot(v >= 0) & 0xFFFFull;
+        const unsigned long long bal = __ballot(v >= 0) & 0xFFFFFFFFull;
         if (bal) chain_write(c, __builtin_amdgcn_readlane(v, 63 - __clzll((long long)bal)));
     }
 #else
@@ -1026,11 +1031,12 @@ HD int pick_first_min(const Ctx& c, int lo, int hi, double& m)  // candidates [l
 {
     const Shared& S = c.S;
 #if defined(__HIP_DEVICE_COMPILE__)
-    const int l = c.tid & 15;
+    const int l = c.tid & 31;
     const bool in = l >= lo && l < hi;
     const double v = in ? S.cd[c.par].cost[l] : 1.7976931348623157e308;
-    const double mn = row_min_f64(v);
-    const unsigned long long bal = __ballot(in && v == mn) & 0xFFFFull;
+    double mn = row_min_f64(v);
+    mn = fmin(mn, __shfl_xor(mn, 16, 64));  // both 16-lane rows of the half-wave
+    const unsigned long long bal = __ballot(in && v == mn) & 0xFFFFFFFFull;
     m = uni(mn);
     return uni(__ffsll((long long)bal) - 1);
 #else
@@ -1163,24 +1169,20 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
             }
         }
     }
-    // MVP and (0,0) candidates, me_ds.c:280-300
-    const int nc0 = (pmv[0] != 0 || pmv[1] != 0) ? 2 : 1;
-    put_cand(c, g.px, g.py, 0, pmv[0], pmv[1], 0, (c.tid & 63) == 0);
-    put_cand(c, g.px, g.py, 1, 0, 0, 0, (c.tid & 63) == 0);
-    eval_candidates(c, g, nc0, pmv);
-    commit_candidates(c, g, nc0);
-    {
-        double m;
-        const int bi = pick_first_min(c, 0, nc0, m);
-        if (m < b.cost) {
-            b.cost = m;
-            b.single = uni(S.cd[c.par].single[bi]);
-            b.dist = uni(S.cd[c.par].dist[bi]);
-            b.cbp = uni(S.cd[c.par].cbp[bi]);
-            b.mv[0] = bi ? 0 : pmv[0];
-            b.mv[1] = bi ? 0 : pmv[1];
-        }
-    }
+    // The search is a sequence of steps (me_ds.c:280-470): the MVP and (0,0)
+    // candidates (stage 3), then diamond steps of the integer (2), half (1)
+    // and quarter (0) stages.  A step that finds no better point ends its
+    // stage, and the next stage's first step is then fully determined by the
+    // unchanged best MV; after the MVP/(0,0) step the next step is known
+    // once its winner is (the MVP is predicted).  One evaluation pass
+    // therefore holds a chain of up to kMaxSeg steps -- the current one and
+    // the speculative continuations that fit the pass (at most kMaxCand
+    // candidates, kMaxPass rows per lane) -- in the reference's evaluation
+    // order, so every nC (quirk 1) and cost in the chain is exact for as long
+    // as the speculation holds.  The chain is resolved step by step; at the
+    // first step whose outcome differs from the prediction the rest is
+    // dropped, and only the candidates of the resolved steps are committed
+    // to the live state.
     // diamond stages, me_ds.c:302-470.  The point offsets and visited-point
     // masks are packed into immediates (3-bit offsets + 2, 9-bit masks).
     // integer: {0,2},{-1,1},{1,1},{-2,0},{0,0},{2,0},{-1,-1},{1,-1},{0,-2}
@@ -1220,39 +1222,10 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         }
         return (int)((w >> (9 * k)) & 0x1FF);
     };
-    // Each step evaluates its diamond points (segment A).  A step that finds
-    // no better point ends its stage, and the next stage's first step is
-    // then fully determined (its centre follows from the unchanged best MV),
-    // so partitions of up to kSpecMaxBlocks blocks evaluate that step
-    // speculatively behind segment A in the same pass (segment B, <= 5 half
-    // or 9 quarter points).  Candidate order inside the pass is the
-    // reference's evaluation order, so every nC (quirk 1) and cost of B is
-    // exact when A fails; when A improves, B is dropped and only A's trial
-    // writes are committed to the live state.
     const int range = c.F.me_range;
-    const bool spec_ok = g.nblk <= kSpecMaxBlocks;
-    int shift = 2, count = 9, flags = 0xFFFFFF;
-    int cx = b.mv[0] >> 2, cy = b.mv[1] >> 2;
-    int left = cx - range, right = cx + range, top = cy - range, bottom = cy + range;
-    auto next_stage = [&]() {  // me_ds.c:360-375: window re-centred, every point enabled
-        flags = 0xFFFFFF;
-        if (shift == 2) {
-            shift = 1;
-            count = 5;
-            cx = b.mv[0] >> 2;  // integer-pel value used as the half-pel centre (me_ds.c:360)
-            cy = b.mv[1] >> 2;
-        }
-        else {
-            shift = 0;
-            count = 9;
-            cx = b.mv[0];
-            cy = b.mv[1];
-        }
-        left = cx - range;
-        right = cx + range;
-        top = cy - range;
-        bottom = cy + range;
-    };
+    const int budget = g.nblk <= kSpecMaxBlocks ? min(kMaxCand, (kMaxPass * kMbRows) >> g.lnb) : 0;  // 0: one step per pass
+    const int nc0 = (pmv[0] != 0 || pmv[1] != 0) ? 2 : 1;
+    int stage = 3, flags = 0x1FF, cx = 0, cy = 0, left = 0, right = 0, top = 0, bottom = 0;
     auto take = [&](int bi, double m) {
         b.cost = m;
         b.single = uni(S.cd[c.par].single[bi]);
@@ -1262,96 +1235,133 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         b.mv[1] = uni((int)S.wc[c.tid >> 6][bi].mvy);
         return uni(S.wc[c.tid >> 6][bi].pad);
     };
-    for (;;) {
+    // first step of stage st from best MV (mx, my): window re-centred, every
+    // point enabled; the half stage starts at the integer MV value read as
+    // half-pel (me_ds.c:360)
+    auto centre_of = [](int st, int m) { return st == 0 ? m : m >> 2; };
+    while (stage >= 0) {
         HL_PROF_T(tgap);
-        const bool spec = spec_ok && shift > 0;
-        // segment B: the next stage's first step as next_stage() would set it up
-        const int sB = shift - 1, cntB = spec ? (sB == 1 ? 5 : 9) : 0;
-        const int bx = sB == 1 ? b.mv[0] >> 2 : b.mv[0], by = sB == 1 ? b.mv[1] >> 2 : b.mv[1];
-        int nA = 0, nB = 0;
-        const uint32_t pkx = shift == 2 ? pIntX : (shift == 1 ? pHalfX : pQuarX);
-        const uint32_t pky = shift == 2 ? pIntY : (shift == 1 ? pHalfY : pQuarY);
-        const uint32_t pkxB = sB == 1 ? pHalfX : pQuarX, pkyB = sB == 1 ? pHalfY : pQuarY;
+        // the chain: step 0 = the current step, then fresh stages from the
+        // predicted best MV (pmv after the MVP/(0,0) step, else unchanged)
+        const int pmx = stage == 3 ? pmv[0] : b.mv[0], pmy = stage == 3 ? pmv[1] : b.mv[1];
+        int nseg = 1, room = budget - (stage == 3 ? 2 : 9);
+        while (nseg < kMaxSeg && stage - nseg >= 0 && room >= (stage - nseg == 1 ? 5 : 9)) {
+            room -= stage - nseg == 1 ? 5 : 9;
+            ++nseg;
+        }
+        int lo[kMaxSeg] = {0, 0, 0, 0}, n[kMaxSeg] = {0, 0, 0, 0};
 #if defined(__HIP_DEVICE_COMPILE__)
-        {  // lane i < 9 of every wave checks point i of A, lane 16 + i point i of B;
-           // enabled points are compacted in that order
-            const int i = c.tid & 63, ia = min(i, 8), ib = min(max(i - 16, 0), 8);
-            bool en;
-            int mx, my, sh, pt;
-            if (i < 16) {
-                mx = cx + (int)((pkx >> (3 * ia)) & 7) - 2;
-                my = cy + (int)((pky >> (3 * ia)) & 7) - 2;
-                en = i < count && ((flags >> i) & 1) && mx >= left && mx <= right && my >= top && my <= bottom;
-                sh = shift;
-                pt = i;
-            }
-            else {
-                mx = bx + (int)((pkxB >> (3 * ib)) & 7) - 2;
-                my = by + (int)((pkyB >> (3 * ib)) & 7) - 2;
-                en = i - 16 < cntB && mx >= bx - range && mx <= bx + range && my >= by - range && my <= by + range;
-                sh = sB;
-                pt = i - 16;
+        {  // lane 16 j + i of every wave checks point i of step j; enabled points are compacted in order
+            const int i = c.tid & 63, j = i >> 4, pt = min(i & 15, 8);
+            const int st = stage - j;  // step j's stage (3 = MVP/(0,0))
+            bool en = false;
+            int mx = 0, my = 0, sh = 0;
+            if (j < nseg) {
+                if (st == 3) {
+                    en = (i & 15) < nc0;
+                    mx = (i & 15) ? 0 : pmv[0];
+                    my = (i & 15) ? 0 : pmv[1];
+                }
+                else {
+                    const uint32_t pkx = st == 2 ? pIntX : (st == 1 ? pHalfX : pQuarX);
+                    const uint32_t pky = st == 2 ? pIntY : (st == 1 ? pHalfY : pQuarY);
+                    const bool fresh = j > 0 || stage == 3;
+                    const int ccx = fresh ? centre_of(st, pmx) : cx, ccy = fresh ? centre_of(st, pmy) : cy;
+                    const int l0 = fresh ? ccx - range : left, r0 = fresh ? ccx + range : right;
+                    const int t0 = fresh ? ccy - range : top, b0 = fresh ? ccy + range : bottom;
+                    const int fl = fresh ? 0x1FF : flags;
+                    mx = ccx + (int)((pkx >> (3 * pt)) & 7) - 2;
+                    my = ccy + (int)((pky >> (3 * pt)) & 7) - 2;
+                    sh = st == 2 ? 2 : (st == 1 ? 1 : 0);
+                    en = (i & 15) < (st == 1 ? 5 : 9) && ((fl >> (i & 15)) & 1) && mx >= l0 && mx <= r0 && my >= t0 && my <= b0;
+                }
             }
             const unsigned long long bal = __ballot(en);
-            nA = __popcll(bal & 0xFFFFull);
-            nB = __popcll(bal & 0xFFFF0000ull);
-            if (en) put_cand(c, g.px, g.py, __popcll(bal & ((1ull << i) - 1ull)), mx << sh, my << sh, pt, true);
+            for (int k = 0; k < kMaxSeg; ++k) {
+                lo[k] = __popcll(bal & ((1ull << (16 * k)) - 1ull));
+                n[k] = __popcll(bal & (0xFFFFull << (16 * k)));
+            }
+            if (en) put_cand(c, g.px, g.py, __popcll(bal & ((1ull << i) - 1ull)), mx << sh, my << sh, i & 15, true);
         }
 #else
-        for (int i = 0; i < count; ++i) {
-            if (!(flags & (1 << i))) continue;
-            const int mx = cx + (int)((pkx >> (3 * i)) & 7) - 2, my = cy + (int)((pky >> (3 * i)) & 7) - 2;
-            if (mx < left || mx > right || my < top || my > bottom) continue;
-            put_cand(c, g.px, g.py, nA++, mx << shift, my << shift, i, true);
-        }
-        for (int i = 0; i < cntB; ++i) {
-            const int mx = bx + (int)((pkxB >> (3 * i)) & 7) - 2, my = by + (int)((pkyB >> (3 * i)) & 7) - 2;
-            if (mx < bx - range || mx > bx + range || my < by - range || my > by + range) continue;
-            put_cand(c, g.px, g.py, nA + nB++, mx << sB, my << sB, i, true);
+        {
+            int tot = 0;
+            for (int j = 0; j < nseg; ++j) {
+                const int st = stage - j;
+                lo[j] = tot;
+                if (st == 3) {
+                    put_cand(c, g.px, g.py, tot++, pmv[0], pmv[1], 0, true);
+                    if (nc0 == 2) put_cand(c, g.px, g.py, tot++, 0, 0, 1, true);
+                }
+                else {
+                    const uint32_t pkx = st == 2 ? pIntX : (st == 1 ? pHalfX : pQuarX);
+                    const uint32_t pky = st == 2 ? pIntY : (st == 1 ? pHalfY : pQuarY);
+                    const bool fresh = j > 0 || stage == 3;
+                    const int ccx = fresh ? centre_of(st, pmx) : cx, ccy = fresh ? centre_of(st, pmy) : cy;
+                    const int l0 = fresh ? ccx - range : left, r0 = fresh ? ccx + range : right;
+                    const int t0 = fresh ? ccy - range : top, b0 = fresh ? ccy + range : bottom;
+                    const int fl = fresh ? 0x1FF : flags;
+                    const int sh = st == 2 ? 2 : (st == 1 ? 1 : 0);
+                    for (int pt = 0; pt < (st == 1 ? 5 : 9); ++pt) {
+                        if (!((fl >> pt) & 1)) continue;
+                        const int mx = ccx + (int)((pkx >> (3 * pt)) & 7) - 2, my = ccy + (int)((pky >> (3 * pt)) & 7) - 2;
+                        if (mx < l0 || mx > r0 || my < t0 || my > b0) continue;
+                        put_cand(c, g.px, g.py, tot++, mx << sh, my << sh, pt, true);
+                    }
+                }
+                n[j] = tot - lo[j];
+            }
         }
 #endif
-        if (nA + nB) {
+        const int total = lo[nseg - 1] + n[nseg - 1];
+        if (total) {
             HL_PROF_ADD(c, 16, tgap);
-            eval_candidates(c, g, nA + nB, pmv);
+            eval_candidates(c, g, total, pmv);
         }
         HL_PROF_T(tsel);
-        int best = -1;
-        if (nA) {
-            double m;
-            const int bi = pick_first_min(c, 0, nA, m);
-            if (m < b.cost) best = take(bi, m);
+        // resolve the chain step by step
+        int used = 0;
+        for (int j = 0; j < nseg; ++j) {
+            used = lo[j] + n[j];
+            if (stage == 3) {  // MVP / (0,0) (me_ds.c:280-300)
+                double m;
+                const int bi = pick_first_min(c, lo[j], lo[j] + n[j], m);
+                if (m < b.cost) take(bi, m);
+                stage = 2;
+                cx = centre_of(2, b.mv[0]);
+                cy = centre_of(2, b.mv[1]);
+                flags = 0x1FF;
+                left = cx - range;
+                right = cx + range;
+                top = cy - range;
+                bottom = cy + range;
+                if (b.mv[0] != pmv[0] || b.mv[1] != pmv[1]) break;  // the continuation assumed the MVP
+                continue;
+            }
+            int best = -1;
+            if (n[j]) {
+                double m;
+                const int bi = pick_first_min(c, lo[j], lo[j] + n[j], m);
+                if (m < b.cost) best = take(bi, m);
+            }
+            if (best >= 0) {  // moved: the stage goes on from the new centre (window kept, me_ds.c:309)
+                cx = b.mv[0] >> (stage == 2 ? 2 : (stage == 1 ? 1 : 0));
+                cy = b.mv[1] >> (stage == 2 ? 2 : (stage == 1 ? 1 : 0));
+                flags = mask_of(stage == 2 ? 2 : (stage == 1 ? 1 : 0), best);  // points the move already visited
+                break;
+            }
+            --stage;  // no better point: the next stage (the chain's next step)
+            if (stage < 0) break;
+            cx = centre_of(stage, b.mv[0]);
+            cy = centre_of(stage, b.mv[1]);
+            flags = 0x1FF;
+            left = cx - range;
+            right = cx + range;
+            top = cy - range;
+            bottom = cy + range;
         }
-        if (best >= 0) {  // A moved the centre: B is dropped, the stage goes on (window kept, me_ds.c:309)
-            commit_candidates(c, g, nA);
-            HL_PROF_ADD(c, 17, tsel);
-            cx = b.mv[0] >> shift;
-            cy = b.mv[1] >> shift;
-            flags = 0xFFFFFF & (mask_of(shift, best) | ~0x1FF);
-            continue;
-        }
-        if (shift == 0 || !spec) {  // no B: commit A, then the next stage (or the end)
-            if (nA) commit_candidates(c, g, nA);
-            HL_PROF_ADD(c, 17, tsel);
-            if (shift == 0) break;
-            next_stage();
-            continue;
-        }
-        next_stage();  // A found nothing: B is the new stage's first step, already evaluated
-        if (nB) {
-            double m;
-            const int bi = pick_first_min(c, nA, nA + nB, m);
-            if (m < b.cost) best = take(bi, m);
-        }
-        if (nA + nB) commit_candidates(c, g, nA + nB);
+        if (used) commit_candidates(c, g, used);
         HL_PROF_ADD(c, 17, tsel);
-        if (best >= 0) {
-            cx = b.mv[0] >> shift;
-            cy = b.mv[1] >> shift;
-            flags = 0xFFFFFF & (mask_of(shift, best) | ~0x1FF);
-            continue;
-        }
-        if (shift == 0) break;
-        next_stage();
     }
     HL_SYNC();
     if (c.tid == 0) {
