@@ -312,8 +312,11 @@ __global__ __launch_bounds__(kMbThreads, 2) void k_pipeline(PipeArgs P, int mbw,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid < 64) {
+#if HL_HOSTREC_SYS
             if (P.progress) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // host-visible records (system scope)
-            else __builtin_amdgcn_fence(__ATOMIC_RELEASE, HL_REL_SCOPE);
+            else
+#endif
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, HL_REL_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (tid == 0) st_relaxed(P.done + t, 1);
             int fo = 0, xo = 0, yo = 0;
@@ -321,7 +324,7 @@ __global__ __launch_bounds__(kMbThreads, 2) void k_pipeline(PipeArgs P, int mbw,
             for (int j = tid; j < ns; j += 64) {
                 task_succ(f, x, y, mbw, mbh, P.reach, P.nframes, j, fo, xo, yo);
                 const int a = yo * mbw + xo;
-                if (__hip_atomic_fetch_add(P.cnt + fo * nmb + a, -1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+                if (__hip_atomic_fetch_add(P.cnt + fo * nmb + a, -1, HL_CNT_ORDER, __HIP_MEMORY_SCOPE_AGENT) == 1) {
                     const int pos = __hip_atomic_fetch_add(P.tail + fo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(P.queue + fo * nmb + pos, a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                 }

@@ -393,6 +393,14 @@ typedef __attribute__((address_space(1))) int32_t gi32;
 #ifndef HL_ACQ_SCOPE
 #define HL_ACQ_SCOPE "agent"
 #endif
+// memory order of the successor-counter decrements of a pipelined task
+#ifndef HL_CNT_ORDER
+#define HL_CNT_ORDER __ATOMIC_ACQ_REL
+#endif
+// 1: tasks that copy their records to host memory release at system scope
+#ifndef HL_HOSTREC_SYS
+#define HL_HOSTREC_SYS 1
+#endif
 #ifndef HL_REL_SCOPE
 #define HL_REL_SCOPE "agent"
 #endif
