@@ -176,12 +176,15 @@ struct Shared {
     int32_t i16_called[16], i16_tc[16], i16_t1[16], i16_sctr[16], i16_bits[16], i16_dist[16];
     int16_t i16_best_ac[16][16], i16_best_dc[16];
     uint8_t i16_best_rec[256], tmp_rec[256];
-    int32_t i4_cost_ok[9], i4_exact[9], i4_nz[9], i4_tc[9], i4_sctr[9], i4_dist[9];
-    double i4_cost[9];
-    int16_t i4_lv[9][16];
-    uint8_t i4_rec[9][16];
+    // I4x4 trials of up to two blocks at once [wavefront slot][mode] (device) / [0][mode] (host)
+    int32_t i4_cost_ok[2][9], i4_exact[2][9], i4_nz[2][9], i4_tc[2][9], i4_sctr[2][9], i4_dist[2][9];
+    double i4_cost[2][9];
+    int16_t i4_lv[2][9][16];
+    uint8_t i4_rec[2][9][16];
+    double i4r_dmin[16];       // per block, in z-order accumulation after the wavefront
+    int32_t i4r_dist[16], i4r_sct[16], i4r_zero[16];
     int32_t luma_level[16][16];
-    int16_t i4nb[16];            // neighbours of the current 4x4 block (p[13] layout)
+    int16_t i4nb[2][16];         // neighbours of the current 4x4 blocks (p[13] layout)
     int32_t dcY[16];             // I16x16: scaled DC per DC-matrix position
     int16_t i16_dcl[16];         // I16x16: DC levels of the current mode (scan order)
     int32_t dcrow[4];            // I16x16: DC block rate, TotalCoeff, single counter
@@ -2069,26 +2072,34 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
         S.pm0 = PM_I4;
     }
 #if defined(__HIP_DEVICE_COMPILE__)
-    // one 16-lane row per mode (rows 0-8), blocks in order
+    // 4x4-block wavefront: step d runs the blocks with bx + 2 by = d (at most
+    // two, z-order indices below).  Every block's left, top, top-left and
+    // available top-right neighbours lie on earlier steps, and so do the
+    // blocks whose TotalCoeffs its nC reads; the z-order effects (cost sum,
+    // counter writes, CBP) are applied in z-order after the wavefront.
+    // One 16-lane row per (slot, mode): rows 0-8 slot 0, rows 9-17 slot 1.
+    constexpr uint8_t kWave[10][2] = {{0, 255}, {1, 255}, {2, 4}, {3, 5}, {6, 8}, {7, 9}, {10, 12}, {11, 13}, {14, 255}, {15, 255}};
     const int row = c.tid >> 4;
     const int qbits = 15 + F.qp / 6, fq = (1 << qbits) / 3;
-    for (int blk = 0; blk < 16; ++blk) {
-        const int xO = blk_x(blk), yO = blk_y(blk);
-        if (c.tid < 13) {
+    for (int d = 0; d < 10; ++d) {
+        const int b0 = kWave[d][0], b1 = kWave[d][1];
+        const int nslot = b1 == 255 ? 1 : 2;
+        if (c.tid < 32 && (c.tid >> 4) < nslot && (c.tid & 15) < 13) {
             int p[13];
-            i4_neighbours(S, blk, p);
-            S.i4nb[c.tid] = (int16_t)p[c.tid];
+            i4_neighbours(S, (c.tid >> 4) ? b1 : b0, p);
+            S.i4nb[c.tid >> 4][c.tid & 15] = (int16_t)p[c.tid & 15];
         }
         HL_SYNC();
-        // nC is the same for all nine modes: they only rewrite this block
-        // (read after the barrier: the caller's last TotalCoeffs writes)
-        const int nC = uni(nc_luma_of(S, blk, [&](int ni) -> int { return S.tc[ni]; }));
-        if (row < 9) {
-            const int m = row;
-            const bool ok = i4_avail(m, S.i4nb);
+        // nC is the same for all nine modes of a block: they only rewrite it
+        const int nC0 = uni(nc_luma_of(S, b0, [&](int ni) -> int { return S.tc[ni]; }));
+        const int nC1 = nslot == 2 ? uni(nc_luma_of(S, b1, [&](int ni) -> int { return S.tc[ni]; })) : 0;
+        if (row < 9 * nslot) {
+            const int sl = row >= 9, m = row - 9 * sl, blk = sl ? b1 : b0;
+            const int xO = blk_x(blk), yO = blk_y(blk);
+            const bool ok = i4_avail(m, S.i4nb[sl]);
             if (ok) {
                 const int x = c.K.p & 3, y = c.K.p >> 2;
-                const int pred = i4_pred_px(m, S.i4nb, x, y);
+                const int pred = i4_pred_px(m, S.i4nb[sl], x, y);
                 const int sv = S.src[(yO + y) * 16 + xO + x];
                 const int res = sv - pred;
                 const bool exact = row_or(res != 0) == 0;
@@ -2096,64 +2107,84 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
                 // reconstruction before the CAVLC chain: the two interleave
                 const int r = coop_idct(c.K, coop_dequant(q, c.K.ls, F.qp));
                 const int rec = clip255(pred + r);
-                const int d = row_sum(iabs(sv - rec));
+                const int dd = row_sum(iabs(sv - rec));
                 const CoopStat st = coop_cavlc(S.ct, q, c.K.s, S.lvs[row]);
-                S.i4_rec[m][c.K.p] = (uint8_t)rec;
-                S.i4_lv[m][c.K.s] = (int16_t)q;
+                S.i4_rec[sl][m][c.K.p] = (uint8_t)rec;
+                S.i4_lv[sl][m][c.K.s] = (int16_t)q;
                 if (c.K.p == 0) {
-                    const int bits = st.tc ? st.rest + coop_token_len(S.ct, nC, st.tc, st.t1) : 0;
-                    S.i4_exact[m] = exact;
-                    S.i4_nz[m] = st.tc > 0;
-                    S.i4_tc[m] = st.tc;
-                    S.i4_sctr[m] = st.sctr;
-                    S.i4_dist[m] = d;
-                    S.i4_cost[m] = exact ? 0.0 : dadd((double)d, dmul(F.lambda, (double)bits));
+                    const int bits = st.tc ? st.rest + coop_token_len(S.ct, sl ? nC1 : nC0, st.tc, st.t1) : 0;
+                    S.i4_exact[sl][m] = exact;
+                    S.i4_nz[sl][m] = st.tc > 0;
+                    S.i4_tc[sl][m] = st.tc;
+                    S.i4_sctr[sl][m] = st.sctr;
+                    S.i4_dist[sl][m] = dd;
+                    S.i4_cost[sl][m] = exact ? 0.0 : dadd((double)dd, dmul(F.lambda, (double)bits));
                 }
             }
-            if (c.K.p == 0) S.i4_cost_ok[m] = ok;
+            if (c.K.p == 0) S.i4_cost_ok[sl][m] = ok;
         }
         HL_SYNC();
-        // resolution in mode order (rdo.c:1931-2014), vectorised: the scan
-        // stops at the first exact mode; before it, the last coded mode
-        // writes the counter and the first strict minimum wins
-        double dmin;
-        int best, lastw;
-        bool best_zero;
+        // resolution in mode order (rdo.c:1931-2014), vectorised, one 16-lane
+        // row per slot: the scan stops at the first exact mode; before it, the
+        // last coded mode writes the counter and the first strict minimum wins
         {
-            const int l = c.tid & 15;
-            const bool ok = l < 9 && S.i4_cost_ok[l];
-            const bool ex = ok && S.i4_exact[l], nz = ok && S.i4_nz[l];
-            const unsigned E = (unsigned)(__ballot(ex) & 0xFFFFull);
-            const int limit = E ? __ffs(E) - 1 : 9;
-            const unsigned W = (unsigned)(__ballot(nz) & 0xFFFFull) & ((1u << limit) - 1u);
-            lastw = W ? 31 - __clz(W) : -1;
-            const int sct = l < 9 ? S.i4_sctr[l] : 0;
-            if (lastw >= 0) chain_write(c, __builtin_amdgcn_readlane(sct, lastw));
-            if (E) {
-                dmin = 0.0;
-                best = limit;
-                best_zero = true;
+            const int sl = (c.tid >> 4) & 1, l = c.tid & 15;
+            const bool ok = sl < nslot && l < 9 && S.i4_cost_ok[sl][l];
+            const bool ex = ok && S.i4_exact[sl][l], nz = ok && S.i4_nz[sl][l];
+            const unsigned long long bex = __ballot(ex), bnz = __ballot(nz);
+            const int sct = ok ? S.i4_sctr[sl][l] : 0;
+            const double v = ok ? S.i4_cost[sl][l] : 1.7976931348623157e308;
+            const double mn = row_min_f64(v);
+            const unsigned long long bmin = __ballot(ok && v == mn);
+            int bests[2], lastws[2];
+            for (int k = 0; k < nslot; ++k) {
+                const int blk = k ? b1 : b0;
+                const unsigned E = (unsigned)(bex >> (16 * k)) & 0xFFFFu;
+                const int limit = E ? __ffs(E) - 1 : 9;
+                const unsigned W = ((unsigned)(bnz >> (16 * k)) & 0xFFFFu) & ((1u << limit) - 1u);
+                const int lastw = W ? 31 - __clz(W) : -1;
+                double dmin;
+                int best;
+                bool best_zero;
+                if (E) {
+                    dmin = 0.0;
+                    best = limit;
+                    best_zero = true;
+                }
+                else {
+                    const unsigned long long b64 = __builtin_bit_cast(unsigned long long, mn);
+                    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b64 >> 32), 16 * k);
+                    const unsigned lw = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b64, 16 * k);
+                    dmin = __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lw);
+                    best = __ffs((unsigned)(bmin >> (16 * k)) & 0xFFFFu) - 1;
+                    best_zero = !((W >> best) & 1);
+                }
+                bests[k] = best;
+                lastws[k] = lastw;
+                if (c.tid == 0) {
+                    S.i4r_dmin[blk] = dmin;
+                    S.i4r_dist[blk] = S.i4_dist[k][best];  // d_min_dist4x4 (rdo.c:2011, 2023); 0 for an exact mode
+                    S.i4r_sct[blk] = lastw >= 0 ? __builtin_amdgcn_readlane(sct, 16 * k + lastw) : -1;
+                    S.i4r_zero[blk] = best_zero;
+                    S.i4mode[blk] = (int8_t)best;
+                    if (lastw >= 0) S.tc[blk] = (int8_t)S.i4_tc[k][lastw];
+                }
             }
-            else {
-                const double v = ok ? S.i4_cost[l] : 1.7976931348623157e308;
-                const double mn = row_min_f64(v);
-                dmin = uni(mn);
-                best = __ffs((unsigned)(__ballot(ok && v == mn) & 0xFFFFull)) - 1;
-                best_zero = !((W >> best) & 1);
+            if (c.tid < 16 * nslot) {
+                const int k = c.tid >> 4, t = c.tid & 15, blk = k ? b1 : b0;
+                const int best = k ? bests[1] : bests[0];
+                S.rec[(blk_y(blk) + (t >> 2)) * 16 + blk_x(blk) + (t & 3)] = S.i4_rec[k][best][t];
+                S.luma_level[blk][t] = S.i4_lv[k][best][t];
             }
-        }
-        best_cost = dadd(best_cost, dmin);
-        best_dist += uni(S.i4_dist[best]);  // d_min_dist4x4 (rdo.c:2011, 2023); 0 for an exact mode
-        if (!best_zero) cbp4 |= 1 << blk;
-        if (c.tid < 16) {
-            S.rec[(yO + (c.tid >> 2)) * 16 + xO + (c.tid & 3)] = S.i4_rec[best][c.tid];
-            S.luma_level[blk][c.tid] = S.i4_lv[best][c.tid];
-        }
-        if (c.tid == 0) {
-            S.i4mode[blk] = (int8_t)best;
-            if (lastw >= 0) S.tc[blk] = (int8_t)S.i4_tc[lastw];
         }
         HL_SYNC();
+    }
+    for (int blk = 0; blk < 16; ++blk) {  // z-order: cost sum, distortion, CBP, counter writes
+        best_cost = dadd(best_cost, uni(S.i4r_dmin[blk]));
+        best_dist += uni(S.i4r_dist[blk]);
+        if (!uni(S.i4r_zero[blk])) cbp4 |= 1 << blk;
+        const int sct = uni(S.i4r_sct[blk]);
+        if (sct >= 0) chain_write(c, sct);
     }
 #else
     for (int blk = 0; blk < 16; ++blk) {
@@ -2164,8 +2195,8 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
         const int nC = nc_luma_of(S, blk, [&](int ni) -> int { return S.tc[ni]; });
         HL_SYNC();
         for (int m = c.tid; m < 9; m += c.nthr) {
-            S.i4_cost_ok[m] = i4_avail(m, p);
-            if (!S.i4_cost_ok[m]) continue;
+            S.i4_cost_ok[0][m] = i4_avail(m, p);
+            if (!S.i4_cost_ok[0][m]) continue;
             int pred[16], res[16];
             i4_pred(m, p, pred);
             bool zero = true;
@@ -2173,17 +2204,17 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
                 res[i] = (int)S.src[(yO + (i >> 2)) * 16 + xO + (i & 3)] - pred[i];
                 zero = zero && res[i] == 0;
             }
-            S.i4_exact[m] = zero;
-            S.i4_nz[m] = 0;
-            S.i4_tc[m] = 0;
-            S.i4_sctr[m] = -1;
+            S.i4_exact[0][m] = zero;
+            S.i4_nz[0][m] = 0;
+            S.i4_tc[0][m] = 0;
+            S.i4_sctr[0][m] = -1;
             if (zero) {
                 for (int i = 0; i < 16; ++i) {
-                    S.i4_rec[m][i] = (uint8_t)pred[i];
-                    S.i4_lv[m][i] = 0;
+                    S.i4_rec[0][m][i] = (uint8_t)pred[i];
+                    S.i4_lv[0][m][i] = 0;
                 }
-                S.i4_cost[m] = 0.0;
-                S.i4_dist[m] = 0;
+                S.i4_cost[0][m] = 0.0;
+                S.i4_dist[0][m] = 0;
                 continue;
             }
             int w[16], q[16], lv[16];
@@ -2193,31 +2224,31 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
             for (int i = 0; i < 16; ++i) {
                 lv[i] = q[kZigzag[i]];
                 lz = lz && lv[i] == 0;
-                S.i4_lv[m][i] = (int16_t)lv[i];
+                S.i4_lv[0][m][i] = (int16_t)lv[i];
             }
             int bits = 0, d = 0;
             if (!lz) {
                 const CavlcStat st = cavlc_stat(lv, 16, 15, false);
                 bits = st.rest + token_len(nC, st.tc, st.t1);
-                S.i4_nz[m] = 1;
-                S.i4_tc[m] = st.tc;
-                S.i4_sctr[m] = st.sctr;
+                S.i4_nz[0][m] = 1;
+                S.i4_tc[0][m] = st.tc;
+                S.i4_sctr[0][m] = st.sctr;
                 int r[16];
                 dequant_idct(F.qp, q, false, r);
                 for (int i = 0; i < 16; ++i) {
                     const int v = clip255(pred[i] + r[i]);
-                    S.i4_rec[m][i] = (uint8_t)v;
+                    S.i4_rec[0][m][i] = (uint8_t)v;
                     d += iabs(res[i] + pred[i] - v);
                 }
             }
             else {
                 for (int i = 0; i < 16; ++i) {
-                    S.i4_rec[m][i] = (uint8_t)pred[i];
+                    S.i4_rec[0][m][i] = (uint8_t)pred[i];
                     d += iabs(res[i]);
                 }
             }
-            S.i4_dist[m] = d;
-            S.i4_cost[m] = dadd((double)d, dmul(F.lambda, (double)bits));
+            S.i4_dist[0][m] = d;
+            S.i4_cost[0][m] = dadd((double)d, dmul(F.lambda, (double)bits));
         }
         HL_SYNC();
         // uniform resolution in mode order (rdo.c:1931-2014)
@@ -2225,31 +2256,31 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
         int best = 2, lastw = -1;
         bool best_zero = false;
         for (int m = 0; m < 9; ++m) {
-            if (!S.i4_cost_ok[m]) continue;
-            if (S.i4_exact[m]) {
+            if (!S.i4_cost_ok[0][m]) continue;
+            if (S.i4_exact[0][m]) {
                 dmin = 0.0;
                 best = m;
                 best_zero = true;
                 break;
             }
-            if (S.i4_nz[m]) lastw = m;
-            if (S.i4_cost[m] < dmin) {
-                dmin = S.i4_cost[m];
+            if (S.i4_nz[0][m]) lastw = m;
+            if (S.i4_cost[0][m] < dmin) {
+                dmin = S.i4_cost[0][m];
                 best = m;
-                best_zero = !S.i4_nz[m];
+                best_zero = !S.i4_nz[0][m];
             }
         }
-        if (lastw >= 0) chain_write(c, S.i4_sctr[lastw]);
+        if (lastw >= 0) chain_write(c, S.i4_sctr[0][lastw]);
         best_cost = dadd(best_cost, dmin);
-        best_dist += S.i4_dist[best];
+        best_dist += S.i4_dist[0][best];
         if (!best_zero) cbp4 |= 1 << blk;
         for (int t = c.tid; t < 16; t += c.nthr) {
-            S.rec[(yO + (t >> 2)) * 16 + xO + (t & 3)] = S.i4_rec[best][t];
-            S.luma_level[blk][t] = S.i4_exact[best] ? 0 : S.i4_lv[best][t];
+            S.rec[(yO + (t >> 2)) * 16 + xO + (t & 3)] = S.i4_rec[0][best][t];
+            S.luma_level[blk][t] = S.i4_exact[0][best] ? 0 : S.i4_lv[0][best][t];
         }
         if (c.tid == 0) {
             S.i4mode[blk] = (int8_t)best;
-            if (lastw >= 0) S.tc[blk] = (int8_t)S.i4_tc[lastw];
+            if (lastw >= 0) S.tc[blk] = (int8_t)S.i4_tc[0][lastw];
         }
         HL_SYNC();
     }
