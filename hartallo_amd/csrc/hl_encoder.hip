@@ -145,12 +145,19 @@ __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
     }
 }
 
-// Wave 0 takes the next ready task, oldest picture first, and claims it:
-// f * nmb + addr, or -1 once the run has finished (or after ~10 s without a
-// task: a wait gave up somewhere and the host re-encodes the run).  A queue
-// entry whose claim fails was taken by workgroup 0 (claim_next) and is
-// skipped.
-__device__ int pop_task(const PipeArgs& P, int nmb)
+// Wave 0 takes the next ready task and claims it: f * nmb + addr, or -1 once
+// the run has finished (or after ~10 s without a task: a wait gave up
+// somewhere and the host re-encodes the run).  A queue entry whose claim
+// fails was taken by workgroup 0 (claim_next) and is skipped.
+//
+// Which picture's queue head: with P.hop < 0 the oldest picture's; else the
+// head with the longest remaining dependency path to the end of the run
+// (highest level first), ties to the older picture.  Inside a picture the
+// path from MB (x, y) to the last MB is (mbw-1-x) + 2 (mbh-1-y) wavefront
+// steps; each later picture adds the lag of task_deps' staircase, about
+// 3 (R+2) steps (P.hop).  The oldest-first order lets the newest pictures'
+// wavefronts start late, and the run ends on their critical path.
+__device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh)
 {
     const int lane = threadIdx.x & 63;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -163,24 +170,49 @@ __device__ int pop_task(const PipeArgs& P, int nmb)
             h = ld_relaxed(P.head + o + lane);
             t = ld_relaxed(P.tail + o + lane);
         }
-        const unsigned long long bal = __ballot(lane < w && h < t);
-        if (bal) {
-            const int i0 = __ffsll((long long)bal) - 1;
-            const int f = o + i0, hh = __builtin_amdgcn_readlane(h, i0);
-            int v = 0;
+        int i0 = -1, hh = 0, v = 0;
+        if (P.hop < 0) {
+            const unsigned long long bal = __ballot(lane < w && h < t);
+            if (bal) {
+                i0 = __ffsll((long long)bal) - 1;
+                hh = __builtin_amdgcn_readlane(h, i0);
+            }
+        }
+        else {
+            // the head entries themselves (0: pushed, not yet written)
+            int q = 0;
+            if (lane < w && h < t) q = ld_relaxed(P.queue + (o + lane) * nmb + h);
+            int key = -1;
+            if (q > 0) {
+                const int a = q - 1, y = a / mbw, x = a - y * mbw;
+                key = (((mbw - 1 - x) + 2 * (mbh - 1 - y) - P.hop * lane + 4096) << 6) | (63 - lane);
+            }
+            for (int s = 1; s < 64; s <<= 1) key = max(key, __shfl_xor(key, s, 64));
+            key = __builtin_amdgcn_readfirstlane(key);
+            if (key >= 0) {
+                i0 = 63 - (key & 63);
+                hh = __builtin_amdgcn_readlane(h, i0);
+                v = __builtin_amdgcn_readlane(q, i0);
+            }
+            // else: empty, or only pushes between their tail and slot stores
+        }
+        if (i0 >= 0) {
+            const int f = o + i0;
+            int r = 0;
             if (lane == 0 && atomicCAS(P.head + f, hh, hh + 1) == hh) {
+                r = v;
                 // the slot is pushed right after the tail moved
-                for (unsigned k = 0; (v = ld_relaxed(P.queue + f * nmb + hh)) == 0; ++k)
+                for (unsigned k = 0; r == 0 && (r = ld_relaxed(P.queue + f * nmb + hh)) == 0; ++k)
                     if (k > (1u << 26)) {
                         atomicAdd(P.err, 1);
-                        v = -1;
+                        r = -1;
                         break;
                     }
-                if (v > 0 && atomicCAS(P.claim + f * nmb + v - 1, 0, 1) != 0) v = 0;
+                if (r > 0 && atomicCAS(P.claim + f * nmb + r - 1, 0, 1) != 0) r = 0;
             }
-            v = __builtin_amdgcn_readfirstlane(v);
-            if (v < 0) return -1;
-            if (v > 0) return f * nmb + v - 1;
+            r = __builtin_amdgcn_readfirstlane(r);
+            if (r < 0) return -1;
+            if (r > 0) return f * nmb + r - 1;
             continue;  // another workgroup took it
         }
         if (__builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 10 s at 100 MHz
@@ -240,7 +272,7 @@ __global__ __launch_bounds__(kMbThreads, 2) void k_pipeline(PipeArgs P, int mbw,
         const unsigned long long pt0 = __builtin_readcyclecounter();
 #endif
         if (threadIdx.x < 64) {
-            const int t = in_order ? claim_next(P, nmb, cursor) : pop_task(P, nmb);
+            const int t = in_order ? claim_next(P, nmb, cursor) : pop_task(P, nmb, mbw, mbh);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
             if (threadIdx.x == 0) s_task = t;
@@ -386,6 +418,7 @@ struct hl_amd_encoder_s {
     unsigned long long* d_prof;  // phase counters (HL_PROFILE builds)
     // pipelined runs of P pictures (hl_pipeline.h)
     int pipe_wg, reach, window;  // workgroups (0: one per resident slot), R in MBs, pictures looked at
+    int hop;                     // pop order (PipeArgs::hop)
     int bcap;                    // pictures the run buffers hold
     uint8_t *d_bpic, *d_bpl;     // per picture: recon (Y|U|V), quarter-pel planes
     MbRecord *d_brec, *h_brec, *dh_brec;  // dh_brec: device address of the pinned h_brec (the run writes it)
@@ -508,6 +541,10 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
     e->pipe_wg = 0;
     e->reach = 2;
     e->window = 64;
+    {
+        const char* h = getenv("HL_AMD_PIPE_HOP");  // A/B knob of the pop order
+        e->hop = h ? atoi(h) : 3 * (e->reach + 2) + 6;  // the staircase lag plus two MB rows (tools/gpu_hop.sh)
+    }
     const StreamParams sp{e->W, e->H, p->qp, p->deblock};
     e->scratch.resize(slice_scratch_bytes(sp));
     e->out.resize(slice_scratch_bytes(sp) + 64);
@@ -929,6 +966,7 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     P.nframes = m;
     P.reach = e->reach;
     P.window = e->window;
+    P.hop = e->hop;
     P.cnt = e->d_cnt;
     P.claim = e->d_cnt + nmb * m;
     P.done = e->d_done;

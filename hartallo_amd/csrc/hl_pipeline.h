@@ -172,6 +172,8 @@ struct PipeArgs {
     int32_t nframes;
     int32_t reach;   // guaranteed reference reach R in MBs
     int32_t window;  // pictures a workgroup looks at for ready tasks (from the oldest unfinished)
+    int32_t hop;     // pop order: < 0 oldest picture first; else longest remaining path first, a picture
+                     // boundary counting hop wavefront steps (pop_task)
     int32_t* cnt;    // [nframes][nmb] unfinished dependencies
     int32_t* claim;  // [nframes][nmb] 1 once a workgroup holds the task
     int32_t* done;   // [nframes][nmb] 1 once the task finished (reach_wait polls it)
