@@ -382,4 +382,258 @@ size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* r
     return put_nal(out, cap, scratch, n);
 }
 
+// ---------------------------------------------------------------------------
+// Spatial SVC
+// ---------------------------------------------------------------------------
+namespace {
+
+// pps.c:265-400 as write_stream_headers writes it, for pic_parameter_set_id =
+// seq_parameter_set_id = id (hl_codec_264.c:607-617)
+size_t put_pps(int id, int qp, uint8_t* out, size_t cap)
+{
+    uint8_t buf[64];
+    memset(buf, 0, sizeof(buf));
+    BitWriter bw(buf, sizeof(buf));
+    bw.u(0, 1);
+    bw.u(1, 2);
+    bw.u(8, 5);
+    bw.ue((uint32_t)id);
+    bw.ue((uint32_t)id);
+    bw.u1(0);
+    bw.u1(0);
+    bw.ue(0);
+    bw.ue(0);
+    bw.ue(0);
+    bw.u1(0);
+    bw.u(0, 2);
+    bw.se(qp - 26);
+    bw.se(0);
+    bw.se(0);
+    bw.u1(1);
+    bw.u1(0);
+    bw.u1(0);
+    bw.trailing();
+    return put_nal(out, cap, buf, bw.bytes());
+}
+
+// subset_seq_parameter_set_rbsp of an enhancement layer (sps.c:535-860):
+// Scalable Baseline (83) with constraint_set0 only, the High-profile fields
+// profile 83 carries, and the SVC extension the encoder sets (sps.c:799-851)
+size_t put_subset_sps(int id, int w, int h, uint8_t* out, size_t cap)
+{
+    uint8_t buf[64];
+    memset(buf, 0, sizeof(buf));
+    BitWriter bw(buf, sizeof(buf));
+    bw.u(0, 1);
+    bw.u(1, 2);
+    bw.u(15, 5);    // nal_unit_type subset SPS
+    bw.u(83, 8);    // profile_idc Scalable Baseline
+    bw.u1(1);       // constraint_set0_flag
+    bw.u(0, 7);     // constraint_set1..5, reserved_zero_2bits
+    bw.u((uint32_t)guess_level(w, h), 8);
+    bw.ue((uint32_t)id);
+    bw.ue(1);       // chroma_format_idc 4:2:0
+    bw.ue(0);       // bit_depth_luma_minus8
+    bw.ue(0);       // bit_depth_chroma_minus8
+    bw.u1(0);       // qpprime_y_zero_transform_bypass_flag
+    bw.u1(0);       // seq_scaling_matrix_present_flag
+    bw.ue(4);       // log2_max_frame_num_minus4
+    bw.ue(2);       // pic_order_cnt_type
+    bw.ue(1);       // max_num_ref_frames
+    bw.u1(0);
+    bw.ue((uint32_t)(w / 16 - 1));
+    bw.ue((uint32_t)(h / 16 - 1));
+    bw.u1(1);       // frame_mbs_only_flag
+    bw.u1(0);       // direct_8x8_inference_flag
+    bw.u1(0);       // frame_cropping_flag
+    bw.u1(0);       // vui_parameters_present_flag
+    // seq_parameter_set_svc_extension() (G.7.3.2.1.4)
+    bw.u1(1);       // inter_layer_deblocking_filter_control_present_flag
+    bw.u(0, 2);     // extended_spatial_scalability_idc
+    bw.u1(1);       // chroma_phase_x_plus1_flag
+    bw.u(1, 2);     // chroma_phase_y_plus1
+    bw.u1(0);       // seq_tcoeff_level_prediction_flag
+    bw.u1(0);       // slice_header_restriction_flag
+    bw.u1(0);       // svc_vui_parameters_present_flag
+    bw.u1(0);       // additional_extension2_flag
+    bw.trailing();
+    return put_nal(out, cap, buf, bw.bytes());
+}
+
+// TotalCoeff of the blocks the writer codes, as the reference leaves them on
+// the macroblock objects during the final write (residual.c:796-806); blocks
+// of uncoded 8x8 / chroma-AC groups count as 0 (utils.h:10-20)
+int tc_luma(const MbRecord& m, int blk)
+{
+    if (!(m.cbp_l & (1 << (blk >> 2)))) return 0;
+    int k = 0;
+    for (int i = 0; i < 16; ++i) k += m.luma[blk][i] != 0;
+    return k;
+}
+int tc_cac(const MbRecord& m, int comp, int b)
+{
+    if (!(m.cbp_c & 2) || !(m.cbp_cac[comp] & (1 << b))) return 0;
+    int k = 0;
+    for (int i = 0; i < 15; ++i) k += m.cac[comp][b][i] != 0;
+    return k;
+}
+
+}  // namespace
+
+int stream_level_idc(int width, int height) { return guess_level(width, height); }
+
+size_t write_svc_headers(const StreamParams& base, const int32_t* widths, const int32_t* heights, int n, uint8_t* out, size_t cap)
+{
+    // SPS 0 and PPS 0 are write_stream_headers' two NAL units
+    uint8_t avc[256];
+    const StreamParams b0{widths[0], heights[0], base.qp, base.deblock};
+    const size_t na = write_stream_headers(b0, avc, sizeof(avc));
+    size_t sps0 = 3;
+    while (sps0 + 2 < na && !(avc[sps0] == 0 && avc[sps0 + 1] == 0 && avc[sps0 + 2] == 1)) ++sps0;
+    size_t k = 0;
+    if (cap < na) return 0;
+    memcpy(out, avc, sps0);
+    k = sps0;
+    for (int l = 1; l < n; ++l) {
+        const size_t m = put_subset_sps(l, widths[l], heights[l], out + k, cap - k);
+        if (!m) return 0;
+        k += m;
+    }
+    for (int l = 0; l < n; ++l) {
+        const size_t m = put_pps(l, base.qp, out + k, cap - k);
+        if (!m) return 0;
+        k += m;
+    }
+    return k;
+}
+
+size_t write_prefix_nal(bool idr, uint8_t* out)
+{
+    out[0] = 0x2E;                          // nal_ref_idc 1, nal_unit_type 14
+    out[1] = (uint8_t)(0x80 | (idr ? 0x40 : 0));  // svc_extension_flag, idr_flag, priority_id 0
+    out[2] = 0x80;                          // no_inter_layer_pred_flag 1, dependency_id 0, quality_id 0
+    out[3] = 0x07;                          // temporal_id 0, use_ref_base 0, discardable 0, output 1, reserved 3
+    out[4] = 32;                            // store_ref_base_pic_flag 0, additional flag 0, trailing (encode.c:355)
+    return 5;
+}
+
+size_t write_svc_slice(const StreamParams& p, const SvcSliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap)
+{
+    static const int16_t kZeros[16] = {0};
+    const size_t scap = slice_scratch_bytes(p);
+    const int mbw = p.width / 16, nmb = mbw * (p.height / 16);
+    const size_t esd_size = ((size_t)nmb << 8) + 4096;
+    memset(scratch, 0, scap);
+    BitWriter bw(scratch, scap, (int64_t)esd_size);
+    // NAL header + nal_unit_header_svc_extension (encode.c:296-328)
+    bw.u(0, 1);
+    bw.u(1, 2);
+    bw.u(20, 5);
+    bw.u1(1);                           // svc_extension_flag
+    bw.u1((uint32_t)s.idr);             // idr_flag
+    bw.u(0, 6);                         // priority_id
+    bw.u1(0);                           // no_inter_layer_pred_flag
+    bw.u((uint32_t)s.dependency_id, 3);
+    bw.u(0, 4);                         // quality_id
+    bw.u(0, 3);                         // temporal_id
+    bw.u1(0);                           // use_ref_base_pic_flag
+    bw.u1(0);                           // discardable_flag
+    bw.u1(1);                           // output_flag
+    bw.u(3, 2);                         // reserved_three_2bits
+    // slice_header_in_scalable_extension (slice.c:722-988)
+    bw.ue(0);                           // first_mb_in_slice
+    bw.ue(s.idr ? 2 : 0);               // slice_type EI / EP
+    bw.ue((uint32_t)s.dependency_id);   // pic_parameter_set_id
+    bw.u((uint32_t)s.frame_num & 0xFF, 8);
+    if (s.idr) bw.ue((uint32_t)s.idr_pic_id);
+    if (!s.idr) {
+        bw.u1(1);                       // num_ref_idx_active_override_flag
+        bw.ue(0);
+        bw.u1(0);                       // ref_pic_list_modification_flag_l0
+        bw.u1(0);                       // adaptive_ref_pic_marking_mode_flag
+    }
+    else {
+        bw.u1(0);                       // no_output_of_prior_pics_flag
+        bw.u1(0);                       // long_term_reference_flag
+    }
+    bw.u1(0);                           // store_ref_base_pic_flag
+    bw.se(s.qp - p.qp);                 // slice_qp_delta
+    bw.ue(p.deblock ? 0 : 1);
+    if (p.deblock) {
+        bw.se(0);
+        bw.se(0);
+    }
+    bw.ue((uint32_t)((s.dependency_id - 1) << 4));  // ref_layer_dq_id
+    bw.ue(0);                           // disable_inter_layer_deblocking_filter_idc (deblock_inter_layer_flag = 1)
+    bw.se(0);
+    bw.se(0);
+    bw.u1(0);                           // constrained_intra_resampling_flag
+    bw.u1(0);                           // slice_skip_flag
+    bw.u1(1);                           // adaptive_base_mode_flag
+    bw.u1(1);                           // adaptive_motion_prediction_flag
+    bw.u1(1);                           // adaptive_residual_prediction_flag
+    bw.u(0, 4);                         // scan_idx_start
+    bw.u(15, 4);                        // scan_idx_end
+    // slice_data_in_scalable_extension: macroblock_layer_in_scalable_extension
+    for (int a = 0; a < nmb; ++a) {
+        const MbRecord& m = recs[a];
+        const int mbx = a % mbw, mby = a / mbw;
+        if (!s.idr) bw.ue(0);           // mb_skip_run (no skipped macroblocks)
+        bw.u1(1);                       // base_mode_flag
+        if (!s.idr) bw.u1(0);           // residual_prediction_flag
+        bw.ue(kCbpCode[m.cbp][1]);      // coded_block_pattern, inter mapping (MbPartPredMode is not Intra_4x4)
+        if (!(m.cbp_l > 0 || m.cbp_c > 0)) continue;
+        bw.se(0);                       // mb_qp_delta
+        for (int i8 = 0; i8 < 4; ++i8)
+            for (int i4 = 0; i4 < 4; ++i4) {
+                if (!(m.cbp_l & (1 << i8))) continue;
+                const int blk = i8 * 4 + i4, bx = blk_x(blk), by = blk_y(blk);
+                int nA = 0, nB = 0;
+                bool aA = true, aB = true;
+                if (bx) nA = tc_luma(m, blk_idx(bx - 4, by));
+                else if (mbx) nA = tc_luma(recs[a - 1], blk_idx(12, by));
+                else aA = false;
+                if (by) nB = tc_luma(m, blk_idx(bx, by - 4));
+                else if (mby) nB = tc_luma(recs[a - mbw], blk_idx(bx, 12));
+                else aB = false;
+                const int nC = aA && aB ? (nA + nB + 1) >> 1 : (aA ? nA : (aB ? nB : 0));
+                write_block(bw, m.luma[blk], 15, 16, nC);
+            }
+        if (m.cbp_c & 3)
+            for (int c = 0; c < 2; ++c) write_block(bw, m.cbp_cdc[c] ? m.cdc[c] : kZeros, 3, 4, -1);
+        if (m.cbp_c & 2)
+            for (int c = 0; c < 2; ++c)
+                for (int i4 = 0; i4 < 4; ++i4) {
+                    int nA = 0, nB = 0;
+                    bool aA = true, aB = true;
+                    if (i4 & 1) nA = tc_cac(m, c, i4 - 1);
+                    else if (mbx) nA = tc_cac(recs[a - 1], c, i4 + 1);
+                    else aA = false;
+                    if (i4 & 2) nB = tc_cac(m, c, i4 - 2);
+                    else if (mby) nB = tc_cac(recs[a - mbw], c, i4 + 2);
+                    else aB = false;
+                    const int nC = aA && aB ? (nA + nB + 1) >> 1 : (aA ? nA : (aB ? nB : 0));
+                    write_block(bw, (m.cbp_cac[c] & (1 << i4)) ? m.cac[c][i4] : kZeros, 14, 15, nC);
+                }
+    }
+    bw.trailing();
+    size_t n = bw.bytes();
+    {
+        size_t zeros = 0, len = n;
+        for (size_t i = 0; i < len; ++i) {
+            if (zeros == 2) {
+                if (scratch[i] == 0x01) {
+                    if (len + 1 >= esd_size) return 0;
+                    memmove(&scratch[i + 1], &scratch[i], len - i + 1);
+                    len++;
+                    scratch[i++] = 0x03;
+                }
+                zeros = 0;
+            }
+            zeros = scratch[i] ? 0 : zeros + 1;
+        }
+    }
+    return put_nal(out, cap, scratch, n);
+}
+
 }  // namespace hl

@@ -67,4 +67,30 @@ int level_code_bits(int suffix_length, int level_code);
 size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap,
                    SliceBits* bits = nullptr);
 
+// ---------------------------------------------------------------------------
+// Spatial SVC (Annex G), the reference's encoder syntax (hl_codec_264.c:
+// 577-687, encode.c:281-365, slice.c:660-1002, mb.c:543-892)
+// ---------------------------------------------------------------------------
+// Header NAL units once layers [0, n) exist: SPS of layer 0 (the AVC SPS),
+// subset SPS of layers 1..n-1, then PPS 0..n-1, each with "00 00 01".
+// level_idc the encoder writes for a picture size (utils.c:14-58)
+int stream_level_idc(int width, int height);
+
+size_t write_svc_headers(const StreamParams& base, const int32_t* widths, const int32_t* heights, int n, uint8_t* out, size_t cap);
+
+// Prefix NAL unit of a base-layer slice (encode.c:296-365), without start
+// code: 5 bytes.
+size_t write_prefix_nal(bool idr, uint8_t* out);
+
+struct SvcSliceState {
+    int32_t idr, frame_num, idr_pic_id, qp;
+    int32_t dependency_id;  // layer index (DQId >> 4)
+};
+
+// "00 00 01" + one escaped enhancement-layer slice NAL (type 20) of the
+// layer's MB records; every macroblock has base_mode_flag = 1 and the nC of
+// each residual block is derived here from the neighbours' levels
+// (residual.c:587-755).  Same return convention as write_slice.
+size_t write_svc_slice(const StreamParams& p, const SvcSliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap);
+
 }  // namespace hl

@@ -35,3 +35,31 @@ def frames(width: int, height: int, n: int, seed: int):
 def clip(width: int, height: int, n: int, seed: int) -> np.ndarray:
     """n frames concatenated as planar Y|U|V bytes, shape (n, w*h*3/2)."""
     return np.stack([np.concatenate([y.ravel(), u.ravel(), v.ravel()]) for y, u, v in frames(width, height, n, seed)])
+
+
+def _down2(p: np.ndarray) -> np.ndarray:
+    # 2x2 box average with rounding
+    a = p.astype(np.uint16)
+    return ((a[0::2, 0::2] + a[0::2, 1::2] + a[1::2, 0::2] + a[1::2, 1::2] + 2) >> 2).astype(np.uint8)
+
+
+def svc_clips(width: int, height: int, layers: int, n: int, seed: int) -> list:
+    """Spatial-SVC input: the top layer is clip(width, height, n, seed); layer
+    l below it is the 2x2 box-average downscale of layer l+1 (planes
+    separately).  Returns [clip of layer 0 (smallest), ..., clip of the top
+    layer], each shaped (n, w_l*h_l*3/2)."""
+    top = clip(width, height, n, seed)
+    out = [top]
+    w, h = width, height
+    for _ in range(layers - 1):
+        fs = w * h
+        cur = out[0]
+        nxt = []
+        for f in range(n):
+            y = cur[f, :fs].reshape(h, w)
+            u = cur[f, fs:fs + fs // 4].reshape(h // 2, w // 2)
+            v = cur[f, fs + fs // 4:].reshape(h // 2, w // 2)
+            nxt.append(np.concatenate([_down2(y).ravel(), _down2(u).ravel(), _down2(v).ravel()]))
+        w, h = w // 2, h // 2
+        out.insert(0, np.stack(nxt))
+    return out

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../hartallo_amd/csrc/hl_pipeline.h"
+#include "../../hartallo_amd/csrc/hl_svc.h"
 #include "../../hartallo_amd/csrc/hl_rc.h"
 #include "../../hartallo_amd/csrc/hl_writer.h"
 
@@ -254,4 +255,221 @@ extern "C" int emu_task_succ(int f, int x, int y, int mbw, int mbh, int R, int n
 extern "C" void emu_reach_task(int X, int Y, int mbw, int mbh, int* out)
 {
     reach_task(X, Y, mbw, mbh, out[0], out[1]);
+}
+
+// ---------------------------------------------------------------------------
+// Spatial SVC: the base layer through EmuEnc, every enhancement layer through
+// the product's svc_encode_mb (hl_svc.h), one lane, raster order.
+// emu_svc_encode() returns what the reference harness (oracle/ref_svc_harness.c)
+// writes for the call: header bytes when they changed, and after the last
+// layer "00 00 01" + the access unit.
+// ---------------------------------------------------------------------------
+struct EmuLayer {
+    int W, H, Wc, Hc, mbw, mbh, nmb, pstride, level;
+    SvcGeom g;
+    std::vector<uint8_t> pic[2][3];
+    std::vector<uint8_t> pl[4];
+    std::vector<MbState> st;
+    std::vector<MbRecord> rec;
+    std::vector<uint8_t> scratch;
+    int cur, pict_count, idr_pic_id;
+    SvcShared* S;
+};
+
+struct EmuSvc {
+    EmuEnc* base;
+    int L, qp, deblock;
+    std::vector<EmuLayer> el;  // layers 1..L-1
+    std::vector<int32_t> ws, hs;
+    std::vector<uint8_t> au, slice, hdr;
+    int next, hdr_layers, au_intra;
+    int32_t unpinned;
+};
+
+extern "C" void* emu_svc_create(int W0, int H0, int L, int qp, int me_range, int deblock, int gop, int early_term)
+{
+    if (L < 2 || L > 4) return nullptr;
+    EmuSvc* s = new EmuSvc();
+    s->base = (EmuEnc*)emu_create(W0, H0, qp, me_range, deblock, gop, early_term);
+    if (!s->base) {
+        delete s;
+        return nullptr;
+    }
+    s->L = L;
+    s->qp = qp;
+    s->deblock = deblock;
+    for (int l = 0; l < L; ++l) {
+        s->ws.push_back(W0 << l);
+        s->hs.push_back(H0 << l);
+    }
+    s->el.resize(L - 1);
+    for (int l = 1; l < L; ++l) {
+        EmuLayer& e = s->el[l - 1];
+        e.W = W0 << l;
+        e.H = H0 << l;
+        e.Wc = e.W / 2;
+        e.Hc = e.H / 2;
+        e.mbw = e.W / 16;
+        e.mbh = e.H / 16;
+        e.nmb = e.mbw * e.mbh;
+        e.pstride = e.W + 2 * kPad;
+        e.g = svc_geom(e.W, e.H, e.W / 2, e.H / 2, stream_level_idc(e.W, e.H));
+        for (int k = 0; k < 2; ++k)
+            for (int c = 0; c < 3; ++c) e.pic[k][c].assign(c ? (size_t)e.Wc * e.Hc : (size_t)e.W * e.H, 0);
+        for (int i = 0; i < 4; ++i) e.pl[i].assign((size_t)e.pstride * (e.H + 2 * kPad), 0);
+        e.st.assign(e.nmb, MbState{});
+        memset(e.st.data(), 0, sizeof(MbState) * e.nmb);
+        e.rec.assign(e.nmb, MbRecord{});
+        const StreamParams sp{e.W, e.H, qp, deblock};
+        e.scratch.resize(slice_scratch_bytes(sp));
+        e.cur = e.pict_count = e.idr_pic_id = 0;
+        e.S = (SvcShared*)calloc(1, sizeof(SvcShared));
+    }
+    s->next = 0;
+    s->hdr_layers = 1;
+    s->unpinned = 0;
+    return s;
+}
+
+extern "C" void emu_svc_destroy(void* h)
+{
+    EmuSvc* s = (EmuSvc*)h;
+    if (!s) return;
+    emu_destroy(s->base);
+    for (auto& e : s->el) free(e.S);
+    delete s;
+}
+
+extern "C" int emu_svc_unpinned(void* h) { return ((EmuSvc*)h)->unpinned; }
+
+extern "C" long emu_svc_encode(void* h, int layer, const uint8_t* y, const uint8_t* u, const uint8_t* v, uint8_t* out, long cap)
+{
+    EmuSvc* s = (EmuSvc*)h;
+    if (layer != s->next) return -2;
+    size_t n = 0;
+    if (layer == 0) {
+        EmuEnc* b = s->base;
+        s->au_intra = b->gop_left <= 0;
+        const bool first = b->frame_index == 0;
+        const size_t hdr = first ? b->hdr.size() : 0;
+        s->slice.resize(b->out.size() + 256);
+        const long m = emu_encode_frame(b, y, u, v, s->slice.data(), (long)s->slice.size());
+        if (m < 0) return -1;
+        if (first) {
+            memcpy(out, s->slice.data(), hdr);
+            n = hdr;
+        }
+        uint8_t pre[5];
+        write_prefix_nal(s->au_intra != 0, pre);
+        s->au.assign(pre, pre + 5);
+        static const uint8_t scp[3] = {0, 0, 1};
+        s->au.insert(s->au.end(), scp, scp + 3);
+        s->au.insert(s->au.end(), s->slice.data() + hdr + 3, s->slice.data() + m);
+        s->next = 1;
+        return (long)n;
+    }
+    EmuLayer& e = s->el[layer - 1];
+    const bool intra = s->au_intra != 0;
+    if (layer >= s->hdr_layers) {
+        const StreamParams bp{s->ws[0], s->hs[0], s->qp, s->deblock};
+        n = write_svc_headers(bp, s->ws.data(), s->hs.data(), layer + 1, out, (size_t)cap);
+        s->hdr_layers = layer + 1;
+    }
+    // reference layer: its current picture and macroblock objects
+    const uint8_t* rl[3];
+    const MbState* rst;
+    if (layer == 1) {
+        for (int c = 0; c < 3; ++c) rl[c] = emu_recon(s->base, c);
+        rst = s->base->st.data();
+    }
+    else {
+        EmuLayer& r = s->el[layer - 2];
+        for (int c = 0; c < 3; ++c) rl[c] = r.pic[r.cur ^ 1][c].data();
+        rst = r.st.data();
+    }
+    auto& cur = e.pic[e.cur];
+    auto& ref = e.pic[e.cur ^ 1];
+    if (!intra)
+        for (int p = 0; p < 4; ++p)
+            for (int py = 0; py < e.H + 2 * kPad; ++py)
+                for (int px = 0; px < e.W + 2 * kPad; ++px)
+                    e.pl[p][(size_t)py * e.pstride + px] = qpel_plane_sample(ref[0].data(), e.W, e.H, p, px - kPad, py - kPad);
+    SvcArgs A{};
+    A.g = e.g;
+    FrameArgs& F = A.F;
+    F.W = e.W;
+    F.H = e.H;
+    F.Wc = e.Wc;
+    F.Hc = e.Hc;
+    F.mbw = e.mbw;
+    F.mbh = e.mbh;
+    F.qp = s->qp;
+    F.qpc = kQpToQpc[s->qp];
+    F.is_intra = intra;
+    F.src[0] = y;
+    F.src[1] = u;
+    F.src[2] = v;
+    for (int c = 0; c < 3; ++c) {
+        F.cur[c] = cur[c].data();
+        F.ref[c] = ref[c].data();
+    }
+    for (int i = 0; i < 4; ++i) F.pl[i] = e.pl[i].data();
+    F.pstride = e.pstride;
+    F.st = e.st.data();
+    F.rec = e.rec.data();
+    for (int c = 0; c < 3; ++c) A.rl[c] = rl[c];
+    A.rst = rst;
+    A.unpinned = &s->unpinned;
+    for (int a = 0; a < e.nmb; ++a) svc_encode_mb(A, *e.S, a, 0, 1);
+    if (s->deblock) {
+        DeblockArgs D;
+        D.W = e.W;
+        D.H = e.H;
+        D.Wc = e.Wc;
+        D.mbw = e.mbw;
+        D.qp = s->qp;
+        D.qpc = kQpToQpc[s->qp];
+        for (int c = 0; c < 3; ++c) D.pic[c] = cur[c].data();
+        D.st = e.st.data();
+        for (int a = 0; a < e.nmb; ++a)
+            for (int step = 0; step < 8; ++step)
+                for (int lane = 0; lane < 32; ++lane) deblock_mb_step(D, a, step, lane);
+    }
+    const StreamParams sp{e.W, e.H, s->qp, s->deblock};
+    const SvcSliceState ss{intra ? 1 : 0, e.pict_count, e.idr_pic_id, s->qp, layer};
+    s->slice.resize(e.scratch.size() + 64);
+    const size_t m = write_svc_slice(sp, ss, e.rec.data(), e.scratch.data(), s->slice.data(), s->slice.size());
+    if (!m) return -1;
+    static const uint8_t scp[3] = {0, 0, 1};
+    s->au.insert(s->au.end(), scp, scp + 3);
+    s->au.insert(s->au.end(), s->slice.data() + 3, s->slice.data() + m);
+    e.cur ^= 1;
+    ++e.pict_count;
+    // idr_pic_id counts IdrPicFlag(nal_unit_type) pictures (encode.c:527-530):
+    // type-20 slices never do, so an enhancement layer's stays 0
+    if (layer == s->L - 1) {
+        if ((long)(n + 3 + s->au.size()) > cap) return -1;
+        memcpy(out + n, scp, 3);
+        memcpy(out + n + 3, s->au.data(), s->au.size());
+        n += 3 + s->au.size();
+        s->next = 0;
+    }
+    else {
+        s->next = layer + 1;
+    }
+    return (long)n;
+}
+
+// reconstructed (deblocked) picture of a layer after its last encode
+extern "C" const uint8_t* emu_svc_recon(void* h, int layer, int plane)
+{
+    EmuSvc* s = (EmuSvc*)h;
+    if (layer == 0) return emu_recon(s->base, plane);
+    EmuLayer& e = s->el[layer - 1];
+    return e.pic[e.cur ^ 1][plane].data();
+}
+extern "C" const void* emu_svc_records(void* h, int layer)
+{
+    EmuSvc* s = (EmuSvc*)h;
+    return layer == 0 ? s->base->rec.data() : s->el[layer - 1].rec.data();
 }

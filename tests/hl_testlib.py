@@ -140,6 +140,50 @@ class EmuEncoder:
             self.lib.emu_destroy(ctypes.c_void_p(self.h_))
 
 
+class EmuSvcEncoder:
+    """Spatial SVC through the host build of the kernel logic: layer l is
+    (w0 << l) x (h0 << l); encode(layer, frame) returns what the reference
+    SVC harness writes for that call (oracle/ref_svc_harness.c)."""
+
+    def __init__(self, w0, h0, layers, qp=28, me_range=16, deblock=1, gop=30, early_term=0):
+        lib = emu_lib()
+        if not hasattr(lib, "_svc_bound"):
+            lib.emu_svc_create.restype = ctypes.c_void_p
+            lib.emu_svc_create.argtypes = [ctypes.c_int] * 8
+            lib.emu_svc_destroy.argtypes = [ctypes.c_void_p]
+            lib.emu_svc_encode.restype = ctypes.c_long
+            lib.emu_svc_encode.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_long]
+            lib.emu_svc_recon.restype = ctypes.c_void_p
+            lib.emu_svc_recon.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+            lib.emu_svc_unpinned.argtypes = [ctypes.c_void_p]
+            lib._svc_bound = True
+        self.lib = lib
+        self.w0, self.h0, self.L = w0, h0, layers
+        self.h_ = lib.emu_svc_create(w0, h0, layers, qp, me_range, deblock, gop, early_term)
+        assert self.h_
+        w, h = w0 << (layers - 1), h0 << (layers - 1)
+        self.out = np.zeros(w * h * 3 * layers + (1 << 20), np.uint8)
+
+    def encode(self, layer: int, frame: np.ndarray) -> bytes:
+        w, h = self.w0 << layer, self.h0 << layer
+        y, u, v = _planes(frame, w, h)
+        n = self.lib.emu_svc_encode(ctypes.c_void_p(self.h_), layer, y.ctypes.data, u.ctypes.data, v.ctypes.data, self.out.ctypes.data,
+                                    self.out.size)
+        assert n >= 0, n
+        return self.out[:n].tobytes()
+
+    def recon(self, layer: int) -> np.ndarray:
+        w, h = self.w0 << layer, self.h0 << layer
+        return _recon(lambda p: self.lib.emu_svc_recon(ctypes.c_void_p(self.h_), layer, p), w, h)
+
+    def unpinned(self) -> int:
+        return self.lib.emu_svc_unpinned(ctypes.c_void_p(self.h_))
+
+    def __del__(self):
+        if getattr(self, "h_", None):
+            self.lib.emu_svc_destroy(ctypes.c_void_p(self.h_))
+
+
 class GpuEncoder:
     """The product (libhartallo_amd.so) with the same encode() shape."""
 
