@@ -18,8 +18,10 @@ HL_AMD_SUCCESS = 0
 HL_AMD_ERROR_INVALID_PARAMETER = 1
 HL_AMD_ERROR_INVALID_STATE = 3
 HL_AMD_ERROR_INVALID_FORMAT = 4
+HL_AMD_ERROR_NOT_FOUND = 6
 HL_AMD_ERROR_NOT_IMPLEMENTED = 7
 HL_AMD_ERROR_OUTOFMEMMORY = 8
+HL_AMD_ERROR_OUTOFCAPACITY = 10
 HL_AMD_ERROR_SYSTEM = 13
 HL_AMD_ERROR_TOOSHORT = 15
 HL_AMD_RESULT_TYPE_DATA = 1
@@ -47,6 +49,15 @@ EXPORTED_SYMBOLS = (
     "hl_amd_record_size",
     "hl_amd_debug_chain",
     "hl_amd_debug_recon",
+    "hl_amd_add_layer",
+    "hl_amd_encode_layer",
+    "hl_amd_get_layer_recon",
+    "hl_amd_svc_unpinned",
+    "hl_amd_set_layer_range",
+    "hl_amd_layer_state_bytes",
+    "hl_amd_export_layer",
+    "hl_amd_import_layer",
+    "hl_amd_svc_layer_ms",
     "hl_amd_version",
 )
 
@@ -147,6 +158,24 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         if hasattr(lib, name):
             getattr(lib, name).argtypes = args
             getattr(lib, name).restype = i32
+    lib.hl_amd_add_layer.argtypes = [vp, i32, i32]
+    lib.hl_amd_add_layer.restype = i32
+    lib.hl_amd_encode_layer.argtypes = [vp, i32, i32, vp, vp, vp, i32, ctypes.POINTER(_Result)]
+    lib.hl_amd_encode_layer.restype = i32
+    lib.hl_amd_get_layer_recon.argtypes = [vp, i32, vp, vp, vp]
+    lib.hl_amd_get_layer_recon.restype = i32
+    lib.hl_amd_svc_unpinned.argtypes = [vp]
+    lib.hl_amd_svc_unpinned.restype = i32
+    lib.hl_amd_set_layer_range.argtypes = [vp, i32, i32]
+    lib.hl_amd_set_layer_range.restype = i32
+    lib.hl_amd_layer_state_bytes.argtypes = [vp, i32]
+    lib.hl_amd_layer_state_bytes.restype = ctypes.c_size_t
+    lib.hl_amd_export_layer.argtypes = [vp, i32, vp]
+    lib.hl_amd_export_layer.restype = i32
+    lib.hl_amd_import_layer.argtypes = [vp, i32, vp]
+    lib.hl_amd_import_layer.restype = i32
+    lib.hl_amd_svc_layer_ms.argtypes = [vp]
+    lib.hl_amd_svc_layer_ms.restype = ctypes.c_float
     lib.hl_amd_version.argtypes = []
     lib.hl_amd_version.restype = ctypes.c_char_p
     _lib = lib
@@ -342,3 +371,78 @@ class Encoder:
 
     def last_mb_launches(self) -> int:
         return self.lib.hl_amd_last_mb_launches(self._h)
+
+
+class SvcEncoder(Encoder):
+    """Spatial SVC stream (hl_codec_add_layer + one encode per layer and
+    access unit, base first): layer l is (width << l) x (height << l)."""
+
+    def __init__(self, width: int, height: int, layers: int, qp: int = 28, me_range: int = 16, deblock: int = 1, gop_size: int = 30,
+                 me_early_term: int = 0, device: int = 0, first: int = 0, last: int = -1):
+        super().__init__(width, height, qp, me_range, deblock, gop_size, me_early_term, device)
+        self.layers = layers
+        for l in range(layers):
+            rc = self.lib.hl_amd_add_layer(self._h, width << l, height << l)
+            if rc != HL_AMD_SUCCESS:
+                raise HlAmdError(rc, "hl_amd_add_layer")
+        self.first, self.last = first, (layers - 1 if last < 0 else last)
+        if (self.first, self.last) != (0, layers - 1):
+            rc = self.lib.hl_amd_set_layer_range(self._h, self.first, self.last)
+            if rc != HL_AMD_SUCCESS:
+                raise HlAmdError(rc, "hl_amd_set_layer_range")
+
+    def size(self, layer: int):
+        return self.width << layer, self.height << layer
+
+    def encode_layer(self, layer: int, y, u, v) -> EncodeResult:
+        """One layer's frame from host memory (numpy uint8 planes)."""
+        import numpy as np
+
+        w, h = self.size(layer)
+        ys = [np.ascontiguousarray(p, dtype=np.uint8) for p in (y, u, v)]
+        if ys[0].size != w * h or ys[1].size != w * h // 4 or ys[2].size != ys[1].size:
+            raise HlAmdError(HL_AMD_ERROR_INVALID_FORMAT, "encode_layer (plane sizes)")
+        r = _Result()
+        rc = self.lib.hl_amd_encode_layer(self._h, w, h, ys[0].ctypes.data, ys[1].ctypes.data, ys[2].ctypes.data, 0, ctypes.byref(r))
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_encode_layer")
+        return self._result(r)
+
+    def encode_layer_device(self, layer: int, y_ptr: int, u_ptr: int, v_ptr: int, collect: bool = True):
+        w, h = self.size(layer)
+        r = _Result()
+        rc = self.lib.hl_amd_encode_layer(self._h, w, h, ctypes.c_void_p(y_ptr), ctypes.c_void_p(u_ptr), ctypes.c_void_p(v_ptr), 1,
+                                          ctypes.byref(r))
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_encode_layer")
+        return self._result(r) if collect else r.data_size
+
+    def layer_recon(self, layer: int):
+        import numpy as np
+
+        w, h = self.size(layer)
+        out = np.empty(w * h * 3 // 2, np.uint8)
+        n = w * h
+        rc = self.lib.hl_amd_get_layer_recon(self._h, layer, out.ctypes.data, out.ctypes.data + n, out.ctypes.data + n + n // 4)
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_get_layer_recon")
+        return out
+
+    def unpinned(self) -> int:
+        return self.lib.hl_amd_svc_unpinned(self._h)
+
+    def layer_state_bytes(self, layer: int) -> int:
+        return self.lib.hl_amd_layer_state_bytes(self._h, layer)
+
+    def export_layer(self, layer: int, dst_ptr: int):
+        rc = self.lib.hl_amd_export_layer(self._h, layer, ctypes.c_void_p(dst_ptr))
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_export_layer")
+
+    def import_layer(self, layer: int, src_ptr: int):
+        rc = self.lib.hl_amd_import_layer(self._h, layer, ctypes.c_void_p(src_ptr))
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_import_layer")
+
+    def layer_ms(self) -> float:
+        return self.lib.hl_amd_svc_layer_ms(self._h)

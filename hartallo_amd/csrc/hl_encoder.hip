@@ -24,6 +24,7 @@
 #include "../../include/hartallo_amd.h"
 #include "hl_rc.h"
 #include "hl_pipeline.h"
+#include "hl_svc.h"
 #include "hl_writer.h"
 
 using namespace hl;
@@ -438,10 +439,14 @@ struct hl_amd_encoder_s {
     std::unique_ptr<hl::RateControl> rc;         // rate control (rc_bitrate > 0), hl_rc.h
     hl::RcConfig rc_cfg;
     int32_t last_qp;                             // SliceQPY of the last encoded picture
+    struct SvcState* svc = nullptr;              // spatial SVC layers (hl_amd_add_layer), else null
 };
+
+static void svc_free(hl_amd_encoder_t* e);
 
 static void free_all(hl_amd_encoder_t* e)
 {
+    svc_free(e);
     for (int c = 0; c < 3; ++c) {
         (void)hipFree(e->d_in[c]);
         (void)hipFree(e->d_pic[0][c]);
@@ -1253,3 +1258,433 @@ extern "C" int32_t hl_amd_debug_recon(hl_amd_encoder_t* e, int32_t k, uint8_t* y
 }
 
 extern "C" const char* hl_amd_version(void) { return "hartallo_amd 0.1 (gfx950)"; }
+
+// ---------------------------------------------------------------------------
+// Spatial SVC (hl_svc.h).  The encoder codes layer 0 as the AVC base layer
+// (encode_frame, plus a prefix NAL unit) and every enhancement layer with one
+// k_svc_mb launch over all its macroblocks, then deblocking.  Like the
+// reference (hl_codec_264.c:470-1018) the caller passes one frame per layer
+// and access unit, base first; the access unit's bytes come back with the
+// last layer's call.  For layer-sharded runs (one rank per layer) an encoder
+// codes only layers [first, last] and imports the layer below first from the
+// rank that coded it (hl_amd_export_layer / hl_amd_import_layer).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_svc_mb(SvcArgs A)
+{
+    __shared__ SvcShared S;
+    svc_encode_mb(A, S, blockIdx.x, threadIdx.x, 64);
+}
+
+struct SvcLayerDev {
+    int W, H, Wc, Hc, mbw, mbh, nmb, pstride;
+    size_t plsz;
+    SvcGeom g;
+    uint8_t* d_in[3];
+    uint8_t* d_pic[2][3];
+    int cur;
+    uint8_t* d_pl;
+    MbState* d_st;
+    MbRecord *d_rec, *h_rec;
+    int pict_count;
+    std::vector<uint8_t> scratch, out;
+};
+
+struct SvcState {
+    std::vector<int32_t> w, h;       // layer sizes, [0] = the encoder's own
+    std::vector<SvcLayerDev> el;     // layers 1.. (allocated when the first frame is coded)
+    int first = 0, last = -1;        // layers coded here; the layer below first is imported
+    int next = 0;                    // layer the next call must code
+    int hdr_layers = 0;              // layers whose header NAL units were signalled
+    int gop_left = 0;                // access-unit GOP counter when the base layer is imported
+    bool au_intra = false;
+    bool started = false;
+    std::vector<uint8_t> au, hdr;
+    int32_t* d_unpinned = nullptr;
+    int32_t unpinned = 0;
+    float ms_el = 0.f;               // enhancement-layer device time of the last access unit
+};
+
+static void svc_free(hl_amd_encoder_t* e)
+{
+    SvcState* s = e->svc;
+    if (!s) return;
+    for (SvcLayerDev& L : s->el) {
+        for (int c = 0; c < 3; ++c) {
+            (void)hipFree(L.d_in[c]);
+            (void)hipFree(L.d_pic[0][c]);
+            (void)hipFree(L.d_pic[1][c]);
+        }
+        (void)hipFree(L.d_pl);
+        (void)hipFree(L.d_st);
+        (void)hipFree(L.d_rec);
+        (void)hipHostFree(L.h_rec);
+    }
+    (void)hipFree(s->d_unpinned);
+    delete s;
+    e->svc = nullptr;
+}
+
+static int32_t svc_alloc(hl_amd_encoder_t* e)
+{
+    SvcState* s = e->svc;
+    s->el.assign(s->w.size() - 1, SvcLayerDev{});
+    bool ok = hipMalloc(&s->d_unpinned, sizeof(int32_t)) == hipSuccess &&
+              hipMemsetAsync(s->d_unpinned, 0, sizeof(int32_t), e->stream) == hipSuccess;
+    for (size_t l = 1; l < s->w.size() && ok; ++l) {
+        SvcLayerDev& L = s->el[l - 1];
+        L.W = s->w[l];
+        L.H = s->h[l];
+        L.Wc = L.W / 2;
+        L.Hc = L.H / 2;
+        L.mbw = L.W / 16;
+        L.mbh = L.H / 16;
+        L.nmb = L.mbw * L.mbh;
+        L.pstride = (L.W + 2 * kPad + 63) & ~63;
+        L.plsz = (size_t)L.pstride * (L.H + 2 * kPad);
+        L.g = svc_geom(L.W, L.H, s->w[l - 1], s->h[l - 1], stream_level_idc(L.W, L.H));
+        for (int c = 0; c < 3 && ok; ++c) {
+            const size_t sz = c ? (size_t)L.Wc * L.Hc : (size_t)L.W * L.H;
+            ok = hipMalloc(&L.d_in[c], sz) == hipSuccess && hipMalloc(&L.d_pic[0][c], sz) == hipSuccess &&
+                 hipMalloc(&L.d_pic[1][c], sz) == hipSuccess && hipMemsetAsync(L.d_pic[0][c], 0, sz, e->stream) == hipSuccess &&
+                 hipMemsetAsync(L.d_pic[1][c], 0, sz, e->stream) == hipSuccess;
+        }
+        ok = ok && hipMalloc(&L.d_pl, 4 * L.plsz) == hipSuccess && hipMalloc(&L.d_st, sizeof(MbState) * L.nmb) == hipSuccess &&
+             hipMemsetAsync(L.d_st, 0, sizeof(MbState) * L.nmb, e->stream) == hipSuccess &&
+             hipMalloc(&L.d_rec, sizeof(MbRecord) * L.nmb) == hipSuccess &&
+             hipHostMalloc(&L.h_rec, sizeof(MbRecord) * L.nmb, hipHostMallocDefault) == hipSuccess;
+        const StreamParams sp{L.W, L.H, e->p.qp, e->p.deblock};
+        L.scratch.resize(slice_scratch_bytes(sp));
+        L.out.resize(slice_scratch_bytes(sp) + 64);
+        L.cur = 0;
+        L.pict_count = 0;
+    }
+    ok = ok && hipStreamSynchronize(e->stream) == hipSuccess;
+    return ok ? HL_AMD_SUCCESS : HL_AMD_ERROR_OUTOFMEMMORY;
+}
+
+// current (deblocked) picture and macroblock objects of layer l
+static void svc_layer_ptrs(hl_amd_encoder_t* e, int l, uint8_t* const*& pic, MbState*& st, int& W, int& H, int& nmb)
+{
+    if (l == 0) {
+        pic = e->d_pic[e->cur ^ 1];
+        st = e->d_st;
+        W = e->W;
+        H = e->H;
+        nmb = e->nmb;
+    }
+    else {
+        SvcLayerDev& L = e->svc->el[l - 1];
+        pic = L.d_pic[L.cur ^ 1];
+        st = L.d_st;
+        W = L.W;
+        H = L.H;
+        nmb = L.nmb;
+    }
+}
+
+// one enhancement-layer picture: planes, k_svc_mb, deblocking, records, slice
+static int32_t svc_encode_el(hl_amd_encoder_t* e, int l, const uint8_t* y, const uint8_t* u, const uint8_t* v)
+{
+    SvcState* s = e->svc;
+    SvcLayerDev& L = s->el[l - 1];
+    const bool intra = s->au_intra;
+    const int qp = e->p.qp, qpc = kQpToQpc[qp];
+    uint8_t** cur = L.d_pic[L.cur];
+    uint8_t** ref = L.d_pic[L.cur ^ 1];
+    uint8_t* const* rpic;
+    MbState* rst;
+    int rW, rH, rn;
+    svc_layer_ptrs(e, l - 1, rpic, rst, rW, rH, rn);
+    if (rW * 2 != L.W || rH * 2 != L.H) return HL_AMD_ERROR_INVALID_STATE;
+    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[4], e->stream));
+    if (!intra) {
+        const dim3 grid((L.W + 2 * kPad + kPlTileW - 1) / kPlTileW, (L.H + 2 * kPad + kPlTileH - 1) / kPlTileH);
+        k_planes<<<grid, 256, 0, e->stream>>>(ref[0], L.W, L.H, L.d_pl, L.pstride, (int)L.plsz);
+        HL_HIP_CHECK(hipGetLastError());
+    }
+    SvcArgs A{};
+    A.g = L.g;
+    FrameArgs& F = A.F;
+    F.W = L.W;
+    F.H = L.H;
+    F.Wc = L.Wc;
+    F.Hc = L.Hc;
+    F.mbw = L.mbw;
+    F.mbh = L.mbh;
+    F.qp = qp;
+    F.qpc = qpc;
+    F.is_intra = intra;
+    F.src[0] = y;
+    F.src[1] = u;
+    F.src[2] = v;
+    for (int c = 0; c < 3; ++c) {
+        F.cur[c] = cur[c];
+        F.ref[c] = ref[c];
+        A.rl[c] = rpic[c];
+    }
+    for (int i = 0; i < 4; ++i) F.pl[i] = L.d_pl + i * L.plsz;
+    F.pstride = L.pstride;
+    F.plsz = (int32_t)L.plsz;
+    F.st = L.d_st;
+    F.rec = L.d_rec;
+    A.rst = rst;
+    A.unpinned = s->d_unpinned;
+    k_svc_mb<<<L.nmb, 64, 0, e->stream>>>(A);
+    HL_HIP_CHECK(hipGetLastError());
+    if (e->p.deblock) {
+        DeblockArgs D;
+        D.W = L.W;
+        D.H = L.H;
+        D.Wc = L.Wc;
+        D.mbw = L.mbw;
+        D.qp = qp;
+        D.qpc = qpc;
+        for (int c = 0; c < 3; ++c) D.pic[c] = cur[c];
+        D.st = L.d_st;
+        const int ndiag = (L.mbw - 1) + 2 * (L.mbh - 1) + 1;
+        for (int d = 0; d < ndiag; ++d) {
+            const int n = diag_count(L.mbw, L.mbh, d);
+            if (n) k_deblock_diag<<<n, 64, 0, e->stream>>>(D, L.mbh, d);
+        }
+        HL_HIP_CHECK(hipGetLastError());
+    }
+    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[5], e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(L.h_rec, L.d_rec, sizeof(MbRecord) * L.nmb, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(&s->unpinned, s->d_unpinned, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipStreamSynchronize(e->stream));
+    if (e->timing) {
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, e->ev[4], e->ev[5]);
+        s->ms_el += t;
+    }
+    const StreamParams sp{L.W, L.H, qp, e->p.deblock};
+    const SvcSliceState ss{intra ? 1 : 0, L.pict_count, 0, qp, l};  // idr_pic_id: encode.c:527-530 counts type-5 slices only
+    const size_t n = write_svc_slice(sp, ss, L.h_rec, L.scratch.data(), L.out.data(), L.out.size());
+    if (!n) return HL_AMD_ERROR_TOOSHORT;
+    s->au.insert(s->au.end(), L.out.data() + 3, L.out.data() + n);
+    L.cur ^= 1;
+    ++L.pict_count;
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_add_layer(hl_amd_encoder_t* e, int32_t width, int32_t height)
+{
+    if (!e || width <= 0 || height <= 0) return HL_AMD_ERROR_INVALID_PARAMETER;
+    if (e->frame_index > 0 || (e->svc && e->svc->started)) return HL_AMD_ERROR_INVALID_STATE;
+    if (!e->svc) e->svc = new SvcState();
+    SvcState* s = e->svc;
+    if ((int)s->w.size() >= 4) return HL_AMD_ERROR_OUTOFCAPACITY;  // HL_ENCODER_MAX_LAYERS
+    if (s->w.empty()) {
+        if (width != e->W || height != e->H) return HL_AMD_ERROR_INVALID_PARAMETER;  // the base layer is the encoder's size
+    }
+    else {
+        const int pw = s->w.back(), ph = s->h.back();
+        if (pw >= width || ph >= height) return HL_AMD_ERROR_INVALID_PARAMETER;  // increasing (hl_codec.c:107-112)
+        const int rw = width / pw, rh = height / ph;
+        if ((rw & (rw - 1)) || (rh & (rh - 1))) return HL_AMD_ERROR_INVALID_PARAMETER;  // power of 2 (hl_codec.c:113-121)
+        if (width != 2 * pw || height != 2 * ph || (width & 15) || (height & 15)) return HL_AMD_ERROR_NOT_IMPLEMENTED;  // dyadic only
+    }
+    s->w.push_back(width);
+    s->h.push_back(height);
+    s->last = (int)s->w.size() - 1;
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_set_layer_range(hl_amd_encoder_t* e, int32_t first, int32_t last)
+{
+    if (!e || !e->svc) return HL_AMD_ERROR_INVALID_STATE;
+    SvcState* s = e->svc;
+    if (s->started) return HL_AMD_ERROR_INVALID_STATE;
+    if (first < 0 || last < first || last >= (int)s->w.size()) return HL_AMD_ERROR_INVALID_PARAMETER;
+    s->first = first;
+    s->last = last;
+    return HL_AMD_SUCCESS;
+}
+
+static int32_t svc_start(hl_amd_encoder_t* e)
+{
+    SvcState* s = e->svc;
+    if (s->started) return HL_AMD_SUCCESS;
+    if (e->rc) return HL_AMD_ERROR_NOT_IMPLEMENTED;
+    const int32_t rc = svc_alloc(e);
+    if (rc != HL_AMD_SUCCESS) return rc;
+    s->started = true;
+    s->next = s->first;
+    s->hdr_layers = 0;
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_encode_layer(hl_amd_encoder_t* e, int32_t width, int32_t height, const uint8_t* y, const uint8_t* u,
+                                       const uint8_t* v, int32_t on_device, hl_amd_result_t* r)
+{
+    if (!e || !y || !u || !v || !r) return HL_AMD_ERROR_INVALID_PARAMETER;
+    SvcState* s = e->svc;
+    if (!s || s->w.size() < 2) {
+        if (width != e->W || height != e->H) return HL_AMD_ERROR_INVALID_FORMAT;
+        return on_device ? hl_amd_encode_device(e, y, u, v, r) : hl_amd_encode(e, y, u, v, r);
+    }
+    int l = -1;
+    for (size_t i = 0; i < s->w.size(); ++i)
+        if (s->w[i] == width && s->h[i] == height) l = (int)i;
+    if (l < 0) return HL_AMD_ERROR_NOT_FOUND;  // hl_codec_264.c:470-481
+    int32_t rc = svc_start(e);
+    if (rc != HL_AMD_SUCCESS) return rc;
+    if (l != s->next || l < s->first || l > s->last) return HL_AMD_ERROR_INVALID_STATE;
+    r->type = 0;
+    r->data = nullptr;
+    r->data_size = 0;
+    r->hdr = nullptr;
+    r->hdr_size = 0;
+    if (l == 0) {
+        s->au_intra = e->gop_left <= 0;
+        s->ms_el = 0.f;
+        hl_amd_result_t b{};
+        rc = on_device ? hl_amd_encode_device(e, y, u, v, &b) : hl_amd_encode(e, y, u, v, &b);
+        if (rc != HL_AMD_SUCCESS) return rc;
+        if (b.type & HL_AMD_RESULT_TYPE_HDR) {
+            s->hdr.assign(b.hdr, b.hdr + b.hdr_size);
+            s->hdr_layers = 1;
+            r->type |= HL_AMD_RESULT_TYPE_HDR;
+        }
+        uint8_t pre[5];
+        write_prefix_nal(s->au_intra, pre);
+        s->au.assign(pre, pre + 5);
+        static const uint8_t scp[3] = {0, 0, 1};
+        s->au.insert(s->au.end(), scp, scp + 3);
+        s->au.insert(s->au.end(), b.data, b.data + b.data_size);
+        // encode_frame counted this picture against the GOP; the reference
+        // decrements gop_left once per access unit, at its last layer
+        ++e->gop_left;
+    }
+    else {
+        SvcLayerDev& L = s->el[l - 1];
+        if (!on_device) {
+            HL_HIP_CHECK(hipMemcpyAsync(L.d_in[0], y, (size_t)L.W * L.H, hipMemcpyHostToDevice, e->stream));
+            HL_HIP_CHECK(hipMemcpyAsync(L.d_in[1], u, (size_t)L.Wc * L.Hc, hipMemcpyHostToDevice, e->stream));
+            HL_HIP_CHECK(hipMemcpyAsync(L.d_in[2], v, (size_t)L.Wc * L.Hc, hipMemcpyHostToDevice, e->stream));
+            y = L.d_in[0];
+            u = L.d_in[1];
+            v = L.d_in[2];
+        }
+        if (l == s->first) s->au.clear();
+        else {
+            static const uint8_t scp[3] = {0, 0, 1};
+            s->au.insert(s->au.end(), scp, scp + 3);
+        }
+        rc = svc_encode_el(e, l, y, u, v);
+        if (rc != HL_AMD_SUCCESS) return rc;
+        if (l >= s->hdr_layers) {  // hl_codec_264.c:577-687: a new (subset) SPS and PPS
+            s->hdr.resize(1024);
+            const StreamParams bp{s->w[0], s->h[0], e->p.qp, e->p.deblock};
+            s->hdr.resize(write_svc_headers(bp, s->w.data(), s->h.data(), l + 1, s->hdr.data(), s->hdr.size()));
+            s->hdr_layers = l + 1;
+            r->type |= HL_AMD_RESULT_TYPE_HDR;
+        }
+    }
+    if (r->type & HL_AMD_RESULT_TYPE_HDR) {
+        r->hdr = s->hdr.data();
+        r->hdr_size = s->hdr.size();
+    }
+    if (l == s->last) {
+        r->type |= HL_AMD_RESULT_TYPE_DATA;
+        r->data = s->au.data();
+        r->data_size = s->au.size();
+        s->next = s->first;
+        if (s->first == 0) --e->gop_left;
+        else --s->gop_left;
+    }
+    else {
+        s->next = l + 1;
+    }
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_svc_unpinned(hl_amd_encoder_t* e) { return e && e->svc ? e->svc->unpinned : -1; }
+
+extern "C" int32_t hl_amd_get_layer_recon(hl_amd_encoder_t* e, int32_t layer, uint8_t* y, uint8_t* u, uint8_t* v)
+{
+    if (!e || !y || !u || !v) return HL_AMD_ERROR_INVALID_PARAMETER;
+    if (layer == 0) return hl_amd_get_recon(e, y, u, v);
+    if (!e->svc || !e->svc->started || layer < 1 || layer >= (int)e->svc->w.size()) return HL_AMD_ERROR_INVALID_PARAMETER;
+    uint8_t* const* pic;
+    MbState* st;
+    int W, H, n;
+    svc_layer_ptrs(e, layer, pic, st, W, H, n);
+    HL_HIP_CHECK(hipMemcpyAsync(y, pic[0], (size_t)W * H, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(u, pic[1], (size_t)W * H / 4, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(v, pic[2], (size_t)W * H / 4, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipStreamSynchronize(e->stream));
+    return HL_AMD_SUCCESS;
+}
+
+// state a layer hands to the layer above: its picture (Y|U|V) and its
+// macroblock objects
+extern "C" size_t hl_amd_layer_state_bytes(hl_amd_encoder_t* e, int32_t layer)
+{
+    if (!e || !e->svc || layer < 0 || layer >= (int)e->svc->w.size()) return 0;
+    const size_t W = e->svc->w[layer], H = e->svc->h[layer];
+    return W * H * 3 / 2 + sizeof(MbState) * (W / 16) * (H / 16);
+}
+
+extern "C" int32_t hl_amd_export_layer(hl_amd_encoder_t* e, int32_t layer, void* dst)
+{
+    if (!e || !dst || !hl_amd_layer_state_bytes(e, layer)) return HL_AMD_ERROR_INVALID_PARAMETER;
+    int32_t rc = svc_start(e);
+    if (rc != HL_AMD_SUCCESS) return rc;
+    uint8_t* const* pic;
+    MbState* st;
+    int W, H, n;
+    svc_layer_ptrs(e, layer, pic, st, W, H, n);
+    uint8_t* d = (uint8_t*)dst;
+    const size_t ys = (size_t)W * H, cs = ys / 4;
+    HL_HIP_CHECK(hipMemcpyAsync(d, pic[0], ys, hipMemcpyDeviceToDevice, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(d + ys, pic[1], cs, hipMemcpyDeviceToDevice, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(d + ys + cs, pic[2], cs, hipMemcpyDeviceToDevice, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(d + ys + 2 * cs, st, sizeof(MbState) * n, hipMemcpyDeviceToDevice, e->stream));
+    HL_HIP_CHECK(hipStreamSynchronize(e->stream));
+    return HL_AMD_SUCCESS;
+}
+
+// The layer below `first` of this access unit, coded elsewhere: it becomes
+// that layer's current picture and macroblock objects, and starts the
+// access unit (its IDR decision follows the GOP like the base layer's).
+extern "C" int32_t hl_amd_import_layer(hl_amd_encoder_t* e, int32_t layer, const void* src)
+{
+    if (!e || !src || !e->svc || !hl_amd_layer_state_bytes(e, layer)) return HL_AMD_ERROR_INVALID_PARAMETER;
+    SvcState* s = e->svc;
+    int32_t rc = svc_start(e);
+    if (rc != HL_AMD_SUCCESS) return rc;
+    if (layer != s->first - 1 || s->next != s->first) return HL_AMD_ERROR_INVALID_STATE;
+    int W, H, n;
+    uint8_t** pic;
+    MbState* st;
+    if (layer == 0) {
+        pic = e->d_pic[e->cur];
+        st = e->d_st;
+        W = e->W;
+        H = e->H;
+        n = e->nmb;
+        e->cur ^= 1;
+    }
+    else {
+        SvcLayerDev& L = s->el[layer - 1];
+        pic = L.d_pic[L.cur];
+        st = L.d_st;
+        W = L.W;
+        H = L.H;
+        n = L.nmb;
+        L.cur ^= 1;
+    }
+    const uint8_t* d = (const uint8_t*)src;
+    const size_t ys = (size_t)W * H, cs = ys / 4;
+    HL_HIP_CHECK(hipMemcpyAsync(pic[0], d, ys, hipMemcpyDeviceToDevice, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(pic[1], d + ys, cs, hipMemcpyDeviceToDevice, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(pic[2], d + ys + cs, cs, hipMemcpyDeviceToDevice, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(st, d + ys + 2 * cs, sizeof(MbState) * n, hipMemcpyDeviceToDevice, e->stream));
+    s->au_intra = s->gop_left <= 0;
+    if (s->au_intra) s->gop_left = e->p.gop_size;
+    s->ms_el = 0.f;
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" float hl_amd_svc_layer_ms(hl_amd_encoder_t* e) { return e && e->svc ? e->svc->ms_el : -1.f; }

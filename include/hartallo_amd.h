@@ -45,8 +45,10 @@ enum {
     HL_AMD_ERROR_INVALID_PARAMETER = 1,
     HL_AMD_ERROR_INVALID_STATE = 3,
     HL_AMD_ERROR_INVALID_FORMAT = 4,
+    HL_AMD_ERROR_NOT_FOUND = 6,
     HL_AMD_ERROR_NOT_IMPLEMENTED = 7,
     HL_AMD_ERROR_OUTOFMEMMORY = 8,
+    HL_AMD_ERROR_OUTOFCAPACITY = 10,
     HL_AMD_ERROR_SYSTEM = 13,
     HL_AMD_ERROR_TOOSHORT = 15
 };
@@ -170,6 +172,55 @@ int32_t hl_amd_record_size(void);
  * the last encode call */
 int32_t hl_amd_debug_chain(hl_amd_encoder_t* encoder, int32_t k, void* out, size_t bytes);
 int32_t hl_amd_debug_recon(hl_amd_encoder_t* encoder, int32_t k, uint8_t* y, uint8_t* u, uint8_t* v);
+
+/* ---- Spatial SVC (Annex G) ----
+ * hl_codec_add_layer (source/hl_codec.c:95-131): layers in increasing order,
+ * the first one of the encoder's own size; each further layer twice the one
+ * below (the reference accepts any power-of-two ratio, its encoder is only
+ * exercised dyadic; other ratios return NOT_IMPLEMENTED).  At most 4 layers
+ * (HL_ENCODER_MAX_LAYERS, OUTOFCAPACITY).  Call before the first frame. */
+int32_t hl_amd_add_layer(hl_amd_encoder_t* encoder, int32_t width, int32_t height);
+
+/* plugin encode() of a frame of the given size (hl_frame_video_t.data_width /
+ * data_height[0]): with layers, the frame's size selects the layer
+ * (hl_codec_264.c:470-483, NOT_FOUND otherwise) and the layers of an access
+ * unit come in increasing order (INVALID_STATE otherwise).  Like the
+ * reference, result.type has HDR whenever the header set grew (the first
+ * frame of each layer; result.hdr then holds every SPS, subset SPS and PPS)
+ * and DATA only with the access unit's last layer (result.data = prefix NAL,
+ * base slice and enhancement slices, "00 00 01"-separated, no leading start
+ * code; hl_codec_264.c:999-1017).  on_device: planes in HBM (else host).
+ * Without layers this is hl_amd_encode / hl_amd_encode_device. */
+int32_t hl_amd_encode_layer(hl_amd_encoder_t* encoder, int32_t width, int32_t height, const uint8_t* y, const uint8_t* u,
+                            const uint8_t* v, int32_t on_device, hl_amd_result_t* result);
+
+/* reconstructed (deblocked) picture of layer `layer` after its last frame */
+int32_t hl_amd_get_layer_recon(hl_amd_encoder_t* encoder, int32_t layer, uint8_t* y, uint8_t* u, uint8_t* v);
+
+/* enhancement-layer macroblocks coded so far whose reference-layer macroblock
+ * was intra in a P picture: the reference's output there depends on its
+ * uninitialised scratch memory (hartallo_amd/csrc/hl_svc.h), so they are
+ * outside the bit-exact guarantee; 0 on every pinned workload */
+int32_t hl_amd_svc_unpinned(hl_amd_encoder_t* encoder);
+
+/* Layer-sharded coding (one process / GPU per layer).  An encoder with all
+ * layers added codes only layers [first, last] (no reference interface: the
+ * reference codes every layer in one hl_codec_t).  Per access unit the rank
+ * coding the layer below `first` exports that layer's state -- picture
+ * Y|U|V and macroblock objects, hl_amd_layer_state_bytes() bytes -- into a
+ * device buffer (hl_amd_export_layer, after its last call of the access
+ * unit), the buffer travels (RCCL over xGMI), and this encoder imports it
+ * (hl_amd_import_layer) before coding `first`.  The DATA of the call for
+ * `last` then holds only layers [first, last] ("00 00 01"-separated); the
+ * access unit is the ranks' parts joined with "00 00 01" in layer order. */
+int32_t hl_amd_set_layer_range(hl_amd_encoder_t* encoder, int32_t first, int32_t last);
+size_t hl_amd_layer_state_bytes(hl_amd_encoder_t* encoder, int32_t layer);
+int32_t hl_amd_export_layer(hl_amd_encoder_t* encoder, int32_t layer, void* dst_device);
+int32_t hl_amd_import_layer(hl_amd_encoder_t* encoder, int32_t layer, const void* src_device);
+
+/* device time (ms) of the enhancement layers of the last access unit (with
+ * hl_amd_set_timing on) */
+float hl_amd_svc_layer_ms(hl_amd_encoder_t* encoder);
 
 const char* hl_amd_version(void);
 

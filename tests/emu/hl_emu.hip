@@ -284,6 +284,8 @@ struct EmuSvc {
     std::vector<uint8_t> au, slice, hdr;
     int next, hdr_layers, au_intra;
     int32_t unpinned;
+    int first, last, gop, gop_left;  // layer-sharded coding (hl_amd_set_layer_range)
+    long last_hdr;                   // header bytes at the start of the last emu_svc_encode output
 };
 
 extern "C" void* emu_svc_create(int W0, int H0, int L, int qp, int me_range, int deblock, int gop, int early_term)
@@ -328,6 +330,10 @@ extern "C" void* emu_svc_create(int W0, int H0, int L, int qp, int me_range, int
     s->next = 0;
     s->hdr_layers = 1;
     s->unpinned = 0;
+    s->first = 0;
+    s->last = L - 1;
+    s->gop = gop;
+    s->gop_left = 0;
     return s;
 }
 
@@ -345,8 +351,9 @@ extern "C" int emu_svc_unpinned(void* h) { return ((EmuSvc*)h)->unpinned; }
 extern "C" long emu_svc_encode(void* h, int layer, const uint8_t* y, const uint8_t* u, const uint8_t* v, uint8_t* out, long cap)
 {
     EmuSvc* s = (EmuSvc*)h;
-    if (layer != s->next) return -2;
+    if (layer != s->next || layer < s->first || layer > s->last) return -2;
     size_t n = 0;
+    s->last_hdr = 0;
     if (layer == 0) {
         EmuEnc* b = s->base;
         s->au_intra = b->gop_left <= 0;
@@ -358,6 +365,7 @@ extern "C" long emu_svc_encode(void* h, int layer, const uint8_t* y, const uint8
         if (first) {
             memcpy(out, s->slice.data(), hdr);
             n = hdr;
+            s->last_hdr = (long)hdr;
         }
         uint8_t pre[5];
         write_prefix_nal(s->au_intra != 0, pre);
@@ -365,15 +373,26 @@ extern "C" long emu_svc_encode(void* h, int layer, const uint8_t* y, const uint8
         static const uint8_t scp[3] = {0, 0, 1};
         s->au.insert(s->au.end(), scp, scp + 3);
         s->au.insert(s->au.end(), s->slice.data() + hdr + 3, s->slice.data() + m);
-        s->next = 1;
+        if (s->last == 0) {
+            if ((long)(n + 3 + s->au.size()) > cap) return -1;
+            memcpy(out + n, scp, 3);
+            memcpy(out + n + 3, s->au.data(), s->au.size());
+            n += 3 + s->au.size();
+            s->next = 0;
+        }
+        else {
+            s->next = 1;
+        }
         return (long)n;
     }
     EmuLayer& e = s->el[layer - 1];
     const bool intra = s->au_intra != 0;
+    if (layer == s->first) s->au.clear();
     if (layer >= s->hdr_layers) {
         const StreamParams bp{s->ws[0], s->hs[0], s->qp, s->deblock};
         n = write_svc_headers(bp, s->ws.data(), s->hs.data(), layer + 1, out, (size_t)cap);
         s->hdr_layers = layer + 1;
+        s->last_hdr = (long)n;
     }
     // reference layer: its current picture and macroblock objects
     const uint8_t* rl[3];
@@ -441,18 +460,19 @@ extern "C" long emu_svc_encode(void* h, int layer, const uint8_t* y, const uint8
     const size_t m = write_svc_slice(sp, ss, e.rec.data(), e.scratch.data(), s->slice.data(), s->slice.size());
     if (!m) return -1;
     static const uint8_t scp[3] = {0, 0, 1};
-    s->au.insert(s->au.end(), scp, scp + 3);
+    if (layer != s->first) s->au.insert(s->au.end(), scp, scp + 3);
     s->au.insert(s->au.end(), s->slice.data() + 3, s->slice.data() + m);
     e.cur ^= 1;
     ++e.pict_count;
     // idr_pic_id counts IdrPicFlag(nal_unit_type) pictures (encode.c:527-530):
     // type-20 slices never do, so an enhancement layer's stays 0
-    if (layer == s->L - 1) {
+    if (layer == s->last) {
         if ((long)(n + 3 + s->au.size()) > cap) return -1;
         memcpy(out + n, scp, 3);
         memcpy(out + n + 3, s->au.data(), s->au.size());
         n += 3 + s->au.size();
-        s->next = 0;
+        s->next = s->first;
+        --s->gop_left;
     }
     else {
         s->next = layer + 1;
@@ -473,3 +493,80 @@ extern "C" const void* emu_svc_records(void* h, int layer)
     EmuSvc* s = (EmuSvc*)h;
     return layer == 0 ? s->base->rec.data() : s->el[layer - 1].rec.data();
 }
+
+// layer-sharded coding, as hl_amd_set_layer_range / _export_layer / _import_layer
+extern "C" int emu_svc_set_range(void* h, int first, int last)
+{
+    EmuSvc* s = (EmuSvc*)h;
+    if (first < 0 || last < first || last >= s->L) return 1;
+    s->first = first;
+    s->last = last;
+    s->next = first;
+    return 0;
+}
+
+static void emu_layer_ptrs(EmuSvc* s, int l, int pick, uint8_t** pic, MbState*& st, int& W, int& H, int& n)
+{
+    if (l == 0) {
+        EmuEnc* b = s->base;
+        const int k = pick ? b->cur : b->cur ^ 1;
+        for (int c = 0; c < 3; ++c) pic[c] = b->pic[k][c].data();
+        st = b->st.data();
+        W = b->W;
+        H = b->H;
+        n = b->nmb;
+    }
+    else {
+        EmuLayer& e = s->el[l - 1];
+        const int k = pick ? e.cur : e.cur ^ 1;
+        for (int c = 0; c < 3; ++c) pic[c] = e.pic[k][c].data();
+        st = e.st.data();
+        W = e.W;
+        H = e.H;
+        n = e.nmb;
+    }
+}
+
+extern "C" long emu_svc_layer_state_bytes(void* h, int layer)
+{
+    EmuSvc* s = (EmuSvc*)h;
+    const long W = s->ws[layer], H = s->hs[layer];
+    return W * H * 3 / 2 + (long)sizeof(MbState) * (W / 16) * (H / 16);
+}
+
+extern "C" int emu_svc_export(void* h, int layer, uint8_t* dst)
+{
+    EmuSvc* s = (EmuSvc*)h;
+    uint8_t* pic[3];
+    MbState* st;
+    int W, H, n;
+    emu_layer_ptrs(s, layer, 0, pic, st, W, H, n);
+    const size_t ys = (size_t)W * H, cs = ys / 4;
+    memcpy(dst, pic[0], ys);
+    memcpy(dst + ys, pic[1], cs);
+    memcpy(dst + ys + cs, pic[2], cs);
+    memcpy(dst + ys + 2 * cs, st, sizeof(MbState) * n);
+    return 0;
+}
+
+extern "C" int emu_svc_import(void* h, int layer, const uint8_t* src)
+{
+    EmuSvc* s = (EmuSvc*)h;
+    if (layer != s->first - 1 || s->next != s->first) return 1;
+    uint8_t* pic[3];
+    MbState* st;
+    int W, H, n;
+    emu_layer_ptrs(s, layer, 1, pic, st, W, H, n);
+    const size_t ys = (size_t)W * H, cs = ys / 4;
+    memcpy(pic[0], src, ys);
+    memcpy(pic[1], src + ys, cs);
+    memcpy(pic[2], src + ys + cs, cs);
+    memcpy(st, src + ys + 2 * cs, sizeof(MbState) * n);
+    if (layer == 0) s->base->cur ^= 1;
+    else s->el[layer - 1].cur ^= 1;
+    s->au_intra = s->gop_left <= 0;
+    if (s->au_intra) s->gop_left = s->gop;
+    return 0;
+}
+
+extern "C" long emu_svc_last_hdr(void* h) { return ((EmuSvc*)h)->last_hdr; }

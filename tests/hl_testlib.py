@@ -156,6 +156,13 @@ class EmuSvcEncoder:
             lib.emu_svc_recon.restype = ctypes.c_void_p
             lib.emu_svc_recon.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
             lib.emu_svc_unpinned.argtypes = [ctypes.c_void_p]
+            lib.emu_svc_set_range.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+            lib.emu_svc_layer_state_bytes.restype = ctypes.c_long
+            lib.emu_svc_layer_state_bytes.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            lib.emu_svc_export.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+            lib.emu_svc_import.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+            lib.emu_svc_last_hdr.restype = ctypes.c_long
+            lib.emu_svc_last_hdr.argtypes = [ctypes.c_void_p]
             lib._svc_bound = True
         self.lib = lib
         self.w0, self.h0, self.L = w0, h0, layers
@@ -178,6 +185,25 @@ class EmuSvcEncoder:
 
     def unpinned(self) -> int:
         return self.lib.emu_svc_unpinned(ctypes.c_void_p(self.h_))
+
+    def last_hdr(self) -> int:
+        """header bytes at the start of the last encode() output"""
+        return self.lib.emu_svc_last_hdr(ctypes.c_void_p(self.h_))
+
+    def set_range(self, first: int, last: int):
+        assert self.lib.emu_svc_set_range(ctypes.c_void_p(self.h_), first, last) == 0
+
+    def layer_state_bytes(self, layer: int) -> int:
+        return self.lib.emu_svc_layer_state_bytes(ctypes.c_void_p(self.h_), layer)
+
+    def export_layer(self, layer: int) -> np.ndarray:
+        buf = np.zeros(self.layer_state_bytes(layer), np.uint8)
+        assert self.lib.emu_svc_export(ctypes.c_void_p(self.h_), layer, buf.ctypes.data) == 0
+        return buf
+
+    def import_layer(self, layer: int, buf: np.ndarray):
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        assert self.lib.emu_svc_import(ctypes.c_void_p(self.h_), layer, buf.ctypes.data) == 0
 
     def __del__(self):
         if getattr(self, "h_", None):
