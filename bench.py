@@ -108,6 +108,137 @@ def check_bitexact(outputs, seed):
     return all(hashlib.md5(o).hexdigest() == g for o, g in zip(outputs, gold["frame_md5"]))
 
 
+SVC_WORKLOAD = "c4_svc3_480x272_s41"  # tests/golden/svc_golden.json (make_svc_golden.py)
+SVC_GOLDEN = os.path.join(ROOT, "tests", "golden", "svc_golden.json")
+
+
+def run_svc(args):
+    """BASELINE config 4: 3 dyadic spatial layers 480x272 / 960x544 /
+    1920x1088 (the reference's layer ratios must be powers of two,
+    hl_codec.c:113-121), IPPP GOP 30, QP 28, ME 16, deblocking.  A step is
+    one access unit (all layers of one frame).  One GPU codes every layer;
+    with N ranks the layers are sharded over ranks (hartallo_amd/
+    svc_pipeline.py: the base layer on one rank, the enhancement layers on
+    the next, the layer state handed over by point-to-point sends -- RCCL
+    over xGMI) and further ranks run further streams.  The reference
+    encoder's per-access-unit MD5s cover 31 access units (the timed ones and
+    the warm-up), checked after the timed region."""
+    import hashlib
+
+    import torch
+
+    from hartallo_amd import SvcEncoder, dist, svc_pipeline, synth
+
+    g = json.load(open(SVC_GOLDEN))[SVC_WORKLOAD]
+    L, w0, h0 = g["layers"], g["w0"], g["h0"]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    # ranks beyond the visible GPUs share them (gloo rehearsals on a one-GPU box)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    nccl = world > 1 and os.environ.get("HL_SVC_BACKEND", "nccl") == "nccl"
+    if world > 1:
+        import torch.distributed as tdist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        tdist.init_process_group("nccl" if nccl else "gloo", rank=rank, world_size=world,
+                                 **({"device_id": torch.device(f"cuda:{local}")} if nccl else {}))
+    role = svc_pipeline.role_of(rank, world, L)
+    n = min(args.warmup + args.steps, g["frames"])
+    steps = n - args.warmup
+    clips = synth.svc_clips(w0 << (L - 1), h0 << (L - 1), L, g["frames"], g["seed"])
+    planes = []
+    for l in range(L):
+        w, h = w0 << l, h0 << l
+        dev = torch.from_numpy(clips[l][:n]).to(f"cuda:{local}")
+        planes.append([(dev[i, :w * h], dev[i, w * h:w * h * 5 // 4], dev[i, w * h * 5 // 4:]) for i in range(n)])
+    torch.cuda.synchronize()
+    enc = SvcEncoder(w0, h0, L, g["qp"], g["me_range"], g["deblock"], g["gop"], g["early_term"], local, role.first, role.last)
+    enc.set_timing(True)
+    ad = svc_pipeline.GpuLayerAdapter(enc, planes)
+    if nccl:
+        mk = lambda nb: torch.empty(nb, dtype=torch.uint8, device=f"cuda:{local}")  # noqa: E731
+    else:
+        # gloo moves host tensors: stage the layer state through host memory
+        class _Host:
+            def __init__(self, a):
+                self.a = a
+
+            def __getattr__(self, k):
+                return getattr(self.a, k)
+
+            def export_layer(self, layer, buf):
+                d = torch.empty(buf.numel(), dtype=torch.uint8, device=f"cuda:{local}")
+                self.a.export_layer(layer, d)
+                buf.copy_(d.cpu())
+
+            def import_layer(self, layer, buf):
+                self.a.import_layer(layer, buf.to(f"cuda:{local}"))
+        ad = _Host(ad)
+        mk = lambda nb: torch.empty(nb, dtype=torch.uint8)  # noqa: E731
+    tdist = None
+    if world > 1:
+        import torch.distributed as tdist
+
+    class _Split:  # warm-up access units, then the timed ones, through one pipeline state
+        def __init__(self, a, off):
+            self.a, self.off = a, off
+
+        def __getattr__(self, k):
+            return getattr(self.a, k)
+
+        def encode(self, layer, t):
+            return self.a.encode(layer, t + self.off)
+
+    parts = svc_pipeline.run_access_units(ad, role, None, args.warmup, tdist, mk) if args.warmup else []
+    if tdist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    parts += svc_pipeline.run_access_units(_Split(ad, args.warmup), role, None, steps, tdist, mk)
+    torch.cuda.synchronize()
+    if tdist:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    if tdist:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        if nccl:
+            t = t.cuda()
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        allp = [None] * world
+        tdist.all_gather_object(allp, parts)
+    else:
+        allp = [parts]
+    groups = sorted({svc_pipeline.role_of(r, world, L).group for r in range(world)})
+    ok = True
+    for gi in groups:
+        members = [r for r in range(world) if svc_pipeline.role_of(r, world, L).group == gi]
+        aus = svc_pipeline.assemble([allp[r] for r in members])
+        ok = ok and [hashlib.md5(a).hexdigest() for a in aus] == g["au_md5"][:n]
+    if rank == 0:
+        total = len(groups) * steps
+        print(json.dumps({
+            "metric": "SVC 3-layer (480x272/960x544/1920x1088) access units/sec (bit-exact)",
+            "value": round(total / elapsed, 4), "unit": "access units/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / steps, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8/int32", "data": "synthetic (hartallo_amd.synth.svc_clips, seed 41)",
+            "config": {"workload": "BASELINE config 4: dyadic spatial SVC, 3 layers, IPPP GOP30 QP28 ME16 deblock",
+                       "layers": [[w0 << l, h0 << l] for l in range(L)], "streams": len(groups),
+                       "parallelism": "layer-sharded" if world > 1 else "all layers on one GPU",
+                       "exchange": ("rccl" if nccl else "gloo-host") if world > 1 else None},
+            "bitexact": ok,
+            "bitexact_check": "every access unit (warm-up and timed) of every stream vs the reference encoder's per-AU MD5s "
+                              "(tests/golden/svc_golden.json, oracle/_ref/ref_svc)",
+            "rank0_layers": [role.first, role.last],
+            "rank0_last_au_ms": {"base_layer_device": round(enc.timing_ms()[3], 3) if role.first == 0 else None,
+                                 "enhancement_layers_device": round(enc.layer_ms(), 3)},
+        }), flush=True)
+    enc.close()
+    if tdist:
+        tdist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -115,7 +246,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=GOP)  # the first GOP (also warms the pipelined path)
     ap.add_argument("--cpu-frames", type=int, default=6)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--svc", action="store_true", help="BASELINE config 4 (spatial SVC) instead of the headline workload")
     args = ap.parse_args()
+    if args.svc:
+        if "--steps" not in sys.argv:
+            args.steps = 30
+        if "--warmup" not in sys.argv:
+            args.warmup = 1
+        return run_svc(args)
 
     import torch
 
