@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <future>
 #include <memory>
 #include <thread>
 #include <vector>
@@ -1287,6 +1288,8 @@ struct SvcLayerDev {
     MbRecord *d_rec, *h_rec;
     int pict_count;
     std::vector<uint8_t> scratch, out;
+    hipEvent_t ev_rec = nullptr, ev_t0 = nullptr, ev_t1 = nullptr;  // records on the host; kernel span (timing)
+    std::future<size_t> writing;  // the slice, written by a host thread while the GPU codes the next layer
 };
 
 struct SvcState {
@@ -1316,8 +1319,12 @@ static void svc_free(hl_amd_encoder_t* e)
         }
         (void)hipFree(L.d_pl);
         (void)hipFree(L.d_st);
+        if (L.writing.valid()) L.writing.wait();
         (void)hipFree(L.d_rec);
         (void)hipHostFree(L.h_rec);
+        if (L.ev_rec) (void)hipEventDestroy(L.ev_rec);
+        if (L.ev_t0) (void)hipEventDestroy(L.ev_t0);
+        if (L.ev_t1) (void)hipEventDestroy(L.ev_t1);
     }
     (void)hipFree(s->d_unpinned);
     delete s;
@@ -1327,7 +1334,7 @@ static void svc_free(hl_amd_encoder_t* e)
 static int32_t svc_alloc(hl_amd_encoder_t* e)
 {
     SvcState* s = e->svc;
-    s->el.assign(s->w.size() - 1, SvcLayerDev{});
+    s->el = std::vector<SvcLayerDev>(s->w.size() - 1);  // value-initialised: null pointers until allocated
     bool ok = hipMalloc(&s->d_unpinned, sizeof(int32_t)) == hipSuccess &&
               hipMemsetAsync(s->d_unpinned, 0, sizeof(int32_t), e->stream) == hipSuccess;
     for (size_t l = 1; l < s->w.size() && ok; ++l) {
@@ -1351,7 +1358,9 @@ static int32_t svc_alloc(hl_amd_encoder_t* e)
         ok = ok && hipMalloc(&L.d_pl, 4 * L.plsz) == hipSuccess && hipMalloc(&L.d_st, sizeof(MbState) * L.nmb) == hipSuccess &&
              hipMemsetAsync(L.d_st, 0, sizeof(MbState) * L.nmb, e->stream) == hipSuccess &&
              hipMalloc(&L.d_rec, sizeof(MbRecord) * L.nmb) == hipSuccess &&
-             hipHostMalloc(&L.h_rec, sizeof(MbRecord) * L.nmb, hipHostMallocDefault) == hipSuccess;
+             hipHostMalloc(&L.h_rec, sizeof(MbRecord) * L.nmb, hipHostMallocDefault) == hipSuccess &&
+             hipEventCreateWithFlags(&L.ev_rec, hipEventDisableTiming) == hipSuccess && hipEventCreate(&L.ev_t0) == hipSuccess &&
+             hipEventCreate(&L.ev_t1) == hipSuccess;
         const StreamParams sp{L.W, L.H, e->p.qp, e->p.deblock};
         L.scratch.resize(slice_scratch_bytes(sp));
         L.out.resize(slice_scratch_bytes(sp) + 64);
@@ -1396,7 +1405,7 @@ static int32_t svc_encode_el(hl_amd_encoder_t* e, int l, const uint8_t* y, const
     int rW, rH, rn;
     svc_layer_ptrs(e, l - 1, rpic, rst, rW, rH, rn);
     if (rW * 2 != L.W || rH * 2 != L.H) return HL_AMD_ERROR_INVALID_STATE;
-    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[4], e->stream));
+    HL_HIP_CHECK(hipEventRecord(L.ev_t0, e->stream));
     if (!intra) {
         const dim3 grid((L.W + 2 * kPad + kPlTileW - 1) / kPlTileW, (L.H + 2 * kPad + kPlTileH - 1) / kPlTileH);
         k_planes<<<grid, 256, 0, e->stream>>>(ref[0], L.W, L.H, L.d_pl, L.pstride, (int)L.plsz);
@@ -1448,23 +1457,48 @@ static int32_t svc_encode_el(hl_amd_encoder_t* e, int l, const uint8_t* y, const
         }
         HL_HIP_CHECK(hipGetLastError());
     }
-    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[5], e->stream));
+    HL_HIP_CHECK(hipEventRecord(L.ev_t1, e->stream));
     HL_HIP_CHECK(hipMemcpyAsync(L.h_rec, L.d_rec, sizeof(MbRecord) * L.nmb, hipMemcpyDeviceToHost, e->stream));
     HL_HIP_CHECK(hipMemcpyAsync(&s->unpinned, s->d_unpinned, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
-    HL_HIP_CHECK(hipStreamSynchronize(e->stream));
-    if (e->timing) {
-        float t = 0.f;
-        (void)hipEventElapsedTime(&t, e->ev[4], e->ev[5]);
-        s->ms_el += t;
-    }
+    HL_HIP_CHECK(hipEventRecord(L.ev_rec, e->stream));
+    // the slice is serialised by host threads once the records arrived, while
+    // the GPU codes the layers above; joined by the access unit's last call
     const StreamParams sp{L.W, L.H, qp, e->p.deblock};
     const SvcSliceState ss{intra ? 1 : 0, L.pict_count, 0, qp, l};  // idr_pic_id: encode.c:527-530 counts type-5 slices only
-    const size_t n = write_svc_slice(sp, ss, L.h_rec, L.scratch.data(), L.out.data(), L.out.size());
-    if (!n) return HL_AMD_ERROR_TOOSHORT;
-    s->au.insert(s->au.end(), L.out.data() + 3, L.out.data() + n);
+    const int threads = l == (int)s->w.size() - 1 ? e->nwriters : std::max(1, e->nwriters / 2);
+    L.writing = std::async(std::launch::async, [&L, sp, ss, threads]() -> size_t {
+        if (hipEventSynchronize(L.ev_rec) != hipSuccess) return 0;
+        return write_svc_slice(sp, ss, L.h_rec, L.scratch.data(), L.out.data(), L.out.size(), threads);
+    });
     L.cur ^= 1;
     ++L.pict_count;
     return HL_AMD_SUCCESS;
+}
+
+// joins the slice writers of layers [first, last] of the access unit and
+// appends their slices to it
+static int32_t svc_join(hl_amd_encoder_t* e, int upto)
+{
+    SvcState* s = e->svc;
+    static const uint8_t scp[3] = {0, 0, 1};
+    int32_t rc = HL_AMD_SUCCESS;
+    for (int l = std::max(1, s->first); l <= upto; ++l) {
+        SvcLayerDev& L = s->el[l - 1];
+        if (!L.writing.valid()) continue;
+        const size_t n = L.writing.get();
+        if (!n) {
+            rc = HL_AMD_ERROR_TOOSHORT;
+            continue;
+        }
+        if (!s->au.empty()) s->au.insert(s->au.end(), scp, scp + 3);
+        s->au.insert(s->au.end(), L.out.data() + 3, L.out.data() + n);
+        if (e->timing) {
+            float t = 0.f;
+            (void)hipEventElapsedTime(&t, L.ev_t0, L.ev_t1);
+            s->ms_el += t;
+        }
+    }
+    return rc;
 }
 
 extern "C" int32_t hl_amd_add_layer(hl_amd_encoder_t* e, int32_t width, int32_t height)
@@ -1567,10 +1601,6 @@ extern "C" int32_t hl_amd_encode_layer(hl_amd_encoder_t* e, int32_t width, int32
             v = L.d_in[2];
         }
         if (l == s->first) s->au.clear();
-        else {
-            static const uint8_t scp[3] = {0, 0, 1};
-            s->au.insert(s->au.end(), scp, scp + 3);
-        }
         rc = svc_encode_el(e, l, y, u, v);
         if (rc != HL_AMD_SUCCESS) return rc;
         if (l >= s->hdr_layers) {  // hl_codec_264.c:577-687: a new (subset) SPS and PPS
@@ -1586,6 +1616,8 @@ extern "C" int32_t hl_amd_encode_layer(hl_amd_encoder_t* e, int32_t width, int32
         r->hdr_size = s->hdr.size();
     }
     if (l == s->last) {
+        rc = svc_join(e, l);
+        if (rc != HL_AMD_SUCCESS) return rc;
         r->type |= HL_AMD_RESULT_TYPE_DATA;
         r->data = s->au.data();
         r->data_size = s->au.size();

@@ -5,6 +5,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "hl_prims.h"
@@ -18,6 +19,24 @@ BitWriter::BitWriter(uint8_t* buf, size_t cap, int64_t limit)
 
 void BitWriter::u(uint32_t v, int n)
 {
+    if (n <= 0) return;
+    // fast path: the whole write lies below the limit and inside the buffer;
+    // up to one byte per step
+    const int64_t last = (nbits_ + n - 1) >> 3;
+    if (last <= limit_ && (uint64_t)last < (uint64_t)cap_) {
+        while (n > 0) {
+            const int room = 8 - (int)(nbits_ & 7);
+            const int take = n < room ? n : room;
+            const uint32_t chunk = (v >> (n - take)) & ((1u << take) - 1u);
+            const int shift = room - take;
+            uint8_t& b = buf_[nbits_ >> 3];
+            const uint32_t mask = ((1u << take) - 1u) << shift;
+            b = (uint8_t)((b & ~mask) | (chunk << shift));
+            nbits_ += take;
+            n -= take;
+        }
+        return;
+    }
     for (int i = n - 1; i >= 0; --i) {
         if ((nbits_ >> 3) > limit_) {
             overflow_ = true;
@@ -517,13 +536,12 @@ size_t write_prefix_nal(bool idr, uint8_t* out)
     return 5;
 }
 
-size_t write_svc_slice(const StreamParams& p, const SvcSliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap)
+size_t write_svc_slice(const StreamParams& p, const SvcSliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap,
+                       int threads)
 {
-    static const int16_t kZeros[16] = {0};
     const size_t scap = slice_scratch_bytes(p);
-    const int mbw = p.width / 16, nmb = mbw * (p.height / 16);
+    const int nmb = (p.width / 16) * (p.height / 16);
     const size_t esd_size = ((size_t)nmb << 8) + 4096;
-    memset(scratch, 0, scap);
     BitWriter bw(scratch, scap, (int64_t)esd_size);
     // NAL header + nal_unit_header_svc_extension (encode.c:296-328)
     bw.u(0, 1);
@@ -575,7 +593,34 @@ size_t write_svc_slice(const StreamParams& p, const SvcSliceState& s, const MbRe
     bw.u(0, 4);                         // scan_idx_start
     bw.u(15, 4);                        // scan_idx_end
     // slice_data_in_scalable_extension: macroblock_layer_in_scalable_extension
-    for (int a = 0; a < nmb; ++a) {
+    write_svc_mbs(bw, p, s, recs, 0, nmb, threads);
+    bw.trailing();
+    size_t n = bw.bytes();
+    {
+        size_t zeros = 0, len = n;
+        for (size_t i = 0; i < len; ++i) {
+            if (zeros == 2) {
+                if (scratch[i] == 0x01) {
+                    if (len + 1 >= esd_size) return 0;
+                    memmove(&scratch[i + 1], &scratch[i], len - i + 1);
+                    len++;
+                    scratch[i++] = 0x03;
+                }
+                zeros = 0;
+            }
+            zeros = scratch[i] ? 0 : zeros + 1;
+        }
+    }
+    return put_nal(out, cap, scratch, n);
+}
+
+namespace {
+// macroblock_layer_in_scalable_extension of macroblocks [a0, a1) (mb.c:543-892)
+void write_svc_mb_range(BitWriter& bw, const StreamParams& p, const SvcSliceState& s, const MbRecord* recs, int a0, int a1)
+{
+    static const int16_t kZeros[16] = {0};
+    const int mbw = p.width / 16;
+    for (int a = a0; a < a1; ++a) {
         const MbRecord& m = recs[a];
         const int mbx = a % mbw, mby = a / mbw;
         if (!s.idr) bw.ue(0);           // mb_skip_run (no skipped macroblocks)
@@ -616,24 +661,49 @@ size_t write_svc_slice(const StreamParams& p, const SvcSliceState& s, const MbRe
                     write_block(bw, (m.cbp_cac[c] & (1 << i4)) ? m.cac[c][i4] : kZeros, 14, 15, nC);
                 }
     }
-    bw.trailing();
-    size_t n = bw.bytes();
-    {
-        size_t zeros = 0, len = n;
-        for (size_t i = 0; i < len; ++i) {
-            if (zeros == 2) {
-                if (scratch[i] == 0x01) {
-                    if (len + 1 >= esd_size) return 0;
-                    memmove(&scratch[i + 1], &scratch[i], len - i + 1);
-                    len++;
-                    scratch[i++] = 0x03;
-                }
-                zeros = 0;
-            }
-            zeros = scratch[i] ? 0 : zeros + 1;
+}
+}  // namespace
+
+// The enhancement-layer macroblocks have no skip runs and their nC contexts
+// come from the records, so ranges of macroblocks are written independently
+// (one bit buffer per thread) and concatenated.
+void write_svc_mbs(BitWriter& bw, const StreamParams& p, const SvcSliceState& s, const MbRecord* recs, int a0, int a1, int threads)
+{
+    const int n = a1 - a0;
+    if (threads <= 1 || n < 64 * threads) {
+        write_svc_mb_range(bw, p, s, recs, a0, a1);
+        return;
+    }
+    struct Part {
+        std::vector<uint8_t> buf;
+        int64_t bits = 0;
+        bool overflow = false;
+    };
+    std::vector<Part> parts(threads);
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] {
+            const int b0 = a0 + (int)((int64_t)n * t / threads), b1 = a0 + (int)((int64_t)n * (t + 1) / threads);
+            Part& P = parts[t];
+            P.buf.assign(((size_t)(b1 - b0) << 9) + 4096, 0);
+            BitWriter w(P.buf.data(), P.buf.size());
+            write_svc_mb_range(w, p, s, recs, b0, b1);
+            P.bits = w.bits();
+            P.overflow = w.overflow();
+        });
+    for (auto& x : th) x.join();
+    for (const Part& P : parts) {
+        if (P.overflow) {  // a range outgrew its buffer: write serially
+            write_svc_mb_range(bw, p, s, recs, a0, a1);
+            return;
         }
     }
-    return put_nal(out, cap, scratch, n);
+    for (const Part& P : parts) {
+        const int64_t full = P.bits >> 3;
+        for (int64_t i = 0; i < full; ++i) bw.u(P.buf[i], 8);
+        const int rest = (int)(P.bits & 7);
+        if (rest) bw.u((uint32_t)P.buf[full] >> (8 - rest), rest);
+    }
 }
 
 }  // namespace hl

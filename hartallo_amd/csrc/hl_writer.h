@@ -91,6 +91,10 @@ struct SvcSliceState {
 // layer's MB records; every macroblock has base_mode_flag = 1 and the nC of
 // each residual block is derived here from the neighbours' levels
 // (residual.c:587-755).  Same return convention as write_slice.
-size_t write_svc_slice(const StreamParams& p, const SvcSliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap);
+// threads > 1: ranges of macroblocks are serialised in parallel
+// (write_svc_mbs) and concatenated.
+size_t write_svc_slice(const StreamParams& p, const SvcSliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap,
+                       int threads = 1);
+void write_svc_mbs(BitWriter& bw, const StreamParams& p, const SvcSliceState& s, const MbRecord* recs, int a0, int a1, int threads);
 
 }  // namespace hl

@@ -457,7 +457,7 @@ extern "C" long emu_svc_encode(void* h, int layer, const uint8_t* y, const uint8
     const StreamParams sp{e.W, e.H, s->qp, s->deblock};
     const SvcSliceState ss{intra ? 1 : 0, e.pict_count, e.idr_pic_id, s->qp, layer};
     s->slice.resize(e.scratch.size() + 64);
-    const size_t m = write_svc_slice(sp, ss, e.rec.data(), e.scratch.data(), s->slice.data(), s->slice.size());
+    const size_t m = write_svc_slice(sp, ss, e.rec.data(), e.scratch.data(), s->slice.data(), s->slice.size(), 4);
     if (!m) return -1;
     static const uint8_t scp[3] = {0, 0, 1};
     if (layer != s->first) s->au.insert(s->au.end(), scp, scp + 3);
