@@ -26,6 +26,7 @@
 #include "hl_rc.h"
 #include "hl_pipeline.h"
 #include "hl_svc.h"
+#include "hl_cavlc.h"
 #include "hl_writer.h"
 
 using namespace hl;
@@ -1276,6 +1277,51 @@ __global__ __launch_bounds__(64) void k_svc_mb(SvcArgs A)
     svc_encode_mb(A, S, blockIdx.x, threadIdx.x, 64);
 }
 
+// Enhancement-layer slice data on the GPU (hl_cavlc.h): bit count of every
+// macroblock_layer(), an exclusive scan, then every macroblock writes its
+// bits at its offset.  One lane per macroblock.
+__global__ __launch_bounds__(64) void k_el_count(const MbRecord* __restrict__ rec, int nmb, int mbw, int idr, int64_t* len)
+{
+    const int a = blockIdx.x * 64 + threadIdx.x;
+    if (a >= nmb) return;
+    BitCount bc;
+    el_mb_bits(bc, rec, a, mbw, idr != 0);
+    len[a] = bc.pos;
+}
+
+// in-place exclusive scan of v[0, n), v[n] = the total (one workgroup)
+__global__ __launch_bounds__(1024) void k_scan_excl(int64_t* v, int n)
+{
+    __shared__ int64_t part[1024];
+    const int t = threadIdx.x, per = (n + 1023) / 1024, lo = t * per, hi = lo + per < n ? lo + per : n;
+    int64_t sum = 0;
+    for (int i = lo; i < hi; ++i) sum += v[i];
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan of the partial sums
+        const int64_t x = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    int64_t run = t ? part[t - 1] : 0;
+    for (int i = lo; i < hi; ++i) {
+        const int64_t x = v[i];
+        v[i] = run;
+        run += x;
+    }
+    if (t == 1023) v[n] = part[1023];
+}
+
+__global__ __launch_bounds__(64) void k_el_write(const MbRecord* __restrict__ rec, int nmb, int mbw, int idr, const int64_t* off,
+                                                 uint32_t* words)
+{
+    const int a = blockIdx.x * 64 + threadIdx.x;
+    if (a >= nmb) return;
+    BitOr bo{words, off[a]};
+    el_mb_bits(bo, rec, a, mbw, idr != 0);
+}
+
 struct SvcLayerDev {
     int W, H, Wc, Hc, mbw, mbh, nmb, pstride;
     size_t plsz;
@@ -1288,7 +1334,11 @@ struct SvcLayerDev {
     MbRecord *d_rec, *h_rec;
     int pict_count;
     std::vector<uint8_t> scratch, out;
-    hipEvent_t ev_rec = nullptr, ev_t0 = nullptr, ev_t1 = nullptr;  // records on the host; kernel span (timing)
+    hipEvent_t ev_rec = nullptr, ev_t0 = nullptr, ev_t1 = nullptr;  // slice bits on the host; kernel span (timing)
+    int64_t* d_len;                 // per MB bit counts, scanned in place; [nmb] = the total
+    uint32_t *d_words, *h_words;    // slice data bits (big-endian words), device / pinned copy of the first esd_size bytes
+    int64_t* h_total;               // pinned: total data bits
+    size_t words_bytes, esd_size;
     std::future<size_t> writing;  // the slice, written by a host thread while the GPU codes the next layer
 };
 
@@ -1320,6 +1370,10 @@ static void svc_free(hl_amd_encoder_t* e)
         (void)hipFree(L.d_pl);
         (void)hipFree(L.d_st);
         if (L.writing.valid()) L.writing.wait();
+        (void)hipFree(L.d_len);
+        (void)hipFree(L.d_words);
+        (void)hipHostFree(L.h_words);
+        (void)hipHostFree(L.h_total);
         (void)hipFree(L.d_rec);
         (void)hipHostFree(L.h_rec);
         if (L.ev_rec) (void)hipEventDestroy(L.ev_rec);
@@ -1361,6 +1415,14 @@ static int32_t svc_alloc(hl_amd_encoder_t* e)
              hipHostMalloc(&L.h_rec, sizeof(MbRecord) * L.nmb, hipHostMallocDefault) == hipSuccess &&
              hipEventCreateWithFlags(&L.ev_rec, hipEventDisableTiming) == hipSuccess && hipEventCreate(&L.ev_t0) == hipSuccess &&
              hipEventCreate(&L.ev_t1) == hipSuccess;
+        // slice data: at most ~1.5 KB per macroblock (16 luma + 10 chroma
+        // CAVLC blocks); the reference's slice buffer holds (nmb << 8) + 4096
+        // bytes (encode.c:192), bits past it are dropped (write_svc_slice_bits)
+        L.esd_size = ((size_t)L.nmb << 8) + 4096;
+        L.words_bytes = (size_t)L.nmb * 2048 + 4096;
+        ok = ok && hipMalloc(&L.d_len, sizeof(int64_t) * (L.nmb + 1)) == hipSuccess && hipMalloc(&L.d_words, L.words_bytes) == hipSuccess &&
+             hipHostMalloc(&L.h_words, L.esd_size + 64, hipHostMallocDefault) == hipSuccess &&
+             hipHostMalloc(&L.h_total, sizeof(int64_t), hipHostMallocDefault) == hipSuccess;
         const StreamParams sp{L.W, L.H, e->p.qp, e->p.deblock};
         L.scratch.resize(slice_scratch_bytes(sp));
         L.out.resize(slice_scratch_bytes(sp) + 64);
@@ -1457,17 +1519,33 @@ static int32_t svc_encode_el(hl_amd_encoder_t* e, int l, const uint8_t* y, const
         }
         HL_HIP_CHECK(hipGetLastError());
     }
+    // slice data serialised on the GPU (hl_cavlc.h)
+    {
+        const int nb = (L.nmb + 63) / 64;
+        HL_HIP_CHECK(hipMemsetAsync(L.d_words, 0, L.words_bytes, e->stream));
+        k_el_count<<<nb, 64, 0, e->stream>>>(L.d_rec, L.nmb, L.mbw, intra, L.d_len);
+        k_scan_excl<<<1, 1024, 0, e->stream>>>(L.d_len, L.nmb);
+        k_el_write<<<nb, 64, 0, e->stream>>>(L.d_rec, L.nmb, L.mbw, intra, L.d_len, L.d_words);
+        HL_HIP_CHECK(hipGetLastError());
+    }
     HL_HIP_CHECK(hipEventRecord(L.ev_t1, e->stream));
-    HL_HIP_CHECK(hipMemcpyAsync(L.h_rec, L.d_rec, sizeof(MbRecord) * L.nmb, hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(L.h_total, L.d_len + L.nmb, sizeof(int64_t), hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(L.h_words, L.d_words, L.esd_size + 64, hipMemcpyDeviceToHost, e->stream));
     HL_HIP_CHECK(hipMemcpyAsync(&s->unpinned, s->d_unpinned, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
     HL_HIP_CHECK(hipEventRecord(L.ev_rec, e->stream));
-    // the slice is serialised by host threads once the records arrived, while
-    // the GPU codes the layers above; joined by the access unit's last call
+    // the header, trailing bits and escaping are added by a host thread once
+    // the bits arrived, while the GPU codes the layers above; joined by the
+    // access unit's last call
     const StreamParams sp{L.W, L.H, qp, e->p.deblock};
     const SvcSliceState ss{intra ? 1 : 0, L.pict_count, 0, qp, l};  // idr_pic_id: encode.c:527-530 counts type-5 slices only
-    const int threads = l == (int)s->w.size() - 1 ? e->nwriters : std::max(1, e->nwriters / 2);
+    const int threads = e->nwriters;
     L.writing = std::async(std::launch::async, [&L, sp, ss, threads]() -> size_t {
         if (hipEventSynchronize(L.ev_rec) != hipSuccess) return 0;
+        const int64_t bits = *L.h_total;
+        if ((bits >> 3) + 64 < (int64_t)L.esd_size)
+            return write_svc_slice_bits(sp, ss, L.h_words, bits, L.scratch.data(), L.out.data(), L.out.size());
+        // a slice past the reference's slice buffer: the host writer reproduces its truncation
+        if (hipMemcpy(L.h_rec, L.d_rec, sizeof(MbRecord) * L.nmb, hipMemcpyDeviceToHost) != hipSuccess) return 0;
         return write_svc_slice(sp, ss, L.h_rec, L.scratch.data(), L.out.data(), L.out.size(), threads);
     });
     L.cur ^= 1;

@@ -536,14 +536,11 @@ size_t write_prefix_nal(bool idr, uint8_t* out)
     return 5;
 }
 
-size_t write_svc_slice(const StreamParams& p, const SvcSliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap,
-                       int threads)
+namespace {
+// NAL header + nal_unit_header_svc_extension (encode.c:296-328) and
+// slice_header_in_scalable_extension (slice.c:722-988)
+void svc_slice_header(BitWriter& bw, const StreamParams& p, const SvcSliceState& s)
 {
-    const size_t scap = slice_scratch_bytes(p);
-    const int nmb = (p.width / 16) * (p.height / 16);
-    const size_t esd_size = ((size_t)nmb << 8) + 4096;
-    BitWriter bw(scratch, scap, (int64_t)esd_size);
-    // NAL header + nal_unit_header_svc_extension (encode.c:296-328)
     bw.u(0, 1);
     bw.u(1, 2);
     bw.u(20, 5);
@@ -558,7 +555,6 @@ size_t write_svc_slice(const StreamParams& p, const SvcSliceState& s, const MbRe
     bw.u1(0);                           // discardable_flag
     bw.u1(1);                           // output_flag
     bw.u(3, 2);                         // reserved_three_2bits
-    // slice_header_in_scalable_extension (slice.c:722-988)
     bw.ue(0);                           // first_mb_in_slice
     bw.ue(s.idr ? 2 : 0);               // slice_type EI / EP
     bw.ue((uint32_t)s.dependency_id);   // pic_parameter_set_id
@@ -592,26 +588,55 @@ size_t write_svc_slice(const StreamParams& p, const SvcSliceState& s, const MbRe
     bw.u1(1);                           // adaptive_residual_prediction_flag
     bw.u(0, 4);                         // scan_idx_start
     bw.u(15, 4);                        // scan_idx_end
-    // slice_data_in_scalable_extension: macroblock_layer_in_scalable_extension
-    write_svc_mbs(bw, p, s, recs, 0, nmb, threads);
+}
+
+// trailing bits, emulation prevention (only 00 00 01, the unescaped length
+// kept: rbsp.c:609-632, encode.c:443-444) and the start code
+size_t svc_slice_finish(BitWriter& bw, uint8_t* scratch, size_t esd_size, uint8_t* out, size_t cap)
+{
     bw.trailing();
     size_t n = bw.bytes();
-    {
-        size_t zeros = 0, len = n;
-        for (size_t i = 0; i < len; ++i) {
-            if (zeros == 2) {
-                if (scratch[i] == 0x01) {
-                    if (len + 1 >= esd_size) return 0;
-                    memmove(&scratch[i + 1], &scratch[i], len - i + 1);
-                    len++;
-                    scratch[i++] = 0x03;
-                }
-                zeros = 0;
+    size_t zeros = 0, len = n;
+    for (size_t i = 0; i < len; ++i) {
+        if (zeros == 2) {
+            if (scratch[i] == 0x01) {
+                if (len + 1 >= esd_size) return 0;
+                memmove(&scratch[i + 1], &scratch[i], len - i + 1);
+                len++;
+                scratch[i++] = 0x03;
             }
-            zeros = scratch[i] ? 0 : zeros + 1;
+            zeros = 0;
         }
+        zeros = scratch[i] ? 0 : zeros + 1;
     }
     return put_nal(out, cap, scratch, n);
+}
+}  // namespace
+
+size_t write_svc_slice(const StreamParams& p, const SvcSliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap,
+                       int threads)
+{
+    const size_t scap = slice_scratch_bytes(p);
+    const int nmb = (p.width / 16) * (p.height / 16);
+    const size_t esd_size = ((size_t)nmb << 8) + 4096;
+    BitWriter bw(scratch, scap, (int64_t)esd_size);
+    svc_slice_header(bw, p, s);
+    write_svc_mbs(bw, p, s, recs, 0, nmb, threads);
+    return svc_slice_finish(bw, scratch, esd_size, out, cap);
+}
+
+size_t write_svc_slice_bits(const StreamParams& p, const SvcSliceState& s, const uint32_t* words, int64_t data_bits, uint8_t* scratch,
+                            uint8_t* out, size_t cap)
+{
+    const size_t scap = slice_scratch_bytes(p);
+    const int nmb = (p.width / 16) * (p.height / 16);
+    const size_t esd_size = ((size_t)nmb << 8) + 4096;
+    BitWriter bw(scratch, scap, (int64_t)esd_size);
+    svc_slice_header(bw, p, s);
+    const int64_t full = data_bits >> 5;
+    for (int64_t i = 0; i < full; ++i) bw.u(words[i], 32);
+    if (data_bits & 31) bw.u(words[full] >> (32 - (int)(data_bits & 31)), (int)(data_bits & 31));
+    return svc_slice_finish(bw, scratch, esd_size, out, cap);
 }
 
 namespace {

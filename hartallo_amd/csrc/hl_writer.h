@@ -96,5 +96,9 @@ struct SvcSliceState {
 size_t write_svc_slice(const StreamParams& p, const SvcSliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap,
                        int threads = 1);
 void write_svc_mbs(BitWriter& bw, const StreamParams& p, const SvcSliceState& s, const MbRecord* recs, int a0, int a1, int threads);
+// Same slice from its macroblock_layer() bits serialised elsewhere (the GPU,
+// hl_cavlc.h): data_bits bits in big-endian 32-bit words.
+size_t write_svc_slice_bits(const StreamParams& p, const SvcSliceState& s, const uint32_t* words, int64_t data_bits, uint8_t* scratch,
+                            uint8_t* out, size_t cap);
 
 }  // namespace hl

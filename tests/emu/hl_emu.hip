@@ -9,11 +9,13 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <memory>
 #include <vector>
 
 #include "../../hartallo_amd/csrc/hl_pipeline.h"
 #include "../../hartallo_amd/csrc/hl_svc.h"
+#include "../../hartallo_amd/csrc/hl_cavlc.h"
 #include "../../hartallo_amd/csrc/hl_rc.h"
 #include "../../hartallo_amd/csrc/hl_writer.h"
 
@@ -457,7 +459,25 @@ extern "C" long emu_svc_encode(void* h, int layer, const uint8_t* y, const uint8
     const StreamParams sp{e.W, e.H, s->qp, s->deblock};
     const SvcSliceState ss{intra ? 1 : 0, e.pict_count, e.idr_pic_id, s->qp, layer};
     s->slice.resize(e.scratch.size() + 64);
-    const size_t m = write_svc_slice(sp, ss, e.rec.data(), e.scratch.data(), s->slice.data(), s->slice.size(), 4);
+    size_t m;
+    if (getenv("HL_EMU_HOST_WRITER")) {
+        m = write_svc_slice(sp, ss, e.rec.data(), e.scratch.data(), s->slice.data(), s->slice.size(), 4);
+    }
+    else {
+        // the product's GPU serialisation (hl_cavlc.h): counts, exclusive scan, writes
+        std::vector<int64_t> off(e.nmb + 1, 0);
+        for (int a = 0; a < e.nmb; ++a) {
+            BitCount bc;
+            el_mb_bits(bc, e.rec.data(), a, e.mbw, intra);
+            off[a + 1] = off[a] + bc.pos;
+        }
+        std::vector<uint32_t> words((size_t)(off[e.nmb] >> 5) + 2, 0);
+        for (int a = 0; a < e.nmb; ++a) {
+            BitOr bo{words.data(), off[a]};
+            el_mb_bits(bo, e.rec.data(), a, e.mbw, intra);
+        }
+        m = write_svc_slice_bits(sp, ss, words.data(), off[e.nmb], e.scratch.data(), s->slice.data(), s->slice.size());
+    }
     if (!m) return -1;
     static const uint8_t scp[3] = {0, 0, 1};
     if (layer != s->first) s->au.insert(s->au.end(), scp, scp + 3);
@@ -570,3 +590,16 @@ extern "C" int emu_svc_import(void* h, int layer, const uint8_t* src)
 }
 
 extern "C" long emu_svc_last_hdr(void* h) { return ((EmuSvc*)h)->last_hdr; }
+
+// diagnostics: seconds per write_svc_slice of layer `layer`'s last records
+extern "C" double emu_svc_write_seconds(void* h, int layer, int threads, int reps)
+{
+    EmuSvc* s = (EmuSvc*)h;
+    EmuLayer& e = s->el[layer - 1];
+    const StreamParams sp{e.W, e.H, s->qp, s->deblock};
+    const SvcSliceState ss{0, 1, 0, s->qp, layer};
+    std::vector<uint8_t> out(e.scratch.size() + 64);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < reps; ++i) write_svc_slice(sp, ss, e.rec.data(), e.scratch.data(), out.data(), out.size(), threads);
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / reps;
+}
