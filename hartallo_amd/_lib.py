@@ -58,6 +58,7 @@ EXPORTED_SYMBOLS = (
     "hl_amd_export_layer",
     "hl_amd_import_layer",
     "hl_amd_svc_layer_ms",
+    "hl_amd_encode_layers_batch",
     "hl_amd_version",
 )
 
@@ -174,6 +175,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_export_layer.restype = i32
     lib.hl_amd_import_layer.argtypes = [vp, i32, vp]
     lib.hl_amd_import_layer.restype = i32
+    lib.hl_amd_encode_layers_batch.argtypes = [vp, i32, i32, pp, ctypes.POINTER(_Result)]
+    lib.hl_amd_encode_layers_batch.restype = i32
     lib.hl_amd_svc_layer_ms.argtypes = [vp]
     lib.hl_amd_svc_layer_ms.restype = ctypes.c_float
     lib.hl_amd_version.argtypes = []
@@ -446,3 +449,15 @@ class SvcEncoder(Encoder):
 
     def layer_ms(self) -> float:
         return self.lib.hl_amd_svc_layer_ms(self._h)
+
+    def encode_layers_batch_device(self, ptrs):
+        """n access units of every layer resident in HBM: ptrs[l][i] =
+        (y_ptr, u_ptr, v_ptr) of layer l's frame of access unit i.  Returns
+        one EncodeResult per access unit (hl_amd_encode_layers_batch)."""
+        L, n = len(ptrs), len(ptrs[0])
+        flat = (ctypes.c_void_p * (3 * L * n))(*[ptrs[l][i][c] for l in range(L) for i in range(n) for c in range(3)])
+        res = (_Result * n)()
+        rc = self.lib.hl_amd_encode_layers_batch(self._h, n, L, flat, res)
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_encode_layers_batch")
+        return [self._result(r) for r in res]

@@ -106,6 +106,34 @@ __global__ __launch_bounds__(64) void k_deblock_diag(DeblockArgs D, int mbh, int
     }
 }
 
+// Deblocking of a whole picture in one launch: one 64-lane workgroup per MB
+// row, its MBs left to right; MB (x, y) waits until row y - 1 has finished
+// MB x + 1 -- the order of the anti-diagonal launches d = x + 2y, so every
+// edge sees the samples the reference's raster-order filter sees
+// (deblock.c:192-284).  Hand-offs as in k_pipeline: waves drained, a release
+// fence with its own wait, a relaxed flag; the consumer acquires.
+__global__ __launch_bounds__(64) void k_deblock_rows(DeblockArgs D, int32_t* row_done, int32_t* err)
+{
+    const int y = blockIdx.x, tid = threadIdx.x;
+    for (int x = 0; x < D.mbw; ++x) {
+        if (y > 0) {
+            if (tid == 0) spin_ge(row_done + y - 1, min(x + 2, D.mbw), err);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+        const int addr = y * D.mbw + x;
+        for (int step = 0; step < 8; ++step) {
+            if (tid < 32) deblock_mb_step(D, addr, step, tid);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tid == 0) st_relaxed(row_done + y, x + 1);
+    }
+}
+
 // Deblocking and plane blocks of task (x, y) (hl_pipeline.h).
 __device__ void task_filters(const PipeFrame& PF, int x, int y, int mbw, int mbh, int tid)
 {
@@ -442,6 +470,7 @@ struct hl_amd_encoder_s {
     hl::RcConfig rc_cfg;
     int32_t last_qp;                             // SliceQPY of the last encoded picture
     struct SvcState* svc = nullptr;              // spatial SVC layers (hl_amd_add_layer), else null
+    int32_t* d_rows = nullptr;                   // k_deblock_rows: per-row progress [mbh], spin failures [mbh]
 };
 
 static void svc_free(hl_amd_encoder_t* e);
@@ -461,6 +490,7 @@ static void free_all(hl_amd_encoder_t* e)
     (void)hipFree(e->d_chain);
     (void)hipFree(e->d_spec);
     (void)hipFree(e->d_prof);
+    (void)hipFree(e->d_rows);
     (void)hipFree(e->d_bpic);
     (void)hipFree(e->d_bpl);
     (void)hipFree(e->d_brec);
@@ -526,6 +556,8 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
          hipHostMalloc(&e->h_chain, sizeof(MbChain) * e->nmb, hipHostMallocDefault) == hipSuccess &&
          hipHostMalloc(&e->h_spec, sizeof(int32_t) * e->mbh, hipHostMallocDefault) == hipSuccess &&
          hipHostMalloc(&e->h_progress, 64, hipHostMallocCoherent) == hipSuccess;
+    ok = ok && hipMalloc(&e->d_rows, sizeof(int32_t) * (e->mbh + 1)) == hipSuccess &&
+         hipMemsetAsync(e->d_rows, 0, sizeof(int32_t) * (e->mbh + 1), e->stream) == hipSuccess;
     // the per-address MB objects start zeroed (calloc'd by the reference, mb.c)
     ok = ok && hipMemsetAsync(e->d_st, 0, sizeof(MbState) * e->nmb, e->stream) == hipSuccess;
 #if defined(HL_PROFILE)
@@ -695,11 +727,8 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
         D.qpc = qpc;
         for (int c = 0; c < 3; ++c) D.pic[c] = cur[c];
         D.st = e->d_st;
-        const int ndiag = (e->mbw - 1) + 2 * (e->mbh - 1) + 1;
-        for (int d = 0; d < ndiag; ++d) {
-            const int n = diag_count(e->mbw, e->mbh, d);
-            if (n) k_deblock_diag<<<n, 64, 0, e->stream>>>(D, e->mbh, d);
-        }
+        HL_HIP_CHECK(hipMemsetAsync(e->d_rows, 0, sizeof(int32_t) * e->mbh, e->stream));
+        k_deblock_rows<<<e->mbh, 64, 0, e->stream>>>(D, e->d_rows, e->d_rows + e->mbh);
         HL_HIP_CHECK(hipGetLastError());
     }
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[3], e->stream));
@@ -1338,6 +1367,7 @@ struct SvcLayerDev {
     int64_t* d_len;                 // per MB bit counts, scanned in place; [nmb] = the total
     uint32_t *d_words, *h_words;    // slice data bits (big-endian words), device / pinned copy of the first esd_size bytes
     int64_t* h_total;               // pinned: total data bits
+    int32_t* d_rows;                // k_deblock_rows progress [mbh] + spin failures
     size_t words_bytes, esd_size;
     std::future<size_t> writing;  // the slice, written by a host thread while the GPU codes the next layer
 };
@@ -1355,6 +1385,13 @@ struct SvcState {
     int32_t* d_unpinned = nullptr;
     int32_t unpinned = 0;
     float ms_el = 0.f;               // enhancement-layer device time of the last access unit
+    // hl_amd_encode_layers_batch: the base layer of access unit i as the
+    // reference layer (picture of the base run, MB objects from its records)
+    uint8_t* ref0_pic[3] = {nullptr, nullptr, nullptr};
+    const MbState* ref0_st = nullptr;
+    MbState *d_bst = nullptr, *h_bst = nullptr;
+    size_t bst_cap = 0;
+    std::vector<std::vector<uint8_t>> bau, bhdr;  // access units / header bytes of the last batch
 };
 
 static void svc_free(hl_amd_encoder_t* e)
@@ -1371,6 +1408,7 @@ static void svc_free(hl_amd_encoder_t* e)
         (void)hipFree(L.d_st);
         if (L.writing.valid()) L.writing.wait();
         (void)hipFree(L.d_len);
+        (void)hipFree(L.d_rows);
         (void)hipFree(L.d_words);
         (void)hipHostFree(L.h_words);
         (void)hipHostFree(L.h_total);
@@ -1381,6 +1419,8 @@ static void svc_free(hl_amd_encoder_t* e)
         if (L.ev_t1) (void)hipEventDestroy(L.ev_t1);
     }
     (void)hipFree(s->d_unpinned);
+    (void)hipFree(s->d_bst);
+    (void)hipHostFree(s->h_bst);
     delete s;
     e->svc = nullptr;
 }
@@ -1422,7 +1462,9 @@ static int32_t svc_alloc(hl_amd_encoder_t* e)
         L.words_bytes = (size_t)L.nmb * 2048 + 4096;
         ok = ok && hipMalloc(&L.d_len, sizeof(int64_t) * (L.nmb + 1)) == hipSuccess && hipMalloc(&L.d_words, L.words_bytes) == hipSuccess &&
              hipHostMalloc(&L.h_words, L.esd_size + 64, hipHostMallocDefault) == hipSuccess &&
-             hipHostMalloc(&L.h_total, sizeof(int64_t), hipHostMallocDefault) == hipSuccess;
+             hipHostMalloc(&L.h_total, sizeof(int64_t), hipHostMallocDefault) == hipSuccess &&
+             hipMalloc(&L.d_rows, sizeof(int32_t) * (L.mbh + 1)) == hipSuccess &&
+             hipMemsetAsync(L.d_rows, 0, sizeof(int32_t) * (L.mbh + 1), e->stream) == hipSuccess;
         const StreamParams sp{L.W, L.H, e->p.qp, e->p.deblock};
         L.scratch.resize(slice_scratch_bytes(sp));
         L.out.resize(slice_scratch_bytes(sp) + 64);
@@ -1436,7 +1478,14 @@ static int32_t svc_alloc(hl_amd_encoder_t* e)
 // current (deblocked) picture and macroblock objects of layer l
 static void svc_layer_ptrs(hl_amd_encoder_t* e, int l, uint8_t* const*& pic, MbState*& st, int& W, int& H, int& nmb)
 {
-    if (l == 0) {
+    if (l == 0 && e->svc->ref0_st) {
+        pic = e->svc->ref0_pic;
+        st = const_cast<MbState*>(e->svc->ref0_st);
+        W = e->W;
+        H = e->H;
+        nmb = e->nmb;
+    }
+    else if (l == 0) {
         pic = e->d_pic[e->cur ^ 1];
         st = e->d_st;
         W = e->W;
@@ -1512,11 +1561,8 @@ static int32_t svc_encode_el(hl_amd_encoder_t* e, int l, const uint8_t* y, const
         D.qpc = qpc;
         for (int c = 0; c < 3; ++c) D.pic[c] = cur[c];
         D.st = L.d_st;
-        const int ndiag = (L.mbw - 1) + 2 * (L.mbh - 1) + 1;
-        for (int d = 0; d < ndiag; ++d) {
-            const int n = diag_count(L.mbw, L.mbh, d);
-            if (n) k_deblock_diag<<<n, 64, 0, e->stream>>>(D, L.mbh, d);
-        }
+        HL_HIP_CHECK(hipMemsetAsync(L.d_rows, 0, sizeof(int32_t) * L.mbh, e->stream));
+        k_deblock_rows<<<L.mbh, 64, 0, e->stream>>>(D, L.d_rows, L.d_rows + L.mbh);
         HL_HIP_CHECK(hipGetLastError());
     }
     // slice data serialised on the GPU (hl_cavlc.h)
@@ -1798,3 +1844,130 @@ extern "C" int32_t hl_amd_import_layer(hl_amd_encoder_t* e, int32_t layer, const
 }
 
 extern "C" float hl_amd_svc_layer_ms(hl_amd_encoder_t* e) { return e && e->svc ? e->svc->ms_el : -1.f; }
+
+// The fields of a macroblock object the inter-layer derivations read
+// (hl_svc.h svc_derive), from the macroblock's record
+static void state_from_record(const MbRecord& r, MbState& m)
+{
+    memset(&m, 0, sizeof(m));
+    m.e_type = r.e_type;
+    m.flags = r.flags;
+    m.pm0 = r.pm0;
+    m.cbp_l = r.cbp_l;
+    m.cbp_c = r.cbp_c;
+    m.cbp_l4x4 = r.cbp_l4x4;
+    m.num_part = r.num_part;
+    const bool p16x8 = r.e_type == ET_P16x8, p8x16 = r.e_type == ET_P8x16, p8x8 = r.e_type == ET_P8x8 || r.e_type == ET_P8x8REF0;
+    m.part_w = (p8x16 || p8x8) ? 8 : 16;
+    m.part_h = (p16x8 || p8x8) ? 8 : 16;
+    for (int i = 0; i < 4; ++i) {
+        const int st = p8x8 ? r.sub_mb_type[i] : 0;
+        m.sub_w[i] = (st == 2 || st == 3) ? 4 : 8;
+        m.sub_h[i] = (st == 1 || st == 3) ? 4 : 8;
+        for (int j = 0; j < 4; ++j) {
+            m.mv[i][j][0] = r.mv[i][j][0];
+            m.mv[i][j][1] = r.mv[i][j][1];
+        }
+    }
+}
+
+// n access units of every layer, planes resident in HBM:
+// planes[(l * n + i) * 3 + c] is plane c of layer l's frame of access unit
+// i.  The base-layer pictures are coded first, frame-pipelined
+// (hl_amd_encode_batch), then the enhancement layers access unit by access
+// unit from the base run's pictures and records.  results[i] = access unit
+// i as the calls of hl_amd_encode_layer would give it: HDR with every header
+// set those calls signal, in order, and DATA.  No reference interface (a
+// throughput entry point, like hl_amd_encode_batch).
+extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, int32_t layers, const uint8_t* const* planes,
+                                              hl_amd_result_t* results)
+{
+    if (!e || n <= 0 || !planes || !results) return HL_AMD_ERROR_INVALID_PARAMETER;
+    SvcState* s = e->svc;
+    if (!s || (int)s->w.size() != layers || layers < 2) return HL_AMD_ERROR_INVALID_STATE;
+    for (int i = 0; i < 3 * n * layers; ++i)
+        if (!planes[i]) return HL_AMD_ERROR_INVALID_PARAMETER;
+    int32_t rc = svc_start(e);
+    if (rc != HL_AMD_SUCCESS) return rc;
+    if (s->first != 0 || s->last != layers - 1 || s->next != 0) return HL_AMD_ERROR_INVALID_STATE;
+    // 1. the base layer, frame-pipelined
+    std::vector<const uint8_t*> Y(n), U(n), V(n);
+    for (int i = 0; i < n; ++i) {
+        Y[i] = planes[i * 3 + 0];
+        U[i] = planes[i * 3 + 1];
+        V[i] = planes[i * 3 + 2];
+    }
+    std::vector<hl_amd_result_t> br(n);
+    rc = hl_amd_encode_batch(e, n, Y.data(), U.data(), V.data(), br.data());
+    if (rc != HL_AMD_SUCCESS) return rc;
+    // 2. the base pictures' macroblock objects (their records hold every field
+    // the derivations read), to the GPU in one copy
+    const size_t nmb0 = e->nmb;
+    if (s->bst_cap < (size_t)n) {
+        (void)hipFree(s->d_bst);
+        (void)hipHostFree(s->h_bst);
+        s->d_bst = s->h_bst = nullptr;
+        s->bst_cap = 0;
+        if (hipMalloc(&s->d_bst, sizeof(MbState) * nmb0 * n) != hipSuccess ||
+            hipHostMalloc(&s->h_bst, sizeof(MbState) * nmb0 * n, hipHostMallocDefault) != hipSuccess)
+            return HL_AMD_ERROR_OUTOFMEMMORY;
+        s->bst_cap = n;
+    }
+    for (int i = 0; i < n; ++i) {
+        if (!e->last_recs[i]) return HL_AMD_ERROR_INVALID_STATE;  // a run re-encoded picture by picture kept no records
+        for (size_t a = 0; a < nmb0; ++a) state_from_record(e->last_recs[i][a], s->h_bst[i * nmb0 + a]);
+    }
+    HL_HIP_CHECK(hipMemcpyAsync(s->d_bst, s->h_bst, sizeof(MbState) * nmb0 * n, hipMemcpyHostToDevice, e->stream));
+    // 3. the enhancement layers, access unit by access unit
+    s->bau.resize(n);
+    s->bhdr.resize(n);
+    const size_t ys = (size_t)e->W * e->H, cs = ys / 4;
+    static const uint8_t scp[3] = {0, 0, 1};
+    for (int i = 0; i < n && rc == HL_AMD_SUCCESS; ++i) {
+        const hl_amd_result_t& b = br[i];
+        s->au_intra = b.data_size > 0 && (b.data[0] & 31) == 5;  // the base picture is an IDR picture
+        uint8_t* bp = const_cast<uint8_t*>(e->last_pic[i]);
+        if (bp) {
+            s->ref0_pic[0] = bp;
+            s->ref0_pic[1] = bp + ys;
+            s->ref0_pic[2] = bp + ys + cs;
+        }
+        else {
+            for (int c = 0; c < 3; ++c) s->ref0_pic[c] = e->d_pic[e->cur ^ 1][c];
+        }
+        s->ref0_st = s->d_bst + i * nmb0;
+        std::vector<uint8_t>& hdr = s->bhdr[i];
+        hdr.clear();
+        if (b.type & HL_AMD_RESULT_TYPE_HDR) {
+            hdr.assign(b.hdr, b.hdr + b.hdr_size);
+            s->hdr_layers = std::max(s->hdr_layers, 1);
+        }
+        uint8_t pre[5];
+        write_prefix_nal(s->au_intra, pre);
+        s->au.assign(pre, pre + 5);
+        s->au.insert(s->au.end(), scp, scp + 3);
+        s->au.insert(s->au.end(), b.data, b.data + b.data_size);
+        s->ms_el = 0.f;
+        for (int l = 1; l < layers && rc == HL_AMD_SUCCESS; ++l) {
+            const uint8_t* const* p = planes + ((size_t)l * n + i) * 3;
+            rc = svc_encode_el(e, l, p[0], p[1], p[2]);
+            if (rc == HL_AMD_SUCCESS && l >= s->hdr_layers) {
+                std::vector<uint8_t> h(1024);
+                const StreamParams bp0{s->w[0], s->h[0], e->p.qp, e->p.deblock};
+                h.resize(write_svc_headers(bp0, s->w.data(), s->h.data(), l + 1, h.data(), h.size()));
+                hdr.insert(hdr.end(), h.begin(), h.end());
+                s->hdr_layers = l + 1;
+            }
+        }
+        if (rc == HL_AMD_SUCCESS) rc = svc_join(e, layers - 1);
+        s->bau[i] = s->au;
+        results[i].type = HL_AMD_RESULT_TYPE_DATA | (hdr.empty() ? 0 : HL_AMD_RESULT_TYPE_HDR);
+        results[i].hdr = hdr.empty() ? nullptr : hdr.data();
+        results[i].hdr_size = hdr.size();
+        results[i].data = s->bau[i].data();
+        results[i].data_size = s->bau[i].size();
+    }
+    s->ref0_st = nullptr;
+    for (int c = 0; c < 3; ++c) s->ref0_pic[c] = nullptr;
+    return rc;
+}

@@ -218,6 +218,17 @@ size_t hl_amd_layer_state_bytes(hl_amd_encoder_t* encoder, int32_t layer);
 int32_t hl_amd_export_layer(hl_amd_encoder_t* encoder, int32_t layer, void* dst_device);
 int32_t hl_amd_import_layer(hl_amd_encoder_t* encoder, int32_t layer, const void* src_device);
 
+/* n access units of every layer (planes in HBM; planes[(l * n + i) * 3 + c]
+ * = plane c of layer l's frame of access unit i), as if by the
+ * hl_amd_encode_layer calls for them: the base-layer pictures are coded
+ * frame-pipelined (hl_amd_encode_batch), then every enhancement layer.
+ * results[i] = access unit i: HDR with every header set those calls signal,
+ * in order, and DATA; valid until the next call.  Needs every layer coded by
+ * this encoder (no layer range).  No reference interface: a throughput entry
+ * point like hl_amd_encode_batch. */
+int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* encoder, int32_t n, int32_t layers, const uint8_t* const* planes,
+                                   hl_amd_result_t* results);
+
 /* device time (ms) of the enhancement layers of the last access unit (with
  * hl_amd_set_timing on) */
 float hl_amd_svc_layer_ms(hl_amd_encoder_t* encoder);

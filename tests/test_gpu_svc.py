@@ -56,6 +56,35 @@ def test_svc_gpu_matches_reference(name):
     assert enc.unpinned() == 0
 
 
+@pytest.mark.parametrize("name,splits", [("c4_svc3_480x272_s41", (1, 31)), ("svc3_64x48_qp30_gop3", (2, 3, 5)),
+                                         ("svc2_qcif_qp36_nodb_gop2", (4,))])
+def test_svc_gpu_layers_batch(name, splits):
+    """hl_amd_encode_layers_batch (frame-pipelined base layer, then the
+    enhancement layers) equals the per-call stream, across batch boundaries."""
+    import torch
+
+    from hartallo_amd import SvcEncoder
+
+    g = GOLD[name]
+    L, w0, h0 = g["layers"], g["w0"], g["h0"]
+    clips = synth.svc_clips(w0 << (L - 1), h0 << (L - 1), L, g["frames"], g["seed"])
+    dev = [torch.from_numpy(clips[l][:splits[-1]]).cuda() for l in range(L)]
+    enc = SvcEncoder(w0, h0, L, g["qp"], g["me_range"], g["deblock"], g["gop"], g["early_term"])
+    md5s, lo = [], 0
+    for hi in splits:
+        ptrs = []
+        for l in range(L):
+            n = (w0 << l) * (h0 << l)
+            ptrs.append([(dev[l][i].data_ptr(), dev[l][i].data_ptr() + n, dev[l][i].data_ptr() + n + n // 4) for i in range(lo, hi)])
+        for r in enc.encode_layers_batch_device(ptrs):
+            md5s.append(md5(r.annexb()))
+        lo = hi
+    assert md5s == g["au_md5"][:splits[-1]]
+    for l in range(L):
+        assert md5(enc.layer_recon(l).tobytes()) == g["recon_md5"][l][splits[-1] - 1]
+    assert enc.unpinned() == 0
+
+
 @pytest.mark.parametrize("ranks", [2, 3])
 def test_svc_gpu_layer_sharded(ranks):
     import torch
