@@ -1083,6 +1083,20 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
             const int32_t rc = encode_frame(e, Y[k], U[k], V[k], &rr);
             if (rc) return rc;
             store_result(e, base + k, rr, &res[k]);
+            // keep every picture's records and reconstruction in the run
+            // buffers, as the pipelined run would (diagnostics, and the
+            // reference layer of hl_amd_encode_layers_batch)
+            memcpy(e->h_brec + nmb * k, e->h_rec, sizeof(MbRecord) * nmb);
+            memcpy(e->h_bchain + nmb * k, e->h_chain, sizeof(MbChain) * nmb);
+            uint8_t* dst = e->d_bpic + pic * k;
+            const size_t ys = (size_t)e->W * e->H, cs = ys / 4;
+            uint8_t** rp = e->d_pic[e->cur ^ 1];
+            HL_HIP_CHECK(hipMemcpyAsync(dst, rp[0], ys, hipMemcpyDeviceToDevice, e->stream));
+            HL_HIP_CHECK(hipMemcpyAsync(dst + ys, rp[1], cs, hipMemcpyDeviceToDevice, e->stream));
+            HL_HIP_CHECK(hipMemcpyAsync(dst + ys + cs, rp[2], cs, hipMemcpyDeviceToDevice, e->stream));
+            e->last_recs[base + k] = e->h_brec + nmb * k;
+            e->last_chain[base + k] = e->h_bchain + nmb * k;
+            e->last_pic[base + k] = dst;
         }
         e->reruns = 1;
         return HL_AMD_SUCCESS;
@@ -1890,6 +1904,9 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
     int32_t rc = svc_start(e);
     if (rc != HL_AMD_SUCCESS) return rc;
     if (s->first != 0 || s->last != layers - 1 || s->next != 0) return HL_AMD_ERROR_INVALID_STATE;
+    // under rate control every base picture takes the per-picture path and no
+    // run keeps the pictures' records: code such streams with hl_amd_encode_layer
+    if (e->rc) return HL_AMD_ERROR_NOT_IMPLEMENTED;
     // 1. the base layer, frame-pipelined
     std::vector<const uint8_t*> Y(n), U(n), V(n);
     for (int i = 0; i < n; ++i) {
@@ -1914,7 +1931,7 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
         s->bst_cap = n;
     }
     for (int i = 0; i < n; ++i) {
-        if (!e->last_recs[i]) return HL_AMD_ERROR_INVALID_STATE;  // a run re-encoded picture by picture kept no records
+        if (!e->last_recs[i]) return HL_AMD_ERROR_INVALID_STATE;
         for (size_t a = 0; a < nmb0; ++a) state_from_record(e->last_recs[i][a], s->h_bst[i * nmb0 + a]);
     }
     HL_HIP_CHECK(hipMemcpyAsync(s->d_bst, s->h_bst, sizeof(MbState) * nmb0 * n, hipMemcpyHostToDevice, e->stream));
