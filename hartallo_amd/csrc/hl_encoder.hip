@@ -110,24 +110,46 @@ __global__ __launch_bounds__(64) void k_deblock_diag(DeblockArgs D, int mbh, int
 // row, its MBs left to right; MB (x, y) waits until row y - 1 has finished
 // MB x + 1 -- the order of the anti-diagonal launches d = x + 2y, so every
 // edge sees the samples the reference's raster-order filter sees
-// (deblock.c:192-284).  Hand-offs as in k_pipeline: waves drained, a release
-// fence with its own wait, a relaxed flag; the consumer acquires.
+// (deblock.c:192-284).  Each MB is filtered in an LDS tile (DbTile,
+// hl_filters.h): its own rows are prefetched into registers during the
+// previous MB, the left apron is carried over, only the 4 rows above wait for
+// the row above; the bS values of the whole row (up to 256 MBs)
+// are computed before its first wait, off the chain of rows.  Hand-offs as
+// in k_pipeline: stores drained, a release fence, a relaxed flag; the
+// consumer acquires.
 __global__ __launch_bounds__(64) void k_deblock_rows(DeblockArgs D, int32_t* row_done, int32_t* err)
 {
-    const int y = blockIdx.x, tid = threadIdx.x;
-    for (int x = 0; x < D.mbw; ++x) {
+    __shared__ DbTile t;
+    const int y = blockIdx.x, tid = threadIdx.x, mbw = D.mbw;
+    uint32_t own_l = db_own_luma(D, 0, y, tid), own_c = tid < 32 ? db_own_chroma(D, 0, y, tid) : 0u;
+    int chunk0 = -kDbChunk;
+    for (int x = 0; x < mbw; ++x) {
+        __syncthreads();  // the previous MB's stores have read the tile
+        if (x - chunk0 >= kDbChunk) {
+            chunk0 = x;
+            const int n = min(kDbChunk, mbw - x) * 32;
+            for (int i = tid; i < n; i += 64) t.B[i >> 5][i & 31] = (uint8_t)deblock_edge_bs(D, y * mbw + x + (i >> 5), (i & 31) >> 2, i & 3);
+        }
+        if (x > 0) db_shift(t, tid);
+        __syncthreads();
+        db_put_own(t, tid, own_l, own_c);
+        if (x + 1 < mbw) {  // the next MB's own rows, in flight during this one
+            own_l = db_own_luma(D, x + 1, y, tid);
+            if (tid < 32) own_c = db_own_chroma(D, x + 1, y, tid);
+        }
         if (y > 0) {
-            if (tid == 0) spin_ge(row_done + y - 1, min(x + 2, D.mbw), err);
+            if (tid == 0) spin_ge(row_done + y - 1, min(x + 2, mbw), err);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
+            db_load_above(D, t, x, y, tid);
         }
-        const int addr = y * D.mbw + x;
+        __syncthreads();
+        const uint8_t* bs = t.B[x - chunk0];
         for (int step = 0; step < 8; ++step) {
-            if (tid < 32) deblock_mb_step(D, addr, step, tid);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            db_tile_step(D, t, bs, step, tid);
             __syncthreads();
         }
+        for (int j = tid; j < db_store_words(); j += 64) db_store(D, t, x, y, j);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (tid == 0) st_relaxed(row_done + y, x + 1);
@@ -454,6 +476,7 @@ struct hl_amd_encoder_s {
     uint8_t *d_bpic, *d_bpl;     // per picture: recon (Y|U|V), quarter-pel planes
     MbRecord *d_brec, *h_brec, *dh_brec;  // dh_brec: device address of the pinned h_brec (the run writes it)
     int32_t* h_progress;                  // pinned: pictures of the running run whose records are in h_brec
+    std::atomic<int> run_live{0};         // 1 while a pipelined run is on the GPU (h_progress counts its pictures)
     std::chrono::steady_clock::time_point run_t0;  // launch time of the running run (writer tracing)
     MbChain *d_bchain, *h_bchain;
     int32_t *d_bspec, *d_err;
@@ -1014,6 +1037,7 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     int32_t* d_progress = nullptr;
     HL_HIP_CHECK(hipHostGetDevicePointer((void**)&d_progress, e->h_progress, 0));
     __atomic_store_n(e->h_progress, 0, __ATOMIC_RELEASE);
+    e->run_live.store(1, std::memory_order_release);
     P.progress = d_progress;
     static const bool trace = getenv("HL_AMD_TRACE_WRITERS") != nullptr;
     static unsigned long long* h_clock = nullptr;
@@ -1024,7 +1048,8 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     }
     k_pipe_init<<<(unsigned)((nmb * m + 255) / 256), 256, 0, e->stream>>>(P, e->mbw, e->mbh);
     HL_HIP_CHECK(hipGetLastError());
-    int wgs = e->pipe_wg;
+    static const int env_wg = getenv("HL_AMD_PIPE_WG") ? atoi(getenv("HL_AMD_PIPE_WG")) : 0;  // experiments
+    int wgs = e->pipe_wg > 0 ? e->pipe_wg : env_wg;
     if (wgs <= 0) {  // one workgroup per resident slot of the device
         int dev = 0, cus = 0, occ = 0;
         HL_HIP_CHECK(hipGetDevice(&dev));
@@ -1052,6 +1077,7 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     std::vector<size_t> wsize;
     std::thread writers([&] { wsize = write_run(e, m, base, &abort); });
     const hipError_t serr = hipStreamSynchronize(e->stream);
+    e->run_live.store(0, std::memory_order_release);
     const auto tw0 = std::chrono::steady_clock::now();
     if (serr != hipSuccess || __atomic_load_n(e->h_progress, __ATOMIC_ACQUIRE) < m) abort = true;
     writers.join();
@@ -1384,6 +1410,7 @@ struct SvcLayerDev {
     int32_t* d_rows;                // k_deblock_rows progress [mbh] + spin failures
     size_t words_bytes, esd_size;
     std::future<size_t> writing;  // the slice, written by a host thread while the GPU codes the next layer
+    uint8_t* d_snap;              // the reference picture at the start of a layers batch (its redo after a base re-encode)
 };
 
 struct SvcState {
@@ -1403,9 +1430,21 @@ struct SvcState {
     // reference layer (picture of the base run, MB objects from its records)
     uint8_t* ref0_pic[3] = {nullptr, nullptr, nullptr};
     const MbState* ref0_st = nullptr;
+    // MB objects of a batch's base pictures (device, pinned staging)
     MbState *d_bst = nullptr, *h_bst = nullptr;
     size_t bst_cap = 0;
-    std::vector<std::vector<uint8_t>> bau, bhdr;  // access units / header bytes of the last batch
+    std::vector<std::vector<uint8_t>> bau, bhdr;    // access units / header bytes of the last batch
+    std::vector<std::vector<uint8_t>> elau, elhdr;  // their enhancement-layer slices / header NAL units
+    // the enhancement layers run on a stream of their own; `linked`: every
+    // enhancement-layer picture is ordered after the work queued on the
+    // encoder's stream and before what is queued there next (one stream's
+    // semantics, hl_amd_encode_layer); hl_amd_encode_layers_batch unlinks
+    // them to code access unit i's enhancement layers while the base run
+    // goes on with the pictures after i
+    hipStream_t est = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_base = nullptr;
+    bool linked = true;
+    int pipe_wg = 128;  // workgroups of a batch's base run: the rest of the device codes the enhancement layers
 };
 
 static void svc_free(hl_amd_encoder_t* e)
@@ -1420,6 +1459,7 @@ static void svc_free(hl_amd_encoder_t* e)
         }
         (void)hipFree(L.d_pl);
         (void)hipFree(L.d_st);
+        (void)hipFree(L.d_snap);
         if (L.writing.valid()) L.writing.wait();
         (void)hipFree(L.d_len);
         (void)hipFree(L.d_rows);
@@ -1435,6 +1475,10 @@ static void svc_free(hl_amd_encoder_t* e)
     (void)hipFree(s->d_unpinned);
     (void)hipFree(s->d_bst);
     (void)hipHostFree(s->h_bst);
+    if (s->ev_base) (void)hipEventDestroy(s->ev_base);
+    if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+    if (s->ev_join) (void)hipEventDestroy(s->ev_join);
+    if (s->est) (void)hipStreamDestroy(s->est);
     delete s;
     e->svc = nullptr;
 }
@@ -1444,7 +1488,11 @@ static int32_t svc_alloc(hl_amd_encoder_t* e)
     SvcState* s = e->svc;
     s->el = std::vector<SvcLayerDev>(s->w.size() - 1);  // value-initialised: null pointers until allocated
     bool ok = hipMalloc(&s->d_unpinned, sizeof(int32_t)) == hipSuccess &&
-              hipMemsetAsync(s->d_unpinned, 0, sizeof(int32_t), e->stream) == hipSuccess;
+              hipMemsetAsync(s->d_unpinned, 0, sizeof(int32_t), e->stream) == hipSuccess &&
+              hipStreamCreateWithFlags(&s->est, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&s->ev_base, hipEventDisableTiming) == hipSuccess;
     for (size_t l = 1; l < s->w.size() && ok; ++l) {
         SvcLayerDev& L = s->el[l - 1];
         L.W = s->w[l];
@@ -1478,6 +1526,7 @@ static int32_t svc_alloc(hl_amd_encoder_t* e)
              hipHostMalloc(&L.h_words, L.esd_size + 64, hipHostMallocDefault) == hipSuccess &&
              hipHostMalloc(&L.h_total, sizeof(int64_t), hipHostMallocDefault) == hipSuccess &&
              hipMalloc(&L.d_rows, sizeof(int32_t) * (L.mbh + 1)) == hipSuccess &&
+             hipMalloc(&L.d_snap, (size_t)L.W * L.H * 3 / 2) == hipSuccess &&
              hipMemsetAsync(L.d_rows, 0, sizeof(int32_t) * (L.mbh + 1), e->stream) == hipSuccess;
         const StreamParams sp{L.W, L.H, e->p.qp, e->p.deblock};
         L.scratch.resize(slice_scratch_bytes(sp));
@@ -1530,10 +1579,15 @@ static int32_t svc_encode_el(hl_amd_encoder_t* e, int l, const uint8_t* y, const
     int rW, rH, rn;
     svc_layer_ptrs(e, l - 1, rpic, rst, rW, rH, rn);
     if (rW * 2 != L.W || rH * 2 != L.H) return HL_AMD_ERROR_INVALID_STATE;
-    HL_HIP_CHECK(hipEventRecord(L.ev_t0, e->stream));
+    hipStream_t st = s->est;
+    if (s->linked) {
+        HL_HIP_CHECK(hipEventRecord(s->ev_fork, e->stream));
+        HL_HIP_CHECK(hipStreamWaitEvent(st, s->ev_fork, 0));
+    }
+    HL_HIP_CHECK(hipEventRecord(L.ev_t0, st));
     if (!intra) {
         const dim3 grid((L.W + 2 * kPad + kPlTileW - 1) / kPlTileW, (L.H + 2 * kPad + kPlTileH - 1) / kPlTileH);
-        k_planes<<<grid, 256, 0, e->stream>>>(ref[0], L.W, L.H, L.d_pl, L.pstride, (int)L.plsz);
+        k_planes<<<grid, 256, 0, st>>>(ref[0], L.W, L.H, L.d_pl, L.pstride, (int)L.plsz);
         HL_HIP_CHECK(hipGetLastError());
     }
     SvcArgs A{};
@@ -1563,7 +1617,7 @@ static int32_t svc_encode_el(hl_amd_encoder_t* e, int l, const uint8_t* y, const
     F.rec = L.d_rec;
     A.rst = rst;
     A.unpinned = s->d_unpinned;
-    k_svc_mb<<<L.nmb, 64, 0, e->stream>>>(A);
+    k_svc_mb<<<L.nmb, 64, 0, st>>>(A);
     HL_HIP_CHECK(hipGetLastError());
     if (e->p.deblock) {
         DeblockArgs D;
@@ -1575,24 +1629,28 @@ static int32_t svc_encode_el(hl_amd_encoder_t* e, int l, const uint8_t* y, const
         D.qpc = qpc;
         for (int c = 0; c < 3; ++c) D.pic[c] = cur[c];
         D.st = L.d_st;
-        HL_HIP_CHECK(hipMemsetAsync(L.d_rows, 0, sizeof(int32_t) * L.mbh, e->stream));
-        k_deblock_rows<<<L.mbh, 64, 0, e->stream>>>(D, L.d_rows, L.d_rows + L.mbh);
+        HL_HIP_CHECK(hipMemsetAsync(L.d_rows, 0, sizeof(int32_t) * L.mbh, st));
+        k_deblock_rows<<<L.mbh, 64, 0, st>>>(D, L.d_rows, L.d_rows + L.mbh);
         HL_HIP_CHECK(hipGetLastError());
     }
     // slice data serialised on the GPU (hl_cavlc.h)
     {
         const int nb = (L.nmb + 63) / 64;
-        HL_HIP_CHECK(hipMemsetAsync(L.d_words, 0, L.words_bytes, e->stream));
-        k_el_count<<<nb, 64, 0, e->stream>>>(L.d_rec, L.nmb, L.mbw, intra, L.d_len);
-        k_scan_excl<<<1, 1024, 0, e->stream>>>(L.d_len, L.nmb);
-        k_el_write<<<nb, 64, 0, e->stream>>>(L.d_rec, L.nmb, L.mbw, intra, L.d_len, L.d_words);
+        HL_HIP_CHECK(hipMemsetAsync(L.d_words, 0, L.words_bytes, st));
+        k_el_count<<<nb, 64, 0, st>>>(L.d_rec, L.nmb, L.mbw, intra, L.d_len);
+        k_scan_excl<<<1, 1024, 0, st>>>(L.d_len, L.nmb);
+        k_el_write<<<nb, 64, 0, st>>>(L.d_rec, L.nmb, L.mbw, intra, L.d_len, L.d_words);
         HL_HIP_CHECK(hipGetLastError());
     }
-    HL_HIP_CHECK(hipEventRecord(L.ev_t1, e->stream));
-    HL_HIP_CHECK(hipMemcpyAsync(L.h_total, L.d_len + L.nmb, sizeof(int64_t), hipMemcpyDeviceToHost, e->stream));
-    HL_HIP_CHECK(hipMemcpyAsync(L.h_words, L.d_words, L.esd_size + 64, hipMemcpyDeviceToHost, e->stream));
-    HL_HIP_CHECK(hipMemcpyAsync(&s->unpinned, s->d_unpinned, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
-    HL_HIP_CHECK(hipEventRecord(L.ev_rec, e->stream));
+    HL_HIP_CHECK(hipEventRecord(L.ev_t1, st));
+    HL_HIP_CHECK(hipMemcpyAsync(L.h_total, L.d_len + L.nmb, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HL_HIP_CHECK(hipMemcpyAsync(L.h_words, L.d_words, L.esd_size + 64, hipMemcpyDeviceToHost, st));
+    HL_HIP_CHECK(hipMemcpyAsync(&s->unpinned, s->d_unpinned, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HL_HIP_CHECK(hipEventRecord(L.ev_rec, st));
+    if (s->linked) {
+        HL_HIP_CHECK(hipEventRecord(s->ev_join, st));
+        HL_HIP_CHECK(hipStreamWaitEvent(e->stream, s->ev_join, 0));
+    }
     // the header, trailing bits and escaping are added by a host thread once
     // the bits arrived, while the GPU codes the layers above; joined by the
     // access unit's last call
@@ -1887,11 +1945,15 @@ static void state_from_record(const MbRecord& r, MbState& m)
 
 // n access units of every layer, planes resident in HBM:
 // planes[(l * n + i) * 3 + c] is plane c of layer l's frame of access unit
-// i.  The base-layer pictures are coded first, frame-pipelined
-// (hl_amd_encode_batch), then the enhancement layers access unit by access
-// unit from the base run's pictures and records.  results[i] = access unit
-// i as the calls of hl_amd_encode_layer would give it: HDR with every header
-// set those calls signal, in order, and DATA.  No reference interface (a
+// i.  The base pictures are coded frame-pipelined (hl_amd_encode_batch, one
+// run on part of the device); a host thread codes access unit i's
+// enhancement layers on their own stream as soon as the run has published
+// base picture i (its records in host memory, its picture in the run's
+// buffers), while the run goes on.  If the run is re-encoded picture by
+// picture (encode_run), the enhancement layers are rolled back and coded
+// again from the final base pictures.  results[i] = access unit i as the
+// calls of hl_amd_encode_layer would give it: HDR with every header set
+// those calls signal, in order, and DATA.  No reference interface (a
 // throughput entry point, like hl_amd_encode_batch).
 extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, int32_t layers, const uint8_t* const* planes,
                                               hl_amd_result_t* results)
@@ -1907,84 +1969,176 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
     // under rate control every base picture takes the per-picture path and no
     // run keeps the pictures' records: code such streams with hl_amd_encode_layer
     if (e->rc) return HL_AMD_ERROR_NOT_IMPLEMENTED;
-    // 1. the base layer, frame-pipelined
-    std::vector<const uint8_t*> Y(n), U(n), V(n);
-    for (int i = 0; i < n; ++i) {
-        Y[i] = planes[i * 3 + 0];
-        U[i] = planes[i * 3 + 1];
-        V[i] = planes[i * 3 + 2];
-    }
-    std::vector<hl_amd_result_t> br(n);
-    rc = hl_amd_encode_batch(e, n, Y.data(), U.data(), V.data(), br.data());
-    if (rc != HL_AMD_SUCCESS) return rc;
-    // 2. the base pictures' macroblock objects (their records hold every field
-    // the derivations read), to the GPU in one copy
-    const size_t nmb0 = e->nmb;
-    if (s->bst_cap < (size_t)n) {
+    const size_t nmb0 = e->nmb, ys = (size_t)e->W * e->H, cs = ys / 4, pic = ys + 2 * cs;
+    const int chunk = std::min(n, kMaxRun);
+    if (s->bst_cap < (size_t)chunk) {
         (void)hipFree(s->d_bst);
         (void)hipHostFree(s->h_bst);
         s->d_bst = s->h_bst = nullptr;
         s->bst_cap = 0;
-        if (hipMalloc(&s->d_bst, sizeof(MbState) * nmb0 * n) != hipSuccess ||
-            hipHostMalloc(&s->h_bst, sizeof(MbState) * nmb0 * n, hipHostMallocDefault) != hipSuccess)
+        if (hipMalloc(&s->d_bst, sizeof(MbState) * nmb0 * chunk) != hipSuccess ||
+            hipHostMalloc(&s->h_bst, sizeof(MbState) * nmb0 * chunk, hipHostMallocDefault) != hipSuccess)
             return HL_AMD_ERROR_OUTOFMEMMORY;
-        s->bst_cap = n;
+        s->bst_cap = chunk;
     }
-    for (int i = 0; i < n; ++i) {
-        if (!e->last_recs[i]) return HL_AMD_ERROR_INVALID_STATE;
-        for (size_t a = 0; a < nmb0; ++a) state_from_record(e->last_recs[i][a], s->h_bst[i * nmb0 + a]);
+    s->bau.assign(n, {});
+    s->bhdr.assign(n, {});
+    s->elau.assign(n, {});
+    s->elhdr.assign(n, {});
+    // picture types of the batch, as the base encoder will choose them
+    std::vector<uint8_t> intra(n);
+    for (int i = 0, gl = e->gop_left; i < n; ++i) {
+        intra[i] = gl <= 0;
+        if (intra[i]) gl = e->p.gop_size;
+        --gl;
     }
-    HL_HIP_CHECK(hipMemcpyAsync(s->d_bst, s->h_bst, sizeof(MbState) * nmb0 * n, hipMemcpyHostToDevice, e->stream));
-    // 3. the enhancement layers, access unit by access unit
-    s->bau.resize(n);
-    s->bhdr.resize(n);
-    const size_t ys = (size_t)e->W * e->H, cs = ys / 4;
-    static const uint8_t scp[3] = {0, 0, 1};
-    for (int i = 0; i < n && rc == HL_AMD_SUCCESS; ++i) {
-        const hl_amd_result_t& b = br[i];
-        s->au_intra = b.data_size > 0 && (b.data[0] & 31) == 5;  // the base picture is an IDR picture
-        uint8_t* bp = const_cast<uint8_t*>(e->last_pic[i]);
-        if (bp) {
-            s->ref0_pic[0] = bp;
-            s->ref0_pic[1] = bp + ys;
-            s->ref0_pic[2] = bp + ys + cs;
-        }
-        else {
-            for (int c = 0; c < 3; ++c) s->ref0_pic[c] = e->d_pic[e->cur ^ 1][c];
-        }
-        s->ref0_st = s->d_bst + i * nmb0;
-        std::vector<uint8_t>& hdr = s->bhdr[i];
-        hdr.clear();
-        if (b.type & HL_AMD_RESULT_TYPE_HDR) {
-            hdr.assign(b.hdr, b.hdr + b.hdr_size);
-            s->hdr_layers = std::max(s->hdr_layers, 1);
-        }
-        uint8_t pre[5];
-        write_prefix_nal(s->au_intra, pre);
-        s->au.assign(pre, pre + 5);
-        s->au.insert(s->au.end(), scp, scp + 3);
-        s->au.insert(s->au.end(), b.data, b.data + b.data_size);
-        s->ms_el = 0.f;
-        for (int l = 1; l < layers && rc == HL_AMD_SUCCESS; ++l) {
-            const uint8_t* const* p = planes + ((size_t)l * n + i) * 3;
-            rc = svc_encode_el(e, l, p[0], p[1], p[2]);
-            if (rc == HL_AMD_SUCCESS && l >= s->hdr_layers) {
-                std::vector<uint8_t> h(1024);
-                const StreamParams bp0{s->w[0], s->h[0], e->p.qp, e->p.deblock};
-                h.resize(write_svc_headers(bp0, s->w.data(), s->h.data(), l + 1, h.data(), h.size()));
-                hdr.insert(hdr.end(), h.begin(), h.end());
-                s->hdr_layers = l + 1;
+    // what the caller queued on the encoder's stream before comes first
+    HL_HIP_CHECK(hipEventRecord(s->ev_fork, e->stream));
+    HL_HIP_CHECK(hipStreamWaitEvent(s->est, s->ev_fork, 0));
+    s->linked = false;
+    std::atomic<bool> base_done{false};
+    // the enhancement layers of access units [i0, i0 + m) (base pictures
+    // k = i - i0 of the current chunk): from the running run while it is
+    // live, else from the chunk's final results
+    auto el_chunk = [&](int i0, int m, bool wait_run) -> int32_t {
+        int32_t r = HL_AMD_SUCCESS;
+        for (int k = 0; k < m && r == HL_AMD_SUCCESS; ++k) {
+            const int i = i0 + k;
+            const MbRecord* recs;
+            const uint8_t* bp;
+            for (;;) {
+                if (base_done.load(std::memory_order_acquire)) {
+                    recs = e->last_recs[k];
+                    bp = e->last_pic[k];
+                    break;
+                }
+                if (wait_run && e->run_live.load(std::memory_order_acquire) && __atomic_load_n(e->h_progress, __ATOMIC_ACQUIRE) > k) {
+                    recs = e->h_brec + nmb0 * k;
+                    bp = e->d_bpic + pic * k;
+                    break;
+                }
+                std::this_thread::sleep_for(std::chrono::microseconds(20));
             }
+            if (!recs) return HL_AMD_ERROR_INVALID_STATE;
+            MbState* hs = s->h_bst + nmb0 * k;
+            for (size_t a = 0; a < nmb0; ++a) state_from_record(recs[a], hs[a]);
+            HL_HIP_CHECK(hipMemcpyAsync(s->d_bst + nmb0 * k, hs, sizeof(MbState) * nmb0, hipMemcpyHostToDevice, s->est));
+            if (bp) {
+                s->ref0_pic[0] = const_cast<uint8_t*>(bp);
+                s->ref0_pic[1] = const_cast<uint8_t*>(bp) + ys;
+                s->ref0_pic[2] = const_cast<uint8_t*>(bp) + ys + cs;
+            }
+            else
+                for (int c = 0; c < 3; ++c) s->ref0_pic[c] = e->d_pic[e->cur ^ 1][c];  // a lone picture: the base encoder's current reference
+            s->ref0_st = s->d_bst + nmb0 * k;
+            s->au_intra = intra[i] != 0;
+            s->au.clear();
+            s->ms_el = 0.f;
+            std::vector<uint8_t>& hdr = s->elhdr[i];
+            hdr.clear();
+            for (int l = 1; l < layers && r == HL_AMD_SUCCESS; ++l) {
+                const uint8_t* const* p = planes + ((size_t)l * n + i) * 3;
+                r = svc_encode_el(e, l, p[0], p[1], p[2]);
+                if (r == HL_AMD_SUCCESS && l >= s->hdr_layers) {  // hl_codec_264.c:577-687: a new (subset) SPS and PPS
+                    std::vector<uint8_t> h(1024);
+                    const StreamParams bp0{s->w[0], s->h[0], e->p.qp, e->p.deblock};
+                    h.resize(write_svc_headers(bp0, s->w.data(), s->h.data(), l + 1, h.data(), h.size()));
+                    hdr.insert(hdr.end(), h.begin(), h.end());
+                    s->hdr_layers = l + 1;
+                }
+            }
+            if (r == HL_AMD_SUCCESS) r = svc_join(e, layers - 1);
+            s->elau[i].swap(s->au);
         }
-        if (rc == HL_AMD_SUCCESS) rc = svc_join(e, layers - 1);
-        s->bau[i] = s->au;
-        results[i].type = HL_AMD_RESULT_TYPE_DATA | (hdr.empty() ? 0 : HL_AMD_RESULT_TYPE_HDR);
-        results[i].hdr = hdr.empty() ? nullptr : hdr.data();
-        results[i].hdr_size = hdr.size();
-        results[i].data = s->bau[i].data();
-        results[i].data_size = s->bau[i].size();
+        return r;
+    };
+    const int saved_wg = e->pipe_wg;
+    const char* wenv = getenv("HL_AMD_PIPE_WG");
+    if (e->pipe_wg == 0 && !(wenv && atoi(wenv) > 0)) e->pipe_wg = s->pipe_wg;
+    std::vector<const uint8_t*> Y(chunk), U(chunk), V(chunk);
+    std::vector<hl_amd_result_t> br(chunk);
+    static const uint8_t scp[3] = {0, 0, 1};
+    for (int i0 = 0; i0 < n && rc == HL_AMD_SUCCESS; i0 += chunk) {
+        const int m = std::min(chunk, n - i0);
+        for (int k = 0; k < m; ++k) {
+            Y[k] = planes[(i0 + k) * 3 + 0];
+            U[k] = planes[(i0 + k) * 3 + 1];
+            V[k] = planes[(i0 + k) * 3 + 2];
+        }
+        // the enhancement layers' cross-access-unit state, for a redo
+        struct Snap {
+            int cur, pict_count;
+        };
+        std::vector<Snap> snap(layers - 1);
+        const int hdr_layers0 = s->hdr_layers;
+        for (int l = 1; l < layers && rc == HL_AMD_SUCCESS; ++l) {
+            SvcLayerDev& L = s->el[l - 1];
+            snap[l - 1] = {L.cur, L.pict_count};
+            const size_t ly = (size_t)L.W * L.H, lc = ly / 4;
+            uint8_t** ref = L.d_pic[L.cur ^ 1];
+            if (hipMemcpyAsync(L.d_snap, ref[0], ly, hipMemcpyDeviceToDevice, s->est) != hipSuccess ||
+                hipMemcpyAsync(L.d_snap + ly, ref[1], lc, hipMemcpyDeviceToDevice, s->est) != hipSuccess ||
+                hipMemcpyAsync(L.d_snap + ly + lc, ref[2], lc, hipMemcpyDeviceToDevice, s->est) != hipSuccess)
+                rc = HL_AMD_ERROR_SYSTEM;
+        }
+        if (rc != HL_AMD_SUCCESS) break;
+        base_done.store(false, std::memory_order_release);
+        std::future<int32_t> el = std::async(std::launch::async, el_chunk, i0, m, true);
+        rc = hl_amd_encode_batch(e, m, Y.data(), U.data(), V.data(), br.data());
+        base_done.store(true, std::memory_order_release);
+        int32_t rel = el.get();
+        if (rc != HL_AMD_SUCCESS) break;
+        if (rel == HL_AMD_SUCCESS && e->reruns) {
+            // the run was re-encoded picture by picture: roll the enhancement
+            // layers back and code them again from the final base pictures
+            if (hipStreamSynchronize(s->est) != hipSuccess) {
+                rc = HL_AMD_ERROR_SYSTEM;
+                break;
+            }
+            for (int l = 1; l < layers; ++l) {
+                SvcLayerDev& L = s->el[l - 1];
+                L.cur = snap[l - 1].cur;
+                L.pict_count = snap[l - 1].pict_count;
+                const size_t ly = (size_t)L.W * L.H, lc = ly / 4;
+                uint8_t** ref = L.d_pic[L.cur ^ 1];
+                HL_HIP_CHECK(hipMemcpyAsync(ref[0], L.d_snap, ly, hipMemcpyDeviceToDevice, s->est));
+                HL_HIP_CHECK(hipMemcpyAsync(ref[1], L.d_snap + ly, lc, hipMemcpyDeviceToDevice, s->est));
+                HL_HIP_CHECK(hipMemcpyAsync(ref[2], L.d_snap + ly + lc, lc, hipMemcpyDeviceToDevice, s->est));
+            }
+            s->hdr_layers = hdr_layers0;
+            HL_HIP_CHECK(hipEventRecord(s->ev_base, e->stream));
+            HL_HIP_CHECK(hipStreamWaitEvent(s->est, s->ev_base, 0));
+            rel = el_chunk(i0, m, false);
+        }
+        rc = rel;
+        // access unit = prefix NAL unit, base slice, enhancement-layer slices
+        for (int k = 0; k < m && rc == HL_AMD_SUCCESS; ++k) {
+            const int i = i0 + k;
+            const hl_amd_result_t& b = br[k];
+            uint8_t pre[5];
+            write_prefix_nal(intra[i] != 0, pre);
+            std::vector<uint8_t>& au = s->bau[i];
+            au.assign(pre, pre + 5);
+            au.insert(au.end(), scp, scp + 3);
+            au.insert(au.end(), b.data, b.data + b.data_size);
+            au.insert(au.end(), scp, scp + 3);
+            au.insert(au.end(), s->elau[i].begin(), s->elau[i].end());
+            std::vector<uint8_t>& hdr = s->bhdr[i];
+            if (b.type & HL_AMD_RESULT_TYPE_HDR) hdr.assign(b.hdr, b.hdr + b.hdr_size);
+            hdr.insert(hdr.end(), s->elhdr[i].begin(), s->elhdr[i].end());
+            results[i].type = HL_AMD_RESULT_TYPE_DATA | (hdr.empty() ? 0 : HL_AMD_RESULT_TYPE_HDR);
+            results[i].hdr = hdr.empty() ? nullptr : hdr.data();
+            results[i].hdr_size = hdr.size();
+            results[i].data = au.data();
+            results[i].data_size = au.size();
+        }
     }
+    e->pipe_wg = saved_wg;
+    s->linked = true;
     s->ref0_st = nullptr;
     for (int c = 0; c < 3; ++c) s->ref0_pic[c] = nullptr;
+    // what is queued on the encoder's stream next sees the enhancement layers
+    HL_HIP_CHECK(hipEventRecord(s->ev_join, s->est));
+    HL_HIP_CHECK(hipStreamWaitEvent(e->stream, s->ev_join, 0));
     return rc;
 }

@@ -150,6 +150,128 @@ struct DeblockArgs {
     const MbState* st;
 };
 
+// bS of segment k (0..3) of luma edge e of macroblock addr -- e 0..3 the
+// vertical edges 0, 4, 8, 12, e 4..7 the horizontal ones -- or 0 where the
+// edge is not filtered (picture border, or an internal edge of a 16x16
+// prediction without luma residual).  The chroma edges 0 / 4 use the bS of
+// luma edges 0 / 8 (8.7.2.1: chroma bS is the bS of the corresponding luma
+// samples).
+HD int deblock_edge_bs(const DeblockArgs& D, int addr, int e, int k)
+{
+    const int mbx = addr % D.mbw, mby = addr / D.mbw;
+    const MbState& Q = D.st[addr];
+    const bool vert = e < 4;
+    const int edge = (e & 3) * 4;
+    const bool mb_edge = edge == 0;
+    if (mb_edge && (vert ? mbx == 0 : mby == 0)) return 0;
+    const bool internal = !((Q.e_type == ET_P16x16 || (Q.flags & FL_SKIP)) && !Q.cbp_l);
+    if (!mb_edge && !internal) return 0;
+    const MbState& P = mb_edge ? (vert ? D.st[addr - 1] : D.st[addr - D.mbw]) : Q;
+    return vert ? deblock_bs(P, Q, mb_edge ? 12 : edge - 4, k * 4, edge, k * 4, mb_edge)
+                : deblock_bs(P, Q, k * 4, mb_edge ? 12 : edge - 4, k * 4, edge, mb_edge);
+}
+
+// ---- Deblocking of a macroblock row in an LDS tile (k_deblock_rows) ----
+// The tile holds the macroblock and its 4-sample apron above and to the left
+// (luma rows / columns -4..15, chroma -4..7), 4-byte words per row.  The left
+// apron is the previous macroblock's right columns, carried over in the
+// tile; the rows above come from the row above once it has finished the
+// macroblock above-right.  Every filter step runs in the tile; the finished
+// words go back to the picture afterwards, the right 4 columns (filtered
+// again by the next macroblock's left edge) with the next macroblock.
+constexpr int kDbL = 20, kDbC = 12, kDbChunk = 256;
+struct DbTile {
+    uint8_t T[kDbL * kDbL];       // luma
+    uint8_t C[2][kDbC * kDbC];    // Cb, Cr
+    uint8_t B[kDbChunk][32];      // bS of a chunk of the row's macroblocks, [mb][e * 4 + k]
+};
+
+// word j (0..63) of macroblock (x, y)'s own luma rows, and word j (0..31) of
+// its chroma rows (comp = j >> 4, row (j >> 1) & 7, word j & 1)
+HD uint32_t db_own_luma(const DeblockArgs& D, int x, int y, int j)
+{
+    return *reinterpret_cast<const uint32_t*>(D.pic[0] + (size_t)(y * 16 + (j >> 2)) * D.W + x * 16 + (j & 3) * 4);
+}
+HD uint32_t db_own_chroma(const DeblockArgs& D, int x, int y, int j)
+{
+    return *reinterpret_cast<const uint32_t*>(D.pic[1 + (j >> 4)] + (size_t)(y * 8 + ((j >> 1) & 7)) * D.Wc + x * 8 + (j & 1) * 4);
+}
+HD void db_put_own(DbTile& t, int j, uint32_t luma, uint32_t chroma)
+{
+    *reinterpret_cast<uint32_t*>(t.T + (4 + (j >> 2)) * kDbL + 4 + (j & 3) * 4) = luma;
+    if (j < 32) *reinterpret_cast<uint32_t*>(t.C[j >> 4] + (4 + ((j >> 1) & 7)) * kDbC + 4 + (j & 1) * 4) = chroma;
+}
+// left apron <- the previous macroblock's right columns (lanes 0..43)
+HD void db_shift(DbTile& t, int j)
+{
+    if (j < kDbL) {
+        uint32_t* r = reinterpret_cast<uint32_t*>(t.T + j * kDbL);
+        r[0] = r[4];
+    }
+    else if (j < kDbL + 2 * kDbC) {
+        const int c = (j - kDbL) / kDbC, row = (j - kDbL) % kDbC;
+        uint32_t* r = reinterpret_cast<uint32_t*>(t.C[c] + row * kDbC);
+        r[0] = r[2];
+    }
+}
+// the 4 rows above (lanes 0..31: 16 luma words, 16 chroma words), y > 0
+HD void db_load_above(const DeblockArgs& D, DbTile& t, int x, int y, int j)
+{
+    if (j < 16) {
+        const int row = j >> 2, w = j & 3;
+        *reinterpret_cast<uint32_t*>(t.T + row * kDbL + 4 + w * 4) =
+            *reinterpret_cast<const uint32_t*>(D.pic[0] + (size_t)(y * 16 - 4 + row) * D.W + x * 16 + w * 4);
+    }
+    else if (j < 32) {
+        const int c = (j - 16) >> 3, row = ((j - 16) >> 1) & 3, w = j & 1;
+        *reinterpret_cast<uint32_t*>(t.C[c] + row * kDbC + 4 + w * 4) =
+            *reinterpret_cast<const uint32_t*>(D.pic[1 + c] + (size_t)(y * 8 - 4 + row) * D.Wc + x * 8 + w * 4);
+    }
+}
+// step (0..7) of the filter of the tile's macroblock for lane 0..31, as
+// deblock_mb_step; bs = the macroblock's 32 bS values
+HD void db_tile_step(const DeblockArgs& D, DbTile& t, const uint8_t* bs, int step, int lane)
+{
+    if (lane < 16) {
+        const bool vert = step < 4;
+        const int edge = (step & 3) * 4, b = bs[step * 4 + (lane >> 2)];
+        if (!b) return;
+        const int indexA = clip3(0, 51, D.qp);
+        uint8_t* s = vert ? t.T + (4 + lane) * kDbL + 4 + edge : t.T + (4 + edge) * kDbL + 4 + lane;
+        deblock_line(s, vert ? 1 : kDbL, b, false, indexA, kAlpha[indexA], kBeta[indexA]);
+    }
+    else if (lane < 32 && step < 4) {
+        const bool vert = step < 2;
+        const int edge = (step & 1) * 4, comp = (lane - 16) >> 3, i = (lane - 16) & 7;
+        const int b = bs[((vert ? 0 : 4) + (step & 1) * 2) * 4 + (i >> 1)];
+        if (!b) return;
+        const int indexA = clip3(0, 51, D.qpc);
+        uint8_t* s = vert ? t.C[comp] + (4 + i) * kDbC + 4 + edge : t.C[comp] + (4 + edge) * kDbC + 4 + i;
+        deblock_line(s, vert ? 1 : kDbC, b, true, indexA, kAlpha[indexA], kBeta[indexA]);
+    }
+}
+// the finished words of macroblock (x, y) back to the picture: columns -4..11
+// (-4..15 for the row's last macroblock), rows -4..15 (0..15 in row 0);
+// word j < db_store_words()
+HD int db_store_words() { return kDbL * 5 + 2 * kDbC * 3; }
+HD void db_store(const DeblockArgs& D, const DbTile& t, int x, int y, int j)
+{
+    const bool last = x == D.mbw - 1;
+    if (j < kDbL * 5) {
+        const int row = j / 5, w = j % 5;
+        if ((y == 0 && row < 4) || (x == 0 && w == 0) || (!last && w == 4)) return;
+        *reinterpret_cast<uint32_t*>(D.pic[0] + (size_t)(y * 16 - 4 + row) * D.W + x * 16 - 4 + w * 4) =
+            *reinterpret_cast<const uint32_t*>(t.T + row * kDbL + w * 4);
+    }
+    else {
+        j -= kDbL * 5;
+        const int c = j / (kDbC * 3), row = (j / 3) % kDbC, w = j % 3;
+        if ((y == 0 && row < 4) || (x == 0 && w == 0) || (!last && w == 2)) return;
+        *reinterpret_cast<uint32_t*>(D.pic[1 + c] + (size_t)(y * 8 - 4 + row) * D.Wc + x * 8 - 4 + w * 4) =
+            *reinterpret_cast<const uint32_t*>(t.C[c] + row * kDbC + w * 4);
+    }
+}
+
 // Step `step` (0..7) of the deblocking of macroblock `addr` for lane `lane`
 // (0..31): lanes 0-15 filter the luma lines of luma edge `step`
 // (vertical 0,4,8,12 then horizontal 0,4,8,12), lanes 16-31 the chroma

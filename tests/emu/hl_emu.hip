@@ -37,6 +37,47 @@ struct EmuEnc {
     int last_qp;
 };
 
+// k_deblock_rows (hl_encoder.hip) lane by lane: every row's tile, prefetch
+// registers and bS chunk as the row's workgroup holds them, the MBs in the
+// tightest order the kernel's waits allow -- MB (x, y) in step x + 2y, rows
+// of one step bottom-up, i.e. before row y - 1's MB x + 2 of the same step.
+static void deblock_rows_emu(const DeblockArgs& D, int mbh)
+{
+    const int mbw = D.mbw;
+    std::vector<DbTile> tiles(mbh);
+    std::vector<uint32_t> own_l((size_t)mbh * 64), own_c((size_t)mbh * 64);
+    std::vector<int> chunk0(mbh, -kDbChunk);
+    for (int y = 0; y < mbh; ++y)
+        for (int j = 0; j < 64; ++j) {
+            own_l[y * 64 + j] = db_own_luma(D, 0, y, j);
+            own_c[y * 64 + j] = j < 32 ? db_own_chroma(D, 0, y, j) : 0u;
+        }
+    for (int d = 0; d < mbw + 2 * mbh; ++d)
+        for (int y = mbh - 1; y >= 0; --y) {
+            const int x = d - 2 * y;
+            if (x < 0 || x >= mbw) continue;
+            DbTile& t = tiles[y];
+            if (x - chunk0[y] >= kDbChunk) {
+                chunk0[y] = x;
+                const int n = std::min(kDbChunk, mbw - x) * 32;
+                for (int i = 0; i < n; ++i) t.B[i >> 5][i & 31] = (uint8_t)deblock_edge_bs(D, y * mbw + x + (i >> 5), (i & 31) >> 2, i & 3);
+            }
+            if (x > 0)
+                for (int j = 0; j < 64; ++j) db_shift(t, j);
+            for (int j = 0; j < 64; ++j) db_put_own(t, j, own_l[y * 64 + j], own_c[y * 64 + j]);
+            if (x + 1 < mbw)
+                for (int j = 0; j < 64; ++j) {
+                    own_l[y * 64 + j] = db_own_luma(D, x + 1, y, j);
+                    if (j < 32) own_c[y * 64 + j] = db_own_chroma(D, x + 1, y, j);
+                }
+            if (y > 0)
+                for (int j = 0; j < 64; ++j) db_load_above(D, t, x, y, j);
+            for (int step = 0; step < 8; ++step)
+                for (int j = 0; j < 64; ++j) db_tile_step(D, t, t.B[x - chunk0[y]], step, j);
+            for (int j = 0; j < db_store_words(); ++j) db_store(D, t, x, y, j);
+        }
+}
+
 extern "C" void* emu_create(int W, int H, int qp, int me_range, int deblock, int gop, int early_term)
 {
     if (W <= 0 || H <= 0 || (W & 15) || (H & 15)) return nullptr;
@@ -168,9 +209,7 @@ extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, co
         D.qpc = qpc;
         for (int c = 0; c < 3; ++c) D.pic[c] = cur[c].data();
         D.st = e->st.data();
-        for (int a = 0; a < e->nmb; ++a)
-            for (int step = 0; step < 8; ++step)
-                for (int lane = 0; lane < 32; ++lane) deblock_mb_step(D, a, step, lane);
+        deblock_rows_emu(D, e->mbh);
     }
     const StreamParams sp{e->W, e->H, e->qp, e->deblock};
     const SliceState ss{intra ? 1 : 0, e->pict_count, e->idr_pic_id, qp};
@@ -452,9 +491,7 @@ extern "C" long emu_svc_encode(void* h, int layer, const uint8_t* y, const uint8
         D.qpc = kQpToQpc[s->qp];
         for (int c = 0; c < 3; ++c) D.pic[c] = cur[c].data();
         D.st = e.st.data();
-        for (int a = 0; a < e.nmb; ++a)
-            for (int step = 0; step < 8; ++step)
-                for (int lane = 0; lane < 32; ++lane) deblock_mb_step(D, a, step, lane);
+        deblock_rows_emu(D, e.mbh);
     }
     const StreamParams sp{e.W, e.H, s->qp, s->deblock};
     const SvcSliceState ss{intra ? 1 : 0, e.pict_count, e.idr_pic_id, s->qp, layer};
