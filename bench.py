@@ -116,11 +116,15 @@ def run_svc(args):
     """BASELINE config 4: 3 dyadic spatial layers 480x272 / 960x544 /
     1920x1088 (the reference's layer ratios must be powers of two,
     hl_codec.c:113-121), IPPP GOP 30, QP 28, ME 16, deblocking.  A step is
-    one access unit (all layers of one frame).  One GPU codes every layer;
-    with N ranks the layers are sharded over ranks (hartallo_amd/
-    svc_pipeline.py: the base layer on one rank, the enhancement layers on
-    the next, the layer state handed over by point-to-point sends -- RCCL
-    over xGMI) and further ranks run further streams.  The reference
+    one access unit (all layers of one frame).  One GPU codes every layer
+    (hl_amd_encode_layers_batch: the enhancement layers of an access unit
+    overlap the base run's later pictures).  With N ranks each rank codes a
+    whole stream (HL_SVC_SHARD=streams, the default: no data-path exchange,
+    weak scaling), or the layers are sharded over ranks (HL_SVC_SHARD=layers,
+    hartallo_amd/svc_pipeline.py: the base layer on one rank, the
+    enhancement layers on the next, the layer state handed over by
+    point-to-point sends -- RCCL over xGMI; lower latency per access unit,
+    lower throughput).  The reference
     encoder's per-access-unit MD5s cover 31 access units (the timed ones and
     the warm-up), checked after the timed region."""
     import hashlib
@@ -143,7 +147,14 @@ def run_svc(args):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         tdist.init_process_group("nccl" if nccl else "gloo", rank=rank, world_size=world,
                                  **({"device_id": torch.device(f"cuda:{local}")} if nccl else {}))
-    role = svc_pipeline.role_of(rank, world, L)
+    shard = os.environ.get("HL_SVC_SHARD", "streams")
+    if shard not in ("streams", "layers"):
+        raise SystemExit(f"HL_SVC_SHARD={shard}: expected streams or layers")
+    streams = world == 1 or shard == "streams"
+    if streams:  # every rank codes every layer of its own stream
+        role = svc_pipeline.Role(rank, 0, 1, 0, L - 1, -1, -1, rank)
+    else:
+        role = svc_pipeline.role_of(rank, world, L)
     n = min(args.warmup + args.steps, g["frames"])
     steps = n - args.warmup
     clips = synth.svc_clips(w0 << (L - 1), h0 << (L - 1), L, g["frames"], g["seed"])
@@ -190,9 +201,10 @@ def run_svc(args):
         def encode(self, layer, t):
             return self.a.encode(layer, t + self.off)
 
-    if world == 1:
+    if streams:
         # every layer on this GPU: hl_amd_encode_layers_batch (the base-layer
-        # pictures frame-pipelined, then the enhancement layers)
+        # pictures frame-pipelined; an access unit's enhancement layers while
+        # the run codes the next base pictures)
         ptrs = [[tuple(p.data_ptr() for p in planes[l][i]) for i in range(n)] for l in range(L)]
 
         def batch(lo, hi):
@@ -200,6 +212,8 @@ def run_svc(args):
 
         parts = batch(0, args.warmup) if args.warmup else []
         torch.cuda.synchronize()
+        if tdist:
+            tdist.barrier()
         t0 = time.perf_counter()
         parts += batch(args.warmup, n)
     else:
@@ -222,10 +236,15 @@ def run_svc(args):
         tdist.all_gather_object(allp, parts)
     else:
         allp = [parts]
-    groups = sorted({svc_pipeline.role_of(r, world, L).group for r in range(world)})
+    if streams:
+        groups = list(range(world))
+        member_of = {r: [r] for r in groups}
+    else:
+        groups = sorted({svc_pipeline.role_of(r, world, L).group for r in range(world)})
+        member_of = {gi: [r for r in range(world) if svc_pipeline.role_of(r, world, L).group == gi] for gi in groups}
     ok = True
     for gi in groups:
-        members = [r for r in range(world) if svc_pipeline.role_of(r, world, L).group == gi]
+        members = member_of[gi]
         aus = svc_pipeline.assemble([allp[r] for r in members])
         ok = ok and [hashlib.md5(a).hexdigest() for a in aus] == g["au_md5"][:n]
     if rank == 0:
@@ -237,8 +256,9 @@ def run_svc(args):
             "vs_baseline": None, "dtype": "u8/int32", "data": "synthetic (hartallo_amd.synth.svc_clips, seed 41)",
             "config": {"workload": "BASELINE config 4: dyadic spatial SVC, 3 layers, IPPP GOP30 QP28 ME16 deblock",
                        "layers": [[w0 << l, h0 << l] for l in range(L)], "streams": len(groups),
-                       "parallelism": "layer-sharded" if world > 1 else "all layers on one GPU, base layer frame-pipelined",
-                       "exchange": ("rccl" if nccl else "gloo-host") if world > 1 else None},
+                       "parallelism": ("all layers on one GPU per stream, base layer frame-pipelined, enhancement layers "
+                                       "overlapping the base run") if streams else "layer-sharded",
+                       "exchange": ("rccl" if nccl else "gloo-host") if not streams else None},
             "bitexact": ok,
             "bitexact_check": "every access unit (warm-up and timed) of every stream vs the reference encoder's per-AU MD5s "
                               "(tests/golden/svc_golden.json, oracle/_ref/ref_svc)",

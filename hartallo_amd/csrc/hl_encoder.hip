@@ -306,7 +306,13 @@ __device__ int claim_next(const PipeArgs& P, int nmb, int& cursor)
 // Pipelined run of P pictures (hl_pipeline.h): persistent workgroups taking
 // ready tasks (decision, then the deblocking and plane blocks it completes)
 // until the run has finished.
-__global__ __launch_bounds__(kMbThreads, 2) void k_pipeline(PipeArgs P, int mbw, int mbh)
+// waves per SIMD the register allocation of k_pipeline must allow (the
+// second __launch_bounds__ argument is waves per EU on AMDGPU): 2 = one
+// 512-lane workgroup per CU with up to 256 VGPRs, 4 = two workgroups with 128
+#ifndef HL_PIPE_WAVES_PER_EU
+#define HL_PIPE_WAVES_PER_EU 2
+#endif
+__global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(PipeArgs P, int mbw, int mbh)
 {
     __shared__ Shared S;
     __shared__ int32_t s_task;

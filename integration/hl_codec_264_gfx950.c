@@ -25,7 +25,8 @@ extern const hl_codec_plugin_def_t* hl_codec_264_plugin_def_t; /* the stock plug
 typedef struct hl_codec_264_gfx950_s {
     HL_DECLARE_CODEC; /* first member (hl_codec.h:171) */
     hl_amd_encoder_t* enc;
-    hl_size_t width, height;
+    hl_size_t width, height; /* the encoder's (base layer's) size */
+    hl_size_t layers;        /* spatial layers the encoder was opened with (0: AVC) */
 } hl_codec_264_gfx950_t;
 
 static hl_object_t* gfx950_ctor(hl_object_t* self, va_list* app)
@@ -48,52 +49,82 @@ static int gfx950_cmp(const hl_object_t* a, const hl_object_t* b) { return (int)
 
 static const hl_object_def_t gfx950_def_s = {sizeof(hl_codec_264_gfx950_t), gfx950_ctor, gfx950_dtor, gfx950_cmp, HL_TRUE};
 
+/* (re)opens the gfx950 encoder at W x H with the hl_codec_t settings */
+static HL_ERROR_T gfx950_open(hl_codec_264_gfx950_t* self, hl_codec_t* base, hl_size_t W, hl_size_t H)
+{
+    hl_amd_params_t p;
+    int32_t err;
+    if (self->enc) {
+        hl_amd_encoder_destroy(self->enc);
+        self->enc = NULL;
+    }
+    self->layers = 0;
+    p.width = (int32_t)W;
+    p.height = (int32_t)H;
+    p.qp = base->qp;
+    p.me_range = base->me_range;
+    p.deblock = base->deblock_flag;
+    p.gop_size = base->gop_size;
+    p.me_early_term = base->me_early_term_flag;
+    p.device = 0; /* one process per GPU (HIP_VISIBLE_DEVICES) */
+    if ((err = hl_amd_encoder_create(&p, &self->enc))) return (HL_ERROR_T)err; /* HL_ERROR_T values (hl_types.h:101-122) */
+    /* rate control: the hl_codec_t fields hl_codec_264.c:719-742 reads */
+    if (base->rc_bitrate > 0 &&
+        (err = hl_amd_set_rate_control(self->enc, base->rc_bitrate, base->fps.num, base->fps.den, base->rc_basicunit,
+                                       base->rc_qp_min, base->rc_qp_max)))
+        return (HL_ERROR_T)err;
+    self->width = W;
+    self->height = H;
+    return HL_ERROR_SUCCESS;
+}
+
 /* plugin encode(): one planar YUV420 frame in host memory -> headers + one
  * slice NAL, as the stock plugin's _hl_codec_264_encode (hl_codec_264.c:
- * 404-1038) returns them */
+ * 404-1038) returns them.  With layers added (hl_codec_add_layer,
+ * hl_codec.c:95-131) it is one layer of an SVC access unit: the caller
+ * encodes the layers of a frame base first, the frame's size selects the
+ * layer (hl_codec_264.c:470-481), and the last layer's DATA is the access
+ * unit. */
 static HL_ERROR_T gfx950_encode(hl_codec_t* base, const hl_frame_t* frame, hl_codec_result_t* result)
 {
     hl_codec_264_gfx950_t* self = (hl_codec_264_gfx950_t*)base;
     const hl_frame_video_t* f = (const hl_frame_video_t*)frame;
     hl_amd_result_t r;
     int32_t err;
+    hl_size_t l, L;
     if (!self || !f || !result) return HL_ERROR_INVALID_PARAMETER;
-    if (!self->enc || f->data_width[0] != self->width || f->data_height[0] != self->height) {
-        hl_amd_params_t p;
-        if (self->enc) {
-            hl_amd_encoder_destroy(self->enc);
-            self->enc = NULL;
+    L = base->layers_active_count;
+    if (L > 1) {
+        if (!self->enc || self->layers != L || self->width != base->layers[0].u_width || self->height != base->layers[0].u_height) {
+            if ((err = gfx950_open(self, base, base->layers[0].u_width, base->layers[0].u_height))) return (HL_ERROR_T)err;
+            for (l = 0; l < L; ++l)
+                if ((err = hl_amd_add_layer(self->enc, (int32_t)base->layers[l].u_width, (int32_t)base->layers[l].u_height)))
+                    return (HL_ERROR_T)err;
+            self->layers = L;
         }
-        p.width = (int32_t)f->data_width[0];
-        p.height = (int32_t)f->data_height[0];
-        p.qp = base->qp;
-        p.me_range = base->me_range;
-        p.deblock = base->deblock_flag;
-        p.gop_size = base->gop_size;
-        p.me_early_term = base->me_early_term_flag;
-        p.device = 0; /* one process per GPU (HIP_VISIBLE_DEVICES) */
-        if ((err = hl_amd_encoder_create(&p, &self->enc))) return (HL_ERROR_T)err; /* HL_ERROR_T values (hl_types.h:101-122) */
-        /* rate control: the hl_codec_t fields hl_codec_264.c:719-742 reads */
-        if (base->rc_bitrate > 0 &&
-            (err = hl_amd_set_rate_control(self->enc, base->rc_bitrate, base->fps.num, base->fps.den, base->rc_basicunit,
-                                           base->rc_qp_min, base->rc_qp_max)))
+        if ((err = hl_amd_encode_layer(self->enc, (int32_t)f->data_width[0], (int32_t)f->data_height[0], f->data_ptr[0],
+                                       f->data_ptr[1], f->data_ptr[2], 0, &r)))
             return (HL_ERROR_T)err;
-        self->width = f->data_width[0];
-        self->height = f->data_height[0];
     }
-    if ((err = hl_amd_encode(self->enc, f->data_ptr[0], f->data_ptr[1], f->data_ptr[2], &r)))
-        return (HL_ERROR_T)err;
+    else {
+        if (!self->enc || self->layers || f->data_width[0] != self->width || f->data_height[0] != self->height)
+            if ((err = gfx950_open(self, base, f->data_width[0], f->data_height[0]))) return (HL_ERROR_T)err;
+        if ((err = hl_amd_encode(self->enc, f->data_ptr[0], f->data_ptr[1], f->data_ptr[2], &r)))
+            return (HL_ERROR_T)err;
+    }
     result->type = HL_CODEC_RESULT_TYPE_NONE;
     if (r.type & HL_AMD_RESULT_TYPE_HDR) { /* hl_codec_264.c:675-686 */
         base->hdr_bytes = r.hdr;
         base->hdr_bytes_count = r.hdr_size;
         result->type |= HL_CODEC_RESULT_TYPE_HDR;
     }
-    result->type |= HL_CODEC_RESULT_TYPE_DATA; /* hl_codec_264.c:1000-1006 */
-    result->data_ptr = r.data; /* owned by the encoder, valid until the next call */
-    result->data_size = r.data_size;
-    result->width = self->width;
-    result->height = self->height;
+    if (r.type & HL_AMD_RESULT_TYPE_DATA) { /* hl_codec_264.c:1000-1006 */
+        result->type |= HL_CODEC_RESULT_TYPE_DATA;
+        result->data_ptr = r.data; /* owned by the encoder, valid until the next call */
+        result->data_size = r.data_size;
+    }
+    result->width = f->data_width[0];
+    result->height = f->data_height[0];
     return HL_ERROR_SUCCESS;
 }
 

@@ -10,6 +10,11 @@
  *
  * usage: drop_in_enc W H N qp me_range deblock gop early_term in.yuv out.264
  *   early_term -1 keeps the hl_codec_create default (hl_types.h:67)
+ * spatial SVC: drop_in_enc svc L W0 H0 N qp me_range deblock gop early_term out_prefix in0.yuv .. in{L-1}.yuv
+ *   hl_codec_add_layer per layer (W0 << l, H0 << l), then per frame one
+ *   hl_codec_encode per layer, base first (test_encoder.c:151-202); writes
+ *   out_prefix.264 as oracle/ref_svc_harness.c does and out_prefix.idx (the
+ *   stream's size after every access unit)
  */
 #include <hartallo/hl_api.h>
 #include <hartallo/hl_codec.h>
@@ -23,8 +28,11 @@
 extern const hl_codec_plugin_def_t hl_codec_264_gfx950_plugin_def_s;
 HL_ERROR_T hl_codec_264_gfx950_install(void);
 
+static int run_svc(int argc, char** argv);
+
 int main(int argc, char** argv)
 {
+    if (argc > 1 && !strcmp(argv[1], "svc")) return run_svc(argc - 1, argv + 1);
     if (argc < 11) {
         fprintf(stderr, "usage: %s W H N qp me_range deblock gop early_term in.yuv out.264\n", argv[0]);
         return 1;
@@ -82,5 +90,82 @@ int main(int argc, char** argv)
     hl_object_unref(c);
     hl_object_unref(f);
     printf("{\"frames\": %d}\n", n);
+    return 0;
+}
+
+/* argv: svc L W0 H0 N qp me_range deblock gop early_term out_prefix in0.yuv .. */
+static int run_svc(int argc, char** argv)
+{
+    if (argc < 11) {
+        fprintf(stderr, "usage: drop_in_enc svc L W0 H0 N qp me_range deblock gop early_term out_prefix in0.yuv ..\n");
+        return 1;
+    }
+    int L = atoi(argv[1]), W0 = atoi(argv[2]), H0 = atoi(argv[3]), N = atoi(argv[4]), qp = atoi(argv[5]);
+    int mer = atoi(argv[6]), db = atoi(argv[7]), gop = atoi(argv[8]), et = atoi(argv[9]);
+    const char* pre = argv[10];
+    if (L < 2 || L > 4 || argc < 11 + L) return 1;
+    hl_debug_set_level(HL_DEBUG_LEVEL_ERROR);
+    if (hl_engine_init()) return 2;
+    if (hl_codec_264_gfx950_install()) return 3;
+    const struct hl_codec_plugin_def_s* pl = 0;
+    struct hl_codec_s* c = 0;
+    struct hl_codec_result_s* r = 0;
+    hl_frame_video_t* f = 0;
+    if (hl_codec_plugin_find(HL_CODEC_TYPE_H264_SVC, &pl) || pl != &hl_codec_264_gfx950_plugin_def_s) return 4;
+    hl_codec_create(pl, &c);
+    hl_codec_result_create(&r);
+    hl_frame_video_create(&f);
+    c->gop_size = gop; c->me_range = mer; c->qp = qp; c->fps.num = 1; c->fps.den = 15;
+    c->rc_bitrate = -1; c->deblock_flag = db; c->threads_count = 1; c->max_ref_frame = 1;
+    c->distortion_mesure_type = HL_VIDEO_DISTORTION_MESURE_TYPE_SAD;
+    if (et >= 0) c->me_early_term_flag = et;
+    for (int l = 0; l < L; ++l)
+        if (hl_codec_add_layer(c, (uint32_t)(W0 << l), (uint32_t)(H0 << l), 0, 0)) return 5;
+    FILE* fi[4] = {0};
+    uint8_t* buf[4] = {0};
+    size_t fs[4];
+    char path[4096];
+    for (int l = 0; l < L; ++l) {
+        fs[l] = (size_t)(W0 << l) * (H0 << l) * 3 / 2;
+        buf[l] = (uint8_t*)malloc(fs[l]);
+        if (!(fi[l] = fopen(argv[11 + l], "rb"))) return 5;
+    }
+    snprintf(path, sizeof(path), "%s.264", pre);
+    FILE* fo = fopen(path, "wb");
+    snprintf(path, sizeof(path), "%s.idx", pre);
+    FILE* fidx = fopen(path, "wb");
+    if (!fo || !fidx) return 5;
+    static const uint8_t scp[3] = {0, 0, 1};
+    int n = 0;
+    for (; n < N; ++n) {
+        int ok = 1;
+        for (int l = 0; l < L; ++l) ok &= fread(buf[l], 1, fs[l], fi[l]) == fs[l];
+        if (!ok) break;
+        for (int l = 0; l < L; ++l) {
+            hl_frame_video_fill(f, HL_VIDEO_CHROMA_YUV420, W0 << l, H0 << l, buf[l], fs[l]);
+            f->encoding = HL_VIDEO_ENCODING_TYPE_AUTO;
+            int e = hl_codec_encode(c, (hl_frame_t*)f, r);
+            if (e) {
+                fprintf(stderr, "encode err %d at frame %d layer %d\n", e, n, l);
+                return 6;
+            }
+            if (r->type & HL_CODEC_RESULT_TYPE_HDR) fwrite(c->hdr_bytes, 1, c->hdr_bytes_count, fo);
+            if (l == L - 1 && (r->type & HL_CODEC_RESULT_TYPE_DATA)) {
+                fwrite(scp, 1, 3, fo);
+                fwrite(r->data_ptr, 1, r->data_size, fo);
+            }
+        }
+        fprintf(fidx, "%ld\n", ftell(fo));
+    }
+    fclose(fo);
+    fclose(fidx);
+    for (int l = 0; l < L; ++l) {
+        fclose(fi[l]);
+        free(buf[l]);
+    }
+    hl_object_unref(r);
+    hl_object_unref(c);
+    hl_object_unref(f);
+    printf("{\"frames\": %d, \"layers\": %d}\n", n, L);
     return 0;
 }
