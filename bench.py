@@ -47,6 +47,7 @@ MAX_RUN = 128  # pictures per pipelined launch (kMaxRun, hl_encoder.hip)
 BENCH_CLIP_FRAMES = 150
 BENCH_GOLDEN = os.path.join(ROOT, "tests", "golden", "bench_golden.json")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+PLANES_PAD = 40  # kPad of the quarter-pel planes (hl_mbcore.h)
 
 
 def cpu_model():
@@ -324,6 +325,12 @@ def main():
     # pictures of the last pipelined launch: runs span GOPs, up to MAX_RUN pictures each
     run_frames = (args.steps - 1) % MAX_RUN + 1 if mb_launches == 1 else 1
 
+    # the HBM-bound kernel of the path on its own: quarter-pel planes of a
+    # 1088p reference, read 1 B/px + write 4 B per padded pixel
+    planes_ms = enc.bench_planes(50)
+    pw, ph = W + 2 * PLANES_PAD, H + 2 * PLANES_PAD
+    planes_bytes = W * H + 4 * pw * ph
+
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         base = cpu_baseline(frames_host, min(args.cpu_frames, n_frames))
@@ -375,6 +382,10 @@ def main():
                          "sq_wait_frac": round(sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"], 3) if sq else None,
                          "sq_issue_frac": round(sq["SQ_ACTIVE_INST_ANY"] / sq["SQ_WAVE_CYCLES"], 3) if sq else None,
                          "valu_insts_per_mb": round(sq["SQ_INSTS_VALU"] / (12 * nmb)) if sq else None},
+            "planes_roofline": {"kernel": "k_planes", "bound": "hbm", "achieved": round(planes_bytes / (planes_ms / 1e3) / 1e9, 1),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(planes_bytes / (planes_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                "bytes_per_launch": planes_bytes, "avg_launch_us": round(planes_ms * 1e3, 2),
+                                "note": "50 back-to-back launches on the reference picture, HIP events on the encoder's stream"},
             "cpu_baseline": base,
         }
         print(json.dumps(line), flush=True)

@@ -38,6 +38,7 @@ EXPORTED_SYMBOLS = (
     "hl_amd_set_rate_control",
     "hl_amd_last_qp",
     "hl_amd_pipeline_occupancy",
+    "hl_amd_bench_planes",
     "hl_amd_get_recon",
     "hl_amd_set_timing",
     "hl_amd_get_timing",
@@ -139,6 +140,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_last_qp.restype = i32
     lib.hl_amd_pipeline_occupancy.argtypes = []
     lib.hl_amd_pipeline_occupancy.restype = i32
+    lib.hl_amd_bench_planes.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_float)]
+    lib.hl_amd_bench_planes.restype = i32
     lib.hl_amd_get_recon.argtypes = [vp, vp, vp, vp]
     lib.hl_amd_get_recon.restype = i32
     lib.hl_amd_set_timing.argtypes = [vp, i32]
@@ -282,6 +285,14 @@ class Encoder:
     def last_qp(self) -> int:
         """SliceQPY of the last encoded picture."""
         return self.lib.hl_amd_last_qp(self._h)
+
+    def bench_planes(self, iters: int = 50) -> float:
+        """average ms per launch of the quarter-pel plane kernel (diagnostics)"""
+        ms = ctypes.c_float()
+        rc = self.lib.hl_amd_bench_planes(self._h, iters, ctypes.byref(ms))
+        if rc:
+            raise HlAmdError(rc, "hl_amd_bench_planes")
+        return ms.value
 
     def set_pipeline(self, workgroups: int, reach: int, window: int):
         rc = self.lib.hl_amd_set_pipeline(self._h, workgroups, reach, window)

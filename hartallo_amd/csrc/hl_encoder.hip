@@ -1283,6 +1283,30 @@ extern "C" int32_t hl_amd_get_timing(hl_amd_encoder_t* e, float* ms4)
 extern "C" int32_t hl_amd_last_reruns(hl_amd_encoder_t* e) { return e ? e->reruns : -1; }
 extern "C" int32_t hl_amd_last_chain_walks(hl_amd_encoder_t* e) { return e ? e->chain_walks : -1; }
 
+// k_planes alone (the HBM-bound kernel of the path): `iters` launches on the
+// encoder's current reference picture and stream, timed with HIP events;
+// *ms = average milliseconds per launch.  Diagnostics, no reference interface.
+extern "C" int32_t hl_amd_bench_planes(hl_amd_encoder_t* e, int32_t iters, float* ms)
+{
+    if (!e || iters <= 0 || !ms) return HL_AMD_ERROR_INVALID_PARAMETER;
+    hipEvent_t a, b;
+    HL_HIP_CHECK(hipEventCreate(&a));
+    HL_HIP_CHECK(hipEventCreate(&b));
+    const uint8_t* ref = e->d_pic[e->cur ^ 1][0];
+    launch_planes(e, ref);  // warm
+    HL_HIP_CHECK(hipEventRecord(a, e->stream));
+    for (int i = 0; i < iters; ++i) launch_planes(e, ref);
+    HL_HIP_CHECK(hipEventRecord(b, e->stream));
+    HL_HIP_CHECK(hipGetLastError());
+    HL_HIP_CHECK(hipEventSynchronize(b));
+    float t = 0.f;
+    (void)hipEventElapsedTime(&t, a, b);
+    *ms = t / iters;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    return HL_AMD_SUCCESS;
+}
+
 extern "C" int32_t hl_amd_last_mb_launches(hl_amd_encoder_t* e) { return e ? e->mb_launches : -1; }
 
 // Phase cycle counters of HL_PROFILE builds (zeros otherwise): 64 phase

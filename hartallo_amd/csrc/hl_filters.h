@@ -28,60 +28,75 @@ HD uint8_t qpel_plane_sample(const uint8_t* ref, int W, int H, int plane, int x,
 #if defined(__HIPCC__)
 // Quarter-pel planes (full, b, h, j) of a reference picture, padded by kPad
 // (qpel_plane_sample, hl_filters.h: every tap coordinate clamped to the
-// picture independently, interpol.c:74-225).  One workgroup per 128x16 tile
+// picture independently, interpol.c:74-225).  One workgroup per 256x16 tile
 // of the padded planes: the clamped source tile with its 6-tap apron is
-// staged in LDS once, the vertical 6-tap sums (h1, |h1| < 2^14) once more,
-// and every lane writes 8 consecutive samples of each plane as one 8-byte
-// store.  HBM-bound: 1 B/px read (cached), 4 B/px written.
-constexpr int kPlTileW = 128, kPlTileH = 16;
+// staged in LDS as 4-byte words (one aligned global load per word inside the
+// picture), then every lane computes 16 consecutive samples of one row of
+// each plane from 6 LDS rows and writes them as one 16-byte store per plane.
+// HBM-bound: 1 B/px read, 4 B per padded pixel written.
+constexpr int kPlTileW = 256, kPlTileH = 16;
 __global__ __launch_bounds__(256) void k_planes(const uint8_t* __restrict__ ref, int W, int H, uint8_t* __restrict__ pl0, int pstride,
                                                 int plsz)
 {
-    constexpr int TW = kPlTileW + 6, TR = kPlTileH + 5;
-    __shared__ uint8_t T[TR][TW + 2];
-    __shared__ int16_t V[kPlTileH][TW + 2];
+    constexpr int TWW = (kPlTileW + 8) / 4, TR = kPlTileH + 5;  // words per tile row (apron 2 + 3, alignment 3), rows
+    __shared__ uint32_t T[TR][TWW + 1];
     const int PW = W + 2 * kPad, PH = H + 2 * kPad;
     const int tx = blockIdx.x * kPlTileW, ty = blockIdx.y * kPlTileH;  // tile origin, padded coordinates
-    const int x0 = tx - kPad - 2, y0 = ty - kPad - 2;                   // picture coordinates of T[0][0]
-    for (int i = threadIdx.x; i < TR * TW; i += 256) {
-        const int r = i / TW, c = i - r * TW;
-        T[r][c] = ref[clip3(0, H - 1, y0 + r) * W + clip3(0, W - 1, x0 + c)];
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kPlTileH * TW; i += 256) {
-        const int r = i / TW, c = i - r * TW;
-        V[r][c] = (int16_t)tap6(T[r][c], T[r + 1][c], T[r + 2][c], T[r + 3][c], T[r + 4][c], T[r + 5][c]);
-    }
-    __syncthreads();
-    const int row = threadIdx.x >> 4, xs = (threadIdx.x & 15) * 8;
-    const int py = ty + row, px = tx + xs;
-    if (py >= PH || px >= PW) return;  // PW is a multiple of 16: an 8-sample group never straddles it
-    uint64_t f = 0, b = 0, h = 0, j = 0;
+    const int xs = tx - kPad - 2, x0 = xs & ~3, o = xs - x0;          // picture x of T column 0 (4-aligned); offset of the first tap
+    const int y0 = ty - kPad - 2;                                      // picture y of T row 0
+    // every load of the tile in flight at once, then the LDS stores
+    constexpr int kIt = (TR * TWW + 255) / 256;
+    uint32_t v[kIt];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int c = xs + k + 2;
-        const uint8_t* t = T[row + 2];
-        const int16_t* v = V[row];
-        const uint64_t sf = t[c];
-        int vb = (tap6(t[c - 2], t[c - 1], t[c], t[c + 1], t[c + 2], t[c + 3]) + 16) >> 5;
-        int vh = (v[c] + 16) >> 5;
-        int vj = (tap6(v[c - 2], v[c - 1], v[c], v[c + 1], v[c + 2], v[c + 3]) + 512) >> 10;
+    for (int it = 0; it < kIt; ++it) {
+        const int i = threadIdx.x + it * 256, r = min(i / TWW, TR - 1), w = i - (i / TWW) * TWW;
+        const uint8_t* row = ref + (size_t)clip3(0, H - 1, y0 + r) * W;
+        const int x = x0 + 4 * w;
+        if (x >= 0 && x + 3 < W) v[it] = *reinterpret_cast<const uint32_t*>(row + x);
+        else
+            v[it] = (uint32_t)row[clip3(0, W - 1, x)] | (uint32_t)row[clip3(0, W - 1, x + 1)] << 8 |
+                    (uint32_t)row[clip3(0, W - 1, x + 2)] << 16 | (uint32_t)row[clip3(0, W - 1, x + 3)] << 24;
+    }
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+        const int i = threadIdx.x + it * 256;
+        if (i < TR * TWW) T[i / TWW][i % TWW] = v[it];
+    }
+    __syncthreads();
+    const int tr = threadIdx.x >> 4, tc = threadIdx.x & 15;
+    const int py = ty + tr, px = tx + tc * 16;
+    if (py >= PH || px >= PW) return;  // PW is a multiple of 16: a 16-sample group never straddles it
+    // columns tc*16 + o + j (j = 0..20) of rows tr..tr+5: bytes of words tc*4 .. tc*4+5
+    auto byte_at = [&](int r, int j) -> int {
+        const int c = tc * 16 + o + j;
+        return (int)((T[tr + r][c >> 2] >> (8 * (c & 3))) & 0xffu);
+    };
+    int vs[21];
+#pragma unroll
+    for (int j = 0; j < 21; ++j) vs[j] = tap6(byte_at(0, j), byte_at(1, j), byte_at(2, j), byte_at(3, j), byte_at(4, j), byte_at(5, j));
+    uint32_t f[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, h[4] = {0, 0, 0, 0}, jj[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int sf = byte_at(2, k + 2);
+        int vb = (tap6(byte_at(2, k), byte_at(2, k + 1), sf, byte_at(2, k + 3), byte_at(2, k + 4), byte_at(2, k + 5)) + 16) >> 5;
+        int vh = (vs[k + 2] + 16) >> 5;
+        int vj = (tap6(vs[k], vs[k + 1], vs[k + 2], vs[k + 3], vs[k + 4], vs[k + 5]) + 512) >> 10;
         // opaque: keeps hipcc (ROCm 7.2) from fusing shift + clamp + byte
         // packing into v_ashr_pk_u8_i32, whose result's upper half it then
         // ORs as if zero -- wrong bytes 2 and 3 of every packed pair on gfx950
         // (tests/test_gpu_unit.py::test_planes_kernel)
         asm volatile("" : "+v"(vb), "+v"(vh), "+v"(vj));
-        const uint64_t sb = (uint64_t)clip255(vb), sh = (uint64_t)clip255(vh), sj = (uint64_t)clip255(vj);
-        f |= sf << (8 * k);
-        b |= sb << (8 * k);
-        h |= sh << (8 * k);
-        j |= sj << (8 * k);
+        const int sh = 8 * (k & 3), q = k >> 2;
+        f[q] |= (uint32_t)sf << sh;
+        b[q] |= (uint32_t)clip255(vb) << sh;
+        h[q] |= (uint32_t)clip255(vh) << sh;
+        jj[q] |= (uint32_t)clip255(vj) << sh;
     }
-    const size_t o = (size_t)py * pstride + px;
-    *reinterpret_cast<uint64_t*>(pl0 + o) = f;
-    *reinterpret_cast<uint64_t*>(pl0 + plsz + o) = b;
-    *reinterpret_cast<uint64_t*>(pl0 + 2 * (size_t)plsz + o) = h;
-    *reinterpret_cast<uint64_t*>(pl0 + 3 * (size_t)plsz + o) = j;
+    const size_t at = (size_t)py * pstride + px;
+    *reinterpret_cast<uint4*>(pl0 + at) = make_uint4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<uint4*>(pl0 + plsz + at) = make_uint4(b[0], b[1], b[2], b[3]);
+    *reinterpret_cast<uint4*>(pl0 + 2 * (size_t)plsz + at) = make_uint4(h[0], h[1], h[2], h[3]);
+    *reinterpret_cast<uint4*>(pl0 + 3 * (size_t)plsz + at) = make_uint4(jj[0], jj[1], jj[2], jj[3]);
 }
 #endif
 

@@ -151,6 +151,11 @@ int32_t hl_amd_last_reruns(hl_amd_encoder_t* encoder);
  * pipelined run -- diagnostics */
 int32_t hl_amd_last_chain_walks(hl_amd_encoder_t* encoder);
 
+/* Diagnostics: `iters` launches of the quarter-pel plane kernel on the
+ * encoder's current reference picture; *ms = average ms per launch (the
+ * HBM-bound kernel's own roofline line in bench.py).  No reference interface. */
+int32_t hl_amd_bench_planes(hl_amd_encoder_t* encoder, int32_t iters, float* ms);
+
 /* number of macroblock-decision kernel launches of the last frame */
 int32_t hl_amd_last_mb_launches(hl_amd_encoder_t* encoder);
 
