@@ -94,6 +94,37 @@ def cpu_baseline(frames_host, n_frames):
     }
 
 
+def svc_cpu_baseline(clips, g, n_aus):
+    """Times the reference encoder as an SVC encoder (oracle/_ref/ref_svc,
+    the reference sources through hl_codec_add_layer + hl_codec_encode) on
+    the first n_aus access units of the config-4 stream, single thread."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_svc")
+    if not os.path.exists(exe) or n_aus < 2:
+        return None
+    L = g["layers"]
+    with tempfile.TemporaryDirectory() as td:
+        ins = []
+        for l in range(L):
+            ins.append(os.path.join(td, f"in{l}.yuv"))
+            clips[l][:n_aus].tofile(ins[-1])
+        cmd = [exe, str(L), str(g["w0"]), str(g["h0"]), str(n_aus), str(g["qp"]), str(g["me_range"]), str(g["deblock"]), str(g["gop"]),
+               str(g["early_term"]), os.path.join(td, "o")] + ins + ["quiet"]
+        r = subprocess.run(cmd, capture_output=True, text=True, check=True)
+        info = json.loads(r.stdout.strip().splitlines()[-1])
+    t_p = info["p_seconds"] / (n_aus - 1)
+    t_i = info["seconds"] - info["p_seconds"]
+    gop_aus = GOP / (t_i + (GOP - 1) * t_p)
+    return {
+        "value": round(gop_aus, 4),
+        "unit": "access units/s",
+        "cores": 1,
+        "kind": "reference",
+        "sample": f"pure-C build of the reference sources as an SVC encoder (oracle/_ref/ref_svc), first {n_aus} access units "
+                  f"(1 I + {n_aus - 1} P) of the same 3-layer stream, encode time only, 1 thread on {cpu_model()}: I access unit "
+                  f"{t_i:.2f} s, P access units {t_p:.2f} s each, rate of a GOP{GOP} (1 I + {GOP - 1} P) from these",
+    }
+
+
 def check_bitexact(outputs, seed):
     """True / False when every frame's Annex-B output matches the reference
     encoder's MD5 for this stream (tests/golden/bench_golden.json), None when
@@ -248,6 +279,20 @@ def run_svc(args):
         members = member_of[gi]
         aus = svc_pipeline.assemble([allp[r] for r in members])
         ok = ok and [hashlib.md5(a).hexdigest() for a in aus] == g["au_md5"][:n]
+    roofline = base = None
+    if rank == 0 and streams:
+        # dominant kernel: k_pipeline of the base run (one launch per batch);
+        # algorithmic bytes = 2752 B per base MB x MBs per launch
+        ms = enc.timing_ms()
+        if enc.last_mb_launches() == 1 and ms[1] > 0:
+            nmb0 = (w0 // 16) * (h0 // 16)
+            ach = BYTES_PER_MB * nmb0 * steps / (ms[1] / 1e3) / 1e9
+            roofline = {"bound": "hbm", "achieved": round(ach, 4), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                        "traffic": None, "kernel": "k_pipeline (base layer run)", "avg_launch_us": round(ms[1] * 1e3, 2),
+                        "frames_per_launch": steps,
+                        "note": "latency-bound MB wavefront of the 480x272 base layer; the enhancement layers run beside it"}
+        if world == 1 and not args.no_cpu_baseline:
+            base = svc_cpu_baseline(clips, g, min(args.cpu_frames, n))
     if rank == 0:
         total = len(groups) * steps
         print(json.dumps({
@@ -266,6 +311,8 @@ def run_svc(args):
             "rank0_layers": [role.first, role.last],
             "rank0_last_au_ms": {"base_layer_device": round(enc.timing_ms()[3], 3) if role.first == 0 else None,
                                  "enhancement_layers_device": round(enc.layer_ms(), 3)},
+            "roofline": roofline,
+            "cpu_baseline": base,
         }), flush=True)
     enc.close()
     if tdist:

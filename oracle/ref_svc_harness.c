@@ -93,7 +93,7 @@ int main(int argc, char** argv)
     static const uint8_t scp[3] = { 0, 0, 1 };
     int32_t rec[MBR_STRIDE];
     int n = 0;
-    double tot = 0;
+    double tot = 0, tot_p = 0;  /* all access units; those after the first */
     for (; n < N; ++n) {
         int ok = 1;
         for (int l = 0; l < L; ++l) ok &= fread(buf[l], 1, fs[l], fi[l]) == fs[l];
@@ -108,6 +108,7 @@ int main(int argc, char** argv)
             clock_gettime(CLOCK_MONOTONIC, &t1);
             if (e) { fprintf(stderr, "encode err %d at frame %d layer %d\n", e, n, l); return 4; }
             tot += (t1.tv_sec - t0.tv_sec) + (t1.tv_nsec - t0.tv_nsec) * 1e-9;
+            if (n > 0) tot_p += (t1.tv_sec - t0.tv_sec) + (t1.tv_nsec - t0.tv_nsec) * 1e-9;
             if (r->type & HL_CODEC_RESULT_TYPE_HDR) fwrite(c->hdr_bytes, 1, c->hdr_bytes_count, fo);
             if (l == L - 1 && (r->type & HL_CODEC_RESULT_TYPE_DATA)) {
                 fwrite(scp, 1, 3, fo);
@@ -133,6 +134,6 @@ int main(int argc, char** argv)
         fclose(frec[l]);
         if (fmb[l]) fclose(fmb[l]);
     }
-    printf("{\"frames\": %d, \"layers\": %d, \"seconds\": %.6f, \"fps\": %.4f}\n", n, L, tot, n / tot);
+    printf("{\"frames\": %d, \"layers\": %d, \"seconds\": %.6f, \"fps\": %.4f, \"p_seconds\": %.6f}\n", n, L, tot, n / tot, tot_p);
     return 0;
 }
