@@ -78,6 +78,90 @@ static void deblock_rows_emu(const DeblockArgs& D, int mbh)
         }
 }
 
+// Randomised check of the tiled row deblocking (k_deblock_rows' code, in
+// deblock_rows_emu's order) against the per-MB raster filter
+// (deblock_mb_step, the reference's order): random samples (smooth with
+// steps, so that every filter branch is taken) and random MB objects (intra,
+// skip, 16x16 .. 4x4 partitions, coded blocks, motion).  Returns the number
+// of differing samples (-1 if the filter changed no sample at all).
+extern "C" long emu_deblock_selftest(int W, int H, int qp, unsigned seed)
+{
+    uint64_t st = seed * 0x9E3779B97F4A7C15ull + 1;
+    auto rnd = [&]() -> uint32_t {
+        st ^= st << 13;
+        st ^= st >> 7;
+        st ^= st << 17;
+        return (uint32_t)(st >> 11);
+    };
+    const int mbw = W / 16, mbh = H / 16, Wc = W / 2, Hc = H / 2;
+    std::vector<MbState> mbs((size_t)mbw * mbh);
+    for (MbState& m : mbs) {
+        m = MbState{};
+        const uint32_t k = rnd() % 8;
+        if (k == 0) {
+            m.e_type = ET_I16;
+            m.flags = FL_INTRA;
+        }
+        else if (k == 1) {
+            m.e_type = ET_I_NXN;
+            m.flags = FL_INTRA;
+        }
+        else if (k == 2) {
+            m.e_type = ET_P16x16;
+            m.flags = FL_SKIP;
+        }
+        else {
+            static const int et[5] = {ET_P16x16, ET_P16x8, ET_P8x16, ET_P8x8, ET_P8x8REF0};
+            m.e_type = et[rnd() % 5];
+        }
+        m.part_w = m.e_type == ET_P16x8 ? 16 : (m.e_type == ET_P8x16 || m.e_type == ET_P8x8 || m.e_type == ET_P8x8REF0 ? 8 : 16);
+        m.part_h = m.e_type == ET_P8x16 ? 16 : (m.e_type == ET_P16x8 || m.e_type == ET_P8x8 || m.e_type == ET_P8x8REF0 ? 8 : 16);
+        for (int i = 0; i < 4; ++i) {
+            m.sub_w[i] = rnd() & 1 ? 4 : 8;
+            m.sub_h[i] = rnd() & 1 ? 4 : 8;
+        }
+        m.cbp_l4x4 = rnd() % 3 == 0 ? 0 : (int)(rnd() & 0xFFFF);
+        m.cbp_l = m.cbp_l4x4 ? 1 + (int)(rnd() % 15) : 0;
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j)
+                for (int c = 0; c < 2; ++c) m.mv[i][j][c] = (int16_t)((int)(rnd() % 13) - 6);
+    }
+    std::vector<uint8_t> a[3], b[3];
+    for (int c = 0; c < 3; ++c) {
+        const int w = c ? Wc : W, h = c ? Hc : H;
+        a[c].resize((size_t)w * h);
+        int base = 128;
+        for (int y = 0; y < h; ++y)
+            for (int x = 0; x < w; ++x) {
+                if ((x & 3) == 0 && rnd() % 5 == 0) base = 40 + (int)(rnd() % 176);  // steps at block edges
+                a[c][(size_t)y * w + x] = (uint8_t)clip255(base + (int)(rnd() % 9) - 4);
+            }
+        b[c] = a[c];
+    }
+    DeblockArgs D;
+    D.W = W;
+    D.H = H;
+    D.Wc = Wc;
+    D.mbw = mbw;
+    D.qp = qp;
+    D.qpc = kQpToQpc[qp];
+    D.st = mbs.data();
+    std::vector<uint8_t> orig[3] = {a[0], a[1], a[2]};
+    for (int c = 0; c < 3; ++c) D.pic[c] = a[c].data();
+    for (int m = 0; m < mbw * mbh; ++m)
+        for (int step = 0; step < 8; ++step)
+            for (int lane = 0; lane < 32; ++lane) deblock_mb_step(D, m, step, lane);
+    for (int c = 0; c < 3; ++c) D.pic[c] = b[c].data();
+    deblock_rows_emu(D, mbh);
+    long diff = 0, filtered = 0;
+    for (int c = 0; c < 3; ++c)
+        for (size_t i = 0; i < a[c].size(); ++i) {
+            diff += a[c][i] != b[c][i];
+            filtered += a[c][i] != orig[c][i];
+        }
+    return diff ? diff : (filtered ? 0 : -1);  // -1: the filter changed nothing (a vacuous case)
+}
+
 extern "C" void* emu_create(int W, int H, int qp, int me_range, int deblock, int gop, int early_term)
 {
     if (W <= 0 || H <= 0 || (W & 15) || (H & 15)) return nullptr;
