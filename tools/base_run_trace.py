@@ -29,5 +29,6 @@ if wg or reach != 2:
     enc.set_pipeline(wg, reach, 64)
 enc.set_timing(True)
 enc.encode_batch_device(ptrs)
-print("reach", reach, "workgroups", wg, "kernel ms", enc.timing_ms()[1], "reruns", enc.last_reruns(), flush=True)
+print(f"{W}x{H} reach {reach} workgroups {wg} kernel ms {enc.timing_ms()[1]:.1f} per picture {enc.timing_ms()[1] / N:.2f} "
+      f"chain walks {enc.last_chain_walks()} reruns {enc.last_reruns()}", flush=True)
 enc.close()
