@@ -991,7 +991,9 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
 // every block = its last writer (residual.c:796-806); rdo.Single_ctr = the
 // last candidate that wrote it (residual.c:881-897).  The next reader of
 // S.tc is behind a barrier.
-HD void commit_candidates(Ctx& c, const PartGeo& g, int n)
+// last_l: candidate (tid & 31)'s R.last when the caller has it in a register
+// (device; -2 = read it here)
+HD void commit_candidates(Ctx& c, const PartGeo& g, int n, int last_l = -2)
 {
     Shared& S = c.S;
     const Shared::CandRes& R = S.cd[c.par];
@@ -1005,11 +1007,12 @@ HD void commit_candidates(Ctx& c, const PartGeo& g, int n)
     }
     {  // last candidate that wrote the counter (vectorised over the pass)
         const int l = c.tid & 31;
-        const int v = l < n ? R.last[l] : -1;
+        const int v = l < n ? (last_l == -2 ? R.last[l] : last_l) : -1;
         const unsigned long long bal = __ballot(v >= 0) & 0xFFFFFFFFull;
         if (bal) chain_write(c, __builtin_amdgcn_readlane(v, 63 - __clzll((long long)bal)));
     }
 #else
+    (void)last_l;
     for (int k = 0; k < g.nblk; ++k) {
         const int hx = k % g.nbw, hy = k / g.nbw;
         const int bi = blk_idx(g.px + (hx << 2), g.py + (hy << 2));
@@ -1229,6 +1232,38 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     const int budget = g.nblk <= kSpecMaxBlocks ? min(kMaxCand, (kMaxPass * kMbRows) >> g.lnb) : 0;  // 0: one step per pass
     const int nc0 = (pmv[0] != 0 || pmv[1] != 0) ? 2 : 1;
     int stage = 3, flags = 0x1FF, cx = 0, cy = 0, left = 0, right = 0, top = 0, bottom = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // a pass's candidate results, lane l (and l + 32) holding candidate l:
+    // loaded once per pass, then every pick and take is register work
+    double pv_cost = 0.0;
+    int pv_single = 0, pv_dist = 0, pv_cbp = 0, pv_mvx = 0, pv_mvy = 0, pv_pad = 0, pv_last = -1;
+    auto take = [&](int bi, double m) {
+        b.cost = m;
+        b.single = __builtin_amdgcn_readlane(pv_single, bi);
+        b.dist = __builtin_amdgcn_readlane(pv_dist, bi);
+        b.cbp = __builtin_amdgcn_readlane(pv_cbp, bi);
+        b.mv[0] = __builtin_amdgcn_readlane(pv_mvx, bi);
+        b.mv[1] = __builtin_amdgcn_readlane(pv_mvy, bi);
+        return __builtin_amdgcn_readlane(pv_pad, bi);
+    };
+    // the sequential strict-< scan of candidates [lo, hi) (me_ds.c:339-347):
+    // index of the first candidate with the smallest cost, and that cost
+    auto pick = [&](int lo, int hi, double& m) -> int {
+        const int l = c.tid & 31;
+        const bool in = l >= lo && l < hi;
+        const double v = in ? pv_cost : 1.7976931348623157e308;
+        const double rm = row_min_f64(v);
+        const unsigned long long b0 = __builtin_bit_cast(unsigned long long, rm);
+        const double m0 = __builtin_bit_cast(double, (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(b0 >> 32), 0) << 32 |
+                                                         (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b0, 0));
+        const double m1 = __builtin_bit_cast(double, (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(b0 >> 32), 16) << 32 |
+                                                         (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b0, 16));
+        const double mn = fmin(m0, m1);
+        const unsigned long long bal = __ballot(in && v == mn) & 0xFFFFFFFFull;
+        m = mn;
+        return __ffsll((long long)bal) - 1;
+    };
+#else
     auto take = [&](int bi, double m) {
         b.cost = m;
         b.single = uni(S.cd[c.par].single[bi]);
@@ -1238,6 +1273,8 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         b.mv[1] = uni((int)S.wc[c.tid >> 6][bi].mvy);
         return uni(S.wc[c.tid >> 6][bi].pad);
     };
+    auto pick = [&](int lo, int hi, double& m) -> int { return pick_first_min(c, lo, hi, m); };
+#endif
     // first step of stage st from best MV (mx, my): window re-centred, every
     // point enabled; the half stage starts at the integer MV value read as
     // half-pel (me_ds.c:360)
@@ -1322,13 +1359,28 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
             eval_candidates(c, g, total, pmv);
         }
         HL_PROF_T(tsel);
+#if defined(__HIP_DEVICE_COMPILE__)
+        {
+            const int l = c.tid & 31;
+            const Shared::CandRes& R = S.cd[c.par];
+            const CandSlot cs = S.wc[c.tid >> 6][l];
+            pv_cost = R.cost[l];
+            pv_single = R.single[l];
+            pv_dist = R.dist[l];
+            pv_cbp = R.cbp[l];
+            pv_last = R.last[l];
+            pv_mvx = cs.mvx;
+            pv_mvy = cs.mvy;
+            pv_pad = cs.pad;
+        }
+#endif
         // resolve the chain step by step
         int used = 0;
         for (int j = 0; j < nseg; ++j) {
             used = lo[j] + n[j];
             if (stage == 3) {  // MVP / (0,0) (me_ds.c:280-300)
                 double m;
-                const int bi = pick_first_min(c, lo[j], lo[j] + n[j], m);
+                const int bi = pick(lo[j], lo[j] + n[j], m);
                 if (m < b.cost) take(bi, m);
                 stage = 2;
                 cx = centre_of(2, b.mv[0]);
@@ -1344,7 +1396,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
             int best = -1;
             if (n[j]) {
                 double m;
-                const int bi = pick_first_min(c, lo[j], lo[j] + n[j], m);
+                const int bi = pick(lo[j], lo[j] + n[j], m);
                 if (m < b.cost) best = take(bi, m);
             }
             if (best >= 0) {  // moved: the stage goes on from the new centre (window kept, me_ds.c:309)
@@ -1363,7 +1415,11 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
             top = cy - range;
             bottom = cy + range;
         }
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (used) commit_candidates(c, g, used, pv_last);
+#else
         if (used) commit_candidates(c, g, used);
+#endif
         HL_PROF_ADD(c, 17, tsel);
     }
     HL_SYNC();
