@@ -9,6 +9,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
+from hartallo_amd import _lib  # noqa: E402
+
+if os.environ.get("HL_LIB"):
+    _lib.load_library(os.environ["HL_LIB"])
 from hartallo_amd import Encoder, synth  # noqa: E402
 
 W, H, N = (int(v) for v in sys.argv[1:4])
