@@ -1044,6 +1044,10 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     HL_HIP_CHECK(hipHostGetDevicePointer((void**)&d_progress, e->h_progress, 0));
     __atomic_store_n(e->h_progress, 0, __ATOMIC_RELEASE);
     e->run_live.store(1, std::memory_order_release);
+    struct RunLive {  // cleared on every way out of the run (an error return included)
+        std::atomic<int>& r;
+        ~RunLive() { r.store(0, std::memory_order_release); }
+    } run_live_guard{e->run_live};
     P.progress = d_progress;
     static const bool trace = getenv("HL_AMD_TRACE_WRITERS") != nullptr;
     static unsigned long long* h_clock = nullptr;
