@@ -7,8 +7,11 @@
 //                    launch d = x + 2y; one 512-lane workgroup per MB
 //   3. row-start validation of the rdo.Single_ctr speculation (host), with a
 //      re-run of the wavefront from the first mispredicted row
-//   4. k_deblock_diag the in-place Baseline deblocking, same wavefront order
+//   4. k_deblock_rows the in-place Baseline deblocking in one launch (one
+//                    workgroup per MB row, LDS tiles, raster causality)
 //   5. host CAVLC serialisation of the MB records (hl_writer.cpp)
+// Runs of pictures: k_pipeline (hl_pipeline.h), one persistent launch.
+// Spatial SVC layers: k_svc_mb, k_deblock_rows, k_el_count / k_el_write.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -93,17 +96,6 @@ __global__ __launch_bounds__(kMbThreads, 2) void k_mb_diag(FrameArgs F, int diag
     const int s_in = x == 0 ? F.spec[y] : F.chain[addr - 1].s_out;
     HL_POISON(S, (uint32_t)addr * 7919u + (uint32_t)diag);
     encode_mb(F, S, addr, threadIdx.x, kMbThreads, s_in);
-}
-
-__global__ __launch_bounds__(64) void k_deblock_diag(DeblockArgs D, int mbh, int diag)
-{
-    int x, y;
-    diag_mb(D.mbw, mbh, 0, diag, blockIdx.x, x, y);
-    const int addr = y * D.mbw + x;
-    for (int step = 0; step < 8; ++step) {
-        if (threadIdx.x < 32) deblock_mb_step(D, addr, step, threadIdx.x);
-        __syncthreads();
-    }
 }
 
 // Deblocking of a whole picture in one launch: one 64-lane workgroup per MB
