@@ -340,6 +340,7 @@ def main():
     from hartallo_amd import Encoder, dist, synth
 
     rank, world, local = dist.init_from_env()
+    local %= max(1, torch.cuda.device_count())  # ranks beyond the visible GPUs share them (rehearsals on a one-GPU box)
     torch.cuda.set_device(local)
 
     n_frames = args.warmup + args.steps
@@ -368,7 +369,9 @@ def main():
     # bit-exactness of everything this rank encoded, outside the timed region
     outputs += [r.annexb() for r in enc.last_batch_results()]
     bitexact = check_bitexact(outputs, seed)
-    bitexact_all = dist.min_over_ranks(1 if bitexact else 0) if bitexact is not None else None
+    # every rank joins the collective (-1: no reference MD5s cover this rank's stream)
+    ex = dist.min_over_ranks(-1 if bitexact is None else (1 if bitexact else 0))
+    bitexact_all = None if ex < 0 else ex
     # pictures of the last pipelined launch: runs span GOPs, up to MAX_RUN pictures each
     run_frames = (args.steps - 1) % MAX_RUN + 1 if mb_launches == 1 else 1
 
