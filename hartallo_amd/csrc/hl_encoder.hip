@@ -149,18 +149,32 @@ __global__ __launch_bounds__(64) void k_deblock_rows(DeblockArgs D, int32_t* row
 }
 
 // Deblocking and plane blocks of task (x, y) (hl_pipeline.h).
-__device__ void task_filters(const PipeFrame& PF, int x, int y, int mbw, int mbh, int tid)
+// The deblocking of one MB in the LDS tile (DbMbTile, hl_filters.h) that
+// aliases the decision's prediction scratch (free once the MB is decided):
+// one load round, the eight edges by wave 0 in LDS, one store round.
+__device__ void deblock_mb_lds(const DeblockArgs& D, int X, int Y, int tid, DbMbTile& t)
 {
+    for (int j = tid; j < db_mb_load_words(); j += kMbThreads) db_mb_load(D, t, X, Y, j);
+    if (tid < 32) t.bs[tid] = (uint8_t)deblock_edge_bs(D, Y * D.mbw + X, tid >> 2, tid & 3);
+    __syncthreads();
+    if (tid < 64)
+        for (int step = 0; step < 8; ++step) {
+            db_tile_step(D, t, t.bs, step, tid);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: the next edge reads what this one wrote
+        }
+    __syncthreads();
+    for (int j = tid; j < db_mb_store_slots(); j += kMbThreads) db_mb_store(D, t, X, Y, j);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+__device__ void task_filters(const PipeFrame& PF, Shared& S, int x, int y, int mbw, int mbh, int tid)
+{
+    static_assert(sizeof(DbMbTile) <= sizeof(S.pred), "the tile aliases Shared::pred");
     int blk[kMaxTaskBlocks][2];
     const int nd = PF.deblock ? task_blocks(0, x, y, mbw, mbh, blk) : 0;
-    for (int i = 0; i < nd; ++i) {
-        const int a = blk[i][1] * mbw + blk[i][0];
-        for (int step = 0; step < 8; ++step) {
-            if (tid < 32) deblock_mb_step(PF.D, a, step, tid);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-        }
-    }
+    DbMbTile& tile = *reinterpret_cast<DbMbTile*>(S.pred);
+    for (int i = 0; i < nd; ++i) deblock_mb_lds(PF.D, blk[i][0], blk[i][1], tid, tile);
     const int np = task_blocks(1, x, y, mbw, mbh, blk);
     for (int i = 0; i < np; ++i)
         plane_block(PF.F.cur[0], PF.F.W, PF.F.H, mbw, mbh, PF.pl_out, PF.F.pstride, PF.F.plsz, blk[i][0], blk[i][1], tid, kMbThreads);
@@ -379,7 +393,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         const unsigned long long pt2 = __builtin_readcyclecounter();
 #endif
         // deblocking, then quarter-pel planes, this decision completed
-        task_filters(PF, x, y, mbw, mbh, tid);
+        task_filters(PF, S, x, y, mbw, mbh, tid);
 #if defined(HL_PROFILE)
         pw_wait += pt1 - pt0;
         pw_mb += pt2 - pt1;

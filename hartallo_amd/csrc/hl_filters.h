@@ -245,7 +245,8 @@ HD void db_load_above(const DeblockArgs& D, DbTile& t, int x, int y, int j)
 }
 // step (0..7) of the filter of the tile's macroblock for lane 0..31, as
 // deblock_mb_step; bs = the macroblock's 32 bS values
-HD void db_tile_step(const DeblockArgs& D, DbTile& t, const uint8_t* bs, int step, int lane)
+template <class Tile>
+HD void db_tile_step(const DeblockArgs& D, Tile& t, const uint8_t* bs, int step, int lane)
 {
     if (lane < 16) {
         const bool vert = step < 4;
@@ -284,6 +285,69 @@ HD void db_store(const DeblockArgs& D, const DbTile& t, int x, int y, int j)
         if ((y == 0 && row < 4) || (x == 0 && w == 0) || (!last && w == 2)) return;
         *reinterpret_cast<uint32_t*>(D.pic[1 + c] + (size_t)(y * 8 - 4 + row) * D.Wc + x * 8 - 4 + w * 4) =
             *reinterpret_cast<const uint32_t*>(t.C[c] + row * kDbC + w * 4);
+    }
+}
+
+// ---- Deblocking of one macroblock in an LDS tile (the tasks of k_pipeline) ----
+// The tile of DbTile without the row state: the MB and its 4-sample apron,
+// loaded in one round (the apron is final: the MBs left of and above it are
+// deblocked in earlier tasks, hl_pipeline.h), filtered in LDS, and the
+// samples a filter may change (luma: 3 columns left / 3 rows above and the
+// MB; chroma: 1 column / 1 row and the MB) stored back byte by byte.
+struct DbMbTile {
+    uint8_t T[kDbL * kDbL];
+    uint8_t C[2][kDbC * kDbC];
+    uint8_t bs[32];
+};
+HD int db_mb_load_words() { return kDbL * 5 + 2 * kDbC * 3; }
+// word j of the tile of MB (X, Y) from the picture (words outside it are not read by any filter that runs)
+HD void db_mb_load(const DeblockArgs& D, DbMbTile& t, int X, int Y, int j)
+{
+    if (j < kDbL * 5) {
+        const int row = j / 5, w = j % 5, py = Y * 16 - 4 + row, px = X * 16 - 4 + w * 4;
+        if (py < 0 || px < 0) return;
+        *reinterpret_cast<uint32_t*>(t.T + row * kDbL + w * 4) = *reinterpret_cast<const uint32_t*>(D.pic[0] + (size_t)py * D.W + px);
+    }
+    else {
+        j -= kDbL * 5;
+        const int c = j / (kDbC * 3), row = (j / 3) % kDbC, w = j % 3, py = Y * 8 - 4 + row, px = X * 8 - 4 + w * 4;
+        if (py < 0 || px < 0) return;
+        *reinterpret_cast<uint32_t*>(t.C[c] + row * kDbC + w * 4) = *reinterpret_cast<const uint32_t*>(D.pic[1 + c] + (size_t)py * D.Wc + px);
+    }
+}
+// store slot j (< db_mb_store_slots()): one sample a filter of MB (X, Y) may have changed
+HD int db_mb_store_slots() { return 16 * 19 + 3 * 16 + 2 * (8 * 9 + 8); }
+HD void db_mb_store(const DeblockArgs& D, const DbMbTile& t, int X, int Y, int j)
+{
+    int tr, tc, comp = -1;  // tile row / column (apron included)
+    if (j < 16 * 19) {
+        tr = 4 + j / 19;
+        tc = 1 + j % 19;  // columns -3..15
+    }
+    else if ((j -= 16 * 19) < 3 * 16) {
+        tr = 1 + j / 16;  // rows -3..-1
+        tc = 4 + j % 16;
+    }
+    else {
+        j -= 3 * 16;
+        comp = j / 80;
+        j %= 80;
+        if (j < 72) {
+            tr = 4 + j / 9;
+            tc = 3 + j % 9;  // columns -1..7
+        }
+        else {
+            tr = 3;  // row -1
+            tc = 4 + (j - 72);
+        }
+    }
+    if (comp < 0) {
+        const int py = Y * 16 - 4 + tr, px = X * 16 - 4 + tc;
+        if (py >= 0 && px >= 0) D.pic[0][(size_t)py * D.W + px] = t.T[tr * kDbL + tc];
+    }
+    else {
+        const int py = Y * 8 - 4 + tr, px = X * 8 - 4 + tc;
+        if (py >= 0 && px >= 0) D.pic[1 + comp][(size_t)py * D.Wc + px] = t.C[comp][tr * kDbC + tc];
     }
 }
 

@@ -84,7 +84,32 @@ static void deblock_rows_emu(const DeblockArgs& D, int mbh)
 // steps, so that every filter branch is taken) and random MB objects (intra,
 // skip, 16x16 .. 4x4 partitions, coded blocks, motion).  Returns the number
 // of differing samples (-1 if the filter changed no sample at all).
-extern "C" long emu_deblock_selftest(int W, int H, int qp, unsigned seed)
+// mode 0: the row kernel's order (deblock_rows_emu); mode 1: k_pipeline's
+// per-MB LDS tiles (DbMbTile), MB by MB in the tasks of the pipelined
+// schedule (task_blocks), tasks in wavefront order
+static void deblock_tasks_emu(const DeblockArgs& D, int mbh)
+{
+    const int mbw = D.mbw;
+    DbMbTile t;
+    for (int d = 0; d < mbw + 2 * mbh; ++d)
+        for (int y = 0; y < mbh; ++y) {
+            const int x = d - 2 * y;
+            if (x < 0 || x >= mbw) continue;
+            int blk[kMaxTaskBlocks][2];
+            const int nd = task_blocks(0, x, y, mbw, mbh, blk);
+            for (int i = 0; i < nd; ++i) {
+                const int X = blk[i][0], Y = blk[i][1];
+                memset(&t, 0xA5, sizeof(t));  // stale scratch: every sample a filter reads must be loaded
+                for (int j = 0; j < db_mb_load_words(); ++j) db_mb_load(D, t, X, Y, j);
+                for (int l = 0; l < 32; ++l) t.bs[l] = (uint8_t)deblock_edge_bs(D, Y * mbw + X, l >> 2, l & 3);
+                for (int step = 0; step < 8; ++step)
+                    for (int l = 0; l < 64; ++l) db_tile_step(D, t, t.bs, step, l);
+                for (int j = 0; j < db_mb_store_slots(); ++j) db_mb_store(D, t, X, Y, j);
+            }
+        }
+}
+
+extern "C" long emu_deblock_selftest(int W, int H, int qp, unsigned seed, int mode)
 {
     uint64_t st = seed * 0x9E3779B97F4A7C15ull + 1;
     auto rnd = [&]() -> uint32_t {
@@ -152,7 +177,8 @@ extern "C" long emu_deblock_selftest(int W, int H, int qp, unsigned seed)
         for (int step = 0; step < 8; ++step)
             for (int lane = 0; lane < 32; ++lane) deblock_mb_step(D, m, step, lane);
     for (int c = 0; c < 3; ++c) D.pic[c] = b[c].data();
-    deblock_rows_emu(D, mbh);
+    if (mode == 1) deblock_tasks_emu(D, mbh);
+    else deblock_rows_emu(D, mbh);
     long diff = 0, filtered = 0;
     for (int c = 0; c < 3; ++c)
         for (size_t i = 0; i < a[c].size(); ++i) {
