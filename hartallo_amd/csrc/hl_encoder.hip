@@ -168,6 +168,53 @@ __device__ void deblock_mb_lds(const DeblockArgs& D, int X, int Y, int tid, DbMb
     __syncthreads();
 }
 
+// Quarter-pel plane samples of an interior MB (no padding to own, every tap
+// inside the picture): the 21x21 source neighbourhood and its vertical 6-tap
+// sums staged in LDS, then 64 lanes write 4 samples of each plane as one
+// 4-byte store per plane.  Same values as plane_block / qpel_plane_sample.
+__device__ void plane_block_lds(const uint8_t* ref, int W, uint8_t* pl0, int pstride, int plsz, int X, int Y, int tid, uint8_t* T,
+                                int16_t* V)
+{
+    constexpr int TS = 24;  // T row stride
+    const int x0 = X * 16 - 2, y0 = Y * 16 - 2;
+    for (int i = tid; i < 21 * 21; i += kMbThreads) {
+        const int r = i / 21, c = i - r * 21;
+        T[r * TS + c] = ref[(size_t)(y0 + r) * W + x0 + c];
+    }
+    __syncthreads();
+    for (int i = tid; i < 16 * 21; i += kMbThreads) {
+        const int r = i / 21, c = i - r * 21;
+        const uint8_t* t = T + r * TS + c;
+        V[r * 21 + c] = (int16_t)tap6(t[0], t[TS], t[2 * TS], t[3 * TS], t[4 * TS], t[5 * TS]);
+    }
+    __syncthreads();
+    if (tid < 64) {
+        const int r = tid >> 2, c0 = (tid & 3) * 4;
+        uint32_t f = 0, b = 0, h = 0, j = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint8_t* t = T + (r + 2) * TS + c0 + k;  // t[2]: the sample itself
+            const int16_t* v = V + r * 21 + c0 + k;        // v[2]: its vertical sum
+            int vb = (tap6(t[0], t[1], t[2], t[3], t[4], t[5]) + 16) >> 5;
+            int vh = (v[2] + 16) >> 5;
+            int vj = (tap6(v[0], v[1], v[2], v[3], v[4], v[5]) + 512) >> 10;
+            // opaque: keeps hipcc from fusing shift + clamp + packing into
+            // v_ashr_pk_u8_i32 (miscompiled on gfx950, see k_planes)
+            asm volatile("" : "+v"(vb), "+v"(vh), "+v"(vj));
+            f |= (uint32_t)t[2] << (8 * k);
+            b |= (uint32_t)clip255(vb) << (8 * k);
+            h |= (uint32_t)clip255(vh) << (8 * k);
+            j |= (uint32_t)clip255(vj) << (8 * k);
+        }
+        const size_t o = (size_t)(Y * 16 + r + kPad) * pstride + X * 16 + c0 + kPad;
+        *reinterpret_cast<uint32_t*>(pl0 + o) = f;
+        *reinterpret_cast<uint32_t*>(pl0 + plsz + o) = b;
+        *reinterpret_cast<uint32_t*>(pl0 + 2 * (size_t)plsz + o) = h;
+        *reinterpret_cast<uint32_t*>(pl0 + 3 * (size_t)plsz + o) = j;
+    }
+    __syncthreads();  // the scratch is reused by the next block
+}
+
 __device__ void task_filters(const PipeFrame& PF, Shared& S, int x, int y, int mbw, int mbh, int tid)
 {
     static_assert(sizeof(DbMbTile) <= sizeof(S.pred), "the tile aliases Shared::pred");
@@ -176,8 +223,16 @@ __device__ void task_filters(const PipeFrame& PF, Shared& S, int x, int y, int m
     DbMbTile& tile = *reinterpret_cast<DbMbTile*>(S.pred);
     for (int i = 0; i < nd; ++i) deblock_mb_lds(PF.D, blk[i][0], blk[i][1], tid, tile);
     const int np = task_blocks(1, x, y, mbw, mbh, blk);
-    for (int i = 0; i < np; ++i)
-        plane_block(PF.F.cur[0], PF.F.W, PF.F.H, mbw, mbh, PF.pl_out, PF.F.pstride, PF.F.plsz, blk[i][0], blk[i][1], tid, kMbThreads);
+    static_assert(21 * 24 <= sizeof(S.pred) && 16 * 21 * sizeof(int16_t) <= sizeof(S.i16_ac), "plane scratch");
+    uint8_t* T = reinterpret_cast<uint8_t*>(S.pred);      // free once the MB is decided
+    int16_t* V = reinterpret_cast<int16_t*>(S.i16_ac);
+    for (int i = 0; i < np; ++i) {
+        const int X = blk[i][0], Y = blk[i][1];
+        if (X > 0 && Y > 0 && X < mbw - 1 && Y < mbh - 1)
+            plane_block_lds(PF.F.cur[0], PF.F.W, PF.pl_out, PF.F.pstride, PF.F.plsz, X, Y, tid, T, V);
+        else
+            plane_block(PF.F.cur[0], PF.F.W, PF.F.H, mbw, mbh, PF.pl_out, PF.F.pstride, PF.F.plsz, X, Y, tid, kMbThreads);
+    }
 }
 
 // Dependency counters and ready queues of a run (hl_pipeline.h): only task
