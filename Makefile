@@ -31,27 +31,28 @@ tests/emu/libhl_emu.so: tests/emu/hl_emu.hip $(HOSTSRC) $(HDRS)
 tests/gpu_unit/libhl_unit.so: tests/gpu_unit/hl_unit.hip $(HDRS)
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -shared -o $@ tests/gpu_unit/hl_unit.hip
 
-# profiling build: same library with per-phase clock64 counters (tools/phase_profile.py)
+# profiling build: same library (same device scheduling flags) with per-phase
+# clock64 counters (tools/phase_profile.py)
 profile: build/prof/hartallo_amd/libhartallo_amd.so
 build/prof/hartallo_amd/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(HOSTSRC) $(HDRS)
 	mkdir -p build/prof/hartallo_amd
-	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DHL_PROFILE=1 -shared -o $@ $(CSRC)/hl_encoder.hip $(HOSTSRC)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) $(DEVFLAGS) -DHL_PROFILE=1 -shared -o $@ $(CSRC)/hl_encoder.hip $(HOSTSRC)
 
 # debug builds: LDS poisoned before every macroblock with two different salts
 # (tools/gpu_diag.sh); any output difference names a read of uninitialised LDS
 poison: build/poison1/libhartallo_amd.so build/poison2/libhartallo_amd.so
 build/poison%/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(HOSTSRC) $(HDRS)
 	mkdir -p build/poison$*
-	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DHL_POISON_LDS=$* -shared -o $@ $(CSRC)/hl_encoder.hip $(HOSTSRC)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) $(DEVFLAGS) -DHL_POISON_LDS=$* -shared -o $@ $(CSRC)/hl_encoder.hip $(HOSTSRC)
 
 # memory-scope variants of the pipelined run's fences (diagnostics)
 scopes: build/acqsys/libhartallo_amd.so build/relacqsys/libhartallo_amd.so
 build/acqsys/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(HOSTSRC) $(HDRS)
 	mkdir -p build/acqsys
-	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) '-DHL_ACQ_SCOPE=""' -shared -o $@ $(CSRC)/hl_encoder.hip $(HOSTSRC)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) $(DEVFLAGS) '-DHL_ACQ_SCOPE=""' -shared -o $@ $(CSRC)/hl_encoder.hip $(HOSTSRC)
 build/relacqsys/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(HOSTSRC) $(HDRS)
 	mkdir -p build/relacqsys
-	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) '-DHL_ACQ_SCOPE=""' '-DHL_REL_SCOPE=""' -shared -o $@ $(CSRC)/hl_encoder.hip $(HOSTSRC)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) $(DEVFLAGS) '-DHL_ACQ_SCOPE=""' '-DHL_REL_SCOPE=""' -shared -o $@ $(CSRC)/hl_encoder.hip $(HOSTSRC)
 
 oracle: product  # oracle/_ref/drop_in_enc links the product library
 	$(MAKE) -C oracle

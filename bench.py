@@ -32,12 +32,14 @@ sys.path.insert(0, ROOT)
 W, H = 1920, 1088
 QP, ME_RANGE, DEBLOCK, GOP = 28, 16, 1, 30
 BYTES_PER_MB = 2752  # compulsory HBM bytes per macroblock, DESIGN.md / SURVEY §8(d)
-# HBM traffic of k_pipeline per macroblock, from rocprofv3 FETCH_SIZE / WRITE_SIZE
-# passes on this workload (tools/pmc_traffic.sh, corrected per MI355X_MICROARCH.md)
-# (kept under tools/pmc/, which travels to the GPU box; copies in profiles/)
-PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "pmc", "r02_pmc_traffic_k_pipeline.json")
-# SQ issue / wait counters of the same kernel (tools/pmc_sq.sh): what bounds it
-PMC_SQ = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "pmc", "r02_pmc_sq_k_pipeline.txt")
+# rocprofv3 PMC counters of k_pipeline on this workload (tools/pmc_record.sh:
+# SQ issue / wait counters and FETCH_SIZE / WRITE_SIZE, corrected per
+# MI355X_MICROARCH.md), summarised per launch of the timed call by
+# tools/pmc_summary.py; kept under tools/pmc/ (travels to the GPU box; a copy
+# in profiles/).  They describe the library whose SHA-256 they name.
+PMC_FILE = os.path.join(ROOT, "tools", "pmc", "pmc_k_pipeline.json")
+LIB_FILE = os.path.join(ROOT, "hartallo_amd", "libhartallo_amd.so")
+STAT_KEYS = ("runs", "per_picture", "fallbacks", "waits_gave_up", "chain_walks")
 MAX_RUN = 128  # pictures per pipelined launch (kMaxRun, hl_encoder.hip)
 # The synthetic stream is always generated for BENCH_CLIP_FRAMES frames (its
 # texture depends on the clip length) and its first warmup + steps frames are
@@ -50,6 +52,22 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.
 PLANES_PAD = 40  # kPad of the quarter-pel planes (hl_mbcore.h)
 
 
+def load_pmc(warmup, steps):
+    """The recorded counters when they were taken on this exact library and
+    workload, else (None, why not)."""
+    import hashlib
+
+    if not os.path.exists(PMC_FILE):
+        return None, "no counters recorded (tools/pmc_record.sh)"
+    pmc = json.load(open(PMC_FILE))
+    sha = hashlib.sha256(open(LIB_FILE, "rb").read()).hexdigest()
+    if pmc.get("lib_sha256") != sha:
+        return None, f"stale: recorded on library {pmc.get('lib_sha256', '?')[:12]}, this one is {sha[:12]} (rerun tools/pmc_record.sh)"
+    if (pmc.get("warmup"), pmc.get("steps")) != (warmup, steps):
+        return None, f"recorded at --warmup {pmc.get('warmup')} --steps {pmc.get('steps')}, not this workload"
+    return pmc, f"tools/pmc/pmc_k_pipeline.json, library sha256 {sha[:12]}, recorded {pmc.get('recorded', '?')}"
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -60,47 +78,91 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(frames_host, n_frames):
-    """Times the reference encoder on the first n_frames of this rank's
-    workload, single thread: its x86-intrinsic build (oracle/_ref/ref_enc_sse,
-    the encoder BASELINE.json's north star names), else its pure-C build
-    (oracle/_ref/ref_enc), else the bit-exact C restatement (oracle/)."""
-    cands = [(os.path.join(ROOT, "oracle", "_ref", "ref_enc_sse"), "reference", "x86-intrinsic (SSE2-SSE4.2) build of the reference sources"),
+def _ref_encoders():
+    """The reference encoder builds a CPU baseline can time, best first: its
+    x86-intrinsic build (oracle/_ref/ref_enc_sse, the encoder BASELINE.json's
+    north star names), its pure-C build (oracle/_ref/ref_enc), else the
+    bit-exact C restatement (oracle/)."""
+    cands = [(os.path.join(ROOT, "oracle", "_ref", "ref_enc_sse"), "reference",
+              "x86-intrinsic (SSE2-SSE4.2) build of the reference sources (hl_codec_264_deblock.c keeps its C path: its "
+              "SSE header declares the threshold table const, which gcc rejects, oracle/Makefile)"),
              (os.path.join(ROOT, "oracle", "_ref", "ref_enc"), "reference", "pure-C build of the reference sources"),
              (os.path.join(ROOT, "oracle", "_build", "hlenc_oracle"), "port", "bit-exact C restatement (oracle/hl_oracle.c)")]
-    found = [c for c in cands if os.path.exists(c[0])]
+    return [c for c in cands if os.path.exists(c[0])]
+
+
+def _timed_mix(first, steps):
+    """IDR and P pictures among the timed frames [first, first + steps)."""
+    n_i = sum(1 for f in range(first, first + steps) if f % GOP == 0)
+    return n_i, steps - n_i
+
+
+def cpu_baseline(frames_host, n_frames, first, steps, parallel=8):
+    """Times the reference encoder on the first n_frames of this rank's
+    workload (1 I + n_frames-1 P pictures), encode time only, and weights
+    its measured I- and P-picture times to the timed frames' mix (the
+    driver's --warmup 5 --steps 20 times P pictures only).  Then the same
+    sample on `parallel` processes at once (one per core, SURVEY §6's
+    N-process figure): their summed rate."""
+    found = _ref_encoders()
     if not found:
         return None
     exe, kind, what = found[0]
+    n_i, n_p = _timed_mix(first, steps)
+
+    def rate(info):
+        t_p = info["p_seconds"] / (n_frames - 1)
+        t_i = info["seconds"] - info["p_seconds"]
+        return steps / (n_i * t_i + n_p * t_p), t_i, t_p
+
     with tempfile.TemporaryDirectory() as td:
         inp = os.path.join(td, "in.yuv")
         frames_host[:n_frames].tofile(inp)
-        cmd = [exe, str(W), str(H), str(n_frames), str(QP), str(ME_RANGE), str(DEBLOCK), str(GOP), "0", inp, os.path.join(td, "o"), "quiet"]
-        r = subprocess.run(cmd, capture_output=True, text=True, check=True)
-        info = json.loads(r.stdout.strip().splitlines()[-1])
-    # the GPU line times whole GOPs (1 I + GOP-1 P pictures): weight the
-    # reference's measured I- and P-picture times the same way
-    t_p = info["p_seconds"] / (n_frames - 1)
-    t_i = info["seconds"] - info["p_seconds"]
-    gop_fps = GOP / (t_i + (GOP - 1) * t_p)
+
+        def cmd(k):
+            return [exe, str(W), str(H), str(n_frames), str(QP), str(ME_RANGE), str(DEBLOCK), str(GOP), "0", inp,
+                    os.path.join(td, f"o{k}"), "quiet"]
+
+        r = subprocess.run(cmd(0), capture_output=True, text=True, check=True)
+        fps1, t_i, t_p = rate(json.loads(r.stdout.strip().splitlines()[-1]))
+        try:
+            cores = len(os.sched_getaffinity(0))
+        except AttributeError:
+            cores = os.cpu_count() or 1
+        npar = max(1, min(parallel, cores))
+        procs = [subprocess.Popen(cmd(k + 1), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for k in range(npar)]
+        outs = [p.communicate() for p in procs]
+        if any(p.returncode for p in procs):
+            par = None
+        else:
+            rates = [rate(json.loads(o[0].strip().splitlines()[-1]))[0] for o in outs]
+            par = {"value": round(sum(rates), 4), "unit": "frames/s", "cores": npar, "kind": kind,
+                   "sample": f"{npar} processes of the same build at once, each on the same sample, summed rates "
+                             f"(per process {min(rates):.4f}-{max(rates):.4f} frames/s)"}
     return {
-        "value": round(gop_fps, 4),
+        "value": round(fps1, 4),
         "unit": "frames/s",
         "cores": 1,
         "kind": kind,
         "sample": f"{what}, first {n_frames} frames (1 I + {n_frames - 1} P) of the same 1920x1088 QP{QP} stream, encode time only, "
-                  f"1 thread on {cpu_model()}: I picture {t_i:.2f} s, P pictures {t_p:.2f} s each, rate of a GOP{GOP} "
-                  f"(1 I + {GOP - 1} P) from these (--cpu-frames {GOP} times a whole GOP)",
+                  f"1 thread on {cpu_model()}: I picture {t_i:.2f} s, P pictures {t_p:.2f} s each, weighted to the timed "
+                  f"frames ({n_i} I + {n_p} P)",
+        "parallel": par,
     }
 
 
-def svc_cpu_baseline(clips, g, n_aus):
-    """Times the reference encoder as an SVC encoder (oracle/_ref/ref_svc,
-    the reference sources through hl_codec_add_layer + hl_codec_encode) on
-    the first n_aus access units of the config-4 stream, single thread."""
-    exe = os.path.join(ROOT, "oracle", "_ref", "ref_svc")
-    if not os.path.exists(exe) or n_aus < 2:
+def svc_cpu_baseline(clips, g, n_aus, first, steps):
+    """Times the reference encoder as an SVC encoder (the reference sources
+    through hl_codec_add_layer + hl_codec_encode: oracle/_ref/ref_svc_sse,
+    its x86-intrinsic build, else ref_svc, the pure-C one) on the first n_aus
+    access units of the config-4 stream, single thread, weighted to the timed
+    access units' I/P mix."""
+    cands = [(os.path.join(ROOT, "oracle", "_ref", "ref_svc_sse"), "x86-intrinsic (SSE2-SSE4.2) build"),
+             (os.path.join(ROOT, "oracle", "_ref", "ref_svc"), "pure-C build")]
+    found = [c for c in cands if os.path.exists(c[0])]
+    if not found or n_aus < 2:
         return None
+    exe, what = found[0]
     L = g["layers"]
     with tempfile.TemporaryDirectory() as td:
         ins = []
@@ -113,15 +175,16 @@ def svc_cpu_baseline(clips, g, n_aus):
         info = json.loads(r.stdout.strip().splitlines()[-1])
     t_p = info["p_seconds"] / (n_aus - 1)
     t_i = info["seconds"] - info["p_seconds"]
-    gop_aus = GOP / (t_i + (GOP - 1) * t_p)
+    n_i = sum(1 for f in range(first, first + steps) if f % g["gop"] == 0)
+    n_p = steps - n_i
     return {
-        "value": round(gop_aus, 4),
+        "value": round(steps / (n_i * t_i + n_p * t_p), 4),
         "unit": "access units/s",
         "cores": 1,
         "kind": "reference",
-        "sample": f"pure-C build of the reference sources as an SVC encoder (oracle/_ref/ref_svc), first {n_aus} access units "
+        "sample": f"{what} of the reference sources as an SVC encoder ({os.path.basename(exe)}), first {n_aus} access units "
                   f"(1 I + {n_aus - 1} P) of the same 3-layer stream, encode time only, 1 thread on {cpu_model()}: I access unit "
-                  f"{t_i:.2f} s, P access units {t_p:.2f} s each, rate of a GOP{GOP} (1 I + {GOP - 1} P) from these",
+                  f"{t_i:.2f} s, P access units {t_p:.2f} s each, weighted to the timed access units ({n_i} I + {n_p} P)",
     }
 
 
@@ -292,7 +355,7 @@ def run_svc(args):
                         "frames_per_launch": steps,
                         "note": "latency-bound MB wavefront of the 480x272 base layer; the enhancement layers run beside it"}
         if world == 1 and not args.no_cpu_baseline:
-            base = svc_cpu_baseline(clips, g, min(args.cpu_frames, n))
+            base = svc_cpu_baseline(clips, g, min(args.cpu_frames, n), args.warmup, steps)
     if rank == 0:
         total = len(groups) * steps
         print(json.dumps({
@@ -309,8 +372,9 @@ def run_svc(args):
             "bitexact_check": "every access unit (warm-up and timed) of every stream vs the reference encoder's per-AU MD5s "
                               "(tests/golden/svc_golden.json, oracle/_ref/ref_svc)",
             "rank0_layers": [role.first, role.last],
-            "rank0_last_au_ms": {"base_layer_device": round(enc.timing_ms()[3], 3) if role.first == 0 else None,
-                                 "enhancement_layers_device": round(enc.layer_ms(), 3)},
+            # batch path: [1] = the base run's k_pipeline launch (HIP events); per access unit: the base picture's run
+            "rank0_last_batch_ms": {"base_run_device": round(enc.timing_ms()[1], 3) if role.first == 0 else None,
+                                    "last_au_enhancement_layers_device": round(enc.layer_ms(), 3)},
             "roofline": roofline,
             "cpu_baseline": base,
         }), flush=True)
@@ -354,8 +418,10 @@ def main():
 
     enc = Encoder(W, H, QP, ME_RANGE, DEBLOCK, GOP, 0, local)
     outputs = []
+    warm = {k: 0 for k in STAT_KEYS}
     if args.warmup:  # same entry point as the timed frames (warms the pipelined path and its buffers)
         outputs += [r.annexb() for r in enc.encode_batch_device(ptrs[:args.warmup])]
+        warm = enc.last_batch_stats()
     enc.set_timing(True)
     dist.barrier()
     torch.cuda.synchronize()
@@ -366,6 +432,12 @@ def main():
     elapsed = dist.max_over_ranks(time.perf_counter() - t0)
     ms = enc.timing_ms()
     mb_ms, mb_launches = ms[1], enc.last_mb_launches()  # the (last) pipelined launch
+    stats = enc.last_batch_stats()
+    # how every rank's calls ran (fallbacks to the per-picture path would show here), summed over ranks
+    tot = dist.sum_over_ranks([stats[k] for k in STAT_KEYS] + [warm["fallbacks"] + warm["waits_gave_up"] + warm["per_picture"]])
+    pipeline = dict(zip(STAT_KEYS, tot[:len(STAT_KEYS)]))
+    pipeline["warmup_off_pipeline"] = tot[-1]
+    pipeline["scope"] = "timed call (hl_amd_last_batch_stats), summed over ranks; warmup_off_pipeline = warm-up pictures not coded by a clean run"
     # bit-exactness of everything this rank encoded, outside the timed region
     outputs += [r.annexb() for r in enc.last_batch_results()]
     bitexact = check_bitexact(outputs, seed)
@@ -382,27 +454,19 @@ def main():
     planes_bytes = W * H + 4 * pw * ph
 
     base = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        base = cpu_baseline(frames_host, min(args.cpu_frames, n_frames))
+    if rank == 0 and not args.no_cpu_baseline:  # after the timed region, on rank 0 only
+        base = cpu_baseline(frames_host, min(args.cpu_frames, n_frames), args.warmup, args.steps)
 
     if rank == 0:
         total = world * args.steps
         fps = total / elapsed
         nmb = (W // 16) * (H // 16)
-        # dominant kernel: k_pipeline (one launch per run of P pictures);
+        # dominant kernel: k_pipeline (one launch per run of pictures);
         # algorithmic bytes per launch = 2752 B x MBs per launch
         avg_launch_s = (mb_ms / 1e3) / mb_launches
         bytes_per_launch = BYTES_PER_MB * nmb * run_frames / mb_launches
         achieved = bytes_per_launch / avg_launch_s / 1e9
-        traffic = None
-        if mb_launches == 1 and os.path.exists(PMC_TRAFFIC):
-            traffic = round(json.load(open(PMC_TRAFFIC))["traffic_bytes_per_mb"] * nmb * run_frames)
-        sq = {}
-        if os.path.exists(PMC_SQ):
-            for ln in open(PMC_SQ):
-                f = ln.split()
-                if len(f) == 2 and f[0].startswith("SQ_"):
-                    sq[f[0]] = float(f[1])
+        pmc, pmc_note = load_pmc(args.warmup, args.steps)
         line = {
             "metric": "1080p encoded frames/sec (bit-exact) at 1/2/4/8 MI355X; macroblocks/sec/GPU",
             "value": round(fps, 4),
@@ -422,16 +486,19 @@ def main():
             "bitexact": bitexact_all if bitexact_all is None else bool(bitexact_all),
             "bitexact_check": "every frame of every rank (warm-up and timed) vs the reference encoder's per-frame MD5s "
                               "(tests/golden/bench_golden.json, oracle/_ref/ref_enc on the same synthetic stream)",
+            "pipeline": pipeline,
             "bitstream_bytes_per_frame": round(out_bytes / args.steps, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": round(pmc["traffic_bytes_per_mb"] * nmb * run_frames) if pmc and mb_launches == 1 else None,
                          "kernel": "k_pipeline", "avg_launch_us": round(avg_launch_s * 1e6, 2),
                          "frames_per_launch": run_frames,
                          "note": "latency-bound MB wavefront, frames pipelined; achieved = 2752 B/MB x MBs per launch / launch time",
-                         # what bounds it instead (rocprofv3 SQ counters, tools/pmc/r02_pmc_sq_k_pipeline.txt)
-                         "sq_wait_frac": round(sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"], 3) if sq else None,
-                         "sq_issue_frac": round(sq["SQ_ACTIVE_INST_ANY"] / sq["SQ_WAVE_CYCLES"], 3) if sq else None,
-                         "valu_insts_per_mb": round(sq["SQ_INSTS_VALU"] / (12 * nmb)) if sq else None},
+                         # what bounds it instead (rocprofv3 SQ counters of this library on this workload, tools/pmc_record.sh)
+                         "sq_wait_frac": pmc["sq_wait_frac"] if pmc else None,
+                         "sq_issue_frac": pmc["sq_issue_frac"] if pmc else None,
+                         "valu_insts_per_mb": pmc["valu_insts_per_mb"] if pmc else None,
+                         "pmc": pmc_note},
             "planes_roofline": {"kernel": "k_planes", "bound": "hbm", "achieved": round(planes_bytes / (planes_ms / 1e3) / 1e9, 1),
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(planes_bytes / (planes_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                                 "bytes_per_launch": planes_bytes, "avg_launch_us": round(planes_ms * 1e3, 2),

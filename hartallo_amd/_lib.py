@@ -45,6 +45,7 @@ EXPORTED_SYMBOLS = (
     "hl_amd_last_reruns",
     "hl_amd_last_chain_walks",
     "hl_amd_last_mb_launches",
+    "hl_amd_last_batch_stats",
     "hl_amd_profile_counters",
     "hl_amd_debug_records",
     "hl_amd_record_size",
@@ -154,6 +155,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_last_chain_walks.restype = i32
     lib.hl_amd_last_mb_launches.argtypes = [vp]
     lib.hl_amd_last_mb_launches.restype = i32
+    lib.hl_amd_last_batch_stats.argtypes = [vp, ctypes.POINTER(i32)]
+    lib.hl_amd_last_batch_stats.restype = i32
     lib.hl_amd_profile_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong), i32]
     lib.hl_amd_profile_counters.restype = i32
     # diagnostics entry points (absent from older builds loaded through HL_LIB)
@@ -385,6 +388,16 @@ class Encoder:
 
     def last_mb_launches(self) -> int:
         return self.lib.hl_amd_last_mb_launches(self._h)
+
+    def last_batch_stats(self) -> dict:
+        """How the last encode call ran (hl_amd_last_batch_stats): pipelined
+        runs, pictures on the per-picture path, runs that fell back to it,
+        bounded waits that gave up, in-kernel rdo.Single_ctr walks."""
+        a = (ctypes.c_int32 * 5)()
+        rc = self.lib.hl_amd_last_batch_stats(self._h, a)
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_last_batch_stats")
+        return dict(zip(("runs", "per_picture", "fallbacks", "waits_gave_up", "chain_walks"), list(a)))
 
 
 class SvcEncoder(Encoder):

@@ -22,6 +22,7 @@
 #include <chrono>
 #include <future>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -553,6 +554,17 @@ struct hl_amd_encoder_s {
     int nwriters;                            // host slice writer threads of a run
     std::vector<std::vector<uint8_t>> wscratch, wout;
     std::vector<int32_t> run_intra, run_idr_id;  // per picture of the run: IDR, idr_pic_id
+    std::vector<int32_t> run_qp;                 // per picture of the run: SliceQPY (rate control: one picture per run)
+    std::vector<SliceBits> run_bits;             // per picture of the run: header / texture bits (rate control)
+    // accounting of the last encode call (hl_amd_last_batch_stats)
+    int32_t calls_runs = 0, calls_per_picture = 0, calls_fallbacks = 0, calls_gave_up = 0, calls_walks = 0;
+    bool run_fallback = false;                   // the last run was re-encoded picture by picture
+    bool broken = false;                         // a failed layers batch left the encoder unusable
+    // SVC batches: the enhancement-layer thread consumes pictures of a live
+    // run; a run that falls back stops it (run_aborted) and waits for the
+    // picture it is queuing (el_mu) before the run's buffers are rewritten
+    std::atomic<bool> run_aborted{false};
+    std::mutex el_mu;
     std::vector<const MbRecord*> last_recs;      // host records per picture of the last encode call (diagnostics)
     std::vector<const MbChain*> last_chain;      // host chain records, same
     std::vector<const uint8_t*> last_pic;        // device recon (Y|U|V planes contiguous) or null = the current reference
@@ -564,6 +576,7 @@ struct hl_amd_encoder_s {
 };
 
 static void svc_free(hl_amd_encoder_t* e);
+static hipError_t svc_drain_el(hl_amd_encoder_t* e);
 
 static void free_all(hl_amd_encoder_t* e)
 {
@@ -735,12 +748,17 @@ static int validate_chain(hl_amd_encoder_t* e, int row0, int& chain_end)
     return -1;
 }
 
-static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t* u, const uint8_t* v, hl_amd_result_t* r)
+// The per-picture path: one k_mb_diag launch per anti-diagonal.  It is the
+// fallback of a pipelined run (encode_run) whose bounded waits gave up.
+// qp_set >= 0: the picture's QP was already taken from the rate controller
+// (by the run that fell back); the picture's statistics still go back to it.
+static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t* u, const uint8_t* v, hl_amd_result_t* r,
+                            int qp_set = -1)
 {
     const bool intra = e->gop_left <= 0;
     if (intra) e->gop_left = e->p.gop_size;
     // rate control picks the picture's QP before it is coded (hl_codec_264.c:719-742)
-    const int qp = e->rc ? e->rc->begin_picture(intra) : e->p.qp;
+    const int qp = qp_set >= 0 ? qp_set : (e->rc ? e->rc->begin_picture(intra) : e->p.qp);
     const int qpc = kQpToQpc[qp];
     uint8_t** cur = e->d_pic[e->cur];
     uint8_t** ref = e->d_pic[e->cur ^ 1];
@@ -833,6 +851,7 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
     const SliceState ss{intra ? 1 : 0, e->pict_count, e->idr_pic_id, qp};
     SliceBits sb{};
     const size_t n = write_slice(sp, ss, e->h_rec, e->scratch.data(), e->out.data(), e->out.size(), &sb);
+    ++e->calls_per_picture;  // pictures coded on this path (hl_amd_last_batch_stats)
     if (!n) return HL_AMD_ERROR_TOOSHORT;
     if (e->rc) {  // hl_codec_264_rc_end_frame / _end_gop, hl_codec_264.c:1018-1031
         RcPictureStats st{};
@@ -869,9 +888,10 @@ static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
     const size_t pic = (size_t)e->W * e->H * 3 / 2, nmb = e->nmb;
     // Sized for a whole run of kMaxRun pictures at the first batch when that
     // fits in 4 GB of HBM (about 22 MB per 1088p picture, 2.8 GB at 1088p),
-    // so that later, longer batches never reallocate between runs.
+    // so that later, longer batches never reallocate between runs.  One
+    // picture per call (the plugin path) allocates for one picture.
     const size_t per_pic = pic + 4 * e->plsz + (sizeof(MbRecord) + sizeof(MbChain) + 3 * sizeof(int32_t)) * nmb;
-    if (per_pic * kMaxRun <= (4ull << 30)) n = std::max(n, kMaxRun);
+    if (n > 1 && per_pic * kMaxRun <= (4ull << 30)) n = std::max(n, kMaxRun);
     // free and forget every run buffer first, so that a failed allocation
     // below never leaves a dangling pointer for free_all or a later retry
     auto dfree = [](auto*& p) {
@@ -939,7 +959,7 @@ static bool validate_rows(const MbChain* ch, int mbw, int mbh, int spec, int32_t
     return true;
 }
 
-static FrameArgs frame_args(hl_amd_encoder_t* e, bool intra)
+static FrameArgs frame_args(hl_amd_encoder_t* e, bool intra, int qp)
 {
     FrameArgs F{};
     F.W = e->W;
@@ -948,12 +968,12 @@ static FrameArgs frame_args(hl_amd_encoder_t* e, bool intra)
     F.Hc = e->Hc;
     F.mbw = e->mbw;
     F.mbh = e->mbh;
-    F.qp = e->p.qp;
-    F.qpc = e->qpc;
+    F.qp = qp;
+    F.qpc = kQpToQpc[qp];
     F.is_intra = intra;
     F.me_range = std::min(64, std::max(1, e->p.me_range));
     F.early_term = e->p.me_early_term != 0;
-    F.lambda = 0.852 * (double)(1 << ((e->p.qp - 12) / 3));
+    F.lambda = 0.852 * (double)(1 << ((qp - 12) / 3));  // slice.c:1766
     F.pstride = e->pstride;
     F.plsz = (int32_t)e->plsz;
     F.st = e->d_st;
@@ -993,11 +1013,12 @@ static std::vector<size_t> write_run(hl_amd_encoder_t* e, int m, int base, const
                 if (abort->load()) return;
                 std::this_thread::sleep_for(std::chrono::microseconds(50));
             }
-            const SliceState ss{e->run_intra[k], e->pict_count + k, e->run_idr_id[k], e->p.qp};
+            const SliceState ss{e->run_intra[k], e->pict_count + k, e->run_idr_id[k], e->run_qp[k]};
             uint8_t* out = e->wout[w].data();
             static const bool trace = getenv("HL_AMD_TRACE_WRITERS") != nullptr;
             const auto tk = std::chrono::steady_clock::now();
-            const size_t nb = write_slice(sp, ss, e->h_brec + (size_t)e->nmb * k, e->wscratch[w].data(), out, e->wout[w].size());
+            const size_t nb = write_slice(sp, ss, e->h_brec + (size_t)e->nmb * k, e->wscratch[w].data(), out, e->wout[w].size(),
+                                          &e->run_bits[k]);
             if (trace)
                 fprintf(stderr, "writer %d picture %d: start %.2f ms, write %.2f ms\n", w, k,
                         std::chrono::duration<double, std::milli>(tk - e->run_t0).count(),
@@ -1013,17 +1034,22 @@ static std::vector<size_t> write_run(hl_amd_encoder_t* e, int m, int base, const
     return size;
 }
 
-// m consecutive pictures (IDR and P, in GOP order) in one pipelined launch;
-// falls back to the per-picture path when a bounded wait gave up or a
-// row-start speculation turned out to matter (resolve_chain makes the latter
-// exact inside a run).
+// m consecutive pictures (IDR and P, in GOP order) in one pipelined launch
+// (a single picture too: one persistent launch instead of a launch per
+// anti-diagonal); falls back to the per-picture path when a bounded wait gave
+// up or a row-start speculation turned out to matter (resolve_chain makes the
+// latter exact inside a run).  Under rate control m is 1 and the picture's QP
+// comes from the rate controller.
 static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, const uint8_t* const* U, const uint8_t* const* V,
                           hl_amd_result_t* res, int base)
 {
+    if (e->rc && m != 1) return HL_AMD_ERROR_INVALID_STATE;
     HL_HIP_CHECK(ensure_batch(e, m));
-    // picture types and idr_pic_id of the run, as m encode_frame calls would set them
+    // picture types, idr_pic_id and QP of the run, as m encode_frame calls would set them
     e->run_intra.resize(m);
     e->run_idr_id.resize(m);
+    e->run_qp.assign(m, e->p.qp);
+    e->run_bits.assign(m, SliceBits{});
     for (int k = 0, gl = e->gop_left, idr = e->idr_pic_id; k < m; ++k) {
         const bool intra = gl <= 0;
         if (intra) gl = e->p.gop_size;
@@ -1032,6 +1058,10 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         idr += intra;
         --gl;
     }
+    // rate control picks the picture's QP before it is coded (hl_codec_264.c:719-742)
+    if (e->rc) e->run_qp[0] = e->rc->begin_picture(e->run_intra[0] != 0);
+    e->run_fallback = false;
+    e->run_aborted.store(false, std::memory_order_release);
     const size_t pic = (size_t)e->W * e->H * 3 / 2, nmb = e->nmb;
     uint8_t** ref0 = e->d_pic[e->cur ^ 1];
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[0], e->stream));
@@ -1046,7 +1076,7 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         PipeFrame& pf = e->h_pf[k];
         pf = PipeFrame{};
         FrameArgs& F = pf.F;
-        F = frame_args(e, e->run_intra[k] != 0);
+        F = frame_args(e, e->run_intra[k] != 0, e->run_qp[k]);
         uint8_t* cur = e->d_bpic + pic * k;
         F.src[0] = Y[k];
         F.src[1] = U[k];
@@ -1078,8 +1108,8 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         pf.D.H = e->H;
         pf.D.Wc = e->Wc;
         pf.D.mbw = e->mbw;
-        pf.D.qp = e->p.qp;
-        pf.D.qpc = e->qpc;
+        pf.D.qp = F.qp;
+        pf.D.qpc = F.qpc;
         for (int c = 0; c < 3; ++c) pf.D.pic[c] = F.cur[c];
         pf.D.st = e->d_st;
         pf.pl_out = e->d_bpl + 4 * e->plsz * k;
@@ -1169,15 +1199,33 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     e->chain_walks = errw[1];
     e->mb_launches = 1;
     e->reruns = 0;
+    ++e->calls_runs;
+    e->calls_gave_up += err;
+    e->calls_walks += errw[1];
     if (err) fprintf(stderr, "hartallo_amd: pipelined run: %d bounded waits gave up; re-encoding the run picture by picture\n", err);
     int32_t carry = e->chain_end;
     bool ok = err == 0;
     for (int k = 0; k < m && ok; ++k) ok = validate_rows(e->h_bchain + nmb * k, e->mbw, e->mbh, 9, carry);
+    {  // diagnostics: HL_AMD_FORCE_FALLBACK=1 takes the fallback below for every run (tests)
+        const char* ff = getenv("HL_AMD_FORCE_FALLBACK");
+        if (ff && atoi(ff) > 0) ok = false;
+    }
     if (!ok) {  // a speculated row start mattered (or a wait gave up): redo the run picture by picture
+        e->run_fallback = true;
+        ++e->calls_fallbacks;
+        // an SVC batch's enhancement-layer thread may be coding from this
+        // run's pictures: stop it and drain what it queued before they are
+        // rewritten (hl_amd_encode_layers_batch re-codes those layers)
+        e->run_aborted.store(true, std::memory_order_release);
+        {
+            std::lock_guard<std::mutex> lk(e->el_mu);
+            HL_HIP_CHECK(svc_drain_el(e));
+        }
         HL_HIP_CHECK(hipMemcpyAsync(e->d_st, e->d_snap, sizeof(MbState) * nmb, hipMemcpyDeviceToDevice, e->stream));
         for (int k = 0; k < m; ++k) {
             hl_amd_result_t rr;
-            const int32_t rc = encode_frame(e, Y[k], U[k], V[k], &rr);
+            // under rate control the run's picture already has its QP (m == 1)
+            const int32_t rc = encode_frame(e, Y[k], U[k], V[k], &rr, e->rc ? e->run_qp[k] : -1);
             if (rc) return rc;
             store_result(e, base + k, rr, &res[k]);
             // keep every picture's records and reconstruction in the run
@@ -1213,6 +1261,16 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         o.hdr_size = e->hdr.size();
         if (e->frame_index == 0) o.type |= HL_AMD_RESULT_TYPE_HDR;
         if (e->run_intra[k]) e->gop_left = e->p.gop_size;  // encode_frame's bookkeeping, picture by picture
+        if (e->rc) {  // hl_codec_264_rc_end_frame / _end_gop, hl_codec_264.c:1018-1031
+            RcPictureStats st{};
+            const MbRecord* rr = e->h_brec + nmb * k;
+            for (size_t a = 0; a < nmb; ++a) st.mad_sum += rr[a].mad;
+            st.header_bits = e->run_bits[k].header_bits;
+            st.texture_bits = e->run_bits[k].texture_bits;
+            st.nbits = (int32_t)((wsize[k] - 3) * 8);
+            e->rc->end_picture(e->run_intra[k] != 0, st, e->gop_left - 1 <= 0);
+        }
+        e->last_qp = e->run_qp[k];
         ++e->pict_count;
         if (e->run_intra[k]) ++e->idr_pic_id;
         --e->gop_left;
@@ -1230,38 +1288,47 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     return HL_AMD_SUCCESS;
 }
 
+// n consecutive pictures of the stream, every one through a pipelined run:
+// runs span GOPs (IDR pictures included), kMaxRun bounds the run's buffers
+// (~22 MB of HBM and 9 MB of pinned host memory per 1088p picture); under
+// rate control every run is one picture (its QP needs the previous
+// picture's bits).  Results are those of n per-picture calls.
+static int32_t encode_pictures(hl_amd_encoder_t* e, int n, const uint8_t* const* y, const uint8_t* const* u, const uint8_t* const* v,
+                               hl_amd_result_t* results)
+{
+    if (e->broken) return HL_AMD_ERROR_INVALID_STATE;
+    e->bout.resize(n);
+    e->last_recs.assign(n, nullptr);
+    e->last_chain.assign(n, nullptr);
+    e->last_pic.assign(n, nullptr);
+    e->calls_runs = e->calls_per_picture = e->calls_fallbacks = e->calls_gave_up = e->calls_walks = 0;
+    for (int i = 0; i < n;) {
+        const int m = e->rc ? 1 : std::min(n - i, kMaxRun);
+        const int32_t rc = encode_run(e, m, y + i, u + i, v + i, results + i, i);
+        if (rc) return rc;
+        i += m;
+    }
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_last_batch_stats(hl_amd_encoder_t* e, int32_t* out5)
+{
+    if (!e || !out5) return HL_AMD_ERROR_INVALID_PARAMETER;
+    out5[0] = e->calls_runs;
+    out5[1] = e->calls_per_picture;
+    out5[2] = e->calls_fallbacks;
+    out5[3] = e->calls_gave_up;
+    out5[4] = e->calls_walks;
+    return HL_AMD_SUCCESS;
+}
+
 extern "C" int32_t hl_amd_encode_batch(hl_amd_encoder_t* e, int32_t n, const uint8_t* const* y, const uint8_t* const* u,
                                        const uint8_t* const* v, hl_amd_result_t* results)
 {
     if (!e || n <= 0 || !y || !u || !v || !results) return HL_AMD_ERROR_INVALID_PARAMETER;
     for (int i = 0; i < n; ++i)
         if (!y[i] || !u[i] || !v[i]) return HL_AMD_ERROR_INVALID_PARAMETER;
-    e->bout.resize(n);
-    e->last_recs.assign(n, nullptr);
-    e->last_chain.assign(n, nullptr);
-    e->last_pic.assign(n, nullptr);
-    int i = 0;
-    while (i < n) {
-        // a lone picture, and every picture under rate control (its QP needs
-        // the previous picture's bits), takes the per-picture path
-        if (n - i == 1 || e->rc) {
-            hl_amd_result_t r;
-            const int32_t rc = encode_frame(e, y[i], u[i], v[i], &r);
-            if (rc) return rc;
-            store_result(e, i, r, &results[i]);
-            e->last_recs[i] = e->h_rec;
-            e->last_chain[i] = e->h_chain;
-            ++i;
-            continue;
-        }
-        // runs span GOPs (IDR pictures included); kMaxRun bounds the run's
-        // buffers (~22 MB of HBM and 9 MB of pinned host memory per 1088p picture)
-        const int m = std::min(n - i, kMaxRun);
-        const int32_t rc = encode_run(e, m, y + i, u + i, v + i, results + i, i);
-        if (rc) return rc;
-        i += m;
-    }
-    return HL_AMD_SUCCESS;
+    return encode_pictures(e, n, y, u, v, results);
 }
 
 extern "C" int32_t hl_amd_set_rate_control(hl_amd_encoder_t* e, int64_t bitrate, int32_t fps_num, int32_t fps_den,
@@ -1299,13 +1366,14 @@ extern "C" int32_t hl_amd_pipeline_occupancy(void)
     return n;
 }
 
+// One picture per call (the plugin's encode(), hl_codec.c:152-159): a
+// pipelined run of one picture -- one persistent launch whose workgroups take
+// the picture's macroblocks as they become ready, with deblocking and the
+// next reference's quarter-pel planes fused into the tasks.
 extern "C" int32_t hl_amd_encode_device(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t* u, const uint8_t* v, hl_amd_result_t* r)
 {
     if (!e || !y || !u || !v || !r) return HL_AMD_ERROR_INVALID_PARAMETER;
-    e->last_recs.assign(1, e->h_rec);
-    e->last_chain.assign(1, e->h_chain);
-    e->last_pic.assign(1, nullptr);
-    return encode_frame(e, y, u, v, r);
+    return encode_pictures(e, 1, &y, &u, &v, r);
 }
 
 extern "C" int32_t hl_amd_encode(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t* u, const uint8_t* v, hl_amd_result_t* r)
@@ -1314,10 +1382,8 @@ extern "C" int32_t hl_amd_encode(hl_amd_encoder_t* e, const uint8_t* y, const ui
     HL_HIP_CHECK(hipMemcpyAsync(e->d_in[0], y, (size_t)e->W * e->H, hipMemcpyHostToDevice, e->stream));
     HL_HIP_CHECK(hipMemcpyAsync(e->d_in[1], u, (size_t)e->Wc * e->Hc, hipMemcpyHostToDevice, e->stream));
     HL_HIP_CHECK(hipMemcpyAsync(e->d_in[2], v, (size_t)e->Wc * e->Hc, hipMemcpyHostToDevice, e->stream));
-    e->last_recs.assign(1, e->h_rec);
-    e->last_chain.assign(1, e->h_chain);
-    e->last_pic.assign(1, nullptr);
-    return encode_frame(e, e->d_in[0], e->d_in[1], e->d_in[2], r);
+    const uint8_t *dy = e->d_in[0], *du = e->d_in[1], *dv = e->d_in[2];
+    return encode_pictures(e, 1, &dy, &du, &dv, r);
 }
 
 extern "C" int32_t hl_amd_get_recon(hl_amd_encoder_t* e, uint8_t* y, uint8_t* u, uint8_t* v)
@@ -1576,6 +1642,12 @@ static void svc_free(hl_amd_encoder_t* e)
     if (s->est) (void)hipStreamDestroy(s->est);
     delete s;
     e->svc = nullptr;
+}
+
+// waits for the enhancement-layer work queued on the layers' own stream
+static hipError_t svc_drain_el(hl_amd_encoder_t* e)
+{
+    return e->svc && e->svc->est ? hipStreamSynchronize(e->svc->est) : hipSuccess;
 }
 
 static int32_t svc_alloc(hl_amd_encoder_t* e)
@@ -2087,11 +2159,35 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
         if (intra[i]) gl = e->p.gop_size;
         --gl;
     }
+    if (e->broken) return HL_AMD_ERROR_INVALID_STATE;
     // what the caller queued on the encoder's stream before comes first
     HL_HIP_CHECK(hipEventRecord(s->ev_fork, e->stream));
     HL_HIP_CHECK(hipStreamWaitEvent(s->est, s->ev_fork, 0));
     s->linked = false;
+    // Every way out (error returns included) restores the encoder's
+    // single-call state: the run geometry, the stream linking, the reference
+    // layer pointers into this batch, and the order of the two streams.  A
+    // batch that fails part-way has advanced the enhancement layers for
+    // access units whose base picture did not finish: the encoder is then
+    // marked unusable (INVALID_STATE from then on).
+    struct Restore {
+        hl_amd_encoder_t* e;
+        SvcState* s;
+        int saved_wg;
+        bool ok = false;
+        ~Restore()
+        {
+            e->pipe_wg = saved_wg;
+            s->linked = true;
+            s->ref0_st = nullptr;
+            for (int c = 0; c < 3; ++c) s->ref0_pic[c] = nullptr;
+            // what is queued on the encoder's stream next sees the enhancement layers
+            if (hipEventRecord(s->ev_join, s->est) != hipSuccess || hipStreamWaitEvent(e->stream, s->ev_join, 0) != hipSuccess) ok = false;
+            if (!ok) e->broken = true;
+        }
+    } restore{e, s, e->pipe_wg};
     std::atomic<bool> base_done{false};
+    constexpr int32_t kAborted = -1;  // the run fell back while the thread coded from it
     // the enhancement layers of access units [i0, i0 + m) (base pictures
     // k = i - i0 of the current chunk): from the running run while it is
     // live, else from the chunk's final results
@@ -2102,6 +2198,7 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
             const MbRecord* recs;
             const uint8_t* bp;
             for (;;) {
+                if (wait_run && e->run_aborted.load(std::memory_order_acquire)) return kAborted;
                 if (base_done.load(std::memory_order_acquire)) {
                     recs = e->last_recs[k];
                     bp = e->last_pic[k];
@@ -2113,6 +2210,13 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
                     break;
                 }
                 std::this_thread::sleep_for(std::chrono::microseconds(20));
+            }
+            // a run that falls back takes this lock before it rewrites the
+            // pictures this one reads (encode_run)
+            std::unique_lock<std::mutex> lk(e->el_mu, std::defer_lock);
+            if (wait_run) {
+                lk.lock();
+                if (e->run_aborted.load(std::memory_order_acquire)) return kAborted;
             }
             if (!recs) return HL_AMD_ERROR_INVALID_STATE;
             MbState* hs = s->h_bst + nmb0 * k;
@@ -2147,7 +2251,6 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
         }
         return r;
     };
-    const int saved_wg = e->pipe_wg;
     const char* wenv = getenv("HL_AMD_PIPE_WG");
     if (e->pipe_wg == 0 && !(wenv && atoi(wenv) > 0)) e->pipe_wg = s->pipe_wg;
     std::vector<const uint8_t*> Y(chunk), U(chunk), V(chunk);
@@ -2183,12 +2286,16 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
         base_done.store(true, std::memory_order_release);
         int32_t rel = el.get();
         if (rc != HL_AMD_SUCCESS) break;
-        if (rel == HL_AMD_SUCCESS && e->reruns) {
+        if ((rel == HL_AMD_SUCCESS || rel == kAborted) && e->calls_fallbacks) {
             // the run was re-encoded picture by picture: roll the enhancement
             // layers back and code them again from the final base pictures
             if (hipStreamSynchronize(s->est) != hipSuccess) {
                 rc = HL_AMD_ERROR_SYSTEM;
                 break;
+            }
+            for (int l = 1; l < layers; ++l) {  // the slice writers of the discarded pictures
+                SvcLayerDev& L = s->el[l - 1];
+                if (L.writing.valid()) L.writing.wait();
             }
             for (int l = 1; l < layers; ++l) {
                 SvcLayerDev& L = s->el[l - 1];
@@ -2205,7 +2312,7 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
             HL_HIP_CHECK(hipStreamWaitEvent(s->est, s->ev_base, 0));
             rel = el_chunk(i0, m, false);
         }
-        rc = rel;
+        rc = rel == kAborted ? HL_AMD_ERROR_SYSTEM : rel;
         // access unit = prefix NAL unit, base slice, enhancement-layer slices
         for (int k = 0; k < m && rc == HL_AMD_SUCCESS; ++k) {
             const int i = i0 + k;
@@ -2228,12 +2335,6 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
             results[i].data_size = au.size();
         }
     }
-    e->pipe_wg = saved_wg;
-    s->linked = true;
-    s->ref0_st = nullptr;
-    for (int c = 0; c < 3; ++c) s->ref0_pic[c] = nullptr;
-    // what is queued on the encoder's stream next sees the enhancement layers
-    HL_HIP_CHECK(hipEventRecord(s->ev_join, s->est));
-    HL_HIP_CHECK(hipStreamWaitEvent(e->stream, s->ev_join, 0));
+    restore.ok = rc == HL_AMD_SUCCESS;
     return rc;
 }

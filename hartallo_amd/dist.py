@@ -50,6 +50,18 @@ def min_over_ranks(value: float) -> float:
     return float(t.item())
 
 
+def sum_over_ranks(values):
+    """Element-wise sum of a list of integers over the ranks."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        return [int(v) for v in values]
+    t = torch.tensor([int(v) for v in values], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [int(v) for v in t.tolist()]
+
+
 def stream_seed(rank: int, base: int = 11) -> int:
     """Each rank encodes its own synthetic stream (weak scaling)."""
     return base + rank

@@ -159,6 +159,14 @@ int32_t hl_amd_bench_planes(hl_amd_encoder_t* encoder, int32_t iters, float* ms)
 /* number of macroblock-decision kernel launches of the last frame */
 int32_t hl_amd_last_mb_launches(hl_amd_encoder_t* encoder);
 
+/* How the last encode call (hl_amd_encode*, or one base-layer chunk of
+ * hl_amd_encode_layers_batch) ran -- diagnostics, no reference interface:
+ * out5[0] pipelined runs launched, [1] pictures coded on the per-picture
+ * wavefront path, [2] runs that fell back to it (re-encoded picture by
+ * picture), [3] bounded waits that gave up, [4] in-kernel rdo.Single_ctr
+ * walks.  A healthy call has [1] = [2] = [3] = 0. */
+int32_t hl_amd_last_batch_stats(hl_amd_encoder_t* encoder, int32_t* out5);
+
 /* per-phase shader-clock counters of the macroblock kernel; filled only by
  * the profiling build (make profile); out[2k] = cycles, out[2k+1] = calls
  * for k < 32, then out[64 + addr] = cycles of macroblock addr in the last

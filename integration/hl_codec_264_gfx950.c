@@ -17,6 +17,7 @@
 #include <hartallo/hl_frame.h>
 #include <hartallo/hl_object.h>
 #include <stdarg.h>
+#include <stdio.h>
 
 #include "hartallo_amd.h" /* include/hartallo_amd.h of the gfx950 library */
 
@@ -95,6 +96,13 @@ static HL_ERROR_T gfx950_encode(hl_codec_t* base, const hl_frame_t* frame, hl_co
     if (!self || !f || !result) return HL_ERROR_INVALID_PARAMETER;
     L = base->layers_active_count;
     if (L > 1) {
+        if (base->rc_bitrate > 0) {
+            /* known gap: no reference golden pins rate control of
+             * an SVC stream, and the gfx950 encoder does not implement it; refused
+             * before any layer is coded */
+            fprintf(stderr, "hl_codec_264_gfx950: spatial SVC with rate control (rc_bitrate > 0) is not implemented\n");
+            return HL_ERROR_NOT_IMPLEMENTED;
+        }
         if (!self->enc || self->layers != L || self->width != base->layers[0].u_width || self->height != base->layers[0].u_height) {
             if ((err = gfx950_open(self, base, base->layers[0].u_width, base->layers[0].u_height))) return (HL_ERROR_T)err;
             for (l = 0; l < L; ++l)

@@ -24,6 +24,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 extern const hl_codec_plugin_def_t hl_codec_264_gfx950_plugin_def_s;
 HL_ERROR_T hl_codec_264_gfx950_install(void);
@@ -69,10 +70,15 @@ int main(int argc, char** argv)
     if (!fi || !fo) return 5;
     static const uint8_t scp[3] = {0, 0, 1};
     int n = 0;
+    double* ms = (double*)calloc(N > 0 ? N : 1, sizeof(double)); /* wall time of each hl_codec_encode call */
     while (n < N && fread(buf, 1, fs, fi) == fs) {
         hl_frame_video_fill(f, HL_VIDEO_CHROMA_YUV420, W, H, buf, fs);
         f->encoding = HL_VIDEO_ENCODING_TYPE_AUTO;
+        struct timespec t0, t1;
+        clock_gettime(CLOCK_MONOTONIC, &t0);
         int e = hl_codec_encode(c, (hl_frame_t*)f, r);
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        ms[n] = (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_nsec - t0.tv_nsec) * 1e-6;
         if (e) {
             fprintf(stderr, "encode err %d at frame %d\n", e, n);
             return 6;
@@ -89,7 +95,10 @@ int main(int argc, char** argv)
     hl_object_unref(r);
     hl_object_unref(c);
     hl_object_unref(f);
-    printf("{\"frames\": %d}\n", n);
+    printf("{\"frames\": %d, \"encode_ms\": [", n);
+    for (int i = 0; i < n; ++i) printf("%s%.3f", i ? ", " : "", ms[i]);
+    printf("]}\n");
+    free(ms);
     return 0;
 }
 

@@ -53,6 +53,15 @@ def _check(name, first, outs, recons):
             assert _md5(r) == g["recon_md5"][first + i], f"{name} frame {first + i}: reconstruction differs from the reference"
 
 
+def _check_clean_runs(enc, m):
+    """The call ran as pipelined runs of up to 128 pictures, with no fallback
+    to the per-picture path and no bounded wait that gave up (a silent
+    fallback would still produce the right bytes)."""
+    st = enc.last_batch_stats()
+    assert st == {"runs": (m + 127) // 128, "per_picture": 0, "fallbacks": 0, "waits_gave_up": 0, "chain_walks": st["chain_walks"]}, st
+    assert enc.last_mb_launches() == 1 and enc.last_reruns() == 0
+
+
 def _batch(name, calls, geometry=None):
     """Encodes the stream's first sum(calls) frames with one
     encode_batch_device call per entry of `calls`."""
@@ -68,6 +77,7 @@ def _batch(name, calls, geometry=None):
     outs, recons, i = [], [], 0
     for m in calls:
         outs += [r.annexb() for r in enc.encode_batch_device(ptrs[i:i + m])]
+        _check_clean_runs(enc, m)
         recons += [enc.debug_recon(k) for k in range(m)]
         i += m
     enc.close()
@@ -107,6 +117,7 @@ def test_bench_stream_per_picture(gpu):
     outs, recons = [], []
     for p in _ptrs(dev, w, h):
         outs.append(enc.encode_device(*p).annexb())
+        _check_clean_runs(enc, 1)  # one persistent launch per picture
         recons.append(np.concatenate(enc.recon()))
     enc.close()
     _check("bench_1088p_s11", 0, outs, recons)
@@ -126,6 +137,22 @@ def test_config2_720p_per_picture(gpu):
     outs, recons = [], []
     for p in _ptrs(dev, w, h):
         outs.append(enc.encode_device(*p).annexb())
+        _check_clean_runs(enc, 1)
         recons.append(np.concatenate(enc.recon()))
     enc.close()
     _check("c2_720p_s7", 0, outs, recons)
+
+
+def test_bench_stream_per_picture_fallback(gpu, monkeypatch):
+    # the per-picture wavefront path (what a run falls back to) on the bench stream
+    monkeypatch.setenv("HL_AMD_FORCE_FALLBACK", "1")
+    g = BENCH["bench_1088p_s11"]
+    dev = torch.from_numpy(np.ascontiguousarray(_clip("bench_1088p_s11")[:3])).cuda()
+    torch.cuda.synchronize()
+    enc = Encoder(g["width"], g["height"], g["qp"], g["me_range"], g["deblock"], g["gop"])
+    outs = [r.annexb() for r in enc.encode_batch_device(_ptrs(dev, g["width"], g["height"]))]
+    st = enc.last_batch_stats()
+    assert st["fallbacks"] == 1 and st["per_picture"] == 3, st
+    recons = [enc.debug_recon(k) for k in range(3)]
+    enc.close()
+    _check("bench_1088p_s11", 0, outs, recons)

@@ -56,14 +56,21 @@ def test_svc_gpu_matches_reference(name):
     assert enc.unpinned() == 0
 
 
-@pytest.mark.parametrize("name,splits", [("c4_svc3_480x272_s41", (1, 31)), ("svc3_64x48_qp30_gop3", (2, 3, 5)),
-                                         ("svc2_qcif_qp36_nodb_gop2", (4,))])
-def test_svc_gpu_layers_batch(name, splits):
+@pytest.mark.parametrize("name,splits,fallback", [("c4_svc3_480x272_s41", (1, 31), False), ("svc3_64x48_qp30_gop3", (2, 3, 5), False),
+                                                  ("svc2_qcif_qp36_nodb_gop2", (4,), False), ("svc3_64x48_qp30_gop3", (1, 4, 5), True),
+                                                  ("c4_svc3_480x272_s41", (6,), True)])
+def test_svc_gpu_layers_batch(name, splits, fallback, monkeypatch):
     """hl_amd_encode_layers_batch (frame-pipelined base layer, then the
-    enhancement layers) equals the per-call stream, across batch boundaries."""
+    enhancement layers) equals the per-call stream, across batch boundaries.
+    fallback: every base run is re-encoded picture by picture
+    (HL_AMD_FORCE_FALLBACK), so the enhancement layers coded from the live
+    run are rolled back and coded again from the final base pictures."""
     import torch
 
     from hartallo_amd import SvcEncoder
+
+    if fallback:
+        monkeypatch.setenv("HL_AMD_FORCE_FALLBACK", "1")
 
     g = GOLD[name]
     L, w0, h0 = g["layers"], g["w0"], g["h0"]
@@ -78,6 +85,8 @@ def test_svc_gpu_layers_batch(name, splits):
             ptrs.append([(dev[l][i].data_ptr(), dev[l][i].data_ptr() + n, dev[l][i].data_ptr() + n + n // 4) for i in range(lo, hi)])
         for r in enc.encode_layers_batch_device(ptrs):
             md5s.append(md5(r.annexb()))
+        st = enc.last_batch_stats()
+        assert st["fallbacks"] == (st["runs"] if fallback else 0) and st["waits_gave_up"] == 0, st
         lo = hi
     assert md5s == g["au_md5"][:splits[-1]]
     for l in range(L):

@@ -73,3 +73,29 @@ def test_sse_reference_build_matches_goldens(name, tmp_path):
     subprocess.run([REF_ENC_SSE, str(w), str(h), str(n), str(qp), str(mer), str(db), str(gop), str(GOLD[name].get("early_term", 0)),
                     str(inp), str(tmp_path / "o"), "quiet"], check=True, capture_output=True)
     assert (tmp_path / "o.264").read_bytes() == open(os.path.join(GOLDEN, name + ".264"), "rb").read()
+
+
+REF_SVC_SSE = os.path.join(os.path.dirname(GOLDEN), "..", "oracle", "_ref", "ref_svc_sse")
+
+
+@pytest.mark.skipif(not os.path.exists(REF_SVC_SSE), reason="oracle/_ref/ref_svc_sse is built where the reference sources are")
+@pytest.mark.parametrize("name", ["svc3_64x48_qp30_gop3", "svc2_qcif_qp36_nodb_gop2"])
+def test_sse_reference_svc_build_matches_goldens(name, tmp_path):
+    """The x86-intrinsic build of the reference as an SVC encoder (bench.py
+    --svc's CPU baseline) produces the pure-C build's streams."""
+    import hashlib
+    import json
+    import subprocess
+
+    from hartallo_amd import synth
+
+    g = json.load(open(os.path.join(GOLDEN, "svc_golden.json")))[name]
+    L, w0, h0 = g["layers"], g["w0"], g["h0"]
+    clips = synth.svc_clips(w0 << (L - 1), h0 << (L - 1), L, g["frames"], g["seed"])
+    ins = []
+    for l in range(L):
+        ins.append(str(tmp_path / f"in{l}.yuv"))
+        clips[l].tofile(ins[-1])
+    subprocess.run([REF_SVC_SSE, str(L), str(w0), str(h0), str(g["frames"]), str(g["qp"]), str(g["me_range"]), str(g["deblock"]),
+                    str(g["gop"]), str(g["early_term"]), str(tmp_path / "o")] + ins + ["quiet"], check=True, capture_output=True)
+    assert hashlib.md5((tmp_path / "o.264").read_bytes()).hexdigest() == g["stream_md5"]

@@ -1,0 +1,50 @@
+"""Per-frame path through the reference's own API: oracle/_ref/drop_in_enc
+(the reference's hl_codec_encode with the gfx950 plugin installed, one frame
+per call, host planes in and the slice NAL out) on the bench stream, with
+the wall time of every hl_codec_encode call and every frame's output checked
+against the reference encoder's MD5s (tests/golden/bench_golden.json).
+
+  python tools/per_frame_api.py [frames] [name]     (name: bench_1088p_s11 or c2_720p_s7)
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from hartallo_amd import synth  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    name = sys.argv[2] if len(sys.argv) > 2 else "bench_1088p_s11"
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "bench_golden.json")))[name]
+    w, h = g["width"], g["height"]
+    clip = synth.clip(w, h, g["frames"], g["seed"])[:n]
+    exe = os.path.join(ROOT, "oracle", "_ref", "drop_in_enc")
+    with tempfile.TemporaryDirectory() as td:
+        inp, out = os.path.join(td, "in.yuv"), os.path.join(td, "o.264")
+        clip.tofile(inp)
+        r = subprocess.run([exe, str(w), str(h), str(n), str(g["qp"]), str(g["me_range"]), str(g["deblock"]), str(g["gop"]), "0", inp, out],
+                           capture_output=True, text=True, check=True)
+        info = json.loads(r.stdout.strip().splitlines()[-1])
+        stream = open(out, "rb").read()
+    # per-frame check: the golden holds per-frame MD5s of the harness output
+    pos, frames_ok = 0, True
+    for i, (md5, nb) in enumerate(zip(g["frame_md5"][:n], g["frame_bytes"][:n])):
+        frames_ok = frames_ok and hashlib.md5(stream[pos:pos + nb]).hexdigest() == md5
+        pos += nb
+    ms = info["encode_ms"]
+    p_ms = [m for i, m in enumerate(ms) if i % g["gop"] and i > 1]  # P pictures after the first (warm) one
+    print(json.dumps({"name": name, "width": w, "height": h, "frames": n, "bitexact": frames_ok and pos == len(stream),
+                      "encode_ms": ms, "mean_p_ms": round(sum(p_ms) / max(1, len(p_ms)), 2),
+                      "p_fps": round(1e3 * len(p_ms) / max(1e-9, sum(p_ms)), 3),
+                      "path": "hl_codec_encode (reference API) -> gfx950 plugin -> hl_amd_encode, one frame per call"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
