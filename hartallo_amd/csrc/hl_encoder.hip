@@ -437,14 +437,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         encode_mb(PF.F, S, addr, tid, kMbThreads, s_in, gx, gy, spec_in);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (PF.hrec) {  // the record to host memory in 16-byte words; the publish fence below is system scope
-            static_assert(sizeof(MbRecord) % 16 == 0, "MbRecord copies in 16-byte words");
-            const int32_t* src = reinterpret_cast<const int32_t*>(PF.F.rec + addr);
-            uint4* dst = reinterpret_cast<uint4*>(PF.hrec + addr);
-            for (int i = tid; i < (int)(sizeof(MbRecord) / 16); i += kMbThreads)
-                dst[i] = make_uint4(ld_relaxed(src + 4 * i), ld_relaxed(src + 4 * i + 1), ld_relaxed(src + 4 * i + 2),
-                                    ld_relaxed(src + 4 * i + 3));
-        }
+        // (encode_mb stored the record into host memory, PF.F.hrec; the publish fence below is system scope)
 #if defined(HL_PROFILE)
         const unsigned long long pt2 = __builtin_readcyclecounter();
 #endif
@@ -787,6 +780,8 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
     F.plsz = (int32_t)e->plsz;
     F.st = e->d_st;
     F.rec = e->d_rec;
+    F.hrec = nullptr;
+    F.rec_dev = 1;
     F.chain = e->d_chain;
     F.spec = e->d_spec;
     F.prof = e->d_prof;
@@ -1095,6 +1090,12 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         const uint8_t* plb = k == 0 ? e->d_pl[0] : e->d_bpl + 4 * e->plsz * (k - 1);
         for (int i = 0; i < 4; ++i) F.pl[i] = plb + i * e->plsz;
         F.rec = e->d_brec + nmb * k;
+        F.hrec = e->dh_brec + nmb * k;  // the slice writers read the records from host memory during the run
+#if defined(HL_DIAG_INPUTS)
+        F.rec_dev = 1;
+#else
+        F.rec_dev = 0;
+#endif
         F.chain = e->d_bchain + nmb * k;
         F.spec = e->d_bspec + e->mbh * k;
         F.ref_done = k == 0 ? nullptr : e->d_done + (k - 1) * nmb;
@@ -1114,7 +1115,6 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         pf.D.st = e->d_st;
         pf.pl_out = e->d_bpl + 4 * e->plsz * k;
         pf.deblock = e->p.deblock;
-        pf.hrec = e->dh_brec + nmb * k;
     }
     HL_HIP_CHECK(hipMemcpyAsync(e->d_pf, e->h_pf, sizeof(PipeFrame) * m, hipMemcpyHostToDevice, e->stream));
     PipeArgs P;

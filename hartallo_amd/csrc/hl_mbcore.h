@@ -97,6 +97,8 @@ struct FrameArgs {
     int32_t plsz;           // pl[i] = pl[0] + i * plsz (device buffers)
     MbState* st;
     MbRecord* rec;
+    MbRecord* hrec;         // host-mapped copy of the records (pipelined runs: the slice writers read it), or null
+    int32_t rec_dev;        // 1 = write the records to rec (device memory) too
     MbChain* chain;
     const int32_t* spec;  // speculated Single_ctr at each row start
     unsigned long long* prof;  // phase cycle counters (profiling build), may be null
@@ -128,6 +130,10 @@ static constexpr PartDef kParts[7] = {
     {4, 4, 4, 4, 8, 8, 27, 3}};
 
 struct Shared {
+    MbState nbst[5];  // MB start (device): the MB objects of the current address, A, B, C, D as loaded;
+                      // nbst[0] becomes the MB's new object at the MB end
+    MbRecord recb;    // MB end (device): the record, assembled before its 16-byte stores
+    int8_t tcn[16], tccn[2][4];  // MB end (device): TotalCoeffs after the final CAVLC write
     NbInfo nb[5];  // 0 = current MB (live search state), 1 = A, 2 = B, 3 = C, 4 = D
     int32_t mvg[5][6];  // motion grid, see MvN
     int8_t mvs[5][6];
@@ -463,6 +469,239 @@ HD void load_nbinfo(const MbState& m, NbInfo& n)
         }
 }
 
+// diagnostic builds (-DHL_DIAG_INPUTS): digests of everything the decision
+// reads from other macroblocks, so that a parity failure names the input that
+// differed
+HD void mb_diag_inputs(Ctx& c)
+{
+#if defined(HL_DIAG_INPUTS)
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    const int tid = c.tid, a = c.addr;
+    // diagnostic builds: digests of everything the decision reads from other
+    // macroblocks, so that a parity failure names the input that differed
+    if (tid == 0) {
+        auto fnv = [](const void* p, int n, uint32_t h) {
+            const uint8_t* b = (const uint8_t*)p;
+            for (int i = 0; i < n; ++i) h = (h ^ b[i]) * 16777619u;
+            return h;
+        };
+#if defined(__HIP_DEVICE_COMPILE__)
+        uint32_t* d = S.recb.dbg;  // stored with the record at the MB end
+        (void)F;
+        (void)a;
+#else
+        uint32_t* d = F.rec[a].dbg;
+#endif
+        d[0] = fnv(S.top, sizeof(S.top), 2166136261u);
+        d[1] = fnv(S.left, sizeof(S.left), 2166136261u);
+        d[2] = fnv(S.cleft, sizeof(S.cleft), fnv(S.ctop, sizeof(S.ctop), 2166136261u));
+        uint32_t h = 2166136261u;
+        for (int w = 1; w < 5; ++w) {
+            h = fnv(&S.nb[w].avail, 4, h);
+            if (S.nb[w].avail) h = fnv(&S.nb[w], sizeof(NbInfo), h);
+        }
+        d[3] = fnv(S.mvs, sizeof(S.mvs), fnv(S.mvg, sizeof(S.mvg), h));
+        d[4] = fnv(S.extCB, 4, fnv(S.extCA, 4, fnv(S.extB, 16, fnv(S.extA, 16, fnv(S.nb_i4, sizeof(S.nb_i4), fnv(S.nb_pm0, 12, 2166136261u))))));
+        d[5] = fnv(&S.cbp_c, 4, fnv(&S.cbp_l, 4, fnv(S.tcc, 8, fnv(S.tc, 16, 2166136261u))));
+        d[6] = fnv(S.cac, sizeof(S.cac), fnv(S.src, 256, 2166136261u));
+        d[7] = (uint32_t)(c.chain & 0xFF) | ((uint32_t)c.spec << 8);
+    }
+#else
+    (void)c;
+#endif
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// MB start on the device: every global load of the MB start is issued in one
+// round -- the MB objects of this address and of A, B, C, D (16-byte words),
+// the source samples, the intra neighbour samples of the current picture and
+// the CAVLC length tables -- and lands in LDS; the derivations then run from
+// LDS, each on its own lanes.  Same results as the host version below.
+__device__ __forceinline__ void mb_begin(Ctx& c)
+{
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    const int tid = c.tid;
+    const int a = c.addr;
+    const int hasA = c.mbx > 0, hasB = c.mby > 0, hasC = c.mby > 0 && c.mbx < F.mbw - 1, hasD = c.mbx > 0 && c.mby > 0;
+    const int xc = c.xL >> 1, yc = c.yL >> 1;
+    constexpr int kW = (int)(sizeof(MbState) / 16);  // 16-byte words per MB object
+    // ---- round 1: loads (addresses clamped to valid memory, values unused there)
+    uint4 q = make_uint4(0, 0, 0, 0);
+    int b1 = kNA, b2 = 0, b3 = 0;
+    if (tid < 5 * kW) {
+        const int w = tid / kW, i = tid - w * kW;
+        const int off = w == 0 ? 0 : (w == 1 ? -1 : (w == 2 ? -F.mbw : (w == 3 ? -F.mbw + 1 : -F.mbw - 1)));
+        const bool avw = w == 0 || (w == 1 ? hasA : (w == 2 ? hasB : (w == 3 ? hasC : hasD)));
+        q = reinterpret_cast<const uint4*>(F.st + (avw ? a + off : a))[i];
+    }
+    else if (tid < 5 * kW + 16) {
+        q = *reinterpret_cast<const uint4*>(F.src[0] + (size_t)(c.yL + tid - 5 * kW) * F.W + c.xL);
+    }
+    else if (tid < 5 * kW + 32) {
+        const int k = tid - 5 * kW - 16, comp = k >> 3;
+        const uint2 d = *reinterpret_cast<const uint2*>(F.src[1 + comp] + (size_t)(yc + (k & 7)) * F.Wc + xc);
+        q.x = d.x;
+        q.y = d.y;
+    }
+    // intra neighbour samples from the (unfiltered) current picture
+    if (tid < 25) {
+        const int x = tid - 1;
+        if (x < 0 ? hasD : (x < 16 ? hasB : (x < 20 ? hasC : false))) b1 = F.cur[0][(size_t)(c.yL - 1) * F.W + c.xL + x];
+    }
+    else if (tid >= 32 && tid < 48) {
+        if (hasA) b1 = F.cur[0][(size_t)(c.yL + tid - 32) * F.W + c.xL - 1];
+    }
+    else if (tid >= 64 && tid < 82) {
+        const int comp = (tid - 64) / 9, x = (tid - 64) % 9 - 1;
+        if (x < 0 ? hasD : hasB) b1 = F.cur[1 + comp][(size_t)(yc - 1) * F.Wc + xc + x];
+    }
+    else if (tid >= 96 && tid < 112) {
+        const int comp = (tid - 96) >> 3, y = (tid - 96) & 7;
+        if (hasA) b1 = F.cur[1 + comp][(size_t)(yc + y) * F.Wc + xc - 1];
+    }
+    if (tid < 15 * 16) b2 = kTzLen[tid >> 4][tid & 15];
+    if (tid < 3 * 4 * 17) b3 = kTokLen[tid / 68][(tid / 17) % 4][tid % 17];
+    // ---- stores
+    if (tid < 5 * kW) reinterpret_cast<uint4*>(S.nbst)[tid] = q;
+    else if (tid < 5 * kW + 16) reinterpret_cast<uint4*>(S.src)[tid - 5 * kW] = q;
+    else if (tid < 5 * kW + 32) {
+        const int k = tid - 5 * kW - 16;
+        *reinterpret_cast<uint2*>(&S.srcc[k >> 3][(k & 7) * 8]) = make_uint2(q.x, q.y);
+    }
+    if (tid < 25) S.top[tid] = (int16_t)b1;
+    else if (tid >= 32 && tid < 48) S.left[tid - 32] = (int16_t)b1;
+    else if (tid >= 64 && tid < 82) S.ctop[(tid - 64) / 9][(tid - 64) % 9] = (int16_t)b1;
+    else if (tid >= 96 && tid < 112) S.cleft[(tid - 96) >> 3][(tid - 96) & 7] = (int16_t)b1;
+    if (tid < 15 * 16) S.ct.tz[tid >> 4][tid & 15] = (uint8_t)b2;
+    if (tid < 3 * 4 * 17) S.ct.tok[tid / 68][(tid / 17) % 4][tid % 17] = (uint8_t)b3;
+    if (tid >= 448 && tid < 464) {
+        const int8_t* e = kQpelTab[tid - 448];
+        S.qtab[tid - 448] = (uint32_t)(e[0] | (e[1] << 2) | (e[2] << 3) | ((e[3] >= 0) << 4) | ((e[3] >= 0 ? e[3] : 0) << 5) | (e[4] << 7) | (e[5] << 8));
+    }
+    HL_SYNC();
+    // ---- round 2: derivations from LDS, spread over the waves
+    // availability of MB w (no dynamically indexed array: it would live in scratch)
+    auto av = [&](int w) -> bool { return w == 0 || (w == 1 ? hasA : (w == 2 ? hasB : (w == 3 ? hasC : hasD))); };
+    if (tid < 30) {  // motion grid: row -1 from D / B / C, column -1 from A, inside undecided
+        const int gy = tid / 6, gx = tid % 6, bx = gx - 1, by = gy - 1;
+        int w = 0, st = 0, v = 0;
+        if (by < 0) w = bx < 0 ? 4 : (bx < 4 ? 2 : 3);
+        else if (bx < 0) w = 1;
+        if (w && av(w)) {
+            const MbState& M = S.nbst[w];
+            const int xW = (bx + 4) & 3, yW = (by + 4) & 3;  // 4x4 block of the neighbour
+            if (M.flags & FL_INTRA) st = 1;
+            else {
+                const int x = xW * 4, y = yW * 4;
+                const int pi = (16 / M.part_w) * (y / M.part_h) + (x / M.part_w);
+                const int spi = is8x8(M.e_type) ? (8 / M.sub_w[pi]) * ((y % 8) / M.sub_h[pi]) + ((x % 8) / M.sub_w[pi]) : 0;
+                st = 2;
+                v = (M.mv[pi][spi][0] & 0xFFFF) | (M.mv[pi][spi][1] << 16);
+            }
+        }
+        S.mvs[gy][gx] = (int8_t)st;
+        S.mvg[gy][gx] = v;
+    }
+    else if (tid >= 64 && tid < 128) {  // neighbour summaries: motion (one word per lane)
+        const int w = ((tid - 64) >> 4) + 1, k = (tid - 64) & 15;
+        if (av(w)) reinterpret_cast<int32_t*>(&S.nb[w].mv[0][0][0])[k] = reinterpret_cast<const int32_t*>(&S.nbst[w].mv[0][0][0])[k];
+    }
+    else if (tid >= 128 && tid < 132) {  // neighbour summaries: shape
+        const int w = tid - 127;
+        NbInfo& n = S.nb[w];
+        if (av(w)) {
+            const MbState& m = S.nbst[w];
+            n.avail = 1;
+            n.intra = (m.flags & FL_INTRA) ? 1 : 0;
+            n.e_type = m.e_type;
+            n.part_w = m.part_w;
+            n.part_h = m.part_h;
+            for (int i = 0; i < 4; ++i) {
+                n.sub_w[i] = m.sub_w[i];
+                n.sub_h[i] = m.sub_h[i];
+            }
+        }
+        else n.avail = 0;
+    }
+    else if (tid >= 132 && tid < 164) {  // A / B intra modes
+        const int w = ((tid - 132) >> 4) + 1, i = (tid - 132) & 15;
+        if (i == 0) S.nb_pm0[w] = av(w) ? S.nbst[w].pm0 : 0;
+        S.nb_i4[w][i] = av(w) ? S.nbst[w].i4mode[i] : 2;
+    }
+    else if (tid >= 192 && tid < 208) {  // external nC contributions (neighbour MBs are final for this frame)
+        const int t = tid - 192, bx = blk_x(t), by = blk_y(t);
+        int8_t ea = -2, eb = -2;
+        if (bx == 0) {
+            if (!hasA) ea = -1;
+            else {
+                const MbState& A = S.nbst[1];
+                const int nb = blk_idx(12, by);
+                ea = (A.e_type == ET_PSKIP || !(A.cbp_l & (1 << (nb >> 2)))) ? 0 : A.tc_luma[nb];
+            }
+        }
+        if (by == 0) {
+            if (!hasB) eb = -1;
+            else {
+                const MbState& B = S.nbst[2];
+                const int nb = blk_idx(bx, 12);
+                eb = (B.e_type == ET_PSKIP || !(B.cbp_l & (1 << (nb >> 2)))) ? 0 : B.tc_luma[nb];
+            }
+        }
+        S.extA[t] = ea;
+        S.extB[t] = eb;
+    }
+    else if (tid >= 208 && tid < 212) {  // chroma external nC: extCA[c*2 + row], extCB[c*2 + col]
+        const int t = tid - 208, comp = t >> 1, k = t & 1;
+        int8_t ea = -1, eb = -1;
+        if (hasA) {
+            const MbState& A = S.nbst[1];
+            ea = (A.e_type == ET_PSKIP || !(A.cbp_c & 2)) ? 0 : A.tc_cac[comp][k * 2 + 1];
+        }
+        if (hasB) {
+            const MbState& B = S.nbst[2];
+            eb = (B.e_type == ET_PSKIP || !(B.cbp_c & 2)) ? 0 : B.tc_cac[comp][2 + k];
+        }
+        S.extCA[t] = ea;
+        S.extCB[t] = eb;
+    }
+    else if (tid >= 256 && tid < 384) {  // live state of this address (stale from the previous frame)
+        const int t = tid - 256;
+        S.cac[t >> 6][(t >> 4) & 3][t & 15] = S.nbst[0].cac_level[t >> 6][(t >> 4) & 3][t & 15];
+        if (t < 16) S.tc[t] = S.nbst[0].tc_luma[t];
+        else if (t < 24) S.tcc[(t - 16) >> 2][(t - 16) & 3] = S.nbst[0].tc_cac[(t - 16) >> 2][(t - 16) & 3];
+    }
+    else if (tid >= 384 && tid < 400) {  // this MB's decision fields, initial values
+        const int i = tid - 384;
+        S.i4mode[i] = 2;
+        S.prev_flag[i] = 0;
+        S.rem_mode[i] = 0;
+        reinterpret_cast<int32_t*>(&S.mvd[0][0][0])[i] = 0;
+        if (i < 4) {
+            S.num_sub[i] = 1;
+            S.sub_type[i] = -1;
+        }
+        if (i == 0) {
+            const MbState& M = S.nbst[0];
+            S.cbp_l = M.cbp_l;
+            S.cbp_c = M.cbp_c;
+            S.cbp_l4x4 = 0;
+            S.cbp_cac[0] = S.cbp_cac[1] = 0;
+            S.cbp_cdc[0] = S.cbp_cdc[1] = 0;
+            S.nb[0].avail = 1;
+            S.nb[0].intra = 0;
+            S.nb[0].e_type = M.e_type;
+            S.num_part = 1;
+            S.i16mode = 2;
+            S.chroma_mode = 0;
+            S.mb_type = 0;
+        }
+    }
+    HL_SYNC();
+    mb_diag_inputs(c);
+}
+#else
 HD void mb_begin(Ctx& c)
 {
     const FrameArgs& F = c.F;
@@ -617,32 +856,9 @@ HD void mb_begin(Ctx& c)
         S.mb_type = 0;
     }
     HL_SYNC();
-#if defined(HL_DIAG_INPUTS)
-    // diagnostic builds: digests of everything the decision reads from other
-    // macroblocks, so that a parity failure names the input that differed
-    if (tid == 0) {
-        auto fnv = [](const void* p, int n, uint32_t h) {
-            const uint8_t* b = (const uint8_t*)p;
-            for (int i = 0; i < n; ++i) h = (h ^ b[i]) * 16777619u;
-            return h;
-        };
-        uint32_t* d = F.rec[a].dbg;
-        d[0] = fnv(S.top, sizeof(S.top), 2166136261u);
-        d[1] = fnv(S.left, sizeof(S.left), 2166136261u);
-        d[2] = fnv(S.cleft, sizeof(S.cleft), fnv(S.ctop, sizeof(S.ctop), 2166136261u));
-        uint32_t h = 2166136261u;
-        for (int w = 1; w < 5; ++w) {
-            h = fnv(&S.nb[w].avail, 4, h);
-            if (S.nb[w].avail) h = fnv(&S.nb[w], sizeof(NbInfo), h);
-        }
-        d[3] = fnv(S.mvs, sizeof(S.mvs), fnv(S.mvg, sizeof(S.mvg), h));
-        d[4] = fnv(S.extCB, 4, fnv(S.extCA, 4, fnv(S.extB, 16, fnv(S.extA, 16, fnv(S.nb_i4, sizeof(S.nb_i4), fnv(S.nb_pm0, 12, 2166136261u))))));
-        d[5] = fnv(&S.cbp_c, 4, fnv(&S.cbp_l, 4, fnv(S.tcc, 8, fnv(S.tc, 16, 2166136261u))));
-        d[6] = fnv(S.cac, sizeof(S.cac), fnv(S.src, 256, 2166136261u));
-        d[7] = (uint32_t)(c.chain & 0xFF) | ((uint32_t)c.spec << 8);
-    }
-#endif
+    mb_diag_inputs(c);
 }
+#endif
 
 // --------------------------------------------------------------------------
 // Inter candidate evaluation (me_ds.c:527-688 for a list of MVs)
@@ -1373,14 +1589,50 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
             pv_mvy = cs.mvy;
             pv_pad = cs.pad;
         }
+        // The sequential strict-< scans of every step of the chain
+        // (me_ds.c:339-347) at once: four independent DPP minimum chains over
+        // the candidate lanes of each step, then each step's smallest cost and
+        // the first candidate holding it as uniform values.  Resolving the
+        // chain below is then scalar work.
+        double sm[kMaxSeg];
+        int sb[kMaxSeg];
+        {
+            const int l = c.tid & 31;
+            bool in[kMaxSeg];
+            double v[kMaxSeg], rm[kMaxSeg];
+#pragma unroll
+            for (int j = 0; j < kMaxSeg; ++j) {
+                in[j] = j < nseg && l >= lo[j] && l < lo[j] + n[j];
+                v[j] = in[j] ? pv_cost : 1.7976931348623157e308;
+                rm[j] = row_min_f64(v[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < kMaxSeg; ++j) {
+                const unsigned long long b0 = __builtin_bit_cast(unsigned long long, rm[j]);
+                const double m0 = __builtin_bit_cast(double, (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(b0 >> 32), 0) << 32 |
+                                                                 (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b0, 0));
+                const double m1 = __builtin_bit_cast(double, (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(b0 >> 32), 16) << 32 |
+                                                                 (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b0, 16));
+                sm[j] = fmin(m0, m1);
+                sb[j] = __ffsll((long long)(__ballot(in[j] && v[j] == sm[j]) & 0xFFFFFFFFull)) - 1;
+            }
+        }
+        auto seg_pick = [&](int j, double& m) -> int {
+            m = sm[j];
+            return sb[j];
+        };
+#else
+        auto seg_pick = [&](int j, double& m) -> int { return pick(lo[j], lo[j] + n[j], m); };
 #endif
         // resolve the chain step by step
         int used = 0;
-        for (int j = 0; j < nseg; ++j) {
+#pragma unroll
+        for (int j = 0; j < kMaxSeg; ++j) {
+            if (j >= nseg) break;
             used = lo[j] + n[j];
             if (stage == 3) {  // MVP / (0,0) (me_ds.c:280-300)
                 double m;
-                const int bi = pick(lo[j], lo[j] + n[j], m);
+                const int bi = seg_pick(j, m);
                 if (m < b.cost) take(bi, m);
                 stage = 2;
                 cx = centre_of(2, b.mv[0]);
@@ -1396,7 +1648,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
             int best = -1;
             if (n[j]) {
                 double m;
-                const int bi = pick(lo[j], lo[j] + n[j], m);
+                const int bi = seg_pick(j, m);
                 if (m < b.cost) best = take(bi, m);
             }
             if (best >= 0) {  // moved: the stage goes on from the new centre (window kept, me_ds.c:309)
@@ -1911,8 +2163,12 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp, int& best_dist)
             bcbp |= 1 << b;
             if (uni(S.i16_tc[b]) > 0) chain_write(c, uni(S.i16_sctr[b]));
             else if (!c.fresh) {
-                if (c.spec && F.run_done) resolve_chain(c);  // pipelined run: read the exact value
-                else c.dep = 1;
+                // pipelined run: a speculated value is resolved here; once it
+                // is exact (resolved in this MB or to its left) the read is
+                // exact too.  The per-picture path records the stale read for
+                // the host's row validation.
+                if (!F.run_done) c.dep = 1;
+                else if (c.spec) resolve_chain(c);
             }
             single += c.chain;
         }
@@ -2815,6 +3071,180 @@ HD void final_write(Shared& S)
 // --------------------------------------------------------------------------
 // MB end: write recon, persistent state and the record
 // --------------------------------------------------------------------------
+#if defined(__HIP_DEVICE_COMPILE__)
+// count of non-zero entries
+template <typename T>
+__device__ __forceinline__ int count_nz(const T* v, int n)
+{
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) k += (i < n && v[i] != 0) ? 1 : 0;
+    return k;
+}
+
+// MB end on the device: final_write's TotalCoeff updates and nC (one lane
+// per block: the z-order loop of mb.c:543-892 reads only neighbours that
+// precede the block, whose values are final by then), then the new MB
+// object and the record assembled in LDS by many lanes at once and stored
+// as 16-byte words (the record to the host-mapped copy of a pipelined run
+// and / or device memory).  Same results as the host version below.
+__device__ __forceinline__ void mb_end(Ctx& c)
+{
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    const int tid = c.tid;
+    const int e_type = S.e_type, pm0 = S.pm0, cbp_l = S.cbp_l, cbp_c = S.cbp_c;
+    const bool coded = e_type != ET_PSKIP && (cbp_l > 0 || cbp_c > 0 || pm0 == PM_I16);
+    const bool intra = (S.flags & FL_INTRA) != 0;
+    // ---- TotalCoeffs after the write
+    if (tid < 16) {
+        const int blk = tid;
+        int t = S.tc[blk];
+        if (coded) {
+            if (cbp_l & (1 << (blk >> 2))) t = pm0 == PM_I16 ? count_nz(S.i16_best_ac[blk], 15) : count_nz(S.luma_level[blk], 16);
+            else if (blk == 0 && pm0 == PM_I16) t = count_nz(S.i16_best_dc, 16);
+        }
+        S.tcn[blk] = (int8_t)t;
+    }
+    else if (tid >= 64 && tid < 72) {
+        const int comp = (tid - 64) >> 2, i4 = (tid - 64) & 3;
+        int t = S.tcc[comp][i4];
+        if (coded && (cbp_c & 2)) t = (S.cbp_cac[comp] & (1 << i4)) ? count_nz(S.cac[comp][i4], 15) : 0;
+        S.tccn[comp][i4] = (int8_t)t;
+    }
+    HL_SYNC();
+    // ---- nC of every written block
+    if (tid < 16) {
+        const int blk = tid;
+        int nc = 0;
+        if (coded && (cbp_l & (1 << (blk >> 2)))) nc = nc_luma_of(S, blk, [&](int ni) -> int { return S.tcn[ni]; });
+        S.nc_luma[blk] = (int8_t)nc;
+        if (blk == 0) S.nc_dc = (int8_t)(coded && pm0 == PM_I16 ? nc_luma_of(S, 0, [&](int ni) -> int { return S.tcn[ni]; }) : 0);
+    }
+    else if (tid >= 64 && tid < 72) {
+        const int comp = (tid - 64) >> 2, i4 = (tid - 64) & 3;
+        int nc = 0;
+        if (coded && (cbp_c & 2)) {
+            int nA, nB;
+            bool aA, aB;
+            if (i4 & 1) {
+                aA = true;
+                nA = S.tccn[comp][i4 - 1];
+            }
+            else {
+                aA = S.extCA[comp * 2 + (i4 >> 1)] >= 0;
+                nA = aA ? S.extCA[comp * 2 + (i4 >> 1)] : 0;
+            }
+            if (i4 & 2) {
+                aB = true;
+                nB = S.tccn[comp][i4 - 2];
+            }
+            else {
+                aB = S.extCB[comp * 2 + (i4 & 1)] >= 0;
+                nB = aB ? S.extCB[comp * 2 + (i4 & 1)] : 0;
+            }
+            nc = aA && aB ? (nA + nB + 1) >> 1 : (aA ? nA : (aB ? nB : 0));
+        }
+        S.nc_cac[comp][i4] = (int8_t)nc;
+    }
+    HL_SYNC();
+    // ---- the MB object (over the one loaded at the MB start) and the record, in LDS
+    MbState& M = S.nbst[0];
+    MbRecord& R = S.recb;
+    if (tid < 64) {  // ChromaACLevel of both
+        const int32_t w = reinterpret_cast<const int32_t*>(&S.cac[0][0][0])[tid];
+        reinterpret_cast<int32_t*>(&M.cac_level[0][0][0])[tid] = w;
+        reinterpret_cast<int32_t*>(&R.cac[0][0][0])[tid] = w;
+    }
+    else if (tid < 192) {  // LumaLevel / Intra16x16ACLevel, two levels per lane
+        const int k = (tid - 64) * 2, b = k >> 4, i = k & 15;
+        const int l0 = pm0 == PM_I16 ? S.i16_best_ac[b][i] : S.luma_level[b][i];
+        const int l1 = pm0 == PM_I16 ? S.i16_best_ac[b][i + 1] : S.luma_level[b][i + 1];
+        reinterpret_cast<int32_t*>(&R.luma[0][0])[k >> 1] = (int32_t)((l0 & 0xFFFF) | ((uint32_t)l1 << 16));
+    }
+    else if (tid < 208) {  // motion: the record's mvd and mv, the object's mv (inter MBs)
+        const int k = tid - 192;
+        const int32_t mv = reinterpret_cast<const int32_t*>(&S.nb[0].mv[0][0][0])[k];
+        reinterpret_cast<int32_t*>(&R.mvd[0][0][0])[k] = reinterpret_cast<const int32_t*>(&S.mvd[0][0][0])[k];
+        reinterpret_cast<int32_t*>(&R.mv[0][0][0])[k] = mv;
+        if (!intra) reinterpret_cast<int32_t*>(&M.mv[0][0][0])[k] = mv;
+    }
+    else if (tid < 224) {  // per-block bytes and the I16x16 DC levels
+        const int i = tid - 208;
+        R.prev_flag[i] = S.prev_flag[i];
+        R.rem_mode[i] = S.rem_mode[i];
+        R.i4mode[i] = S.i4mode[i];
+        R.nc_luma[i] = S.nc_luma[i];
+        R.i16dc[i] = S.i16_best_dc[i];
+        M.i4mode[i] = S.i4mode[i];
+        M.tc_luma[i] = S.tcn[i];
+        if (i < 8) {
+            R.nc_cac[i >> 2][i & 3] = S.nc_cac[i >> 2][i & 3];
+            R.cdc[i >> 2][i & 3] = (int16_t)S.cdc_level[i >> 2][i & 3];
+            M.tc_cac[i >> 2][i & 3] = S.tccn[i >> 2][i & 3];
+        }
+        if (i < 4) {
+            R.num_sub[i] = S.num_sub[i];
+            R.sub_mb_type[i] = S.sub_type[i];
+            if (!intra) {
+                M.sub_w[i] = S.nb[0].sub_w[i];
+                M.sub_h[i] = S.nb[0].sub_h[i];
+            }
+        }
+    }
+    else if (tid == 224) {  // the scalar fields
+        M.e_type = e_type;
+        M.flags = S.flags;
+        M.pm0 = pm0;
+        M.cbp_l = cbp_l;
+        M.cbp_c = cbp_c;
+        M.cbp_l4x4 = S.cbp_l4x4;
+        if (!intra) {
+            M.num_part = S.num_part;
+            M.part_w = S.nb[0].part_w;
+            M.part_h = S.nb[0].part_h;
+        }
+        R.e_type = e_type;
+        R.mb_type = S.mb_type;
+        R.flags = S.flags;
+        R.pm0 = pm0;
+        R.cbp = S.cbp;
+        R.cbp_l = cbp_l;
+        R.cbp_c = cbp_c;
+        R.cbp_l4x4 = S.cbp_l4x4;
+        for (int i = 0; i < 2; ++i) {
+            R.cbp_cdc[i] = S.cbp_cdc[i];
+            R.cbp_cac[i] = S.cbp_cac[i];
+        }
+        R.num_part = S.num_part;
+        R.chroma_mode = S.chroma_mode;
+        R.i16mode = S.i16mode;
+        R.nc_dc = S.nc_dc;
+        R.pad0[0] = R.pad0[1] = R.pad0[2] = 0;
+        R.mad = S.mad;
+        R.pad1 = 0;
+        MbChain& ch = F.chain[c.addr];
+        ch.s_out = c.chain;
+        ch.dep = c.dep;
+        ch.fresh = c.fresh;
+        ch.spec = c.spec;
+    }
+    HL_SYNC();
+    // ---- 16-byte stores: the reconstruction, the MB object, the record
+    constexpr int kSW = (int)(sizeof(MbState) / 16), kRW = (int)(sizeof(MbRecord) / 16);
+    static_assert(sizeof(MbRecord) % 16 == 0, "MbRecord in whole 16-byte words");
+    if (tid < 16)
+        *reinterpret_cast<uint4*>(F.cur[0] + (size_t)(c.yL + tid) * F.W + c.xL) = reinterpret_cast<const uint4*>(S.rec)[tid];
+    else if (tid >= 64 && tid < 64 + kSW)
+        reinterpret_cast<uint4*>(F.st + c.addr)[tid - 64] = reinterpret_cast<const uint4*>(&M)[tid - 64];
+    else if (tid >= 128 && tid < 128 + kRW) {
+        const uint4 w = reinterpret_cast<const uint4*>(&R)[tid - 128];
+        if (F.hrec) reinterpret_cast<uint4*>(F.hrec + c.addr)[tid - 128] = w;
+        if (F.rec_dev) reinterpret_cast<uint4*>(F.rec + c.addr)[tid - 128] = w;
+    }
+    HL_SYNC();
+}
+#else
 HD void mb_end(Ctx& c)
 {
     const FrameArgs& F = c.F;
@@ -2906,6 +3336,7 @@ HD void mb_end(Ctx& c)
     }
     HL_SYNC();
 }
+#endif
 
 // One macroblock, start to end.  s_in = rdo.Single_ctr on entry (spec_in = 1
 // while it is a row-start speculation); (gx, gy) = reference region already

@@ -108,7 +108,6 @@ struct PipeFrame {
     DeblockArgs D;
     uint8_t* pl_out;  // this picture's quarter-pel planes (plane p at pl_out + p * F.plsz)
     int32_t deblock;  // deblocking enabled (disable_deblocking_filter_idc 0)
-    MbRecord* hrec;   // host-mapped copy of the picture's records (the slice writers read it during the run), or null
 };
 
 // Dependencies of task (f, x, y) inside a run: the wavefront neighbours

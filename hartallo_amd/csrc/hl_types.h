@@ -31,7 +31,7 @@ enum : int32_t { FL_INTRA = 1, FL_INTER = 2, FL_SKIP = 4 };
 // MbPartPredMode[0]
 enum : int32_t { PM_L0 = 1, PM_I4 = 2, PM_I16 = 3 };
 
-struct MbState {
+struct alignas(16) MbState {  // 432 bytes: whole 16-byte words (mb_begin loads neighbours as uint4)
     int32_t e_type, flags, pm0;
     int32_t cbp_l, cbp_c, cbp_l4x4;
     int32_t num_part, part_w, part_h;
@@ -41,7 +41,9 @@ struct MbState {
     int8_t tc_luma[16];           // TotalCoeffsLuma
     int8_t tc_cac[2][4];          // TotalCoeffsChromaACCbCr
     int16_t cac_level[2][4][16];  // ChromaACLevel (read stale by decode_chroma)
+    int32_t pad;
 };
+static_assert(sizeof(MbState) % 16 == 0, "MbState in whole 16-byte words");
 
 struct MbRecord {
     int32_t e_type, mb_type, flags, pm0;

@@ -1,0 +1,26 @@
+#!/bin/bash
+# rocprofv3 PMC counters of k_pipeline on bench.py's driver workload
+# (--steps 20 --warmup 5), run on the GPU box from the repo root:
+#   bash tools/pmc_record.sh
+# Four passes, each in a run of its own (MI355X_MICROARCH.md: counter slots
+# per block, FETCH_SIZE and WRITE_SIZE cannot share a pass): two SQ sets,
+# FETCH_SIZE, WRITE_SIZE.  tools/pmc_summary.py then writes
+# tools/pmc/pmc_k_pipeline.json for the timed launch (the last k_pipeline
+# dispatch), stamped with the SHA-256 of the library it measured; bench.py
+# uses the counters only when that hash is the loaded library's.
+set -o pipefail
+mkdir -p gpurun_out/pmc
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+sets=("SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD"
+      "SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_LDS SQ_INSTS_SMEM SQ_INST_LEVEL_SMEM"
+      "FETCH_SIZE" "WRITE_SIZE")
+i=0
+for set in "${sets[@]}"; do
+  i=$((i+1))
+  timeout -s KILL 300 rocprofv3 --pmc $set -d $R/gpurun_out/pmc/p$i -o run --output-format csv -- \
+      python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $R/gpurun_out/pmc/p$i.log 2>&1 || exit $?
+done
+cd $R
+python3 tools/pmc_summary.py --warmup 5 --steps 20 gpurun_out/pmc/p1 gpurun_out/pmc/p2 gpurun_out/pmc/p3 gpurun_out/pmc/p4 \
+    > tools/pmc/pmc_k_pipeline.json && cat tools/pmc/pmc_k_pipeline.json

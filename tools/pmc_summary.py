@@ -1,36 +1,72 @@
-"""Summarises rocprofv3 FETCH_SIZE / WRITE_SIZE passes for the pipelined
-kernel into bytes per launch and per macroblock (JSON on stdout).
+"""Summarises rocprofv3 --pmc passes over bench.py (tools/pmc_record.sh)
+into the counters of the timed k_pipeline launch (the last dispatch of the
+kernel: the warm-up call's launch comes first), per launch and per
+macroblock, stamped with the SHA-256 of the library that ran (JSON on
+stdout).
 
-FETCH_SIZE is doubled as MI355X_MICROARCH.md (HBM) prescribes for gfx950
-(it tallies 128-B requests at 64 B); both counters are in KiB units as
-rocprofv3 reports them (TCC_EA0_*REQ x 64 B / 1024).
+Units and corrections (MI355X_MICROARCH.md): SQ_WAVE_CYCLES / SQ_WAIT_* /
+SQ_ACTIVE_INST_* count quad-cycles (the ratios between them are unit-free);
+FETCH_SIZE / WRITE_SIZE are KiB (TCC_EA0_*REQ x 64 B / 1024) and FETCH_SIZE
+is doubled for gfx950 (128-B requests tallied at 64 B; calibrated for
+16 B/lane streaming reads -- this kernel's byte gathers are uncalibrated, and
+Infinity-Cache hits are counted, not excluded).
+
+  python tools/pmc_summary.py --warmup W --steps S DIR [DIR ...]
 """
+import argparse
 import collections
 import csv
+import glob
+import hashlib
 import json
-import sys
+import os
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_kernel(path):
-    acc = collections.defaultdict(lambda: [0.0, 0])
+def timed_launch(d):
+    """{counter: value} of the last k_pipeline dispatch in one pass."""
+    path = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+    acc = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(path)):
-        k = r["Kernel_Name"].split("(")[0]
-        acc[(k, r["Counter_Name"])][0] += float(r["Counter_Value"])
-        acc[(k, r["Counter_Name"])][1] += 1
-    return acc
+        if not r["Kernel_Name"].startswith("k_pipeline"):
+            continue
+        key = r.get("Dispatch_Id") or r.get("Correlation_Id") or r.get("Start_Timestamp")
+        acc[int(key)][r["Counter_Name"]] += float(r["Counter_Value"])
+    return acc[max(acc)], len(acc)
 
 
 def main():
-    f, w = per_kernel(sys.argv[1]), per_kernel(sys.argv[2])
-    fetch = f[("k_pipeline", "FETCH_SIZE")]
-    write = w[("k_pipeline", "WRITE_SIZE")]
-    launches = fetch[1]
-    mbs = 12 * (1920 // 16) * (1088 // 16)  # bench --steps 12 --warmup 0: one launch of 12 pictures (IDR + 11 P)
-    rd = 2.0 * fetch[0] * 1024 / launches
-    wr = write[0] * 1024 / launches
-    out = {"kernel": "k_pipeline", "launches": launches, "macroblocks_per_launch": mbs, "fetch_bytes_per_launch_x2": rd,
-           "write_bytes_per_launch": wr, "traffic_bytes_per_launch": rd + wr, "traffic_bytes_per_mb": (rd + wr) / mbs,
-           "note": "FETCH_SIZE x2 (gfx950 correction, calibrated for 16 B/lane reads; this kernel's byte gathers are uncalibrated)"}
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--warmup", type=int, required=True)
+    ap.add_argument("--steps", type=int, required=True)
+    ap.add_argument("dirs", nargs="+")
+    a = ap.parse_args()
+    c, launches = {}, set()
+    for d in a.dirs:
+        v, n = timed_launch(d)
+        c.update(v)
+        launches.add(n)
+    mbs = a.steps * (1920 // 16) * (1088 // 16)  # the timed call: one launch of `steps` pictures
+    lib = os.path.join(ROOT, "hartallo_amd", "libhartallo_amd.so")
+    out = {
+        "kernel": "k_pipeline", "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
+        "recorded": time.strftime("%Y-%m-%d"), "warmup": a.warmup, "steps": a.steps,
+        "k_pipeline_dispatches_per_pass": sorted(launches), "macroblocks_per_launch": mbs,
+        "counters": {k: c[k] for k in sorted(c)},
+    }
+    if "SQ_WAVE_CYCLES" in c:
+        out["sq_wait_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+        out["sq_issue_frac"] = round(c["SQ_ACTIVE_INST_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+        out["valu_insts_per_mb"] = round(c["SQ_INSTS_VALU"] / mbs)
+        out["lds_insts_per_mb"] = round(c["SQ_INSTS_LDS"] / mbs)
+        out["salu_insts_per_mb"] = round(c["SQ_INSTS_SALU"] / mbs)
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        rd, wr = 2.0 * c["FETCH_SIZE"] * 1024, c["WRITE_SIZE"] * 1024
+        out.update({"fetch_bytes_per_launch_x2": rd, "write_bytes_per_launch": wr, "traffic_bytes_per_launch": rd + wr,
+                    "fetch_bytes_per_mb_x2": round(rd / mbs, 1), "write_bytes_per_mb": round(wr / mbs, 1),
+                    "traffic_bytes_per_mb": round((rd + wr) / mbs, 1)})
     print(json.dumps(out, indent=1))
 
 
