@@ -2155,14 +2155,18 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp, int& best_dist)
             }
         }
         HL_SYNC();
-        // uniform: single counter with stale reads, cbp, rate
-        int single = 0, bcbp = 0, rate = 0;
-        for (int b = 0; b < 16; ++b) {
-            if (!uni(S.i16_called[b])) continue;
-            rate += uni(S.i16_bits[b]);
-            bcbp |= 1 << b;
-            if (uni(S.i16_tc[b]) > 0) chain_write(c, uni(S.i16_sctr[b]));
-            else if (!c.fresh) {
+        // The blocks' effects in block order (residual.c:881-897), vectorised:
+        // lane b of every 16-lane row holds block b.  rdo.Single_ctr after
+        // block b is the counter of the last coding block at or before b
+        // (the entry value if none); a block without coefficients before the
+        // first writer reads the entry value stale.
+        int single, bcbp, rate;
+        {
+            const int l = c.tid & 15;
+            const int called = S.i16_called[l], tcb = S.i16_tc[l], sct = S.i16_sctr[l], bits = S.i16_bits[l];
+            const unsigned bc = (unsigned)__ballot(called != 0) & 0xFFFFu, bw = (unsigned)__ballot(called && tcb > 0) & 0xFFFFu;
+            const unsigned before = bw ? (bw & (0u - bw)) - 1u : 0xFFFFu;  // blocks before the first writer
+            if ((bc & ~bw & before) && !c.fresh) {
                 // pipelined run: a speculated value is resolved here; once it
                 // is exact (resolved in this MB or to its left) the read is
                 // exact too.  The per-picture path records the stale read for
@@ -2170,7 +2174,14 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp, int& best_dist)
                 if (!F.run_done) c.dep = 1;
                 else if (c.spec) resolve_chain(c);
             }
-            single += c.chain;
+            const unsigned upto = bw & ((2u << l) - 1u);  // writers at or before block l
+            const int wl = upto ? 31 - __clz(upto) : 0;
+            const int sv = __shfl(sct, (c.tid & 48) | wl, 64);  // the writer's counter (same row)
+            const int ch = upto ? sv : c.chain;
+            single = uni(row_sum(called ? ch : 0));
+            rate = uni(row_sum(called ? bits : 0));
+            bcbp = (int)bc;
+            if (bw) chain_write(c, __builtin_amdgcn_readlane(sct, 31 - __clz(bw)));
         }
         if (bcbp && single < 6) bcbp = 0;
         if (bcbp) {
@@ -2204,8 +2215,7 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp, int& best_dist)
             if (c.K.p == 0) S.i16_dist[t] = d;
         }
         HL_SYNC();
-        int dist = 0;
-        for (int b = 0; b < 16; ++b) dist += uni(S.i16_dist[b]);
+        const int dist = uni(row_sum(S.i16_dist[c.tid & 15]));
         const double cost = dadd((double)dist, dmul(F.lambda, (double)rate));
         if (cost < best_cost) {
             best_cost = cost;
