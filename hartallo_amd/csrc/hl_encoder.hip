@@ -88,15 +88,30 @@ __device__ __forceinline__ void diag_mb(int mbw, int mbh, int row0, int diag, in
     x = diag - 2 * yy;
 }
 
+// The frame arguments of a macroblock task, copied into LDS: their fields are
+// then LDS reads the compiler knows cannot alias the global stores and the
+// LDS stores of the decision (read through a generic pointer, every field
+// was reloaded with a flat load after each store).
+__device__ __forceinline__ void frame_args_to_lds(FrameArgs& dst, const FrameArgs& src, int tid)
+{
+    static_assert(sizeof(FrameArgs) % 4 == 0 && sizeof(FrameArgs) / 4 <= kMbThreads, "FrameArgs copied one word per lane");
+    if (tid < (int)(sizeof(FrameArgs) / 4))
+        reinterpret_cast<uint32_t*>(&dst)[tid] = gmem(reinterpret_cast<const uint32_t*>(&src))[tid];
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(kMbThreads, 2) void k_mb_diag(FrameArgs F, int diag, int row0)
 {
     __shared__ Shared S;
+    __shared__ FrameArgs sF;
     int x, y;
     diag_mb(F.mbw, F.mbh, row0, diag, blockIdx.x, x, y);
     const int addr = y * F.mbw + x;
     const int s_in = x == 0 ? F.spec[y] : F.chain[addr - 1].s_out;
     HL_POISON(S, (uint32_t)addr * 7919u + (uint32_t)diag);
-    encode_mb(F, S, addr, threadIdx.x, kMbThreads, s_in);
+    if (threadIdx.x < (int)(sizeof(FrameArgs) / 4)) reinterpret_cast<uint32_t*>(&sF)[threadIdx.x] = reinterpret_cast<const uint32_t*>(&F)[threadIdx.x];
+    __syncthreads();
+    encode_mb(sF, S, addr, threadIdx.x, kMbThreads, s_in);
 }
 
 // Deblocking of a whole picture in one launch: one 64-lane workgroup per MB
@@ -180,7 +195,7 @@ __device__ void plane_block_lds(const uint8_t* ref, int W, uint8_t* pl0, int pst
     const int x0 = X * 16 - 2, y0 = Y * 16 - 2;
     for (int i = tid; i < 21 * 21; i += kMbThreads) {
         const int r = i / 21, c = i - r * 21;
-        T[r * TS + c] = ref[(size_t)(y0 + r) * W + x0 + c];
+        T[r * TS + c] = gmem(ref)[(size_t)(y0 + r) * W + x0 + c];
     }
     __syncthreads();
     for (int i = tid; i < 16 * 21; i += kMbThreads) {
@@ -208,10 +223,10 @@ __device__ void plane_block_lds(const uint8_t* ref, int W, uint8_t* pl0, int pst
             j |= (uint32_t)clip255(vj) << (8 * k);
         }
         const size_t o = (size_t)(Y * 16 + r + kPad) * pstride + X * 16 + c0 + kPad;
-        *reinterpret_cast<uint32_t*>(pl0 + o) = f;
-        *reinterpret_cast<uint32_t*>(pl0 + plsz + o) = b;
-        *reinterpret_cast<uint32_t*>(pl0 + 2 * (size_t)plsz + o) = h;
-        *reinterpret_cast<uint32_t*>(pl0 + 3 * (size_t)plsz + o) = j;
+        *gmem(reinterpret_cast<uint32_t*>(pl0 + o)) = f;
+        *gmem(reinterpret_cast<uint32_t*>(pl0 + plsz + o)) = b;
+        *gmem(reinterpret_cast<uint32_t*>(pl0 + 2 * (size_t)plsz + o)) = h;
+        *gmem(reinterpret_cast<uint32_t*>(pl0 + 3 * (size_t)plsz + o)) = j;
     }
     __syncthreads();  // the scratch is reused by the next block
 }
@@ -377,6 +392,7 @@ __device__ int claim_next(const PipeArgs& P, int nmb, int& cursor)
 __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(PipeArgs P, int mbw, int mbh)
 {
     __shared__ Shared S;
+    __shared__ FrameArgs sF;  // the task's frame arguments (frame_args_to_lds)
     __shared__ int32_t s_task;
     const int nmb = mbw * mbh;
     const bool in_order = blockIdx.x == 0;  // claims tasks in run order (claim_next)
@@ -434,7 +450,8 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #elif defined(HL_DIAG) && HL_DIAG == 6
         if (threadIdx.x < 64) __builtin_amdgcn_s_sleep(20);
 #endif
-        encode_mb(PF.F, S, addr, tid, kMbThreads, s_in, gx, gy, spec_in);
+        frame_args_to_lds(sF, PF.F, tid);
+        encode_mb(sF, S, addr, tid, kMbThreads, s_in, gx, gy, spec_in);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         // (encode_mb stored the record into host memory, PF.F.hrec; the publish fence below is system scope)

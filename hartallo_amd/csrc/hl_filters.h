@@ -174,14 +174,14 @@ struct DeblockArgs {
 HD int deblock_edge_bs(const DeblockArgs& D, int addr, int e, int k)
 {
     const int mbx = addr % D.mbw, mby = addr / D.mbw;
-    const MbState& Q = D.st[addr];
+    const auto& Q = *gmem(D.st + addr);
     const bool vert = e < 4;
     const int edge = (e & 3) * 4;
     const bool mb_edge = edge == 0;
     if (mb_edge && (vert ? mbx == 0 : mby == 0)) return 0;
     const bool internal = !((Q.e_type == ET_P16x16 || (Q.flags & FL_SKIP)) && !Q.cbp_l);
     if (!mb_edge && !internal) return 0;
-    const MbState& P = mb_edge ? (vert ? D.st[addr - 1] : D.st[addr - D.mbw]) : Q;
+    const auto& P = *gmem(D.st + (mb_edge ? (vert ? addr - 1 : addr - D.mbw) : addr));
     return vert ? deblock_bs(P, Q, mb_edge ? 12 : edge - 4, k * 4, edge, k * 4, mb_edge)
                 : deblock_bs(P, Q, k * 4, mb_edge ? 12 : edge - 4, k * 4, edge, mb_edge);
 }
@@ -205,11 +205,11 @@ struct DbTile {
 // its chroma rows (comp = j >> 4, row (j >> 1) & 7, word j & 1)
 HD uint32_t db_own_luma(const DeblockArgs& D, int x, int y, int j)
 {
-    return *reinterpret_cast<const uint32_t*>(D.pic[0] + (size_t)(y * 16 + (j >> 2)) * D.W + x * 16 + (j & 3) * 4);
+    return *gmem(reinterpret_cast<const uint32_t*>(D.pic[0] + (size_t)(y * 16 + (j >> 2)) * D.W + x * 16 + (j & 3) * 4));
 }
 HD uint32_t db_own_chroma(const DeblockArgs& D, int x, int y, int j)
 {
-    return *reinterpret_cast<const uint32_t*>(D.pic[1 + (j >> 4)] + (size_t)(y * 8 + ((j >> 1) & 7)) * D.Wc + x * 8 + (j & 1) * 4);
+    return *gmem(reinterpret_cast<const uint32_t*>(D.pic[1 + (j >> 4)] + (size_t)(y * 8 + ((j >> 1) & 7)) * D.Wc + x * 8 + (j & 1) * 4));
 }
 HD void db_put_own(DbTile& t, int j, uint32_t luma, uint32_t chroma)
 {
@@ -306,13 +306,13 @@ HD void db_mb_load(const DeblockArgs& D, DbMbTile& t, int X, int Y, int j)
     if (j < kDbL * 5) {
         const int row = j / 5, w = j % 5, py = Y * 16 - 4 + row, px = X * 16 - 4 + w * 4;
         if (py < 0 || px < 0) return;
-        *reinterpret_cast<uint32_t*>(t.T + row * kDbL + w * 4) = *reinterpret_cast<const uint32_t*>(D.pic[0] + (size_t)py * D.W + px);
+        *reinterpret_cast<uint32_t*>(t.T + row * kDbL + w * 4) = *gmem(reinterpret_cast<const uint32_t*>(D.pic[0] + (size_t)py * D.W + px));
     }
     else {
         j -= kDbL * 5;
         const int c = j / (kDbC * 3), row = (j / 3) % kDbC, w = j % 3, py = Y * 8 - 4 + row, px = X * 8 - 4 + w * 4;
         if (py < 0 || px < 0) return;
-        *reinterpret_cast<uint32_t*>(t.C[c] + row * kDbC + w * 4) = *reinterpret_cast<const uint32_t*>(D.pic[1 + c] + (size_t)py * D.Wc + px);
+        *reinterpret_cast<uint32_t*>(t.C[c] + row * kDbC + w * 4) = *gmem(reinterpret_cast<const uint32_t*>(D.pic[1 + c] + (size_t)py * D.Wc + px));
     }
 }
 // store slot j (< db_mb_store_slots()): one sample a filter of MB (X, Y) may have changed
@@ -343,11 +343,11 @@ HD void db_mb_store(const DeblockArgs& D, const DbMbTile& t, int X, int Y, int j
     }
     if (comp < 0) {
         const int py = Y * 16 - 4 + tr, px = X * 16 - 4 + tc;
-        if (py >= 0 && px >= 0) D.pic[0][(size_t)py * D.W + px] = t.T[tr * kDbL + tc];
+        if (py >= 0 && px >= 0) gmem(D.pic[0])[(size_t)py * D.W + px] = t.T[tr * kDbL + tc];
     }
     else {
         const int py = Y * 8 - 4 + tr, px = X * 8 - 4 + tc;
-        if (py >= 0 && px >= 0) D.pic[1 + comp][(size_t)py * D.Wc + px] = t.C[comp][tr * kDbC + tc];
+        if (py >= 0 && px >= 0) gmem(D.pic[1 + comp])[(size_t)py * D.Wc + px] = t.C[comp][tr * kDbC + tc];
     }
 }
 

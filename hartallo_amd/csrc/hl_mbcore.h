@@ -255,7 +255,7 @@ HD void pred_luma4x4(const FrameArgs& F, int X, int Y, int xF, int yF, int* p)
 {
     const int ph = (yF << 2) | xF;
     const int s = F.pstride;
-    const uint8_t* p1 = F.pl[kQpelTab[ph][0]] + (Y + kPad + kQpelTab[ph][2]) * s + X + kPad + kQpelTab[ph][1];
+    const auto p1 = gmem(F.pl[kQpelTab[ph][0]]) + (Y + kPad + kQpelTab[ph][2]) * s + X + kPad + kQpelTab[ph][1];
     if (kQpelTab[ph][3] < 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -263,7 +263,7 @@ HD void pred_luma4x4(const FrameArgs& F, int X, int Y, int xF, int yF, int* p)
             for (int i = 0; i < 4; ++i) p[j * 4 + i] = p1[j * s + i];
     }
     else {
-        const uint8_t* p2 = F.pl[kQpelTab[ph][3]] + (Y + kPad + kQpelTab[ph][5]) * s + X + kPad + kQpelTab[ph][4];
+        const auto p2 = gmem(F.pl[kQpelTab[ph][3]]) + (Y + kPad + kQpelTab[ph][5]) * s + X + kPad + kQpelTab[ph][4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -534,32 +534,32 @@ __device__ __forceinline__ void mb_begin(Ctx& c)
         const int w = tid / kW, i = tid - w * kW;
         const int off = w == 0 ? 0 : (w == 1 ? -1 : (w == 2 ? -F.mbw : (w == 3 ? -F.mbw + 1 : -F.mbw - 1)));
         const bool avw = w == 0 || (w == 1 ? hasA : (w == 2 ? hasB : (w == 3 ? hasC : hasD)));
-        q = reinterpret_cast<const uint4*>(F.st + (avw ? a + off : a))[i];
+        q = gmem(reinterpret_cast<const uint4*>(F.st + (avw ? a + off : a)))[i];
     }
     else if (tid < 5 * kW + 16) {
-        q = *reinterpret_cast<const uint4*>(F.src[0] + (size_t)(c.yL + tid - 5 * kW) * F.W + c.xL);
+        q = *gmem(reinterpret_cast<const uint4*>(F.src[0] + (size_t)(c.yL + tid - 5 * kW) * F.W + c.xL));
     }
     else if (tid < 5 * kW + 32) {
         const int k = tid - 5 * kW - 16, comp = k >> 3;
-        const uint2 d = *reinterpret_cast<const uint2*>(F.src[1 + comp] + (size_t)(yc + (k & 7)) * F.Wc + xc);
+        const uint2 d = *gmem(reinterpret_cast<const uint2*>(F.src[1 + comp] + (size_t)(yc + (k & 7)) * F.Wc + xc));
         q.x = d.x;
         q.y = d.y;
     }
     // intra neighbour samples from the (unfiltered) current picture
     if (tid < 25) {
         const int x = tid - 1;
-        if (x < 0 ? hasD : (x < 16 ? hasB : (x < 20 ? hasC : false))) b1 = F.cur[0][(size_t)(c.yL - 1) * F.W + c.xL + x];
+        if (x < 0 ? hasD : (x < 16 ? hasB : (x < 20 ? hasC : false))) b1 = gmem(F.cur[0])[(size_t)(c.yL - 1) * F.W + c.xL + x];
     }
     else if (tid >= 32 && tid < 48) {
-        if (hasA) b1 = F.cur[0][(size_t)(c.yL + tid - 32) * F.W + c.xL - 1];
+        if (hasA) b1 = gmem(F.cur[0])[(size_t)(c.yL + tid - 32) * F.W + c.xL - 1];
     }
     else if (tid >= 64 && tid < 82) {
         const int comp = (tid - 64) / 9, x = (tid - 64) % 9 - 1;
-        if (x < 0 ? hasD : hasB) b1 = F.cur[1 + comp][(size_t)(yc - 1) * F.Wc + xc + x];
+        if (x < 0 ? hasD : hasB) b1 = gmem(F.cur[1 + comp])[(size_t)(yc - 1) * F.Wc + xc + x];
     }
     else if (tid >= 96 && tid < 112) {
         const int comp = (tid - 96) >> 3, y = (tid - 96) & 7;
-        if (hasA) b1 = F.cur[1 + comp][(size_t)(yc + y) * F.Wc + xc - 1];
+        if (hasA) b1 = gmem(F.cur[1 + comp])[(size_t)(yc + y) * F.Wc + xc - 1];
     }
     if (tid < 15 * 16) b2 = kTzLen[tid >> 4][tid & 15];
     if (tid < 3 * 4 * 17) b3 = kTokLen[tid / 68][(tid / 17) % 4][tid % 17];
@@ -960,7 +960,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         const int n = ncand << g.lnb;
         const int qbits = 15 + F.qp / 6, f = (1 << qbits) / 6;
         const int pr = c.K.p >> 2, pc = c.K.p & 3;
-        const uint8_t* base = F.pl[0];
+        const auto base = gmem(F.pl[0]);
         int pa[kMaxPass], pb[kMaxPass], sv[kMaxPass];
         // single-block partitions: both nC neighbours lie outside the partition,
         // so nC is fixed for its whole search (read here, beside the loads)
@@ -1872,15 +1872,18 @@ HD void reconstruct_chroma(Ctx& c, bool intra_flag)
             fwd4x4(res, w);
             quant4x4(F.qpc, true, w, q);  // intra rounding for every MB (rdo.c:2588,2618)
             bool az = true;
+            int lv[16];  // the block's ChromaACLevel as the CAVLC statistics read it (entry 15 stays stale)
             for (int i = 1; i < 16; ++i) {
-                S.cac[comp][b][i - 1] = (int16_t)q[kZigzag[i]];
-                az = az && q[kZigzag[i]] == 0;
+                lv[i - 1] = (int16_t)q[kZigzag[i]];
+                S.cac[comp][b][i - 1] = (int16_t)lv[i - 1];
+                az = az && lv[i - 1] == 0;
             }
-            az = az && S.cac[comp][b][15] == 0;
+            lv[15] = S.cac[comp][b][15];
+            az = az && lv[15] == 0;
             dc = w[0];
             cacb = !az;
             cdcb = w[0] != 0;
-            if (cacb) st = cavlc_stat(S.cac[comp][b], 16, 15, false);
+            if (cacb) st = cavlc_stat(lv, 16, 15, false);
         }
         S.cres_dc[comp][b] = dc;
         S.cres_cac[comp][b] = cacb;
@@ -1958,7 +1961,7 @@ HD void reconstruct_chroma(Ctx& c, bool intra_flag)
         for (int i = 0; i < 16; ++i) {
             const int o = (yO + (i >> 2)) * 8 + xO + (i & 3);
             const int v = have ? clip255(S.predc[comp][o] + r[i]) : S.predc[comp][o];
-            F.cur[1 + comp][((c.yL >> 1) + yO + (i >> 2)) * F.Wc + (c.xL >> 1) + xO + (i & 3)] = (uint8_t)v;
+            gmem(F.cur[1 + comp])[((c.yL >> 1) + yO + (i >> 2)) * F.Wc + (c.xL >> 1) + xO + (i & 3)] = (uint8_t)v;
         }
     }
     HL_SYNC();
@@ -2757,7 +2760,7 @@ HD void inter_pred_mb(Ctx& c, bool chroma_only_16x16, bool luma)
         const int xa = clip3(0, F.Wc - 1, xi), xb = clip3(0, F.Wc - 1, xi + 1);
         const int ya = clip3(0, F.Hc - 1, yi), yb = clip3(0, F.Hc - 1, yi + 1);
         for (int comp = 0; comp < 2; ++comp) {
-            const uint8_t* r = F.ref[1 + comp];
+            const auto r = gmem(F.ref[1 + comp]);
             S.predc[comp][t] = ((8 - xF) * (8 - yF) * r[ya * F.Wc + xa] + xF * (8 - yF) * r[ya * F.Wc + xb] +
                                 (8 - xF) * yF * r[yb * F.Wc + xa] + xF * yF * r[yb * F.Wc + xb] + 32) >> 6;
         }
@@ -2823,8 +2826,8 @@ constexpr int kHomoTh16x16 = 20000, kHomoTh8x8 = 5000, kHomoTh8x4 = 7500;  // hl
 
 HD int homo_sample(const FrameArgs& F, int x, int y)  // |dx| + |dy| at source sample (x, y), eq. 2-35
 {
-    const uint8_t* u = F.src[0] + y * F.W + x;
-    const uint8_t *um = u - F.W, *up = u + F.W;
+    const auto u = gmem(F.src[0]) + y * F.W + x;
+    const auto um = u - F.W, up = u + F.W;
     const int dx = up[-1] + (up[0] << 1) + up[1] - um[-1] - (um[0] << 1) - um[1];
     const int dy = um[1] + (u[1] << 1) + up[1] - um[-1] - (u[-1] << 1) - up[-1];
     return iabs(dx) + iabs(dy);
@@ -3233,24 +3236,24 @@ __device__ __forceinline__ void mb_end(Ctx& c)
         R.pad0[0] = R.pad0[1] = R.pad0[2] = 0;
         R.mad = S.mad;
         R.pad1 = 0;
-        MbChain& ch = F.chain[c.addr];
-        ch.s_out = c.chain;
-        ch.dep = c.dep;
-        ch.fresh = c.fresh;
-        ch.spec = c.spec;
+        const auto ch = gmem(F.chain) + c.addr;
+        ch->s_out = c.chain;
+        ch->dep = c.dep;
+        ch->fresh = c.fresh;
+        ch->spec = c.spec;
     }
     HL_SYNC();
     // ---- 16-byte stores: the reconstruction, the MB object, the record
     constexpr int kSW = (int)(sizeof(MbState) / 16), kRW = (int)(sizeof(MbRecord) / 16);
     static_assert(sizeof(MbRecord) % 16 == 0, "MbRecord in whole 16-byte words");
     if (tid < 16)
-        *reinterpret_cast<uint4*>(F.cur[0] + (size_t)(c.yL + tid) * F.W + c.xL) = reinterpret_cast<const uint4*>(S.rec)[tid];
+        *gmem(reinterpret_cast<uint4*>(F.cur[0] + (size_t)(c.yL + tid) * F.W + c.xL)) = reinterpret_cast<const uint4*>(S.rec)[tid];
     else if (tid >= 64 && tid < 64 + kSW)
-        reinterpret_cast<uint4*>(F.st + c.addr)[tid - 64] = reinterpret_cast<const uint4*>(&M)[tid - 64];
+        gmem(reinterpret_cast<uint4*>(F.st + c.addr))[tid - 64] = reinterpret_cast<const uint4*>(&M)[tid - 64];
     else if (tid >= 128 && tid < 128 + kRW) {
         const uint4 w = reinterpret_cast<const uint4*>(&R)[tid - 128];
-        if (F.hrec) reinterpret_cast<uint4*>(F.hrec + c.addr)[tid - 128] = w;
-        if (F.rec_dev) reinterpret_cast<uint4*>(F.rec + c.addr)[tid - 128] = w;
+        if (F.hrec) gmem(reinterpret_cast<uint4*>(F.hrec + c.addr))[tid - 128] = w;
+        if (F.rec_dev) gmem(reinterpret_cast<uint4*>(F.rec + c.addr))[tid - 128] = w;
     }
     HL_SYNC();
 }
@@ -3359,7 +3362,7 @@ HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, in
 #if defined(__HIP_DEVICE_COMPILE__)
     c.K = make_lanek(tid, F.qp, F.qpc);
 #endif
-    if (tid == 0) F.chain[addr].s_in = s_in;
+    if (tid == 0) gmem(F.chain + addr)->s_in = s_in;
     HL_PROF_T(t0);
     mb_begin(c);
     HL_PROF_ADD(c, 6, t0);

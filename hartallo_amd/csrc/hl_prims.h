@@ -38,6 +38,25 @@ HD double dmul(double a, double b)
 #endif
 }
 
+// Global-memory view of a pointer the kernels hold as a generic one (picture
+// planes, MB objects, records): its loads and stores become global_* instead
+// of flat_* instructions, which also count against the LDS counter (every
+// LDS wait then waits for them too) and, aliasing LDS as far as the compiler
+// knows, force values it already loaded to be reloaded after every LDS store.
+#if defined(__HIP_DEVICE_COMPILE__)
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gmem(T* p)
+{
+    return (__attribute__((address_space(1))) T*)p;
+}
+#else
+template <typename T>
+__host__ __device__ inline T* gmem(T* p)
+{
+    return p;
+}
+#endif
+
 // Values every lane computes identically from LDS: tell the compiler they
 // are wave-uniform (SGPRs, scalar branches) instead of divergent VGPRs.
 HD int uni(int v)
