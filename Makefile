@@ -15,7 +15,7 @@ CXXFLAGS := -std=c++17 -O3 -fPIC -ffp-contract=off -Wall -Wno-unused-function -W
 # profiles/r02_sched_strategy_ab.log)
 DEVFLAGS := -mllvm -amdgpu-sched-strategy=iterative-ilp
 
-.PHONY: all product emu unit oracle profile poison clean
+.PHONY: all product emu unit oracle profile poison variant clean
 all: product emu unit oracle
 
 product: hartallo_amd/libhartallo_amd.so
@@ -53,6 +53,12 @@ build/acqsys/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(HOSTSRC) $(HDRS)
 build/relacqsys/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(HOSTSRC) $(HDRS)
 	mkdir -p build/relacqsys
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) $(DEVFLAGS) '-DHL_ACQ_SCOPE=""' '-DHL_REL_SCOPE=""' -shared -o $@ $(CSRC)/hl_encoder.hip $(HOSTSRC)
+
+# variants of the product for A/B runs: make variant V=<name> VDEFS="-D..."
+variant: build/$(V)/libhartallo_amd.so
+build/$(V)/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(HOSTSRC) $(HDRS)
+	mkdir -p build/$(V)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) $(DEVFLAGS) $(VDEFS) -shared -o $@ $(CSRC)/hl_encoder.hip $(HOSTSRC)
 
 oracle: product  # oracle/_ref/drop_in_enc links the product library
 	$(MAKE) -C oracle

@@ -30,6 +30,7 @@
 #pragma once
 #include "hl_coop.h"
 #include "hl_prims.h"
+#include "hl_quad.h"
 #include "hl_types.h"
 
 namespace hl {
@@ -74,6 +75,13 @@ constexpr int kMaxCand = 32;
 constexpr int kMaxSeg = 4;
 constexpr int kSpecMaxBlocks = 8;
 constexpr int kMaxPass = (9 * 16 + kMbRows - 1) / kMbRows;  // rows per lane for the largest step
+// Candidate evaluation with one 4-lane quad per 4x4 block (hl_quad.h, the
+// default) or one 16-lane row per block (hl_coop.h): blocks a pass can hold.
+#ifndef HL_QUAD_EVAL
+#define HL_QUAD_EVAL 1
+#endif
+constexpr int kQPass = 2;  // quad rounds per pass: 2 x 128 blocks
+constexpr int kPassItems = HL_QUAD_EVAL ? kQPass * (kMbThreads >> 2) : kMaxPass * kMbRows;
 
 // One candidate of a step: plane offsets of its quarter-pel prediction
 // (second plane = first when the phase needs no average) and its MV.
@@ -164,6 +172,7 @@ struct Shared {
     // step before the previous one, whose readers all passed a barrier since.
     alignas(16) uint8_t be_tcb[2][16][kMaxCand];         // TotalCoeff [parity][block][candidate]
     alignas(16) int32_t lvs[kMaxWaves * 4][16];          // per-row level scratch of coop_cavlc
+    alignas(16) int32_t lvq[kMaxWaves * 16][16];         // per-quad level scratch of quad_cavlc
     CoopTables ct;
     uint32_t qtab[16];                                   // packed quarter-pel phase table
     struct CandRes {
@@ -215,6 +224,9 @@ struct Ctx {
     int addr, mbx, mby, xL, yL;
     int chain, fresh, dep;  // rdo.Single_ctr emulation (uniform)
     LaneK K;                // per-lane constants of the 16-lane block pipeline (device)
+#if defined(__HIP_DEVICE_COMPILE__)
+    LaneQ Q{};              // per-lane constants of the quad block pipeline
+#endif
     int gx, gy;             // reference planes known complete for MBs (X <= gx, Y <= gy) (pipelined runs)
     int spec = 0;           // 1 = chain is still a row-start speculation (uniform)
     int par = 0;            // buffer parity of the last candidate step (Shared::cd, be_tcb)
@@ -953,6 +965,90 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
     uint8_t(&tcb)[16][kMaxCand] = S.be_tcb[c.par];
     HL_PROF_T(tp0);
 #if defined(__HIP_DEVICE_COMPILE__)
+#if HL_QUAD_EVAL
+    // phase 1: one 4-lane quad per (candidate, 4x4 block), lane r = block row
+    // r (hl_quad.h); every quad issues its prediction loads for both rounds
+    // before computing
+    {
+        const int wave = c.tid >> 6, qg = c.tid >> 2, nq = c.nthr >> 2;
+        const int n = ncand << g.lnb;
+        const int qbits = 15 + F.qp / 6, f = (1 << qbits) / 6;
+        const LaneQ& Q = c.Q;
+        const auto base = gmem(F.pl[0]);
+        // single-block partitions: both nC neighbours lie outside the partition,
+        // so nC is fixed for its whole search (read here, beside the loads)
+        const int nc1 = g.nblk == 1 ? nc_luma_of(S, blk_idx(g.px, g.py), [&](int ni) -> int { return S.tc[ni]; }) : 0;
+        int o1[kQPass], o2[kQPass];
+        uint32_t sv[kQPass], pr[kQPass];
+#pragma unroll
+        for (int j = 0; j < kQPass; ++j) {
+            const int item = min(qg + j * nq, n - 1);  // clamped: no divergence, valid addresses
+            const int ci = item >> g.lnb, k = item & (g.nblk - 1);
+            const int hx = k & (g.nbw - 1), hy = k >> g.lbw;
+            const int2 cs = *reinterpret_cast<const int2*>(&S.wc[wave][ci]);
+            const int o = ((hy << 2) + Q.r) * F.pstride + (hx << 2);
+            o1[j] = cs.x + o;
+            o2[j] = cs.y + o;
+            sv[j] = *reinterpret_cast<const uint32_t*>(&S.src[(g.py + (hy << 2) + Q.r) * 16 + g.px + (hx << 2)]);
+        }
+#pragma unroll
+        for (int j = 0; j < kQPass; ++j)
+            if (qg + j * nq < n) pr[j] = avg_u8x4(ld_u8x4(base, o1[j]), ld_u8x4(base, o2[j]));
+#pragma unroll
+        for (int j = 0; j < kQPass; ++j) {
+            const int item = qg + j * nq;
+            if (item < n) {
+                const int ci = item >> g.lnb, k = item & (g.nblk - 1);
+                int x[4], y[4], q[4];
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) x[cc] = (int)((sv[j] >> (8 * cc)) & 255) - (int)((pr[j] >> (8 * cc)) & 255);
+                quad_fwd(Q, x, y);
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) q[cc] = quad_q1(y[cc], (cc & 1) ? Q.mfO : Q.mfE, qbits, f);
+                CoopStat st{0, 0, 0, -1};
+                int tok = 0, dist;
+                if (__ballot((q[0] | q[1] | q[2] | q[3]) != 0) == 0) {  // every block of the wave quantised to zero
+                    dist = quad_sum(iabs(x[0]) + iabs(x[1]) + iabs(x[2]) + iabs(x[3]));
+                }
+                else {
+                    // reconstruction distortion first: independent of the CAVLC
+                    // chain, so the two interleave
+                    int r[4];
+                    quad_idct(Q, q, F.qp, r);
+                    int d = 0;
+#pragma unroll
+                    for (int cc = 0; cc < 4; ++cc) {
+                        const int p = (int)((pr[j] >> (8 * cc)) & 255), sp = (int)((sv[j] >> (8 * cc)) & 255);
+                        d += iabs(sp - clip255(p + r[cc]));
+                    }
+                    dist = quad_sum(d);
+                    st = quad_cavlc(S.ct, Q, q, 0, S.lvq[qg]);
+                    if (Q.r == 0 && st.tc)  // coeff_token lengths for the four nC classes
+                        tok = S.ct.tok[0][st.t1][st.tc] | (S.ct.tok[1][st.t1][st.tc] << 5) | (S.ct.tok[2][st.t1][st.tc] << 10) | (6 << 15);
+                }
+                if (Q.r == 0) {
+                    S.be_w0[ci][k] = st.tc | (st.t1 << 5) | ((st.sctr + 1) << 8);
+                    S.be_w1[ci][k] = st.rest | (dist << 16);
+                    S.be_w2[ci][k] = tok;
+                    tcb[k][ci] = (uint8_t)st.tc;
+                    if (g.nblk == 1) {
+                        // a single-block partition: both nC neighbours lie outside it, so the
+                        // nC (and the candidate's cost) needs no other block (phase 2 skipped)
+                        int bits = 0;
+                        if (st.tc) bits = st.rest + ((tok >> (5 * (nc1 < 2 ? 0 : (nc1 < 4 ? 1 : (nc1 < 8 ? 2 : 3))))) & 31);
+                        const CandSlot cs = S.wc[wave][ci];
+                        R.cost[ci] = mv_cost(F, dist, bits, cs.mvx, cs.mvy, pmv);
+                        R.bits[ci] = bits;
+                        R.dist[ci] = dist;
+                        R.single[ci] = st.tc ? st.sctr : 0;
+                        R.cbp[ci] = st.tc ? 1 << blk_idx(g.px, g.py) : 0;
+                        R.last[ci] = st.tc ? st.sctr : -1;
+                    }
+                }
+            }
+        }
+    }
+#else
     // phase 1: one 16-lane row per (candidate, 4x4 block); every row of the
     // wave issues its prediction loads for all its passes before computing
     {
@@ -1046,6 +1142,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
             }
         }
     }
+#endif
     HL_SYNC();
     HL_PROF_ADD(c, 0, tp0);
     HL_PROF_T(tp1);
@@ -1445,7 +1542,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         return (int)((w >> (9 * k)) & 0x1FF);
     };
     const int range = c.F.me_range;
-    const int budget = g.nblk <= kSpecMaxBlocks ? min(kMaxCand, (kMaxPass * kMbRows) >> g.lnb) : 0;  // 0: one step per pass
+    const int budget = g.nblk <= kSpecMaxBlocks ? min(kMaxCand, kPassItems >> g.lnb) : 0;  // 0: one step per pass
     const int nc0 = (pmv[0] != 0 || pmv[1] != 0) ? 2 : 1;
     int stage = 3, flags = 0x1FF, cx = 0, cy = 0, left = 0, right = 0, top = 0, bottom = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -3361,6 +3458,7 @@ HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, in
     c.spec = spec_in;
 #if defined(__HIP_DEVICE_COMPILE__)
     c.K = make_lanek(tid, F.qp, F.qpc);
+    c.Q = make_laneq(tid, F.qp);
 #endif
     if (tid == 0) gmem(F.chain + addr)->s_in = s_in;
     HL_PROF_T(t0);

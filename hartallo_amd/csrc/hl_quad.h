@@ -1,0 +1,221 @@
+// hl_quad.h -- the 4x4 residual pipeline of the macroblock search with one
+// 4-lane quad per 4x4 block (gfx950 only).
+//
+// Lane r of a quad holds row r of the block, its four samples / coefficients
+// in registers.  A 64-lane wave therefore evaluates 16 blocks per
+// instruction stream (the 16-lane rows of hl_coop.h: 4), and a 512-lane
+// workgroup 128 blocks per round -- a whole 16x16 step (9 candidates x 16
+// blocks) in two rounds instead of five.  Row passes of the transforms are
+// register arithmetic; column passes read the other rows of the quad with
+// DPP quad_perm broadcasts; block sums / ORs are two quad_perm exchanges.
+// CAVLC statistics: the scan-order masks OR-reduced over the quad, then the
+// same closed forms as hl_coop.h per coefficient, summed in the lane and over
+// the quad.  Results are bit-identical to the scalar reference paths
+// (hl_prims.h fwd4x4 / quant4x4 / dequant_idct / cavlc_stat):
+//   forward transform      hl_codec_264_transf.c:716-772
+//   quantisation           hl_codec_264_quant.c:116-137
+//   dequant + inverse      hl_codec_264_transf.c:376-458
+//   CAVLC bit count        hl_codec_264_residual.c:587-901
+#pragma once
+#include "hl_coop.h"
+
+namespace hl {
+
+constexpr int kQX1 = 0xB1, kQX2 = 0x4E;  // quad_perm lane ^ 1, lane ^ 2
+
+__device__ __forceinline__ int quad_sum(int x)
+{
+    x += dpp<kQX1>(x);
+    return x + dpp<kQX2>(x);
+}
+__device__ __forceinline__ int quad_or(int x)
+{
+    x |= dpp<kQX1>(x);
+    return x | dpp<kQX2>(x);
+}
+
+// Per-lane constants of the quad pipeline at one QP.
+struct LaneQ {
+    int r;          // the block row this lane holds
+    int mfE, mfO;   // quantisation multipliers of the row's even / odd columns
+    int lsE, lsO;   // dequantisation level scales, same
+    uint32_t zz;    // scan index of (r, c) in bits [4c, 4c + 3]
+};
+
+__device__ __forceinline__ LaneQ make_laneq(int tid, int qp)
+{
+    // kZzInv[r * 4 + c]: scan index of raster position (r, c)
+    constexpr uint64_t kZzRows = 0xFEA9DB83C7426510ull;  // rows of {0,1,5,6},{2,4,7,12},{3,8,11,13},{9,10,14,15}, 4 bits each
+    LaneQ Q;
+    const int r = tid & 3;
+    Q.r = r;
+    Q.zz = (uint32_t)(kZzRows >> (16 * r)) & 0xFFFFu;
+    const int m = qp % 6;
+    const int clsE = (r & 1) ? 2 : 0, clsO = (r & 1) ? 1 : 2;
+    int mfE = 0, mfO = 0, lsE = 0, lsO = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        if (k == m) {
+            mfE = clsE == 0 ? kQuantMF[k][0] : kQuantMF[k][2];
+            mfO = clsO == 1 ? kQuantMF[k][1] : kQuantMF[k][2];
+            lsE = 16 * (clsE == 0 ? kScaleV[k][0] : kScaleV[k][2]);
+            lsO = 16 * (clsO == 1 ? kScaleV[k][1] : kScaleV[k][2]);
+        }
+    Q.mfE = mfE;
+    Q.mfO = mfO;
+    Q.lsE = lsE;
+    Q.lsO = lsO;
+    return Q;
+}
+
+// Forward core transform Cf X Cf^T: x = row r of the residual, y = row r of
+// the coefficients.  Exact integer arithmetic: the pass order does not
+// matter.
+__device__ __forceinline__ void quad_fwd(const LaneQ& Q, const int x[4], int y[4])
+{
+    const int s03 = x[0] + x[3], d03 = x[0] - x[3], s12 = x[1] + x[2], d12 = x[1] - x[2];
+    const int h[4] = {s03 + s12, (d03 << 1) + d12, s03 - s12, d03 - (d12 << 1)};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int a = dpp<kQ0>(h[c]), b = dpp<kQ1>(h[c]), e = dpp<kQ2>(h[c]), d = dpp<kQ3>(h[c]);
+        const int v03 = a + d, w03 = a - d, v12 = b + e, w12 = b - e;
+        const int y01 = Q.r == 0 ? v03 + v12 : (w03 << 1) + w12;
+        const int y23 = Q.r == 2 ? v03 - v12 : w03 - (w12 << 1);
+        y[c] = Q.r < 2 ? y01 : y23;
+    }
+}
+
+// AC quantisation of one coefficient: f = 2^qbits / 3 (intra) or / 6 (inter)
+__device__ __forceinline__ int quad_q1(int w, int mf, int qbits, int f)
+{
+    const int v = (int)((__umul24((unsigned)(w < 0 ? -w : w), (unsigned)mf) + (unsigned)f) >> qbits);  // < 2^32
+    return w >= 0 ? v : -v;
+}
+
+// Dequantisation (8.5.12.1) and inverse transform of row r (rows first, then
+// columns, then (x + 32) >> 6, transf.c:376-458): q = row r of the levels
+// (raster), out = row r of the residual.
+__device__ __forceinline__ void quad_idct(const LaneQ& Q, const int q[4], int qP, int out[4])
+{
+    const int q6 = qP / 6;
+    int d[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int p = __mul24(q[c], (c & 1) ? Q.lsO : Q.lsE);
+        d[c] = qP >= 24 ? p << (q6 - 4) : (p + (1 << (3 - q6))) >> (4 - q6);
+    }
+    const int e0 = d[0] + d[2], e1 = d[0] - d[2], e2 = (d[1] >> 1) - d[3], e3 = d[1] + (d[3] >> 1);
+    const int f[4] = {e0 + e3, e1 + e2, e1 - e2, e0 - e3};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int f0 = dpp<kQ0>(f[c]), f1 = dpp<kQ1>(f[c]), f2 = dpp<kQ2>(f[c]), f3 = dpp<kQ3>(f[c]);
+        const int g0 = f0 + f2, g1 = f0 - f2, g2 = (f1 >> 1) - f3, g3 = f1 + (f3 >> 1);
+        const int h01 = Q.r == 0 ? g0 + g3 : g1 + g2;
+        const int h23 = Q.r == 2 ? g1 - g2 : g0 - g3;
+        out[c] = ((Q.r < 2 ? h01 : h23) + 32) >> 6;
+    }
+}
+
+// run_before length, Table 9-10, zerosLeft 1..6 as one 54-bit constant
+// (2 bits per run value, row zl at bit zl * zl + zl - 2), zerosLeft > 6
+// closed form
+__device__ __forceinline__ int quad_rb_len(int zl, int run)
+{
+    constexpr uint64_t kRb = 0x5ull | (0x29ull << 4) | (0xAAull << 10) | (0x3EAull << 18) | (0xFFAull << 28) | (0x3FFEull << 40);
+    const int sh = min(max(zl * zl + zl - 2 + 2 * run, 0), 62);
+    const int v = (int)((kRb >> sh) & 3);
+    return zl > 6 ? (run < 7 ? 3 : run - 3) : v;
+}
+
+// CAVLC statistics of the quad's block (cavlc_stat with maxNumCoef 16,
+// endIdx 15, the block's levels in scan order): L = this lane's row of
+// levels (raster), ac = 1 for an AC list (scan positions 1..15 at list
+// index 0..14, position 0 not in the list).  lvs = 16 words of LDS scratch
+// owned by this quad.
+__device__ __forceinline__ CoopStat quad_cavlc(const CoopTables& T, const LaneQ& Q, const int L[4], int ac, int* lvs)
+{
+    int li[4], aL[4];
+    bool nzl[4];
+    int mb = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        li[c] = (int)((Q.zz >> (4 * c)) & 15) - ac;
+        aL[c] = L[c] < 0 ? -L[c] : L[c];
+        nzl[c] = li[c] >= 0 && L[c] != 0;
+        mb |= nzl[c] ? (int)((1u << li[c]) | ((uint32_t)(aL[c] == 1) << (li[c] + 16))) : 0;
+    }
+    const uint32_t masks = (uint32_t)quad_or(mb);
+    const uint32_t nz = masks & 0xFFFFu, ones = masks >> 16;
+    CoopStat st;
+    const int tc = __popc(nz);
+    const int hi = 31 - __clz(nz | 1u);
+    const uint32_t big = nz & ~ones;
+    const int hb = big ? 31 - __clz(big) : -1;
+    const int t1a = __popc(nz >> (hb + 1));
+    const int t1 = t1a < 3 ? t1a : 3;
+    const int tzb = (tc > 0 && tc < 16) ? T.tz[tc - 1][hi + 1 - tc] : 0;  // total_zeros length
+    const int sl0 = (tc > 10 && t1 < 3) ? 1 : 0;
+    int sum = 0, slow = 0, m[4], lc[4];
+    bool lvl[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int lis = li[c] < 0 ? 0 : li[c];
+        const int j = __popc(nz >> (lis + 1));  // order from the top
+        const uint32_t lower = nz & ((1u << lis) - 1u);
+        const int zl = lis - __popc(lower);
+        const int run = lower ? lis - 1 - (31 - __clz(lower)) : lis;
+        const int rb = (nzl[c] && j < tc - 1 && zl > 0) ? quad_rb_len(zl, run) : 0;
+        m[c] = j - t1;
+        int l = L[c] > 0 ? (L[c] << 1) - 2 : -(L[c] << 1) - 1;
+        l -= (m[c] == 0 && t1 < 3 && l >= 2) ? 2 : 0;
+        lc[c] = l;
+        lvl[c] = nzl[c] && m[c] >= 0;  // a level coded with level_prefix/suffix
+        slow |= (lvl[c] && aL[c] > 3) ? 1 : 0;
+        // fast path (no level above 3 in the block): suffixLength is sl0 for the
+        // first level and 1 after it; 0: lc + 1 (lc < 14), 1: (lc >> 1) + 2 (lc < 28)
+        sum += rb + (lvl[c] ? ((m[c] == 0 && sl0 == 0) ? l + 1 : (l >> 1) + 2) : 0);
+    }
+    const bool qslow = quad_or(slow) != 0;  // uniform per quad
+    int bits;
+    if (!qslow) bits = t1 + tzb + quad_sum(sum);
+    else {
+        int rbs = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int lis = li[c] < 0 ? 0 : li[c];
+            const int j = __popc(nz >> (lis + 1));
+            const uint32_t lower = nz & ((1u << lis) - 1u);
+            const int zl = lis - __popc(lower);
+            const int run = lower ? lis - 1 - (31 - __clz(lower)) : lis;
+            rbs += (nzl[c] && j < tc - 1 && zl > 0) ? quad_rb_len(zl, run) : 0;
+            if (lvl[c]) lvs[m[c]] = (lc[c] << 16) | aL[c];
+        }
+        bits = t1 + tzb + quad_sum(rbs);
+        // the suffixLength chain over the block's levels, in order (residual.c:813-858)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        int sl = sl0;
+        for (int k = 0; k < tc - t1; ++k) {
+            const int v = lvs[k];
+            bits += level_len(sl, v >> 16);
+            sl = next_sl(sl, v & 0xFFFF);
+        }
+    }
+    st.tc = tc;
+    st.t1 = tc ? t1 : 0;
+    st.rest = tc ? bits : 0;
+    st.sctr = tc == 0 ? -1 : ((tc == 1 && ones == nz) ? (hi == 0 ? 3 : (hi < 3 ? 2 : (hi < 6 ? 1 : 0))) : 9);
+    return st;
+}
+
+// 4 consecutive bytes at p + off (any alignment) from two aligned words
+__device__ __forceinline__ uint32_t ld_u8x4(const __attribute__((address_space(1))) uint8_t* p, int off)
+{
+    const auto w = reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(p + (off & ~3));
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (unsigned)(off & 3));
+}
+// per byte (a + b + 1) >> 1
+__device__ __forceinline__ uint32_t avg_u8x4(uint32_t a, uint32_t b) { return (a | b) - (((a ^ b) & 0xFEFEFEFEu) >> 1); }
+
+}  // namespace hl

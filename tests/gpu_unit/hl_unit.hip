@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include "../../hartallo_amd/csrc/hl_coop.h"
+#include "../../hartallo_amd/csrc/hl_quad.h"
 #include "../../hartallo_amd/csrc/hl_filters.h"
 
 using namespace hl;
@@ -84,6 +85,47 @@ __global__ __launch_bounds__(256) void k_unit_coop(const uint8_t* src, const uin
     }
 }
 
+// the quad pipeline (hl_quad.h): one 4-lane quad per block, lane r = row r
+__global__ __launch_bounds__(256) void k_unit_quad(const uint8_t* src, const uint8_t* pred, int n, int qp, int mode, UnitOut* out)
+{
+    __shared__ CoopTables T;
+    __shared__ int lvs[64][16];
+    coop_tables_init(T, threadIdx.x, 256);
+    __syncthreads();
+    const LaneQ Q = make_laneq(threadIdx.x, qp);
+    const int qg = threadIdx.x >> 2;
+    const int b = blockIdx.x * 64 + qg;
+    if (b >= n) return;  // whole quads
+    int x[4], y[4], q[4], r[4], sv[4], pv[4];
+    for (int c = 0; c < 4; ++c) {
+        sv[c] = src[16 * b + 4 * Q.r + c];
+        pv[c] = pred[16 * b + 4 * Q.r + c];
+        x[c] = sv[c] - pv[c];
+    }
+    quad_fwd(Q, x, y);
+    const int qbits = 15 + qp / 6;
+    const int f = (1 << qbits) / (mode != 0 ? 3 : 6);
+    for (int c = 0; c < 4; ++c) q[c] = quad_q1(y[c], (c & 1) ? Q.mfO : Q.mfE, qbits, f);
+    const CoopStat st = quad_cavlc(T, Q, q, mode == 2 ? 1 : 0, lvs[qg]);
+    quad_idct(Q, q, qp, r);
+    int d = 0;
+    UnitOut& o = out[b];
+    for (int c = 0; c < 4; ++c) {
+        const int v = clip255(pv[c] + r[c]);
+        d += iabs(sv[c] - v);
+        o.q[4 * Q.r + c] = q[c];
+        o.rec[4 * Q.r + c] = v;
+    }
+    const int dist = quad_sum(d);
+    if (Q.r == 0) {
+        o.tc = st.tc;
+        o.t1 = st.t1;
+        o.rest = st.rest;
+        o.sctr = st.sctr;
+        o.dist = dist;
+    }
+}
+
 extern "C" int unit_run(const uint8_t* h_src, const uint8_t* h_pred, int n, int qp, int mode, int coop, UnitOut* h_out)
 {
     uint8_t *d_src = nullptr, *d_pred = nullptr;
@@ -92,7 +134,8 @@ extern "C" int unit_run(const uint8_t* h_src, const uint8_t* h_pred, int n, int 
     (void)hipMemcpy(d_src, h_src, 16 * (size_t)n, hipMemcpyHostToDevice);
     (void)hipMemcpy(d_pred, h_pred, 16 * (size_t)n, hipMemcpyHostToDevice);
     (void)hipMemset(d_out, 0xFF, sizeof(UnitOut) * (size_t)n);
-    if (coop) k_unit_coop<<<(n + 15) / 16, 256>>>(d_src, d_pred, n, qp, mode, d_out);
+    if (coop == 2) k_unit_quad<<<(n + 63) / 64, 256>>>(d_src, d_pred, n, qp, mode, d_out);
+    else if (coop) k_unit_coop<<<(n + 15) / 16, 256>>>(d_src, d_pred, n, qp, mode, d_out);
     else k_unit_scalar<<<(n + 63) / 64, 64>>>(d_src, d_pred, n, qp, mode, d_out);
     const hipError_t e = hipDeviceSynchronize();
     (void)hipMemcpy(h_out, d_out, sizeof(UnitOut) * (size_t)n, hipMemcpyDeviceToHost);

@@ -1,5 +1,6 @@
-"""GPU unit parity of the cooperative 16-lane 4x4 pipeline (hl_coop.h: DPP
-transforms, quantisation, mask-based CAVLC statistics) against the scalar
+"""GPU unit parity of the cooperative 4x4 pipelines -- 16-lane rows (hl_coop.h)
+and 4-lane quads (hl_quad.h, the candidate evaluation): DPP transforms,
+quantisation, mask-based CAVLC statistics -- against the scalar
 primitives (hl_prims.h, the restatement of transf.c / quant.c /
 residual.c) on the same random blocks.  Bit-exact: every field must match.
 """
@@ -35,14 +36,15 @@ def test_coop_block_pipeline(gpu, qp, mode):
     n = 4096
     src, pred = _blocks(n, 1000 * qp + mode)
     outs = []
-    for coop in (0, 1):
+    for coop in (0, 1, 2):
         o = np.zeros((n, FIELDS), dtype=np.int32)
         rc = lib.unit_run(src.ctypes.data_as(ctypes.c_void_p), pred.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(n), ctypes.c_int(qp),
                           ctypes.c_int(mode), ctypes.c_int(coop), o.ctypes.data_as(ctypes.c_void_p))
         assert rc == 0
         outs.append(o)
-    bad = np.nonzero((outs[0] != outs[1]).any(axis=1))[0]
-    assert bad.size == 0, f"{bad.size} blocks differ; first {bad[0]}: scalar {outs[0][bad[0]][:5]} coop {outs[1][bad[0]][:5]}"
+    for k, name in ((1, "coop"), (2, "quad")):
+        bad = np.nonzero((outs[0] != outs[k]).any(axis=1))[0]
+        assert bad.size == 0, f"{name}: {bad.size} blocks differ; first {bad[0]}: scalar {outs[0][bad[0]][:5]} {name} {outs[k][bad[0]][:5]}"
 
 
 @pytest.mark.parametrize("w,h", [(32, 16), (176, 144), (352, 288), (1920, 1088)])

@@ -5,9 +5,11 @@
 # Four passes, each in a run of its own (MI355X_MICROARCH.md: counter slots
 # per block, FETCH_SIZE and WRITE_SIZE cannot share a pass): two SQ sets,
 # FETCH_SIZE, WRITE_SIZE.  tools/pmc_summary.py then writes
-# tools/pmc/pmc_k_pipeline.json for the timed launch (the last k_pipeline
-# dispatch), stamped with the SHA-256 of the library it measured; bench.py
-# uses the counters only when that hash is the loaded library's.
+# gpurun_out/pmc/pmc_k_pipeline.json (copied to tools/pmc/ by the caller:
+# only gpurun_out/ comes back from the GPU box) for the timed launch (the
+# last k_pipeline dispatch), stamped with the SHA-256 of the library it
+# measured; bench.py uses the counters only when that hash is the loaded
+# library's.
 set -o pipefail
 mkdir -p gpurun_out/pmc
 cd /tmp && export TMPDIR=/tmp
@@ -23,4 +25,4 @@ for set in "${sets[@]}"; do
 done
 cd $R
 python3 tools/pmc_summary.py --warmup 5 --steps 20 gpurun_out/pmc/p1 gpurun_out/pmc/p2 gpurun_out/pmc/p3 gpurun_out/pmc/p4 \
-    > tools/pmc/pmc_k_pipeline.json && cat tools/pmc/pmc_k_pipeline.json
+    > gpurun_out/pmc/pmc_k_pipeline.json && cat gpurun_out/pmc/pmc_k_pipeline.json

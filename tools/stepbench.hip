@@ -42,7 +42,7 @@ __global__ __launch_bounds__(kMbThreads) void k_step(FrameArgs F, long long* out
                 for (int i = 0; i < nc; ++i) put_cand(c, g.px, g.py, i, ((it + i) % 7) - 3, ((it * 3 + i) % 5) - 2, i, (tid & 63) == 0);
                 eval_candidates(c, g, nc, pmv);
                 double m;
-                acc += pick_first_min(c, nc, m);
+                acc += pick_first_min(c, 0, nc, m);
             }
             const long long t1 = __builtin_readcyclecounter();
             if (tid == 0) {
