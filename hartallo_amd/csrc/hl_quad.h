@@ -23,6 +23,20 @@ namespace hl {
 
 constexpr int kQX1 = 0xB1, kQX2 = 0x4E;  // quad_perm lane ^ 1, lane ^ 2
 
+// A DPP read kept as its own v_mov_b32_dpp: the empty asm stops LLVM's DPP
+// combiner from folding it into the subtraction that consumes it.  On the
+// MI355X a folded v_subrev_u32_dpp returned src1 - src0 of the lane's own
+// src0, without the permutation (tests/test_gpu_unit.py, quad, every QP: the
+// odd rows of the forward transform's first column); the column passes below
+// subtract DPP operands, so they read them through this.
+template <int CTRL>
+__device__ __forceinline__ int dpp_x(int v)
+{
+    int r = dpp<CTRL>(v);
+    asm volatile("" : "+v"(r));
+    return r;
+}
+
 __device__ __forceinline__ int quad_sum(int x)
 {
     x += dpp<kQX1>(x);
@@ -77,7 +91,7 @@ __device__ __forceinline__ void quad_fwd(const LaneQ& Q, const int x[4], int y[4
     const int h[4] = {s03 + s12, (d03 << 1) + d12, s03 - s12, d03 - (d12 << 1)};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const int a = dpp<kQ0>(h[c]), b = dpp<kQ1>(h[c]), e = dpp<kQ2>(h[c]), d = dpp<kQ3>(h[c]);
+        const int a = dpp_x<kQ0>(h[c]), b = dpp_x<kQ1>(h[c]), e = dpp_x<kQ2>(h[c]), d = dpp_x<kQ3>(h[c]);
         const int v03 = a + d, w03 = a - d, v12 = b + e, w12 = b - e;
         const int y01 = Q.r == 0 ? v03 + v12 : (w03 << 1) + w12;
         const int y23 = Q.r == 2 ? v03 - v12 : w03 - (w12 << 1);
@@ -108,7 +122,7 @@ __device__ __forceinline__ void quad_idct(const LaneQ& Q, const int q[4], int qP
     const int f[4] = {e0 + e3, e1 + e2, e1 - e2, e0 - e3};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const int f0 = dpp<kQ0>(f[c]), f1 = dpp<kQ1>(f[c]), f2 = dpp<kQ2>(f[c]), f3 = dpp<kQ3>(f[c]);
+        const int f0 = dpp_x<kQ0>(f[c]), f1 = dpp_x<kQ1>(f[c]), f2 = dpp_x<kQ2>(f[c]), f3 = dpp_x<kQ3>(f[c]);
         const int g0 = f0 + f2, g1 = f0 - f2, g2 = (f1 >> 1) - f3, g3 = f1 + (f3 >> 1);
         const int h01 = Q.r == 0 ? g0 + g3 : g1 + g2;
         const int h23 = Q.r == 2 ? g1 - g2 : g0 - g3;
