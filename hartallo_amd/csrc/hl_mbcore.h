@@ -991,9 +991,15 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
             o2[j] = cs.y + o;
             sv[j] = *reinterpret_cast<const uint32_t*>(&S.src[(g.py + (hy << 2) + Q.r) * 16 + g.px + (hx << 2)]);
         }
+        HL_PROF_T(ta0);
 #pragma unroll
         for (int j = 0; j < kQPass; ++j)
             if (qg + j * nq < n) pr[j] = avg_u8x4(ld_u8x4(base, o1[j]), ld_u8x4(base, o2[j]));
+#if defined(HL_STEP_PROF)
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the loads' latency (profiling only)
+        HL_PROF_ADD(c, 12, ta0);
+#endif
+        HL_PROF_T(ta1);
 #pragma unroll
         for (int j = 0; j < kQPass; ++j) {
             const int item = qg + j * nq;
@@ -1047,6 +1053,9 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                 }
             }
         }
+#if defined(HL_STEP_PROF)
+        HL_PROF_ADD(c, 13, ta1);
+#endif
     }
 #else
     // phase 1: one 16-lane row per (candidate, 4x4 block); every row of the
@@ -1143,7 +1152,13 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         }
     }
 #endif
+#if defined(HL_STEP_PROF) && HL_QUAD_EVAL
+    HL_PROF_T(tb0);
     HL_SYNC();
+    HL_PROF_ADD(c, 14, tb0);
+#else
+    HL_SYNC();
+#endif
     HL_PROF_ADD(c, 0, tp0);
     HL_PROF_T(tp1);
     // phase 2: one row per candidate, one lane per block: nC as the reference
@@ -1714,6 +1729,9 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
                 sb[j] = __ffsll((long long)(__ballot(in[j] && v[j] == sm[j]) & 0xFFFFFFFFull)) - 1;
             }
         }
+#if defined(HL_STEP_PROF)
+        HL_PROF_ADD(c, 15, tsel);  // results loaded, the steps' minima found
+#endif
         auto seg_pick = [&](int j, double& m) -> int {
             m = sm[j];
             return sb[j];

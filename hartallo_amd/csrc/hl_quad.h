@@ -148,15 +148,19 @@ __device__ __forceinline__ int quad_rb_len(int zl, int run)
 // owned by this quad.
 __device__ __forceinline__ CoopStat quad_cavlc(const CoopTables& T, const LaneQ& Q, const int L[4], int ac, int* lvs)
 {
-    int li[4], aL[4];
-    bool nzl[4];
+    // Branch-free throughout: every condition is a select on bitwise-combined
+    // flags (a short-circuit && here compiled to an exec-mask branch per
+    // coefficient), and shift counts are masked so both arms are defined.
+    int li[4], aL[4], nzl[4];
     int mb = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         li[c] = (int)((Q.zz >> (4 * c)) & 15) - ac;
         aL[c] = L[c] < 0 ? -L[c] : L[c];
-        nzl[c] = li[c] >= 0 && L[c] != 0;
-        mb |= nzl[c] ? (int)((1u << li[c]) | ((uint32_t)(aL[c] == 1) << (li[c] + 16))) : 0;
+        nzl[c] = (int)(li[c] >= 0) & (int)(L[c] != 0);
+        const uint32_t sh = (uint32_t)li[c] & 15u;
+        const uint32_t bits = (1u << sh) | ((uint32_t)(aL[c] == 1) << (sh + 16));
+        mb |= nzl[c] ? (int)bits : 0;
     }
     const uint32_t masks = (uint32_t)quad_or(mb);
     const uint32_t nz = masks & 0xFFFFu, ones = masks >> 16;
@@ -164,46 +168,41 @@ __device__ __forceinline__ CoopStat quad_cavlc(const CoopTables& T, const LaneQ&
     const int tc = __popc(nz);
     const int hi = 31 - __clz(nz | 1u);
     const uint32_t big = nz & ~ones;
-    const int hb = big ? 31 - __clz(big) : -1;
+    const int hb = 31 - __clz(big);  // -1 when big == 0 (__clz(0) = 32)
     const int t1a = __popc(nz >> (hb + 1));
     const int t1 = t1a < 3 ? t1a : 3;
-    const int tzb = (tc > 0 && tc < 16) ? T.tz[tc - 1][hi + 1 - tc] : 0;  // total_zeros length
-    const int sl0 = (tc > 10 && t1 < 3) ? 1 : 0;
-    int sum = 0, slow = 0, m[4], lc[4];
-    bool lvl[4];
+    const int tzi = ((tc - 1) & 15) * 16 + ((hi + 1 - tc) & 15);
+    const int tzv = (&T.tz[0][0])[tzi < 15 * 16 ? tzi : 0];
+    const int tzb = ((int)(tc > 0) & (int)(tc < 16)) ? tzv : 0;  // total_zeros length
+    const int sl0 = ((int)(tc > 10) & (int)(t1 < 3)) ? 1 : 0;
+    int sum = 0, slow = 0, rbs = 0, m[4], lc[4], lvl[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int lis = li[c] < 0 ? 0 : li[c];
         const int j = __popc(nz >> (lis + 1));  // order from the top
         const uint32_t lower = nz & ((1u << lis) - 1u);
         const int zl = lis - __popc(lower);
-        const int run = lower ? lis - 1 - (31 - __clz(lower)) : lis;
-        const int rb = (nzl[c] && j < tc - 1 && zl > 0) ? quad_rb_len(zl, run) : 0;
+        const int run = lis - 1 - (31 - __clz(lower));  // lis when lower == 0 (__clz(0) = 32)
+        const int rb = (nzl[c] & (int)(lower != 0) & (int)(zl > 0)) ? quad_rb_len(zl, run) : 0;
         m[c] = j - t1;
         int l = L[c] > 0 ? (L[c] << 1) - 2 : -(L[c] << 1) - 1;
-        l -= (m[c] == 0 && t1 < 3 && l >= 2) ? 2 : 0;
+        l -= ((int)(m[c] == 0) & (int)(t1 < 3) & (int)(l >= 2)) ? 2 : 0;
         lc[c] = l;
-        lvl[c] = nzl[c] && m[c] >= 0;  // a level coded with level_prefix/suffix
-        slow |= (lvl[c] && aL[c] > 3) ? 1 : 0;
+        lvl[c] = nzl[c] & (int)(m[c] >= 0);  // a level coded with level_prefix/suffix
+        slow |= lvl[c] & (int)(aL[c] > 3);
         // fast path (no level above 3 in the block): suffixLength is sl0 for the
         // first level and 1 after it; 0: lc + 1 (lc < 14), 1: (lc >> 1) + 2 (lc < 28)
-        sum += rb + (lvl[c] ? ((m[c] == 0 && sl0 == 0) ? l + 1 : (l >> 1) + 2) : 0);
+        const int len = ((int)(m[c] == 0) & (int)(sl0 == 0)) ? l + 1 : (l >> 1) + 2;
+        rbs += rb;
+        sum += rb + (lvl[c] ? len : 0);
     }
     const bool qslow = quad_or(slow) != 0;  // uniform per quad
     int bits;
     if (!qslow) bits = t1 + tzb + quad_sum(sum);
     else {
-        int rbs = 0;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int lis = li[c] < 0 ? 0 : li[c];
-            const int j = __popc(nz >> (lis + 1));
-            const uint32_t lower = nz & ((1u << lis) - 1u);
-            const int zl = lis - __popc(lower);
-            const int run = lower ? lis - 1 - (31 - __clz(lower)) : lis;
-            rbs += (nzl[c] && j < tc - 1 && zl > 0) ? quad_rb_len(zl, run) : 0;
+        for (int c = 0; c < 4; ++c)
             if (lvl[c]) lvs[m[c]] = (lc[c] << 16) | aL[c];
-        }
         bits = t1 + tzb + quad_sum(rbs);
         // the suffixLength chain over the block's levels, in order (residual.c:813-858)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
