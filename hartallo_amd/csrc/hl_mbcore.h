@@ -73,7 +73,12 @@ constexpr int kMbRows = kMbThreads / 16;           // 16-lane rows
 // speculative (see search_partition); at most kMaxPass rows per lane.
 constexpr int kMaxCand = 32;
 constexpr int kMaxSeg = 4;
-constexpr int kSpecMaxBlocks = 8;
+// partitions whose passes chain speculative steps: with the quad pipeline a
+// pass holds 256 blocks, so even a 16x16 chain (MVP/(0,0) + integer + half
+// step, 16 candidates) fits one pass
+#ifndef HL_SPEC_MAX_BLOCKS
+#define HL_SPEC_MAX_BLOCKS 16
+#endif
 constexpr int kMaxPass = (9 * 16 + kMbRows - 1) / kMbRows;  // rows per lane for the largest step
 // Candidate evaluation with one 4-lane quad per 4x4 block (hl_quad.h, the
 // default) or one 16-lane row per block (hl_coop.h): blocks a pass can hold.
@@ -82,6 +87,7 @@ constexpr int kMaxPass = (9 * 16 + kMbRows - 1) / kMbRows;  // rows per lane for
 #endif
 constexpr int kQPass = 2;  // quad rounds per pass: 2 x 128 blocks
 constexpr int kPassItems = HL_QUAD_EVAL ? kQPass * (kMbThreads >> 2) : kMaxPass * kMbRows;
+constexpr int kSpecMaxBlocks = HL_QUAD_EVAL ? HL_SPEC_MAX_BLOCKS : 8;
 
 // One candidate of a step: plane offsets of its quarter-pel prediction
 // (second plane = first when the phase needs no average) and its MV.
