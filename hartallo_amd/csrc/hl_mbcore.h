@@ -51,7 +51,7 @@ namespace hl {
         (c).pacc[slot] += __builtin_readcyclecounter() - (t0);   \
         (c).pcnt[slot] += 1;                                     \
     } while (0)
-constexpr int kProfSlots = 18;  // prof[2 * slot], prof[2 * slot + 1] (< 40: the pipelined kernel uses 40-44)
+constexpr int kProfSlots = 20;  // prof[2 * slot], prof[2 * slot + 1] (< 40: the pipelined kernel uses 40-44)
 #else
 #define HL_PROF_T(v) const unsigned long long v = 0
 #define HL_PROF_ADD(c, slot, t0) ((void)(t0))
@@ -1625,6 +1625,9 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         }
         int lo[kMaxSeg] = {0, 0, 0, 0}, n[kMaxSeg] = {0, 0, 0, 0};
 #if defined(__HIP_DEVICE_COMPILE__)
+#if defined(HL_STEP_PROF)
+        HL_PROF_T(tgen);
+#endif
         {  // lane 16 j + i of every wave checks point i of step j; enabled points are compacted in order
             const int i = c.tid & 63, j = i >> 4, pt = min(i & 15, 8);
             const int st = stage - j;  // step j's stage (3 = MVP/(0,0))
@@ -1657,6 +1660,9 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
             }
             if (en) put_cand(c, g.px, g.py, __popcll(bal & ((1ull << i) - 1ull)), mx << sh, my << sh, i & 15, true);
         }
+#if defined(HL_STEP_PROF)
+        HL_PROF_ADD(c, 19, tgen);  // the pass's candidates generated and stored
+#endif
 #else
         {
             int tot = 0;
@@ -1737,6 +1743,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         }
 #if defined(HL_STEP_PROF)
         HL_PROF_ADD(c, 15, tsel);  // results loaded, the steps' minima found
+        HL_PROF_T(tres);
 #endif
         auto seg_pick = [&](int j, double& m) -> int {
             m = sm[j];
@@ -1789,6 +1796,9 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
             bottom = cy + range;
         }
 #if defined(__HIP_DEVICE_COMPILE__)
+#if defined(HL_STEP_PROF)
+        HL_PROF_ADD(c, 18, tres);  // the chain resolved
+#endif
         if (used) commit_candidates(c, g, used, pv_last);
 #else
         if (used) commit_candidates(c, g, used);

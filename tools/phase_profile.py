@@ -17,7 +17,7 @@ from hartallo_amd import _lib, synth  # noqa: E402
 
 PHASES = ["eval:block", "eval:nC", "eval:reduce", "search_partition", "mvp", "guess_intra(P)", "mb_begin", "mb_end", "whole MB",
           "reach_wait", "intra:i16", "intra:i4", "step:slots+loads", "step:fwd+quant", "step:idct+cavlc", "step:-", "step:candidates",
-          "step:selection"]
+          "step:selection", "sel:resolve", "cand:generate"]
 
 
 def main():
