@@ -417,6 +417,14 @@ def main():
     ptrs = [(dev[i].data_ptr(), dev[i].data_ptr() + ny, dev[i].data_ptr() + ny + nc) for i in range(n_frames)]
 
     enc = Encoder(W, H, QP, ME_RANGE, DEBLOCK, GOP, 0, local)
+    # streams sharing one GPU (more ranks on this node than visible GPUs):
+    # each rank's persistent run takes its share of the CUs, so the runs
+    # execute side by side instead of taking turns for the whole device
+    # (several streams per GPU fill the MB wavefront's ramp and tail)
+    share = -(-int(os.environ.get("LOCAL_WORLD_SIZE", "1")) // max(1, torch.cuda.device_count()))
+    if share > 1:
+        cus = torch.cuda.get_device_properties(local).multi_processor_count
+        enc.set_pipeline(max(1, cus // share), 2, 64)
     outputs = []
     warm = {k: 0 for k in STAT_KEYS}
     if args.warmup:  # same entry point as the timed frames (warms the pipelined path and its buffers)
@@ -481,8 +489,8 @@ def main():
             "dtype": "u8/int32",
             "data": "synthetic (hartallo_amd.synth, seeded per rank)",
             "config": {"workload": "1920x1088 YUV420 IPPP GOP30 QP28 ME16 deblock, one stream per GPU, frame-pipelined", "width": W, "height": H,
-                       "qp": QP, "me_range": ME_RANGE, "deblock": DEBLOCK, "gop": GOP, "parallelism": f"streams{world}"},
-            "mb_per_s_per_gpu": round(fps / world * nmb, 1),
+                       "qp": QP, "me_range": ME_RANGE, "deblock": DEBLOCK, "gop": GOP, "parallelism": f"streams{world}", "streams_per_gpu": share},
+            "mb_per_s_per_gpu": round(fps / world * share * nmb, 1),
             "bitexact": bitexact_all if bitexact_all is None else bool(bitexact_all),
             "bitexact_check": "every frame of every rank (warm-up and timed) vs the reference encoder's per-frame MD5s "
                               "(tests/golden/bench_golden.json, oracle/_ref/ref_enc on the same synthetic stream)",
