@@ -221,6 +221,11 @@ struct Shared {
     int16_t mvd[4][4][2];
     int8_t nc_luma[16], nc_cac[2][4], nc_dc;
     int32_t mad;  // distortion of the chosen mode (rate control MAD, rdo.c:211-228, 1266-1268)
+    // per-lane constants of the 16-lane block pipeline at this MB's QP, by
+    // lane position (tid & 15): read from LDS where used instead of held in 9
+    // VGPRs for the whole MB (which the compiler spilled to scratch: those
+    // scratch stores were most of k_pipeline's HBM writes)
+    LaneK lk[16];
 };
 
 struct Ctx {
@@ -229,9 +234,9 @@ struct Ctx {
     int tid, nthr;
     int addr, mbx, mby, xL, yL;
     int chain, fresh, dep;  // rdo.Single_ctr emulation (uniform)
-    LaneK K;                // per-lane constants of the 16-lane block pipeline (device)
+    const LaneK& K;         // per-lane constants of the 16-lane block pipeline (device; Shared::lk)
 #if defined(__HIP_DEVICE_COMPILE__)
-    LaneQ Q{};              // per-lane constants of the quad block pipeline
+    LaneQ Q{};              // per-lane constants of the quad block pipeline (registers: the search loop reads them every pass)
 #endif
     int gx, gy;             // reference planes known complete for MBs (X <= gx, Y <= gy) (pipelined runs)
     int spec = 0;           // 1 = chain is still a row-start speculation (uniform)
@@ -3488,10 +3493,13 @@ HD void mb_end(Ctx& c)
 HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, int s_in, int gx = 1 << 20, int gy = 1 << 20,
                int spec_in = 1)
 {
-    Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0, LaneK{}, gx, gy};
+    Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0, S.lk[tid & 15]};
+    c.gx = gx;
+    c.gy = gy;
     c.spec = spec_in;
 #if defined(__HIP_DEVICE_COMPILE__)
-    c.K = make_lanek(tid, F.qp, F.qpc);
+    // (first read after mb_begin's barriers)
+    if (tid < 16) S.lk[tid] = make_lanek(tid, F.qp, F.qpc);
     c.Q = make_laneq(tid, F.qp);
 #endif
     if (tid == 0) gmem(F.chain + addr)->s_in = s_in;

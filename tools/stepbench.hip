@@ -17,8 +17,10 @@ __global__ __launch_bounds__(kMbThreads) void k_step(FrameArgs F, long long* out
 {
     __shared__ Shared S;
     const int tid = threadIdx.x;
-    Ctx c{F, S, tid, kMbThreads, 5, 1, 1, 16, 16, 9, 0, 0, LaneK{}};
-    c.K = make_lanek(tid, F.qp, F.qpc);
+    Ctx c{F, S, tid, kMbThreads, 5, 1, 1, 16, 16, 9, 0, 0, S.lk[tid & 15]};
+    if (tid < 16) S.lk[tid] = make_lanek(tid, F.qp, F.qpc);
+    c.Q = make_laneq(tid, F.qp);
+    __syncthreads();
     mb_begin(c);
     static constexpr int shapes[7][2] = {{16, 16}, {16, 8}, {8, 16}, {8, 8}, {8, 4}, {4, 8}, {4, 4}};
     for (int sh = 0; sh < 7; ++sh)
