@@ -1868,7 +1868,7 @@ HD bool i4_avail(int mode, const PT& p)
 // Intra4x4 prediction of sample (x, y), modes 0-8 (8.3.1.2); p is the
 // 13-sample neighbour array (p[0] = corner, p[1..4] left, p[5..12] top).
 template <typename PT>
-HD int i4_pred_px(int mode, const PT& p, int x, int y)
+constexpr HD int i4_pred_px(int mode, const PT& p, int x, int y)
 {
     {
         {
@@ -1929,6 +1929,48 @@ HD int i4_pred_px(int mode, const PT& p, int x, int y)
         }
     }
 }
+// Every Intra4x4 mode except DC predicts a sample as (w0 p[i0] + w1 p[i1] +
+// w2 p[i2] + 2) >> 2 over the 13 neighbours (two-tap averages are weights
+// 2, 2; copies weight 4).  The table holds (i0, i1, i2, w0, w1, w2) per
+// (mode, sample), derived at compile time by probing i4_pred_px with unit
+// neighbours; DC reads p[13] = its value.  The device evaluates all nine
+// modes branch-free from it (one row per mode, no per-mode code path);
+// tests/test_emu_golden.py::test_i4_prediction_table checks it against
+// i4_pred_px on random neighbourhoods.
+struct I4Tab {
+    uint32_t e[9][16];
+};
+constexpr I4Tab make_i4_tab()
+{
+    I4Tab t{};
+    for (int m = 0; m < 9; ++m)
+        for (int pos = 0; pos < 16; ++pos) {
+            uint32_t e = 0;
+            if (m == 2) e = 13u | (4u << 12);
+            else {
+                int n = 0;
+                for (int k = 0; k < 13; ++k) {
+                    int pv[13] = {};
+                    pv[k] = 256;
+                    const int w = i4_pred_px(m, pv, pos & 3, pos >> 2) / 64;
+                    if (w) {
+                        e |= (uint32_t)k << (4 * n) | (uint32_t)w << (12 + 3 * n);
+                        ++n;
+                    }
+                }
+            }
+            t.e[m][pos] = e;
+        }
+    return t;
+}
+constexpr I4Tab kI4Tab = make_i4_tab();
+HD int i4_tab_pred(uint32_t e, int a, int b, int c)  // a, b, c = p[i0], p[i1], p[i2]
+{
+    return ((int)((e >> 12) & 7) * a + (int)((e >> 15) & 7) * b + (int)((e >> 18) & 7) * c + 2) >> 2;
+}
+// DC prediction value of a 13-sample neighbourhood (mode 2 of i4_pred_px)
+HD int i4_dc(const int p[13]) { return i4_pred_px(2, p, 0, 0); }
+
 HD void i4_pred(int mode, const int p[13], int* pr)
 {
     for (int y = 0; y < 4; ++y)
@@ -2542,15 +2584,24 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
     constexpr uint8_t kWave[10][2] = {{0, 255}, {1, 255}, {2, 4}, {3, 5}, {6, 8}, {7, 9}, {10, 12}, {11, 13}, {14, 255}, {15, 255}};
     const int row = c.tid >> 4;
     const int qbits = 15 + F.qp / 6, fq = (1 << qbits) / 3;
+    // this lane's prediction taps: row = (slot, mode), lane = sample (kI4Tab)
+    const uint32_t te = kI4Tab.e[row < 18 ? (row >= 9 ? row - 9 : row) : 0][c.tid & 15];
     for (int d = 0; d < 10; ++d) {
+#if defined(HL_I4_PROF)
+        HL_PROF_T(ti0);
+#endif
         const int b0 = kWave[d][0], b1 = kWave[d][1];
         const int nslot = b1 == 255 ? 1 : 2;
-        if (c.tid < 32 && (c.tid >> 4) < nslot && (c.tid & 15) < 13) {
+        if (c.tid < 32 && (c.tid >> 4) < nslot && (c.tid & 15) < 14) {
             int p[13];
             i4_neighbours(S, (c.tid >> 4) ? b1 : b0, p);
-            S.i4nb[c.tid >> 4][c.tid & 15] = (int16_t)p[c.tid & 15];
+            S.i4nb[c.tid >> 4][c.tid & 15] = (int16_t)((c.tid & 15) == 13 ? i4_dc(p) : p[c.tid & 15]);  // [13]: the DC value
         }
         HL_SYNC();
+#if defined(HL_I4_PROF)
+        HL_PROF_ADD(c, 12, ti0);  // neighbours
+        HL_PROF_T(ti1);
+#endif
         // nC is the same for all nine modes of a block: they only rewrite it
         const int nC0 = uni(nc_luma_of(S, b0, [&](int ni) -> int { return S.tc[ni]; }));
         const int nC1 = nslot == 2 ? uni(nc_luma_of(S, b1, [&](int ni) -> int { return S.tc[ni]; })) : 0;
@@ -2560,7 +2611,8 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
             const bool ok = i4_avail(m, S.i4nb[sl]);
             if (ok) {
                 const int x = c.K.p & 3, y = c.K.p >> 2;
-                const int pred = i4_pred_px(m, S.i4nb[sl], x, y);
+                const int16_t* nb = S.i4nb[sl];
+                const int pred = i4_tab_pred(te, nb[te & 15], nb[(te >> 4) & 15], nb[(te >> 8) & 15]);
                 const int sv = S.src[(yO + y) * 16 + xO + x];
                 const int res = sv - pred;
                 const bool exact = row_or(res != 0) == 0;
@@ -2584,7 +2636,15 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
             }
             if (c.K.p == 0) S.i4_cost_ok[sl][m] = ok;
         }
+#if defined(HL_I4_PROF)
+        HL_PROF_ADD(c, 13, ti1);  // the modes' evaluation (own wave)
+        HL_PROF_T(ti2);
+#endif
         HL_SYNC();
+#if defined(HL_I4_PROF)
+        HL_PROF_ADD(c, 14, ti2);  // its barrier
+        HL_PROF_T(ti3);
+#endif
         // resolution in mode order (rdo.c:1931-2014), vectorised, one 16-lane
         // row per slot: the scan stops at the first exact mode; before it, the
         // last coded mode writes the counter and the first strict minimum wins
@@ -2639,6 +2699,9 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
             }
         }
         HL_SYNC();
+#if defined(HL_I4_PROF)
+        HL_PROF_ADD(c, 15, ti3);  // resolution + barrier
+#endif
     }
     for (int blk = 0; blk < 16; ++blk) {  // z-order: cost sum, distortion, CBP, counter writes
         best_cost = dadd(best_cost, uni(S.i4r_dmin[blk]));

@@ -368,6 +368,30 @@ extern "C" int emu_state_size(void) { return (int)sizeof(MbState); }
 extern "C" int emu_level_code_len(int sl, int lc) { return level_code_len(sl, lc); }
 extern "C" int emu_writer_level_bits(int sl, int lc) { return level_code_bits(sl, lc); }
 
+// The device's table-driven Intra4x4 prediction (kI4Tab, i4_tab_pred; DC from
+// i4_dc) against the per-mode definition i4_pred_px on random neighbourhoods,
+// every mode and sample: the number of differing samples.
+extern "C" long emu_i4_table_check(unsigned seed, int n)
+{
+    long bad = 0;
+    unsigned r = seed * 2654435761u + 1u;
+    for (int t = 0; t < n; ++t) {
+        int p[13], nb[14];
+        for (int k = 0; k < 13; ++k) {
+            r = r * 1664525u + 1013904223u;
+            p[k] = (int)(r >> 24);
+            nb[k] = p[k];
+        }
+        nb[13] = i4_dc(p);
+        for (int m = 0; m < 9; ++m)
+            for (int pos = 0; pos < 16; ++pos) {
+                const uint32_t e = kI4Tab.e[m][pos];
+                bad += i4_tab_pred(e, nb[e & 15], nb[(e >> 4) & 15], nb[(e >> 8) & 15]) != i4_pred_px(m, p, pos & 3, pos >> 2);
+            }
+    }
+    return bad;
+}
+
 // The pipelined-run schedule (hl_pipeline.h) for tests/test_pipeline_schedule.py:
 // deblocking (kind 0) or plane (kind 1) blocks of task (x, y) as X, Y pairs.
 extern "C" int emu_task_blocks(int kind, int x, int y, int mbw, int mbh, int* out)

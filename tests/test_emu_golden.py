@@ -73,3 +73,12 @@ def test_level_code_lengths_match_writer_table():
     for sl in range(7):
         for lc in list(range(0, 5000)) + list(range(5000, 62546, 37)):
             assert lib.emu_level_code_len(sl, lc) == lib.emu_writer_level_bits(sl, lc), (sl, lc)
+
+
+def test_i4_prediction_table():
+    """The GPU's branch-free Intra4x4 prediction (hl_mbcore.h kI4Tab: three
+    taps and weights per mode and sample, derived at compile time) equals the
+    per-mode definition (8.3.1.2, i4_pred_px) on random neighbourhoods."""
+    lib = ctypes.CDLL(EMU_LIB)
+    lib.emu_i4_table_check.restype = ctypes.c_long
+    assert lib.emu_i4_table_check(7, 20000) == 0
