@@ -1810,7 +1810,9 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
 #endif
         HL_PROF_ADD(c, 17, tsel);
     }
-    HL_SYNC();
+    // (no barrier before these stores: after the last pass, waves still read
+    // only the pass's candidate results, S.cd / S.wc / S.be_tcb, which lane 0
+    // does not write here; the barrier below orders them for the next search)
     if (c.tid == 0) {
         S.bcost[pi][spi] = b.cost;
         S.bdist[pi][spi] = b.dist;
