@@ -91,11 +91,27 @@ constexpr int kSpecMaxBlocks = HL_QUAD_EVAL ? HL_SPEC_MAX_BLOCKS : 8;
 
 // One candidate of a step: plane offsets of its quarter-pel prediction
 // (second plane = first when the phase needs no average) and its MV.
+#ifndef HL_LDS_WINDOW
+#define HL_LDS_WINDOW 0
+#endif
 struct alignas(16) CandSlot {
     int32_t off1, off2;
     int16_t mvx, mvy;
     int32_t pad;
+#if HL_LDS_WINDOW
+    int32_t w1, w2;  // the same two offsets in the LDS search window (Shared::win), or -1 when the partition leaves it
+    int32_t unused[2];
+#endif
 };
+// LDS-staged search window (device, HL_LDS_WINDOW=1; measured, not the
+// default: profiles/r03_ab_lds_window.log): the four quarter-pel planes of the
+// reference over padded columns [xL, xL + 96) and rows [yL, yL + 88), i.e.
+// picture samples 40 to the left / above the MB to 47 (cols 55) beyond its
+// origin -- the MBs up to (x + 2, y + 2), which a pipelined task's reach R = 2
+// guarantees complete.  Loaded once per MB; a candidate whose whole
+// partition (+1 sample for the second plane) lies inside reads its
+// prediction from LDS, otherwise from the planes in HBM/L2.
+constexpr int kWinW = 96, kWinH = 88, kWinPlane = kWinW * kWinH;
 constexpr int kNA = -1;   // not-available sample marker
 
 struct FrameArgs {
@@ -226,6 +242,9 @@ struct Shared {
     // VGPRs for the whole MB (which the compiler spilled to scratch: those
     // scratch stores were most of k_pipeline's HBM writes)
     LaneK lk[16];
+#if HL_LDS_WINDOW
+    alignas(16) uint8_t win[4 * kWinPlane];  // the search window (kWinW x kWinH per plane)
+#endif
 };
 
 struct Ctx {
@@ -239,6 +258,7 @@ struct Ctx {
     LaneQ Q{};              // per-lane constants of the quad block pipeline (registers: the search loop reads them every pass)
 #endif
     int gx, gy;             // reference planes known complete for MBs (X <= gx, Y <= gy) (pipelined runs)
+    int wux = 0, wuy = 0;   // usable columns / rows of the LDS search window (0: none)
     int spec = 0;           // 1 = chain is still a row-start speculation (uniform)
     int par = 0;            // buffer parity of the last candidate step (Shared::cd, be_tcb)
 #if defined(HL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
@@ -907,7 +927,7 @@ HD constexpr uint64_t qpel_pack(int first, int n)
 // The candidate list of a step is uniform; each wave keeps its own copy in
 // LDS so that no barrier is needed between choosing and evaluating it.
 // (xo, yo) = luma origin of the partition inside the MB.
-HD void put_cand(Ctx& c, int xo, int yo, int i, int mx, int my, int pt = 0, bool writer = true)
+HD void put_cand(Ctx& c, int xo, int yo, int pw, int pht, int i, int mx, int my, int pt = 0, bool writer = true)
 {
     const FrameArgs& F = c.F;
     constexpr uint64_t q0 = qpel_pack(0, 7), q1 = qpel_pack(7, 7), q2 = qpel_pack(14, 2);
@@ -921,6 +941,17 @@ HD void put_cand(Ctx& c, int xo, int yo, int i, int mx, int my, int pt = 0, bool
     cs.mvx = (int16_t)mx;
     cs.mvy = (int16_t)my;
     cs.pad = pt;  // diamond point index
+#if HL_LDS_WINDOW
+    // window-relative origin of the partition (padded coordinates minus the window's)
+    const int rx = X - c.xL, ry = Y - c.yL;  // (the window starts at padded (xL, yL))
+    const bool in = rx >= 0 && ry >= 0 && rx + pw + 1 <= c.wux && ry + pht + 1 <= c.wuy;
+    cs.w1 = in ? (int)(e & 3) * kWinPlane + (ry + (int)((e >> 3) & 1)) * kWinW + rx + (int)((e >> 2) & 1) : -1;
+    cs.w2 = !in ? -1 : ((e & 16) ? (int)((e >> 5) & 3) * kWinPlane + (ry + (int)((e >> 8) & 1)) * kWinW + rx + (int)((e >> 7) & 1) : cs.w1);
+    cs.unused[0] = cs.unused[1] = 0;
+#else
+    (void)pw;
+    (void)pht;
+#endif
     if (writer) c.S.wc[c.tid >> 6][i] = cs;
 }
 
@@ -991,6 +1022,10 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         const int nc1 = g.nblk == 1 ? nc_luma_of(S, blk_idx(g.px, g.py), [&](int ni) -> int { return S.tc[ni]; }) : 0;
         int o1[kQPass], o2[kQPass];
         uint32_t sv[kQPass], pr[kQPass];
+#if HL_LDS_WINDOW
+        int l1[kQPass], l2[kQPass];
+        bool inw = true;
+#endif
 #pragma unroll
         for (int j = 0; j < kQPass; ++j) {
             const int item = min(qg + j * nq, n - 1);  // clamped: no divergence, valid addresses
@@ -1000,12 +1035,29 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
             const int o = ((hy << 2) + Q.r) * F.pstride + (hx << 2);
             o1[j] = cs.x + o;
             o2[j] = cs.y + o;
+#if HL_LDS_WINDOW
+            const int2 cw = *reinterpret_cast<const int2*>(&S.wc[wave][ci].w1);
+            const int ow = ((hy << 2) + Q.r) * kWinW + (hx << 2);
+            l1[j] = cw.x + ow;
+            l2[j] = cw.y + ow;
+            inw = inw && (cw.x >= 0 || qg + j * nq >= n);
+#endif
             sv[j] = *reinterpret_cast<const uint32_t*>(&S.src[(g.py + (hy << 2) + Q.r) * 16 + g.px + (hx << 2)]);
         }
         HL_PROF_T(ta0);
+#if HL_LDS_WINDOW
+        if (__ballot(!inw) == 0) {  // every candidate block of the wave inside the LDS window
 #pragma unroll
-        for (int j = 0; j < kQPass; ++j)
-            if (qg + j * nq < n) pr[j] = avg_u8x4(ld_u8x4(base, o1[j]), ld_u8x4(base, o2[j]));
+            for (int j = 0; j < kQPass; ++j)
+                if (qg + j * nq < n) pr[j] = avg_u8x4(ld_lds_u8x4(S.win, l1[j]), ld_lds_u8x4(S.win, l2[j]));
+        }
+        else
+#endif
+        {
+#pragma unroll
+            for (int j = 0; j < kQPass; ++j)
+                if (qg + j * nq < n) pr[j] = avg_u8x4(ld_u8x4(base, o1[j]), ld_u8x4(base, o2[j]));
+        }
 #if defined(HL_STEP_PROF)
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the loads' latency (profiling only)
         HL_PROF_ADD(c, 12, ta0);
@@ -1500,7 +1552,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         smv[0] = uni(smv[0]);
         smv[1] = uni(smv[1]);
         if (pmv[0] == smv[0] && pmv[1] == smv[1]) {
-            put_cand(c, g.px, g.py, 0, pmv[0], pmv[1], 0, (c.tid & 63) == 0);
+            put_cand(c, g.px, g.py, g.pw, g.ph, 0, pmv[0], pmv[1], 0, (c.tid & 63) == 0);
             eval_candidates(c, g, 1, pmv);
             commit_candidates(c, g, 1);
             if (uni(S.cd[c.par].bits[0]) == 0 || uni(S.cd[c.par].single[0]) < 6) {
@@ -1663,7 +1715,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
                 lo[k] = __popcll(bal & ((1ull << (16 * k)) - 1ull));
                 n[k] = __popcll(bal & (0xFFFFull << (16 * k)));
             }
-            if (en) put_cand(c, g.px, g.py, __popcll(bal & ((1ull << i) - 1ull)), mx << sh, my << sh, i & 15, true);
+            if (en) put_cand(c, g.px, g.py, g.pw, g.ph, __popcll(bal & ((1ull << i) - 1ull)), mx << sh, my << sh, i & 15, true);
         }
 #if defined(HL_STEP_PROF)
         HL_PROF_ADD(c, 19, tgen);  // the pass's candidates generated and stored
@@ -1675,8 +1727,8 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
                 const int st = stage - j;
                 lo[j] = tot;
                 if (st == 3) {
-                    put_cand(c, g.px, g.py, tot++, pmv[0], pmv[1], 0, true);
-                    if (nc0 == 2) put_cand(c, g.px, g.py, tot++, 0, 0, 1, true);
+                    put_cand(c, g.px, g.py, g.pw, g.ph, tot++, pmv[0], pmv[1], 0, true);
+                    if (nc0 == 2) put_cand(c, g.px, g.py, g.pw, g.ph, tot++, 0, 0, 1, true);
                 }
                 else {
                     const uint32_t pkx = st == 2 ? pIntX : (st == 1 ? pHalfX : pQuarX);
@@ -1691,7 +1743,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
                         if (!((fl >> pt) & 1)) continue;
                         const int mx = ccx + (int)((pkx >> (3 * pt)) & 7) - 2, my = ccy + (int)((pky >> (3 * pt)) & 7) - 2;
                         if (mx < l0 || mx > r0 || my < t0 || my > b0) continue;
-                        put_cand(c, g.px, g.py, tot++, mx << sh, my << sh, pt, true);
+                        put_cand(c, g.px, g.py, g.pw, g.ph, tot++, mx << sh, my << sh, pt, true);
                     }
                 }
                 n[j] = tot - lo[j];
@@ -3569,7 +3621,33 @@ HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, in
 #endif
     if (tid == 0) gmem(F.chain + addr)->s_in = s_in;
     HL_PROF_T(t0);
+#if defined(__HIP_DEVICE_COMPILE__) && HL_LDS_WINDOW
+    // the LDS search window: loads issued here, stored after mb_begin's load
+    // round (their latency overlaps it); read after guess_inter's barriers
+    constexpr int kWinChunks = 4 * kWinPlane / 16, kWinRounds = (kWinChunks + kMbThreads - 1) / kMbThreads;
+    uint4 wv[kWinRounds];
+    if (!F.is_intra) {
+        const int bx = c.gx >= F.mbw - 1 ? F.W + 2 * kPad : 16 * (c.gx + 1) + kPad;
+        const int by = c.gy >= F.mbh - 1 ? F.H + 2 * kPad : 16 * (c.gy + 1) + kPad;
+        c.wux = min(kWinW, bx - c.xL);
+        c.wuy = min(kWinH, by - c.yL);
+        const auto pl = gmem(F.pl[0]);
+#pragma unroll
+        for (int k = 0; k < kWinRounds; ++k) {
+            const int i = min(tid + k * kMbThreads, kWinChunks - 1);
+            const int p = i / (kWinPlane / 16), rem = i - p * (kWinPlane / 16), r = rem / (kWinW / 16), cc = rem - r * (kWinW / 16);
+            wv[k] = *reinterpret_cast<const __attribute__((address_space(1))) uint4*>(pl + (size_t)p * F.plsz + (size_t)(c.yL + r) * F.pstride + c.xL + cc * 16);
+        }
+    }
+#endif
     mb_begin(c);
+#if defined(__HIP_DEVICE_COMPILE__) && HL_LDS_WINDOW
+    if (!F.is_intra) {
+#pragma unroll
+        for (int k = 0; k < kWinRounds; ++k)
+            if (tid + k * kMbThreads < kWinChunks) reinterpret_cast<uint4*>(S.win)[tid + k * kMbThreads] = wv[k];
+    }
+#endif
     HL_PROF_ADD(c, 6, t0);
     if (F.is_intra) guess_intra(c);
     else guess_inter(c);

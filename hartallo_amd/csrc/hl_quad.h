@@ -228,6 +228,12 @@ __device__ __forceinline__ uint32_t ld_u8x4(const __attribute__((address_space(1
     const auto w = reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(p + (off & ~3));
     return __builtin_amdgcn_alignbyte(w[1], w[0], (unsigned)(off & 3));
 }
+// the same from LDS
+__device__ __forceinline__ uint32_t ld_lds_u8x4(const uint8_t* p, int off)
+{
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p + (off & ~3));
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (unsigned)(off & 3));
+}
 // per byte (a + b + 1) >> 1
 __device__ __forceinline__ uint32_t avg_u8x4(uint32_t a, uint32_t b) { return (a | b) - (((a ^ b) & 0xFEFEFEFEu) >> 1); }
 
