@@ -1014,7 +1014,8 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
     {
         const int wave = c.tid >> 6, qg = c.tid >> 2, nq = c.nthr >> 2;
         const int n = ncand << g.lnb;
-        const int qbits = 15 + F.qp / 6, f = (1 << qbits) / 6;
+        const int qp = uni(F.qp);  // scalar: the quantiser's shifts and the dequantiser's form are uniform
+        const int qbits = 15 + qp / 6, f = (1 << qbits) / 6;
         const LaneQ& Q = c.Q;
         const auto base = gmem(F.pl[0]);
         // single-block partitions: both nC neighbours lie outside the partition,
@@ -1083,7 +1084,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                     // reconstruction distortion first: independent of the CAVLC
                     // chain, so the two interleave
                     int r[4];
-                    quad_idct(Q, q, F.qp, r);
+                    quad_idct(Q, q, qp, r);
                     int d = 0;
 #pragma unroll
                     for (int cc = 0; cc < 4; ++cc) {
@@ -1811,6 +1812,9 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
 #endif
         // resolve the chain step by step
         int used = 0;
+#if defined(HL_CHAIN_PROF)
+        bool brk = false;
+#endif
 #pragma unroll
         for (int j = 0; j < kMaxSeg; ++j) {
             if (j >= nseg) break;
@@ -1827,7 +1831,13 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
                 right = cx + range;
                 top = cy - range;
                 bottom = cy + range;
-                if (b.mv[0] != pmv[0] || b.mv[1] != pmv[1]) break;  // the continuation assumed the MVP
+                if (b.mv[0] != pmv[0] || b.mv[1] != pmv[1]) {
+#if defined(HL_CHAIN_PROF)
+                    if (j + 1 < nseg) HL_PROF_ADD(c, 12, __builtin_readcyclecounter() - 1);  // (0,0) won: speculation dropped
+                    brk = true;
+#endif
+                    break;  // the continuation assumed the MVP
+                }
                 continue;
             }
             int best = -1;
@@ -1840,6 +1850,10 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
                 cx = b.mv[0] >> (stage == 2 ? 2 : (stage == 1 ? 1 : 0));
                 cy = b.mv[1] >> (stage == 2 ? 2 : (stage == 1 ? 1 : 0));
                 flags = mask_of(stage == 2 ? 2 : (stage == 1 ? 1 : 0), best);  // points the move already visited
+#if defined(HL_CHAIN_PROF)
+                HL_PROF_ADD(c, stage == 2 ? 13 : (stage == 1 ? 14 : 15), __builtin_readcyclecounter() - 1);  // a move ends the pass
+                brk = true;
+#endif
                 break;
             }
             --stage;  // no better point: the next stage (the chain's next step)
@@ -1855,6 +1869,9 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
 #if defined(__HIP_DEVICE_COMPILE__)
 #if defined(HL_STEP_PROF)
         HL_PROF_ADD(c, 18, tres);  // the chain resolved
+#endif
+#if defined(HL_CHAIN_PROF)
+        if (!brk && stage >= 0) HL_PROF_ADD(c, 18, __builtin_readcyclecounter() - 1);  // chain resolved, search goes on: budget-limited
 #endif
         if (used) commit_candidates(c, g, used, pv_last);
 #else

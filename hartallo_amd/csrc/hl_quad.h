@@ -32,7 +32,9 @@ constexpr int kQX1 = 0xB1, kQX2 = 0x4E;  // quad_perm lane ^ 1, lane ^ 2
 template <int CTRL>
 __device__ __forceinline__ int dpp_x(int v)
 {
-    int r = dpp<CTRL>(v);
+    // mov_dpp (no "old" operand: every lane of a quad is written, so no
+    // zero-initialised destination has to be materialised first)
+    int r = __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
     asm volatile("" : "+v"(r));
     return r;
 }
@@ -111,12 +113,15 @@ __device__ __forceinline__ int quad_q1(int w, int mf, int qbits, int f)
 // (raster), out = row r of the residual.
 __device__ __forceinline__ void quad_idct(const LaneQ& Q, const int q[4], int qP, int out[4])
 {
+    // 8.5.12.1 as ((p << a) + r) >> b with a, r, b uniform: qP >= 24 shifts
+    // left by q6 - 4, below it rounds and shifts right by 4 - q6
     const int q6 = qP / 6;
+    const int sa = qP >= 24 ? q6 - 4 : 0, sr = qP >= 24 ? 0 : 1 << (3 - q6), sb = qP >= 24 ? 0 : 4 - q6;
     int d[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int p = __mul24(q[c], (c & 1) ? Q.lsO : Q.lsE);
-        d[c] = qP >= 24 ? p << (q6 - 4) : (p + (1 << (3 - q6))) >> (4 - q6);
+        d[c] = ((p << sa) + sr) >> sb;
     }
     const int e0 = d[0] + d[2], e1 = d[0] - d[2], e2 = (d[1] >> 1) - d[3], e3 = d[1] + (d[3] >> 1);
     const int f[4] = {e0 + e3, e1 + e2, e1 - e2, e0 - e3};
