@@ -2663,10 +2663,25 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
 #endif
         const int b0 = kWave[d][0], b1 = kWave[d][1];
         const int nslot = b1 == 255 ? 1 : 2;
-        if (c.tid < 32 && (c.tid >> 4) < nslot && (c.tid & 15) < 14) {
-            int p[13];
-            i4_neighbours(S, (c.tid >> 4) ? b1 : b0, p);
-            S.i4nb[c.tid >> 4][c.tid & 15] = (int16_t)((c.tid & 15) == 13 ? i4_dc(p) : p[c.tid & 15]);  // [13]: the DC value
+        if (c.tid < 32 && (c.tid >> 4) < nslot) {
+            // lane i of the slot's 16-lane row: neighbour sample i (i4_neighbours,
+            // one sample per lane); lane 13: the DC value (mode 2 of i4_pred_px)
+            const int i = c.tid & 15, base = c.tid & 16, blk = base ? b1 : b0;
+            const int xO = blk_x(blk), yO = blk_y(blk);
+            const int X = i < 5 ? -1 : i - 5, Y = i < 5 ? i - 1 : -1;
+            const int x = xO + X, y = yO + Y;
+            const bool na = i >= 13 || (x > 15 && y >= 0) || (X > 3 && (blk == 3 || blk == 11));
+            const int vl = S.left[y < 0 ? 0 : y], vt = S.top[min(max(x + 1, 0), 24)], vr = S.rec[(y < 0 ? 0 : y) * 16 + min(max(x, 0), 15)];
+            int v = na ? kNA : ((x < 0 && y >= 0) ? vl : (y < 0 ? vt : vr));
+            const int s8 = base ? __builtin_amdgcn_readlane(v, 24) : __builtin_amdgcn_readlane(v, 8);
+            const int s9 = base ? __builtin_amdgcn_readlane(v, 25) : __builtin_amdgcn_readlane(v, 9);
+            if (i >= 9 && i <= 12 && s9 == kNA && s8 != kNA) v = s8;
+            const bool isl = i >= 1 && i <= 4, ist = i >= 5 && i <= 8;
+            const int suml = row_sum(isl ? v : 0), sumt = row_sum(ist ? v : 0);
+            const unsigned al = (unsigned)(__ballot(isl && v != kNA) >> base) & 0xFFFFu, at = (unsigned)(__ballot(ist && v != kNA) >> base) & 0xFFFFu;
+            const bool ya = al == 0x1Eu, xa = at == 0x1E0u;
+            const int dc = (xa && ya) ? (sumt + suml + 4) >> 3 : (ya ? (suml + 2) >> 2 : (xa ? (sumt + 2) >> 2 : 128));
+            if (i < 14) S.i4nb[base >> 4][i] = (int16_t)(i == 13 ? dc : v);  // [13]: the DC value
         }
         HL_SYNC();
 #if defined(HL_I4_PROF)
