@@ -270,11 +270,17 @@ struct Ctx {
 // --------------------------------------------------------------------------
 // small helpers
 // --------------------------------------------------------------------------
+// ue(v) length 2 floor(log2(v + 1)) + 1, closed form (a per-lane loop here
+// ran in every lane of the cost phase); v + 1 < 2^31 for every MV difference
 HD int ue_len(unsigned v)
 {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return 2 * (31 - __clz((int)(v + 1))) + 1;
+#else
     int lz = 0;
     while ((1u << (lz + 1)) <= v + 1) ++lz;
     return 2 * lz + 1;
+#endif
 }
 HD int se_len(int n) { return ue_len(n <= 0 ? (unsigned)(-n) << 1 : ((unsigned)n << 1) - 1); }
 
