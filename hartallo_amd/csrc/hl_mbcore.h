@@ -1229,6 +1229,9 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
 #else
     HL_SYNC();
 #endif
+#if defined(HL_NBLK_PROF)  // phase 1 by partition size: slots 12..15 = 1, 2, 4, 8+ blocks
+    HL_PROF_ADD(c, 12 + (g.nblk >= 8 ? 3 : g.lnb), tp0);
+#endif
     HL_PROF_ADD(c, 0, tp0);
     HL_PROF_T(tp1);
     // phase 2: one row per candidate, one lane per block: nC as the reference
@@ -2070,19 +2073,14 @@ HD void i16_params(const Shared& S, int mode, int& dcv, int& pa, int& pb, int& p
     if (mode == 2) {
         bool xa = true, ya = true;
         int xs = 0, ys = 0;
-        for (int x = 0; x < 16; ++x) {
-            if (S.top[1 + x] == kNA) {
-                xa = false;
-                break;
-            }
-            xs += S.top[1 + x];
-        }
-        for (int y = 0; y < 16; ++y) {
-            if (S.left[y] == kNA) {
-                ya = false;
-                break;
-            }
-            ys += S.left[y];
+        // no early exit: a sum is only used when its side had no kNA, so the
+        // loads are independent and issue together
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            xa = xa && S.top[1 + k] != kNA;
+            ya = ya && S.left[k] != kNA;
+            xs += S.top[1 + k];
+            ys += S.left[k];
         }
         if (xa && ya) dcv = (xs + ys + 16) >> 5;
         else if (ya) dcv = (ys + 8) >> 4;
@@ -2256,18 +2254,11 @@ HD void intra_chroma_pred(Ctx& c, int mode)
             for (int b = 0; b <= ((y >> 2) << 1 | (x >> 2)); ++b) {
                 const int xO = (b & 1) * 4, yO = (b >> 1) * 4;
                 int xs = 0, ys = 0;
+#pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    if (top[xO + k] == kNA) {
-                        xa = false;
-                        break;
-                    }
+                    xa = xa && top[xO + k] != kNA;
+                    ya = ya && left[yO + k] != kNA;
                     xs += top[xO + k];
-                }
-                for (int k = 0; k < 4; ++k) {
-                    if (left[yO + k] == kNA) {
-                        ya = false;
-                        break;
-                    }
                     ys += left[yO + k];
                 }
                 t4 = 128;
