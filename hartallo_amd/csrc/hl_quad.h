@@ -21,7 +21,7 @@
 
 namespace hl {
 
-constexpr int kQX1 = 0xB1, kQX2 = 0x4E;  // quad_perm lane ^ 1, lane ^ 2
+constexpr int kQX1 = 0xB1, kQX2 = 0x4E, kQX3 = 0x1B;  // quad_perm lane ^ 1, lane ^ 2, lane ^ 3
 
 // A DPP read kept as its own v_mov_b32_dpp: the empty asm stops LLVM's DPP
 // combiner from folding it into the subtraction that consumes it.  On the
@@ -52,19 +52,24 @@ __device__ __forceinline__ int quad_or(int x)
 
 // Per-lane constants of the quad pipeline at one QP.
 struct LaneQ {
-    int r;          // the block row this lane holds
+    int r;          // the block row this lane holds (samples and residual)
+    // the rest belong to coefficient row quad_coef_row(r)
     int mfE, mfO;   // quantisation multipliers of the row's even / odd columns
     int lsE, lsO;   // dequantisation level scales, same
     uint32_t zz;    // scan index of (r, c) in bits [4c, 4c + 3]
 };
+
+// The coefficient row lane r of a quad holds between quad_fwd and quad_idct:
+// the two-stage butterflies below leave rows 1 and 2 swapped (0, 2, 1, 3).
+__device__ __forceinline__ int quad_coef_row(int r) { return ((r & 1) << 1) | (r >> 1); }
 
 __device__ __forceinline__ LaneQ make_laneq(int tid, int qp)
 {
     // kZzInv[r * 4 + c]: scan index of raster position (r, c)
     constexpr uint64_t kZzRows = 0xFEA9DB83C7426510ull;  // rows of {0,1,5,6},{2,4,7,12},{3,8,11,13},{9,10,14,15}, 4 bits each
     LaneQ Q;
-    const int r = tid & 3;
-    Q.r = r;
+    Q.r = tid & 3;
+    const int r = quad_coef_row(Q.r);  // the quantiser's, scan's and dequantiser's row
     Q.zz = (uint32_t)(kZzRows >> (16 * r)) & 0xFFFFu;
     const int m = qp % 6;
     const int clsE = (r & 1) ? 2 : 0, clsO = (r & 1) ? 1 : 2;
@@ -84,20 +89,23 @@ __device__ __forceinline__ LaneQ make_laneq(int tid, int qp)
     return Q;
 }
 
-// Forward core transform Cf X Cf^T: x = row r of the residual, y = row r of
-// the coefficients.  Exact integer arithmetic: the pass order does not
-// matter.
+// Forward core transform Cf X Cf^T: x = row r of the residual, y = row
+// quad_coef_row(r) of the coefficients.  Exact integer arithmetic: the pass
+// order does not matter.  The column pass is two butterfly stages with one
+// DPP read each (rows a, b, e, d = 0..3):
+//   stage 1, partner r ^ 3: a + d | b + e | b - e | a - d   (p + s1 x)
+//   stage 2, partner r ^ 1: y0 = (a+d) + (b+e), y2 = (a+d) - (b+e),
+//                           y1 = 2 (a-d) + (b-e), y3 = (a-d) - 2 (b-e)
+// |values| <= 9180 (8-bit residuals), so the 24-bit multiplies are exact.
 __device__ __forceinline__ void quad_fwd(const LaneQ& Q, const int x[4], int y[4])
 {
     const int s03 = x[0] + x[3], d03 = x[0] - x[3], s12 = x[1] + x[2], d12 = x[1] - x[2];
     const int h[4] = {s03 + s12, (d03 << 1) + d12, s03 - s12, d03 - (d12 << 1)};
+    const int s1 = Q.r < 2 ? 1 : -1, kx = Q.r == 1 ? -1 : 1, kp = Q.r < 2 ? 1 : (Q.r == 2 ? 2 : -2);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const int a = dpp_x<kQ0>(h[c]), b = dpp_x<kQ1>(h[c]), e = dpp_x<kQ2>(h[c]), d = dpp_x<kQ3>(h[c]);
-        const int v03 = a + d, w03 = a - d, v12 = b + e, w12 = b - e;
-        const int y01 = Q.r == 0 ? v03 + v12 : (w03 << 1) + w12;
-        const int y23 = Q.r == 2 ? v03 - v12 : w03 - (w12 << 1);
-        y[c] = Q.r < 2 ? y01 : y23;
+        const int t = __mul24(h[c], s1) + dpp_x<kQX3>(h[c]);
+        y[c] = __mul24(dpp_x<kQX1>(t), kp) + __mul24(t, kx);
     }
 }
 
@@ -108,9 +116,15 @@ __device__ __forceinline__ int quad_q1(int w, int mf, int qbits, int f)
     return w >= 0 ? v : -v;
 }
 
-// Dequantisation (8.5.12.1) and inverse transform of row r (rows first, then
-// columns, then (x + 32) >> 6, transf.c:376-458): q = row r of the levels
-// (raster), out = row r of the residual.
+// Dequantisation (8.5.12.1) and inverse transform (rows first, then columns,
+// then (x + 32) >> 6, transf.c:376-458): q = coefficient row
+// quad_coef_row(r) of the levels (raster), out = row r of the residual.  The
+// column pass as two butterfly stages (input rows f0, f2, f1, f3 in lanes
+// 0..3):
+//   stage 1, partner r ^ 1: g0 = f0 + f2 | g1 = f0 - f2 | g2 = (f1 >> 1) - f3 | g3 = f1 + (f3 >> 1)
+//   stage 2, partner r ^ 3: h0 = g0 + g3 | h1 = g1 + g2 | h2 = g1 - g2 | h3 = g0 - g3
+// Dequantised values stay below 2^18 and every sum below 2^22 for levels of
+// 8-bit residuals at any QP, so the 24-bit multiplies are exact.
 __device__ __forceinline__ void quad_idct(const LaneQ& Q, const int q[4], int qP, int out[4])
 {
     // 8.5.12.1 as ((p << a) + r) >> b with a, r, b uniform: qP >= 24 shifts
@@ -125,13 +139,11 @@ __device__ __forceinline__ void quad_idct(const LaneQ& Q, const int q[4], int qP
     }
     const int e0 = d[0] + d[2], e1 = d[0] - d[2], e2 = (d[1] >> 1) - d[3], e3 = d[1] + (d[3] >> 1);
     const int f[4] = {e0 + e3, e1 + e2, e1 - e2, e0 - e3};
+    const int kx = Q.r == 1 ? -1 : 1, sh = Q.r >> 1, kp = Q.r == 2 ? -1 : 1, s1 = Q.r < 2 ? 1 : -1;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const int f0 = dpp_x<kQ0>(f[c]), f1 = dpp_x<kQ1>(f[c]), f2 = dpp_x<kQ2>(f[c]), f3 = dpp_x<kQ3>(f[c]);
-        const int g0 = f0 + f2, g1 = f0 - f2, g2 = (f1 >> 1) - f3, g3 = f1 + (f3 >> 1);
-        const int h01 = Q.r == 0 ? g0 + g3 : g1 + g2;
-        const int h23 = Q.r == 2 ? g1 - g2 : g0 - g3;
-        out[c] = ((Q.r < 2 ? h01 : h23) + 32) >> 6;
+        const int g = __mul24(f[c] >> sh, kx) + __mul24(dpp_x<kQX1>(f[c]), kp);
+        out[c] = (__mul24(g, s1) + dpp_x<kQX3>(g) + 32) >> 6;
     }
 }
 

@@ -113,7 +113,7 @@ __global__ __launch_bounds__(256) void k_unit_quad(const uint8_t* src, const uin
     for (int c = 0; c < 4; ++c) {
         const int v = clip255(pv[c] + r[c]);
         d += iabs(sv[c] - v);
-        o.q[4 * Q.r + c] = q[c];
+        o.q[4 * quad_coef_row(Q.r) + c] = q[c];
         o.rec[4 * Q.r + c] = v;
     }
     const int dist = quad_sum(d);
