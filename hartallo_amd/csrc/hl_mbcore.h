@@ -1084,20 +1084,17 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                 CoopStat st{0, 0, 0, -1};
                 int tok = 0, dist;
                 if (__ballot((q[0] | q[1] | q[2] | q[3]) != 0) == 0) {  // every block of the wave quantised to zero
-                    dist = quad_sum(iabs(x[0]) + iabs(x[1]) + iabs(x[2]) + iabs(x[3]));
+                    dist = quad_sum((int)__builtin_amdgcn_sad_u8(sv[j], pr[j], 0u));  // the row's sum of |residual|
                 }
                 else {
                     // reconstruction distortion first: independent of the CAVLC
                     // chain, so the two interleave
                     int r[4];
                     quad_idct(Q, q, qp, r);
-                    int d = 0;
+                    uint32_t rec = 0;  // the row's reconstructed samples, packed
 #pragma unroll
-                    for (int cc = 0; cc < 4; ++cc) {
-                        const int p = (int)((pr[j] >> (8 * cc)) & 255), sp = (int)((sv[j] >> (8 * cc)) & 255);
-                        d += iabs(sp - clip255(p + r[cc]));
-                    }
-                    dist = quad_sum(d);
+                    for (int cc = 0; cc < 4; ++cc) rec |= (uint32_t)clip255((int)((pr[j] >> (8 * cc)) & 255) + r[cc]) << (8 * cc);
+                    dist = quad_sum((int)__builtin_amdgcn_sad_u8(sv[j], rec, 0u));
                     st = quad_cavlc(S.ct, Q, q, 0, S.lvq[qg]);
                     if (Q.r == 0 && st.tc)  // coeff_token lengths for the four nC classes
                         tok = S.ct.tok[0][st.t1][st.tc] | (S.ct.tok[1][st.t1][st.tc] << 5) | (S.ct.tok[2][st.t1][st.tc] << 10) | (6 << 15);
