@@ -46,6 +46,8 @@ EXPORTED_SYMBOLS = (
     "hl_amd_last_chain_walks",
     "hl_amd_last_mb_launches",
     "hl_amd_last_batch_stats",
+    "hl_amd_set_intra_helpers",
+    "hl_amd_last_helper_stats",
     "hl_amd_profile_counters",
     "hl_amd_debug_records",
     "hl_amd_record_size",
@@ -157,6 +159,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_last_mb_launches.restype = i32
     lib.hl_amd_last_batch_stats.argtypes = [vp, ctypes.POINTER(i32)]
     lib.hl_amd_last_batch_stats.restype = i32
+    lib.hl_amd_set_intra_helpers.argtypes = [vp, i32]
+    lib.hl_amd_set_intra_helpers.restype = i32
+    lib.hl_amd_last_helper_stats.argtypes = [vp, ctypes.POINTER(i32)]
+    lib.hl_amd_last_helper_stats.restype = i32
     lib.hl_amd_profile_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong), i32]
     lib.hl_amd_profile_counters.restype = i32
     # diagnostics entry points (absent from older builds loaded through HL_LIB)
@@ -398,6 +404,21 @@ class Encoder:
         if rc != HL_AMD_SUCCESS:
             raise HlAmdError(rc, "hl_amd_last_batch_stats")
         return dict(zip(("runs", "per_picture", "fallbacks", "waits_gave_up", "chain_walks"), list(a)))
+
+    def set_intra_helpers(self, enable: bool) -> None:
+        rc = self.lib.hl_amd_set_intra_helpers(self._h, 1 if enable else 0)
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_set_intra_helpers")
+
+    def last_helper_stats(self) -> dict:
+        """How the last encode call's intra fallbacks ran
+        (hl_amd_last_helper_stats): helper Intra4x4 decisions kept, rejected,
+        helpers no workgroup had claimed in time."""
+        a = (ctypes.c_int32 * 3)()
+        rc = self.lib.hl_amd_last_helper_stats(self._h, a)
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_last_helper_stats")
+        return dict(zip(("i4_kept", "i4_rejected", "taken_over"), list(a)))
 
 
 class SvcEncoder(Encoder):

@@ -256,22 +256,24 @@ __device__ void task_filters(const PipeFrame& PF, Shared& S, int x, int y, int m
 __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
 {
     const int nmb = mbw * mbh, i = blockIdx.x * 256 + threadIdx.x;
+    const bool h0 = P.helpers && !P.fr[0].F.is_intra;  // the first task's intra helper
     if (i < P.nframes * nmb) {
         const int f = i / nmb, a = i - f * nmb;
         int d[3][3];
         P.cnt[i] = task_deps(f, a % mbw, a / mbw, mbw, mbh, P.reach, d);
         P.done[i] = 0;
-        P.queue[i] = i == 0 ? 1 : 0;
+        P.queue[2 * f * nmb + a] = i == 0 ? 1 : (i == 1 && h0 ? 1 + nmb : 0);
+        P.queue[2 * f * nmb + nmb + a] = 0;
         P.claim[i] = 0;
+        P.hstate[i] = HS_FREE;
     }
     if (i < P.nframes) {
         P.head[i] = 0;
-        P.tail[i] = i == 0 ? 1 : 0;
+        P.tail[i] = i == 0 ? (h0 ? 2 : 1) : 0;
     }
     if (i == 0) {
         *P.oldest = 0;
-        P.err[0] = 0;
-        P.err[1] = 0;
+        for (int k = 0; k < 5; ++k) P.err[k] = 0;  // give-ups, chain walks, helper I4 kept / rejected / taken over
     }
 }
 
@@ -311,10 +313,10 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh)
         else {
             // the head entries themselves (0: pushed, not yet written)
             int q = 0;
-            if (lane < w && h < t) q = ld_relaxed(P.queue + (o + lane) * nmb + h);
+            if (lane < w && h < t) q = ld_relaxed(P.queue + (size_t)(o + lane) * 2 * nmb + h);
             int key = -1;
             if (q > 0) {
-                const int a = q - 1, y = a / mbw, x = a - y * mbw;
+                const int a = q - 1 - (q > nmb ? nmb : 0), y = a / mbw, x = a - y * mbw;
                 key = (((mbw - 1 - x) + 2 * (mbh - 1 - y) - P.hop * lane + 4096) << 6) | (63 - lane);
             }
             for (int s = 1; s < 64; s <<= 1) key = max(key, __shfl_xor(key, s, 64));
@@ -332,16 +334,22 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh)
             if (lane == 0 && atomicCAS(P.head + f, hh, hh + 1) == hh) {
                 r = v;
                 // the slot is pushed right after the tail moved
-                for (unsigned k = 0; r == 0 && (r = ld_relaxed(P.queue + f * nmb + hh)) == 0; ++k)
+                for (unsigned k = 0; r == 0 && (r = ld_relaxed(P.queue + (size_t)f * 2 * nmb + hh)) == 0; ++k)
                     if (k > (1u << 26)) {
                         atomicAdd(P.err, 1);
                         r = -1;
                         break;
                     }
-                if (r > 0 && atomicCAS(P.claim + f * nmb + r - 1, 0, 1) != 0) r = 0;
+                // a macroblock task: claim it (workgroup 0 may have); an intra
+                // helper: claim it unless its macroblock took it over
+                if (r > nmb) {
+                    if (atomicCAS(P.hstate + f * nmb + r - 1 - nmb, HS_FREE, HS_CLAIMED) != HS_FREE) r = 0;
+                }
+                else if (r > 0 && atomicCAS(P.claim + f * nmb + r - 1, 0, 1) != 0) r = 0;
             }
             r = __builtin_amdgcn_readfirstlane(r);
             if (r < 0) return -1;
+            if (r > nmb) return P.nframes * nmb + f * nmb + r - 1 - nmb;  // intra helper of (f, r - 1 - nmb)
             if (r > 0) return f * nmb + r - 1;
             continue;  // another workgroup took it
         }
@@ -400,7 +408,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #if defined(HL_PROFILE)
     // per-workgroup totals (profiling build): prof[40..44] = waits for a ready
     // task, decisions, filters, tasks, workgroup lifetime (shader clock)
-    unsigned long long pw_wait = 0, pw_mb = 0, pw_filt = 0, pw_n = 0;
+    unsigned long long pw_wait = 0, pw_mb = 0, pw_filt = 0, pw_n = 0, pw_hlp = 0, pw_hn = 0;
     const unsigned long long pw_t0 = __builtin_readcyclecounter();
     unsigned long long* prof = P.fr[0].F.prof;
 #endif
@@ -415,8 +423,10 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
             if (threadIdx.x == 0) s_task = t;
         }
         __syncthreads();
-        const int t = __builtin_amdgcn_readfirstlane(s_task);
+        int t = __builtin_amdgcn_readfirstlane(s_task);
         if (t < 0) break;
+        const bool helper = t >= P.nframes * nmb;  // an intra helper task (hl_mbcore.h intra_helper)
+        if (helper) t -= P.nframes * nmb;
 #if defined(HL_DIAG) && HL_DIAG == 1
         __syncthreads();
 #endif
@@ -451,6 +461,22 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         if (threadIdx.x < 64) __builtin_amdgcn_s_sleep(20);
 #endif
         frame_args_to_lds(sF, PF.F, tid);
+        if (helper) {
+            // results, every wave's stores drained, barrier, one release, the state
+            intra_helper(sF, S, addr, tid, kMbThreads, s_in, PF.F.ispec + addr);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid < 64) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, HL_REL_SCOPE);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (tid == 0) st_relaxed(P.hstate + t, HS_DONE);
+            }
+#if defined(HL_PROFILE)
+            pw_hlp += __builtin_readcyclecounter() - pt1;
+            ++pw_hn;
+#endif
+            continue;
+        }
         encode_mb(sF, S, addr, tid, kMbThreads, s_in, gx, gy, spec_in);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -488,8 +514,11 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
                 task_succ(f, x, y, mbw, mbh, P.reach, P.nframes, j, fo, xo, yo);
                 const int a = yo * mbw + xo;
                 if (__hip_atomic_fetch_add(P.cnt + fo * nmb + a, -1, HL_CNT_ORDER, __HIP_MEMORY_SCOPE_AGENT) == 1) {
-                    const int pos = __hip_atomic_fetch_add(P.tail + fo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(P.queue + fo * nmb + pos, a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    // the macroblock, then (P pictures) its intra helper
+                    const bool hp = P.helpers && !ld_relaxed(&P.fr[fo].F.is_intra);
+                    const int pos = __hip_atomic_fetch_add(P.tail + fo, hp ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(P.queue + (size_t)fo * 2 * nmb + pos, a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    if (hp) __hip_atomic_store(P.queue + (size_t)fo * 2 * nmb + pos + 1, a + 1 + nmb, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             // pictures finish in order: the last MB depends on every other one
@@ -509,6 +538,8 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         atomicAdd(prof + 42, pw_filt);
         atomicAdd(prof + 43, pw_n);
         atomicAdd(prof + 44, __builtin_readcyclecounter() - pw_t0);
+        atomicAdd(prof + 45, pw_hlp);  // intra helper tasks: cycles, count
+        atomicAdd(prof + 46, pw_hn);
     }
 #endif
 }
@@ -559,6 +590,10 @@ struct hl_amd_encoder_s {
     MbChain *d_bchain, *h_bchain;
     int32_t *d_bspec, *d_err;
     int32_t *d_cnt, *d_done, *d_queue, *d_head;  // scheduler state (cnt: [cnt | claim], head: [head | tail | oldest])
+    int32_t* d_hstate = nullptr;                 // intra helper task states [picture][MB] (HS_*)
+    IntraSpec* d_ispec = nullptr;                // intra helper results, per MB address
+    bool helpers = true;                         // P macroblocks of pipelined runs get intra helper tasks
+    int32_t helper_kept = 0, helper_rejected = 0, helper_self = 0;  // hl_amd_last_helper_stats
     PipeFrame *d_pf, *h_pf;
     std::vector<std::vector<uint8_t>> bout;  // bitstreams of the last hl_amd_encode_batch
     int nwriters;                            // host slice writer threads of a run
@@ -614,6 +649,8 @@ static void free_all(hl_amd_encoder_t* e)
     (void)hipFree(e->d_done);
     (void)hipFree(e->d_queue);
     (void)hipFree(e->d_head);
+    (void)hipFree(e->d_hstate);
+    (void)hipFree(e->d_ispec);
     (void)hipFree(e->d_pf);
     (void)hipHostFree(e->h_brec);
     (void)hipHostFree(e->h_bchain);
@@ -691,6 +728,10 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
         e->nwriters = wt ? std::max(1, atoi(wt)) : (int)std::max(1u, std::min(16u, hc));
     }
     e->pipe_wg = 0;
+    {
+        const char* h = getenv("HL_AMD_HELPERS");  // A/B knob (hl_amd_set_intra_helpers)
+        e->helpers = !(h && atoi(h) == 0);
+    }
     e->reach = 2;
     e->window = 64;
     {
@@ -902,7 +943,14 @@ static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
     // fits in 4 GB of HBM (about 22 MB per 1088p picture, 2.8 GB at 1088p),
     // so that later, longer batches never reallocate between runs.  One
     // picture per call (the plugin path) allocates for one picture.
-    const size_t per_pic = pic + 4 * e->plsz + (sizeof(MbRecord) + sizeof(MbChain) + 3 * sizeof(int32_t)) * nmb;
+    // device copies of the records only in diagnostic builds (runs write them
+    // to pinned host memory, F.hrec)
+#if defined(HL_DIAG_INPUTS)
+    const size_t drec = sizeof(MbRecord);
+#else
+    const size_t drec = 0;
+#endif
+    const size_t per_pic = pic + 4 * e->plsz + (drec + sizeof(MbChain) + 5 * sizeof(int32_t)) * nmb;
     if (n > 1 && per_pic * kMaxRun <= (4ull << 30)) n = std::max(n, kMaxRun);
     // free and forget every run buffer first, so that a failed allocation
     // below never leaves a dangling pointer for free_all or a later retry
@@ -924,26 +972,29 @@ static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
     dfree(e->d_done);
     dfree(e->d_queue);
     dfree(e->d_head);
+    dfree(e->d_hstate);
+    dfree(e->d_ispec);
     hfree(e->h_brec);
     hfree(e->h_bchain);
     hfree(e->h_pf);
     e->bcap = 0;
     hipError_t r;
     if ((r = hipMalloc(&e->d_bpic, pic * n)) || (r = hipMalloc(&e->d_bpl, 4 * e->plsz * n)) ||
-        (r = hipMalloc(&e->d_brec, sizeof(MbRecord) * nmb * n)) || (r = hipMalloc(&e->d_bchain, sizeof(MbChain) * nmb * n)) ||
+        (drec && (r = hipMalloc(&e->d_brec, drec * nmb * n))) || (r = hipMalloc(&e->d_bchain, sizeof(MbChain) * nmb * n)) ||
         (r = hipMalloc(&e->d_bspec, sizeof(int32_t) * e->mbh * n)) || (r = hipMalloc(&e->d_pf, sizeof(PipeFrame) * n)) ||
         (r = hipHostMalloc(&e->h_brec, sizeof(MbRecord) * nmb * n, hipHostMallocDefault)) ||
         (r = hipHostMalloc(&e->h_bchain, sizeof(MbChain) * nmb * n, hipHostMallocDefault)) ||
         (r = hipHostMalloc(&e->h_pf, sizeof(PipeFrame) * n, hipHostMallocDefault)) ||
         (r = hipMalloc(&e->d_cnt, sizeof(int32_t) * 2 * nmb * n)) || (r = hipMalloc(&e->d_done, sizeof(int32_t) * nmb * n)) ||
-        (r = hipMalloc(&e->d_queue, sizeof(int32_t) * nmb * n)) || (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * n + 1))) ||
+        (r = hipMalloc(&e->d_queue, sizeof(int32_t) * 2 * nmb * n)) || (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * n + 1))) ||
+        (r = hipMalloc(&e->d_hstate, sizeof(int32_t) * nmb * n)) || (r = hipMalloc(&e->d_ispec, sizeof(IntraSpec) * nmb)) ||
         (r = hipHostGetDevicePointer((void**)&e->dh_brec, e->h_brec, 0)))
         return r;
-    if (!e->d_err && (r = hipMalloc(&e->d_err, sizeof(int32_t) * 4))) return r;
+    if (!e->d_err && (r = hipMalloc(&e->d_err, sizeof(int32_t) * 8))) return r;
     // defined contents from the start (nothing reads a run buffer before the
     // run writes it; this keeps any such read deterministic)
     if ((r = hipMemsetAsync(e->d_bpic, 0, pic * n, e->stream)) || (r = hipMemsetAsync(e->d_bpl, 0, 4 * e->plsz * n, e->stream)) ||
-        (r = hipMemsetAsync(e->d_brec, 0, sizeof(MbRecord) * nmb * n, e->stream)) ||
+        (drec && (r = hipMemsetAsync(e->d_brec, 0, drec * nmb * n, e->stream))) ||
         (r = hipMemsetAsync(e->d_bchain, 0, sizeof(MbChain) * nmb * n, e->stream)))
         return r;
     std::vector<int32_t> spec((size_t)e->mbh * n, 9);  // speculated rdo.Single_ctr at every row start
@@ -1106,7 +1157,7 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         }
         const uint8_t* plb = k == 0 ? e->d_pl[0] : e->d_bpl + 4 * e->plsz * (k - 1);
         for (int i = 0; i < 4; ++i) F.pl[i] = plb + i * e->plsz;
-        F.rec = e->d_brec + nmb * k;
+        F.rec = e->d_brec ? e->d_brec + nmb * k : nullptr;
         F.hrec = e->dh_brec + nmb * k;  // the slice writers read the records from host memory during the run
 #if defined(HL_DIAG_INPUTS)
         F.rec_dev = 1;
@@ -1122,6 +1173,10 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         F.run_chain = e->d_bchain;
         F.run_pos = k;
         F.carry_in = e->chain_end;
+        if (e->helpers && !e->run_intra[k]) {
+            F.ispec = e->d_ispec;
+            F.hstate = e->d_hstate + nmb * k;
+        }
         pf.D.W = e->W;
         pf.D.H = e->H;
         pf.D.Wc = e->Wc;
@@ -1144,6 +1199,8 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     P.claim = e->d_cnt + nmb * m;
     P.done = e->d_done;
     P.queue = e->d_queue;
+    P.hstate = e->d_hstate;
+    P.helpers = e->helpers ? 1 : 0;
     P.head = e->d_head;
     P.tail = e->d_head + m;
     P.oldest = e->d_head + 2 * m;
@@ -1189,7 +1246,7 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     // until the kernel ends, and with it the writers)
     int32_t* errw = e->h_progress + 4;
     HL_HIP_CHECK(hipMemcpyAsync(e->h_bchain, e->d_bchain, sizeof(MbChain) * nmb * m, hipMemcpyDeviceToHost, e->stream));
-    HL_HIP_CHECK(hipMemcpyAsync(errw, e->d_err, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(errw, e->d_err, 5 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
     if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[2], e->stream));
     std::atomic<bool> abort{false};
     std::vector<size_t> wsize;
@@ -1219,6 +1276,9 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     ++e->calls_runs;
     e->calls_gave_up += err;
     e->calls_walks += errw[1];
+    e->helper_kept += errw[2];
+    e->helper_rejected += errw[3];
+    e->helper_self += errw[4];
     if (err) fprintf(stderr, "hartallo_amd: pipelined run: %d bounded waits gave up; re-encoding the run picture by picture\n", err);
     int32_t carry = e->chain_end;
     bool ok = err == 0;
@@ -1319,6 +1379,7 @@ static int32_t encode_pictures(hl_amd_encoder_t* e, int n, const uint8_t* const*
     e->last_chain.assign(n, nullptr);
     e->last_pic.assign(n, nullptr);
     e->calls_runs = e->calls_per_picture = e->calls_fallbacks = e->calls_gave_up = e->calls_walks = 0;
+    e->helper_kept = e->helper_rejected = e->helper_self = 0;
     for (int i = 0; i < n;) {
         const int m = e->rc ? 1 : std::min(n - i, kMaxRun);
         const int32_t rc = encode_run(e, m, y + i, u + i, v + i, results + i, i);
@@ -1336,6 +1397,22 @@ extern "C" int32_t hl_amd_last_batch_stats(hl_amd_encoder_t* e, int32_t* out5)
     out5[2] = e->calls_fallbacks;
     out5[3] = e->calls_gave_up;
     out5[4] = e->calls_walks;
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_last_helper_stats(hl_amd_encoder_t* e, int32_t* out3)
+{
+    if (!e || !out3) return HL_AMD_ERROR_INVALID_PARAMETER;
+    out3[0] = e->helper_kept;
+    out3[1] = e->helper_rejected;
+    out3[2] = e->helper_self;
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_set_intra_helpers(hl_amd_encoder_t* e, int32_t enable)
+{
+    if (!e) return HL_AMD_ERROR_INVALID_PARAMETER;
+    e->helpers = enable != 0;
     return HL_AMD_SUCCESS;
 }
 
@@ -2298,6 +2375,10 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
         }
         if (rc != HL_AMD_SUCCESS) break;
         base_done.store(false, std::memory_order_release);
+        // a flag left set by an earlier run that fell back must not stop this
+        // chunk's thread before this chunk's run starts (encode_run clears it
+        // again, and sets it only when this run falls back)
+        e->run_aborted.store(false, std::memory_order_release);
         std::future<int32_t> el = std::async(std::launch::async, el_chunk, i0, m, true);
         rc = hl_amd_encode_batch(e, m, Y.data(), U.data(), V.data(), br.data());
         base_done.store(true, std::memory_order_release);

@@ -28,6 +28,9 @@
 //    I16x16 RDO; it is carried in Ctx::chain and recorded in MbChain so the
 //    host can validate row-start speculation.
 #pragma once
+#include <stddef.h>
+#include <string.h>
+
 #include "hl_coop.h"
 #include "hl_prims.h"
 #include "hl_quad.h"
@@ -114,6 +117,43 @@ struct alignas(16) CandSlot {
 constexpr int kWinW = 96, kWinH = 88, kWinPlane = kWinW * kWinH;
 constexpr int kNA = -1;   // not-available sample marker
 
+// The intra fallback of a P macroblock (rdo.c:1161-1167 -> rdo.c:99-299)
+// split into what only depends on the MB's source and its final neighbours
+// and what depends on the live state its inter search leaves behind (the
+// TotalCoeffs of quirk 1 and rdo.Single_ctr).  The first part -- prediction,
+// transform, quantisation, CAVLC statistics and reconstruction of every
+// Intra16x16 mode, and the whole Intra4x4 decision under a guess of the live
+// TotalCoeffs -- runs in a helper task beside the MB's inter search
+// (intra_helper; pipelined runs, hl_encoder.hip); the MB then resolves the
+// Intra16x16 modes against its live state (i16_light) and keeps the helper's
+// Intra4x4 decision if every nC class it used is the one the live state gives
+// (i4_verify), else decides Intra4x4 itself.  IntraHead is the small part the
+// MB reads first (whole 16-byte words; also the LDS image, Shared::ih).
+struct alignas(16) IntraHead {
+    int32_t blk[4][16];  // I16 mode m, block t: coded | TotalCoeff << 1 | TrailingOnes << 6 | (single + 1) << 8 | rest bits << 16
+    int32_t dcs[4][4];   // I16 mode m, DC block: bits (coeff_token included), TotalCoeff, single counter, -
+    int32_t dist[4][2];  // I16 mode m: distortion with the residual / of the prediction alone
+    int8_t i4_ncls[16];  // I4 block: nC class its mode costs used (-1: no cost used an nC)
+    int8_t i4_lwtc[16];  // I4 block: TotalCoeff its resolution wrote to the live state (-1: none)
+    int8_t i4_mode[16];  // I4 block: chosen mode
+    int32_t i4_cbp, i4_dist, i4_sct, i4_valid;  // coded blocks, distortion, last counter write (-1: none), 1 = present
+    double i4_cost;      // the Intra4x4 cost (z-order sum)
+    int32_t pad[2];
+};
+static_assert(sizeof(IntraHead) % 16 == 0, "IntraHead in whole 16-byte words");
+struct alignas(16) IntraSpec {
+    IntraHead h;
+    uint8_t rec[4][256];   // I16 mode m: reconstruction with the residual
+    uint8_t pred[4][256];  // I16 mode m: prediction
+    int16_t ac[4][16][16]; // I16 mode m: Intra16x16ACLevel per block (15 used)
+    int16_t dcl[4][16];    // I16 mode m: DC levels (scan order)
+    uint8_t i4_rec[256];   // I4: reconstruction of the chosen modes
+    int16_t i4_lv[16][16]; // I4: LumaLevel of the chosen modes
+};
+static_assert(sizeof(IntraSpec) % 16 == 0, "IntraSpec in whole 16-byte words");
+// helper task state (FrameArgs::hstate[addr])
+enum : int32_t { HS_FREE = 0, HS_CLAIMED = 1, HS_MAIN = 2, HS_DONE = 3 };
+
 struct FrameArgs {
     int32_t W, H, Wc, Hc, mbw, mbh;
     int32_t qp, qpc, is_intra, me_range;
@@ -142,6 +182,10 @@ struct FrameArgs {
     const MbChain* run_chain; // chain records of picture 0 of the run (same layout)
     int32_t run_pos;          // this picture's position in the run
     int32_t carry_in;         // exact counter value entering picture 0 of the run
+    // intra helper tasks (P pictures of pipelined runs; null otherwise): the
+    // per-address results and this picture's task states (HS_*)
+    IntraSpec* ispec;
+    int32_t* hstate;
 };
 
 struct NbInfo {
@@ -173,7 +217,7 @@ struct Shared {
     int8_t extCA[4], extCB[4];  // chroma AC nC from neighbouring MBs
     uint8_t src[256];
     uint8_t srcc[2][64];
-    uint8_t rec[256];     // current MB luma recon (intra neighbours read it)
+    alignas(16) uint8_t rec[256];// current MB luma recon (intra neighbours read it)
     int16_t top[25];      // luma row y=-1, x=-1..23 (kNA when not available)
     int16_t left[16];     // luma column x=-1
     int16_t ctop[2][9];   // chroma row y=-1, x=-1..7
@@ -209,10 +253,19 @@ struct Shared {
     int16_t best_mv[4][4][2], best_mvp[4][4][2];
     // --- intra scratch
     int32_t pred[256];
-    int32_t i16_ac[16][16], i16_dc[16], i16_dcc[16];
-    int32_t i16_called[16], i16_tc[16], i16_t1[16], i16_sctr[16], i16_bits[16], i16_dist[16];
-    int16_t i16_best_ac[16][16], i16_best_dc[16];
-    uint8_t i16_best_rec[256], tmp_rec[256];
+    int32_t i16_ac[16][16], i16_dcc[16];  // (i16_ac: scratch of the pipelined task's plane blocks)
+    int32_t i16_called[16], i16_bits[16], i16_dist[16], i16_distz[16];
+    alignas(16) int16_t i16_best_ac[16][16];
+    alignas(16) int16_t i16_best_dc[16];
+    alignas(16) uint8_t i16_best_rec[256];
+    // Intra16x16 statistics of every mode and the Intra4x4 verification record
+    // (IntraHead: computed here by i16_heavy / guess_i4, or imported from the
+    // MB's intra helper task), and the modes' bulk results (i16_heavy)
+    IntraHead ih;
+    alignas(16) uint8_t ih_rec[4][256];
+    alignas(16) uint8_t ih_pred[4][256];
+    alignas(16) int16_t ih_ac[4][16][16];
+    alignas(16) int16_t ih_dcl[4][16];
     // I4x4 trials of up to two blocks at once [wavefront slot][mode] (device) / [0][mode] (host)
     int32_t i4_cost_ok[2][9], i4_exact[2][9], i4_nz[2][9], i4_tc[2][9], i4_sctr[2][9], i4_dist[2][9];
     double i4_cost[2][9];
@@ -223,9 +276,8 @@ struct Shared {
     int32_t luma_level[16][16];
     int16_t i4nb[2][16];         // neighbours of the current 4x4 blocks (p[13] layout)
     int32_t dcY[16];             // I16x16: scaled DC per DC-matrix position
-    int16_t i16_dcl[16];         // I16x16: DC levels of the current mode (scan order)
-    int32_t dcrow[4];            // I16x16: DC block rate, TotalCoeff, single counter
     int32_t chain_x;             // resolve_chain result
+    int32_t hs_x;                // intra helper state seen by the MB (HS_*)
     int32_t homo[4];             // early termination: homogeneity of the four 8x8 source quadrants
     int32_t predc[2][64];
     int32_t cres_dc[2][4], cres_cac[2][4], cres_cdc[2][4], cres_tc[2][4], cres_sctr[2][4];
@@ -2342,62 +2394,211 @@ HD void resolve_chain(Ctx& c)
 #endif
 }
 
-HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp, int& best_dist)
+// Intra16x16 modes the neighbourhood allows (rdo.c:1541-1560), uniform
+HD bool i16_mode_avail(const Shared& S, int mode)
 {
-    best_dist = 0;
+    if (mode == 0) return uni((int)S.top[1]) != kNA;
+    if (mode == 1) return uni((int)S.left[0]) != kNA;
+    if (mode == 3) return uni((int)S.top[0]) != kNA;
+    return true;
+}
+HD int nc_class(int nC) { return nC < 2 ? 0 : (nC < 4 ? 1 : (nC < 8 ? 2 : 3)); }  // the coeff_token table nC selects
+
+// Intra16x16, the part of every mode that depends only on the MB's source and
+// its final neighbours (rdo.c:1526-1700): prediction, transform,
+// quantisation and CAVLC statistics of each 4x4 block and of the DC block,
+// the reconstruction with the residual and the distortions with and without
+// it.  Into S.ih (blk, dcs, dist) and S.ih_rec / ih_pred / ih_ac / ih_dcl.
+HD void i16_heavy(Ctx& c)
+{
     const FrameArgs& F = c.F;
     Shared& S = c.S;
-    best_cost = 1.7976931348623157e308;
-    best_cbp = 0;
-    if (c.tid == 0) {
-        S.e_type = ET_I16;
-        S.flags = FL_INTRA;
-        S.pm0 = PM_I16;
-        S.i16mode = 2;
-    }
 #if defined(__HIP_DEVICE_COMPILE__)
     // one 16-lane row per 4x4 block (rows 0-15), modes in order
     const int row = c.tid >> 4;
     const int qbits = 15 + F.qp / 6, fq = (1 << qbits) / 3;
     const int x = blk_x(row & 15) + (c.K.p & 3), y = blk_y(row & 15) + (c.K.p >> 2);
     for (int mode = 0; mode < 4; ++mode) {
-        if (mode == 0 && uni(S.top[1]) == kNA) continue;
-        if (mode == 1 && uni(S.left[0]) == kNA) continue;
-        if (mode == 3 && uni(S.top[0]) == kNA) continue;
+        if (!i16_mode_avail(S, mode)) continue;
         int dcv, pa, pb, pc;
         i16_params(S, mode, dcv, pa, pb, pc);
         dcv = uni(dcv);
         pa = uni(pa);
         pb = uni(pb);
         pc = uni(pc);
-        int pred = 0, sv = 0;
+        int pred = 0, sv = 0, q = 0;
         if (row < 16) {  // blocks: transform, quant, AC statistics
-            const int t = row;
             pred = i16_pred(S, mode, x, y, dcv, pa, pb, pc);
             sv = S.src[y * 16 + x];
             const int w = coop_fwd(c.K, sv - pred);
-            const int q = coop_quant(w, c.K.mf, qbits, fq);
+            q = coop_quant(w, c.K.mf, qbits, fq);
             const bool qz = row_or(q != 0) == 0;
             const CoopStat st = coop_cavlc(S.ct, q, c.K.s - 1, S.lvs[row]);
-            S.i16_ac[t][c.K.s == 0 ? 15 : c.K.s - 1] = c.K.s == 0 ? 0 : q;
+            S.ih_ac[mode][row][c.K.s == 0 ? 15 : c.K.s - 1] = (int16_t)(c.K.s == 0 ? 0 : q);
+            S.ih_pred[mode][y * 16 + x] = (uint8_t)pred;
             if (c.K.p == 0) {
-                S.i16_dcc[t] = w;
-                S.i16_called[t] = !qz;
-                S.i16_tc[t] = st.tc;
-                S.i16_t1[t] = st.t1;
-                S.i16_sctr[t] = st.sctr;
-                S.i16_bits[t] = st.rest;
+                S.i16_dcc[row] = w;
+                S.ih.blk[mode][row] = (qz ? 0 : 1) | (st.tc << 1) | (st.t1 << 6) | ((st.sctr + 1) << 8) | (st.rest << 16);
             }
         }
         HL_SYNC();
-        // nC of the AC writes: inside the MB, blocks written earlier in this
-        // mode show their own TotalCoeff (even 0), others the live state
+        if (c.tid < 16) {  // the DC block: Hadamard, quant, CAVLC, scaling
+            const int hh = coop_lin(c.K.had, S.i16_dcc[kDcPos[c.K.p]]) >> 1;
+            const int qd = quant_dc(F.qp, true, hh);
+            const CoopStat st = coop_cavlc(S.ct, qd, c.K.s, S.lvs[0]);
+            S.ih_dcl[mode][c.K.s] = (int16_t)qd;
+            const int f = coop_lin(c.K.had, qd);
+            const int scale = level_scale(F.qp % 6, 0, 0), q6 = F.qp / 6;
+            S.dcY[c.K.p] = F.qp >= 36 ? (f * scale) << (q6 - 6) : (f * scale + (1 << (5 - q6))) >> (6 - q6);
+            if (c.tid == 0) {  // block 0's nC neighbours lie outside the MB: the DC rate is fixed
+                const int nC = nc_luma_of(S, 0, [&](int ni) -> int { return S.tc[ni]; });
+                S.ih.dcs[mode][0] = st.rest + coop_token_len(S.ct, nC, st.tc, st.t1);
+                S.ih.dcs[mode][1] = st.tc;
+                S.ih.dcs[mode][2] = st.sctr;
+                S.ih.dcs[mode][3] = 0;
+            }
+        }
+        HL_SYNC();
+        if (row < 16) {  // reconstruction with the residual; both distortions
+            const int r = coop_idct(c.K, c.K.p == 0 ? S.dcY[kDcPos[row]] : coop_dequant(q, c.K.ls, F.qp));
+            const int rec = clip255(pred + r);
+            S.ih_rec[mode][y * 16 + x] = (uint8_t)rec;
+            const int df = row_sum(iabs(sv - rec)), dz = row_sum(iabs(sv - pred));
+            if (c.K.p == 0) {
+                S.i16_dist[row] = df;
+                S.i16_distz[row] = dz;
+            }
+        }
+        HL_SYNC();
+        if (c.tid < 32) {
+            const int v = row_sum(c.tid < 16 ? S.i16_dist[c.tid] : S.i16_distz[c.tid & 15]);
+            if ((c.tid & 15) == 0) S.ih.dist[mode][c.tid >> 4] = v;
+        }
+    }
+    HL_SYNC();
+#else
+    for (int mode = 0; mode < 4; ++mode) {
+        if (!i16_mode_avail(S, mode)) continue;
+        int dcv, pa, pb, pc;
+        i16_params(S, mode, dcv, pa, pb, pc);
+        for (int t = 0; t < 256; ++t) S.ih_pred[mode][t] = (uint8_t)i16_pred(S, mode, t & 15, t >> 4, dcv, pa, pb, pc);
+        int dcc[16];
+        for (int t = 0; t < 16; ++t) {  // blocks: transform, quant, AC statistics
+            const int xO = blk_x(t), yO = blk_y(t);
+            int res[16], w[16], q[16];
+            for (int i = 0; i < 16; ++i) {
+                const int o = (yO + (i >> 2)) * 16 + xO + (i & 3);
+                res[i] = (int)S.src[o] - S.ih_pred[mode][o];
+            }
+            fwd4x4(res, w);
+            quant4x4(F.qp, true, w, q);
+            bool qz = true;
+            for (int i = 0; i < 16; ++i) qz = qz && q[i] == 0;
+            for (int i = 1; i < 16; ++i) S.ih_ac[mode][t][i - 1] = (int16_t)q[kZigzag[i]];
+            S.ih_ac[mode][t][15] = 0;
+            dcc[t] = w[0];
+            CavlcStat st = {0, 0, 0, -1};
+            if (!qz) st = cavlc_stat(S.ih_ac[mode][t], 16, 15, false);
+            S.ih.blk[mode][t] = (qz ? 0 : 1) | (st.tc << 1) | (st.t1 << 6) | ((st.sctr + 1) << 8) | (st.rest << 16);
+        }
+        // the DC block: Hadamard, quant, CAVLC (block 0's nC neighbours lie outside the MB)
+        int h[16], hh[16], qd[16], dcl[16];
+        for (int b = 0; b < 16; ++b) h[kDcPos[b]] = dcc[b];
+        hadamard4x4_fwd(h, hh);
+        for (int i = 0; i < 16; ++i) qd[i] = quant_dc(F.qp, true, hh[i]);
+        for (int i = 0; i < 16; ++i) dcl[i] = qd[kZigzag[i]];
+        const CavlcStat st = cavlc_stat(dcl, 16, 15, false);
+        const int nC = nc_luma_of(S, 0, [&](int ni) -> int { return S.tc[ni]; });
+        S.ih.dcs[mode][0] = st.rest + token_len(nC, st.tc, st.t1);
+        S.ih.dcs[mode][1] = st.tc;
+        S.ih.dcs[mode][2] = st.sctr;
+        S.ih.dcs[mode][3] = 0;
+        for (int i = 0; i < 16; ++i) S.ih_dcl[mode][i] = (int16_t)dcl[i];
+        // scale DC (8.5.10), then the inverse of every block with it
+        int cm[16], dcY[16];
+        unscan(dcl, cm);
+        {
+            int d[16], f[16];
+            for (int j = 0; j < 4; ++j) {
+                d[0 * 4 + j] = cm[0 * 4 + j] + cm[1 * 4 + j] + cm[2 * 4 + j] + cm[3 * 4 + j];
+                d[1 * 4 + j] = cm[0 * 4 + j] + cm[1 * 4 + j] - cm[2 * 4 + j] - cm[3 * 4 + j];
+                d[2 * 4 + j] = cm[0 * 4 + j] - cm[1 * 4 + j] - cm[2 * 4 + j] + cm[3 * 4 + j];
+                d[3 * 4 + j] = cm[0 * 4 + j] - cm[1 * 4 + j] + cm[2 * 4 + j] - cm[3 * 4 + j];
+            }
+            for (int i = 0; i < 4; ++i) {
+                f[i * 4 + 0] = d[i * 4 + 0] + d[i * 4 + 1] + d[i * 4 + 2] + d[i * 4 + 3];
+                f[i * 4 + 1] = d[i * 4 + 0] + d[i * 4 + 1] - d[i * 4 + 2] - d[i * 4 + 3];
+                f[i * 4 + 2] = d[i * 4 + 0] - d[i * 4 + 1] - d[i * 4 + 2] + d[i * 4 + 3];
+                f[i * 4 + 3] = d[i * 4 + 0] - d[i * 4 + 1] + d[i * 4 + 2] - d[i * 4 + 3];
+            }
+            const int scale = level_scale(F.qp % 6, 0, 0), q6 = F.qp / 6;
+            for (int i = 0; i < 16; ++i) dcY[i] = F.qp >= 36 ? (f[i] * scale) << (q6 - 6) : (f[i] * scale + (1 << (5 - q6))) >> (6 - q6);
+        }
+        int df = 0, dz = 0;
+        for (int t = 0; t < 16; ++t) {
+            const int xO = blk_x(t), yO = blk_y(t);
+            int list[16], m[16], r[16];
+            list[0] = dcY[kDcPos[t]];
+            bool nzl = list[0] != 0;
+            for (int i = 1; i < 16; ++i) {
+                list[i] = S.ih_ac[mode][t][i - 1];
+                nzl = nzl || list[i] != 0;
+            }
+            if (nzl) {
+                unscan(list, m);
+                dequant_idct(F.qp, m, true, r);
+            }
+            for (int i = 0; i < 16; ++i) {
+                const int o = (yO + (i >> 2)) * 16 + xO + (i & 3);
+                const int p = S.ih_pred[mode][o];
+                const int v = nzl ? clip255(p + r[i]) : p;
+                S.ih_rec[mode][o] = (uint8_t)v;
+                df += iabs((int)S.src[o] - v);
+                dz += iabs((int)S.src[o] - p);
+            }
+        }
+        S.ih.dist[mode][0] = df;
+        S.ih.dist[mode][1] = dz;
+    }
+#endif
+}
+
+// Intra16x16, the part that depends on the live state (rdo.c:1700-1809), from
+// the modes' statistics in S.ih, modes in order: each mode's coded blocks
+// rewrite the live TotalCoeffs (quirk 1) and read or write rdo.Single_ctr, its
+// DC block writes both.  spec: the intra helper's guess of the live state
+// (no row-start validation of the counter).  Returns the best mode's cost,
+// coded-block mask, distortion and index.
+HD void i16_light(Ctx& c, double& best_cost, int& best_cbp, int& best_dist, int& best_mode, bool spec)
+{
+    const FrameArgs& F = c.F;
+    Shared& S = c.S;
+    best_dist = 0;
+    best_cost = 1.7976931348623157e308;
+    best_cbp = 0;
+    best_mode = 2;
+    if (c.tid == 0) {
+        S.e_type = ET_I16;
+        S.flags = FL_INTRA;
+        S.pm0 = PM_I16;
+        S.i16mode = 2;
+    }
+    for (int mode = 0; mode < 4; ++mode) {
+        if (!i16_mode_avail(S, mode)) continue;
+        int single, bcbp, rate;
+#if defined(__HIP_DEVICE_COMPILE__)
+        // nC of the coded blocks' AC writes: inside the MB, blocks coded
+        // earlier in this mode show their own TotalCoeff (even 0), others the
+        // live state
         if (c.tid < 16) {
-            const int t = c.tid;
-            if (S.i16_called[t]) {
-                const int nC = nc_luma_of(S, t, [&](int ni) -> int { return S.i16_called[ni] ? S.i16_tc[ni] : S.tc[ni]; });
-                S.i16_bits[t] += coop_token_len(S.ct, nC, S.i16_tc[t], S.i16_t1[t]);
-                S.tc[t] = (int8_t)S.i16_tc[t];
+            const int t = c.tid, w = S.ih.blk[mode][t];
+            if (w & 1) {
+                const int nC = nc_luma_of(S, t, [&](int ni) -> int {
+                    const int wn = S.ih.blk[mode][ni];
+                    return (wn & 1) ? (wn >> 1) & 31 : S.tc[ni];
+                });
+                S.i16_bits[t] = (w >> 16) + coop_token_len(S.ct, nC, (w >> 1) & 31, (w >> 6) & 3);
+                S.tc[t] = (int8_t)((w >> 1) & 31);
             }
         }
         HL_SYNC();
@@ -2406,13 +2607,13 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp, int& best_dist)
         // block b is the counter of the last coding block at or before b
         // (the entry value if none); a block without coefficients before the
         // first writer reads the entry value stale.
-        int single, bcbp, rate;
         {
             const int l = c.tid & 15;
-            const int called = S.i16_called[l], tcb = S.i16_tc[l], sct = S.i16_sctr[l], bits = S.i16_bits[l];
+            const int w = S.ih.blk[mode][l];
+            const int called = w & 1, tcb = (w >> 1) & 31, sct = ((w >> 8) & 255) - 1, bits = S.i16_bits[l];
             const unsigned bc = (unsigned)__ballot(called != 0) & 0xFFFFu, bw = (unsigned)__ballot(called && tcb > 0) & 0xFFFFu;
             const unsigned before = bw ? (bw & (0u - bw)) - 1u : 0xFFFFu;  // blocks before the first writer
-            if ((bc & ~bw & before) && !c.fresh) {
+            if (!spec && (bc & ~bw & before) && !c.fresh) {
                 // pipelined run: a speculated value is resolved here; once it
                 // is exact (resolved in this MB or to its left) the read is
                 // exact too.  The per-picture path records the stale read for
@@ -2429,199 +2630,90 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp, int& best_dist)
             bcbp = (int)bc;
             if (bw) chain_write(c, __builtin_amdgcn_readlane(sct, 31 - __clz(bw)));
         }
-        if (bcbp && single < 6) bcbp = 0;
-        if (bcbp) {
-            if (c.tid < 16) {  // the DC block: Hadamard, quant, CAVLC, inverse
-                const int hh = coop_lin(c.K.had, S.i16_dcc[kDcPos[c.K.p]]) >> 1;
-                const int qd = quant_dc(F.qp, true, hh);
-                const CoopStat st = coop_cavlc(S.ct, qd, c.K.s, S.lvs[0]);
-                S.i16_dcl[c.K.s] = (int16_t)qd;
-                const int f = coop_lin(c.K.had, qd);
-                const int scale = level_scale(F.qp % 6, 0, 0), q6 = F.qp / 6;
-                S.dcY[c.K.p] = F.qp >= 36 ? (f * scale) << (q6 - 6) : (f * scale + (1 << (5 - q6))) >> (6 - q6);
-                if (c.tid == 0) {
-                    const int nC = nc_luma_of(S, 0, [&](int ni) -> int { return S.tc[ni]; });
-                    S.dcrow[0] = st.rest + coop_token_len(S.ct, nC, st.tc, st.t1);
-                    S.dcrow[1] = st.tc;
-                    S.dcrow[2] = st.sctr;
-                    S.tc[0] = (int8_t)st.tc;
-                }
-            }
-            HL_SYNC();
-            rate += uni(S.dcrow[0]);
-            if (uni(S.dcrow[1]) > 0) chain_write(c, uni(S.dcrow[2]));
-        }
-        if (row < 16) {  // reconstruction and distortion of each block
-            const int t = row;
-            const int cv = !bcbp ? 0 : (c.K.p == 0 ? S.dcY[kDcPos[t]] : S.i16_ac[t][c.K.s - 1]);
-            const int r = coop_idct(c.K, c.K.p == 0 ? cv : coop_dequant(cv, c.K.ls, F.qp));
-            const int rec = clip255(pred + r);
-            S.tmp_rec[y * 16 + x] = (uint8_t)rec;
-            const int d = row_sum(iabs(sv - rec));
-            if (c.K.p == 0) S.i16_dist[t] = d;
-        }
-        HL_SYNC();
-        const int dist = uni(row_sum(S.i16_dist[c.tid & 15]));
-        const double cost = dadd((double)dist, dmul(F.lambda, (double)rate));
-        if (cost < best_cost) {
-            best_cost = cost;
-            best_dist = dist;
-            best_cbp = bcbp;
-            if (c.tid == 0) S.i16mode = mode;
-            if (c.tid < 16) S.i16_best_dc[c.tid] = bcbp ? S.i16_dcl[c.tid] : 0;
-            for (int t = c.tid; t < 256; t += c.nthr) {
-                S.i16_best_ac[t >> 4][t & 15] = (int16_t)S.i16_ac[t >> 4][t & 15];
-                S.i16_best_rec[t] = S.tmp_rec[t];
-            }
-        }
-        HL_SYNC();
-    }
 #else
-    for (int mode = 0; mode < 4; ++mode) {
-        if (mode == 0 && S.top[1] == kNA) continue;
-        if (mode == 1 && S.left[0] == kNA) continue;
-        if (mode == 3 && S.top[0] == kNA) continue;
-        int dcv, pa, pb, pc;
-        i16_params(S, mode, dcv, pa, pb, pc);
-        HL_SYNC();
-        for (int t = c.tid; t < 256; t += c.nthr) S.pred[t] = i16_pred(S, mode, t & 15, t >> 4, dcv, pa, pb, pc);
-        HL_SYNC();
-        // blocks: transform, quant, AC stats
-        for (int t = c.tid; t < 16; t += c.nthr) {
-            const int xO = blk_x(t), yO = blk_y(t);
-            int res[16], w[16], q[16];
-            for (int i = 0; i < 16; ++i) {
-                const int o = (yO + (i >> 2)) * 16 + xO + (i & 3);
-                res[i] = (int)S.src[o] - S.pred[o];
-            }
-            fwd4x4(res, w);
-            quant4x4(F.qp, true, w, q);
-            bool qz = true;
-            for (int i = 0; i < 16; ++i) qz = qz && q[i] == 0;
-            for (int i = 1; i < 16; ++i) S.i16_ac[t][i - 1] = q[kZigzag[i]];
-            S.i16_ac[t][15] = 0;
-            S.i16_dcc[t] = w[0];
-            S.i16_called[t] = !qz;
-            CavlcStat st = {0, 0, 0, -1};
-            if (!qz) st = cavlc_stat(S.i16_ac[t], 16, 15, false);
-            S.i16_tc[t] = st.tc;
-            S.i16_t1[t] = st.t1;
-            S.i16_sctr[t] = st.sctr;
-            S.i16_bits[t] = st.rest;
+        int bits[16];
+        for (int t = 0; t < 16; ++t) {
+            const int w = S.ih.blk[mode][t];
+            if (!(w & 1)) continue;
+            const int nC = nc_luma_of(S, t, [&](int ni) -> int {
+                const int wn = S.ih.blk[mode][ni];
+                return (wn & 1) ? (wn >> 1) & 31 : S.tc[ni];
+            });
+            bits[t] = (w >> 16) + token_len(nC, (w >> 1) & 31, (w >> 6) & 3);
         }
-        HL_SYNC();
-        // nC of the AC writes: inside the MB, blocks written earlier in this
-        // mode show their own TotalCoeff (even 0), others the live state
-        for (int t = c.tid; t < 16; t += c.nthr) {
-            if (!S.i16_called[t]) continue;
-            const int nC = nc_luma_of(S, t, [&](int ni) -> int { return S.i16_called[ni] ? S.i16_tc[ni] : S.tc[ni]; });
-            S.i16_bits[t] += token_len(nC, S.i16_tc[t], S.i16_t1[t]);
-        }
-        HL_SYNC();
-        // uniform: single counter with stale reads, cbp, rate
-        int single = 0, bcbp = 0, rate = 0;
+        single = bcbp = rate = 0;
         for (int b = 0; b < 16; ++b) {
-            if (!S.i16_called[b]) continue;
-            rate += S.i16_bits[b];
+            const int w = S.ih.blk[mode][b];
+            if (!(w & 1)) continue;
+            rate += bits[b];
             bcbp |= 1 << b;
-            if (S.i16_tc[b] > 0) chain_write(c, S.i16_sctr[b]);
-            else if (!c.fresh) c.dep = 1;
+            if (((w >> 1) & 31) > 0) chain_write(c, ((w >> 8) & 255) - 1);
+            else if (!spec && !c.fresh) c.dep = 1;
             single += c.chain;
         }
-        for (int t = c.tid; t < 16; t += c.nthr)
-            if (S.i16_called[t]) S.tc[t] = (int8_t)S.i16_tc[t];
+        for (int t = 0; t < 16; ++t)
+            if (S.ih.blk[mode][t] & 1) S.tc[t] = (int8_t)((S.ih.blk[mode][t] >> 1) & 31);
+#endif
         if (bcbp && single < 6) bcbp = 0;
-        int dist = 0;
-        int dcl[16];
-        if (bcbp) {
-            int h[16], qd[16];
-            for (int b = 0; b < 16; ++b) h[kDcPos[b]] = S.i16_dcc[b];
-            int hh[16];
-            hadamard4x4_fwd(h, hh);
-            for (int i = 0; i < 16; ++i) qd[i] = quant_dc(F.qp, true, hh[i]);
-            for (int i = 0; i < 16; ++i) dcl[i] = qd[kZigzag[i]];
-            const CavlcStat st = cavlc_stat(dcl, 16, 15, false);
-            const int nC = nc_luma_of(S, 0, [&](int ni) -> int { return S.tc[ni]; });
-            rate += st.rest + token_len(nC, st.tc, st.t1);
-            if (st.tc > 0) chain_write(c, st.sctr);
-            HL_SYNC();
-            if (c.tid == 0) S.tc[0] = (int8_t)st.tc;
-            // scale DC (8.5.10) then per block inverse
-            int cm[16], dcY[16];
-            unscan(dcl, cm);
-            {
-                int d[16], f[16];
-                for (int j = 0; j < 4; ++j) {
-                    d[0 * 4 + j] = cm[0 * 4 + j] + cm[1 * 4 + j] + cm[2 * 4 + j] + cm[3 * 4 + j];
-                    d[1 * 4 + j] = cm[0 * 4 + j] + cm[1 * 4 + j] - cm[2 * 4 + j] - cm[3 * 4 + j];
-                    d[2 * 4 + j] = cm[0 * 4 + j] - cm[1 * 4 + j] - cm[2 * 4 + j] + cm[3 * 4 + j];
-                    d[3 * 4 + j] = cm[0 * 4 + j] - cm[1 * 4 + j] + cm[2 * 4 + j] - cm[3 * 4 + j];
-                }
-                for (int i = 0; i < 4; ++i) {
-                    f[i * 4 + 0] = d[i * 4 + 0] + d[i * 4 + 1] + d[i * 4 + 2] + d[i * 4 + 3];
-                    f[i * 4 + 1] = d[i * 4 + 0] + d[i * 4 + 1] - d[i * 4 + 2] - d[i * 4 + 3];
-                    f[i * 4 + 2] = d[i * 4 + 0] - d[i * 4 + 1] - d[i * 4 + 2] + d[i * 4 + 3];
-                    f[i * 4 + 3] = d[i * 4 + 0] - d[i * 4 + 1] + d[i * 4 + 2] - d[i * 4 + 3];
-                }
-                const int scale = level_scale(F.qp % 6, 0, 0), q6 = F.qp / 6;
-                for (int i = 0; i < 16; ++i)
-                    dcY[i] = F.qp >= 36 ? (f[i] * scale) << (q6 - 6) : (f[i] * scale + (1 << (5 - q6))) >> (6 - q6);
-            }
-            for (int t = c.tid; t < 16; t += c.nthr) {
-                const int xO = blk_x(t), yO = blk_y(t);
-                int list[16], m[16], r[16];
-                list[0] = dcY[kDcPos[t]];
-                bool nzl = list[0] != 0;
-                for (int i = 1; i < 16; ++i) {
-                    list[i] = S.i16_ac[t][i - 1];
-                    nzl = nzl || list[i] != 0;
-                }
-                if (nzl) {
-                    unscan(list, m);
-                    dequant_idct(F.qp, m, true, r);
-                }
-                int d = 0;
-                for (int i = 0; i < 16; ++i) {
-                    const int o = (yO + (i >> 2)) * 16 + xO + (i & 3);
-                    const int v = nzl ? clip255(S.pred[o] + r[i]) : S.pred[o];
-                    S.tmp_rec[o] = (uint8_t)v;
-                    d += iabs((int)S.src[o] - v);
-                }
-                S.i16_dist[t] = d;
-            }
+        if (bcbp) {  // the DC block
+            rate += uni(S.ih.dcs[mode][0]);
+            if (uni(S.ih.dcs[mode][1]) > 0) chain_write(c, uni(S.ih.dcs[mode][2]));
+            if (c.tid == 0) S.tc[0] = (int8_t)S.ih.dcs[mode][1];
         }
-        else {
-            for (int i = 0; i < 16; ++i) dcl[i] = 0;
-            for (int t = c.tid; t < 16; t += c.nthr) {
-                const int xO = blk_x(t), yO = blk_y(t);
-                int d = 0;
-                for (int i = 0; i < 16; ++i) {
-                    const int o = (yO + (i >> 2)) * 16 + xO + (i & 3);
-                    S.tmp_rec[o] = (uint8_t)S.pred[o];
-                    d += iabs((int)S.src[o] - S.pred[o]);
-                }
-                S.i16_dist[t] = d;
-            }
-        }
-        HL_SYNC();
-        for (int b = 0; b < 16; ++b) dist += S.i16_dist[b];
+        const int dist = uni(S.ih.dist[mode][bcbp ? 0 : 1]);
         const double cost = dadd((double)dist, dmul(F.lambda, (double)rate));
         if (cost < best_cost) {
             best_cost = cost;
             best_dist = dist;
             best_cbp = bcbp;
-            if (c.tid == 0) {
-                S.i16mode = mode;
-                for (int i = 0; i < 16; ++i) S.i16_best_dc[i] = (int16_t)dcl[i];
-            }
-            for (int t = c.tid; t < 256; t += c.nthr) {
-                S.i16_best_ac[t >> 4][t & 15] = (int16_t)S.i16_ac[t >> 4][t & 15];
-                S.i16_best_rec[t] = S.tmp_rec[t];
-            }
+            best_mode = mode;
+            if (c.tid == 0) S.i16mode = mode;
         }
         HL_SYNC();
     }
+}
+
+// The chosen Intra16x16 mode's levels and reconstruction into S.i16_best_*:
+// from this MB's own i16_heavy results in LDS, or from its intra helper's in
+// global memory (hin)
+HD void i16_copy_best(Ctx& c, int mode, bool coded, const IntraSpec* hin)
+{
+    Shared& S = c.S;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int t = c.tid;
+    if (hin) {
+        if (t < 16) reinterpret_cast<uint4*>(S.i16_best_rec)[t] = gmem(reinterpret_cast<const uint4*>(coded ? hin->rec[mode] : hin->pred[mode]))[t];
+        else if (t < 48) reinterpret_cast<uint4*>(&S.i16_best_ac[0][0])[t - 16] = gmem(reinterpret_cast<const uint4*>(&hin->ac[mode][0][0]))[t - 16];
+        else if (t < 50) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (coded) v = gmem(reinterpret_cast<const uint4*>(hin->dcl[mode]))[t - 48];
+            reinterpret_cast<uint4*>(S.i16_best_dc)[t - 48] = v;
+        }
+    }
+    else {
+        if (t < 16) reinterpret_cast<uint4*>(S.i16_best_rec)[t] = reinterpret_cast<const uint4*>(coded ? S.ih_rec[mode] : S.ih_pred[mode])[t];
+        else if (t < 48) reinterpret_cast<uint4*>(&S.i16_best_ac[0][0])[t - 16] = reinterpret_cast<const uint4*>(&S.ih_ac[mode][0][0])[t - 16];
+        else if (t < 50) reinterpret_cast<uint4*>(S.i16_best_dc)[t - 48] = coded ? reinterpret_cast<const uint4*>(S.ih_dcl[mode])[t - 48] : make_uint4(0, 0, 0, 0);
+    }
+    HL_SYNC();
+#else
+    const uint8_t* rec = hin ? (coded ? hin->rec[mode] : hin->pred[mode]) : (coded ? S.ih_rec[mode] : S.ih_pred[mode]);
+    const int16_t* ac = hin ? &hin->ac[mode][0][0] : &S.ih_ac[mode][0][0];
+    const int16_t* dcl = hin ? hin->dcl[mode] : S.ih_dcl[mode];
+    for (int t = 0; t < 256; ++t) {
+        S.i16_best_rec[t] = rec[t];
+        S.i16_best_ac[t >> 4][t & 15] = ac[t];
+    }
+    for (int i = 0; i < 16; ++i) S.i16_best_dc[i] = coded ? dcl[i] : 0;
 #endif
+}
+
+HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp, int& best_dist)
+{
+    i16_heavy(c);
+    int bm;
+    i16_light(c, best_cost, best_cbp, best_dist, bm, false);
+    i16_copy_best(c, bm, best_cbp != 0, nullptr);
 }
 
 // --------------------------------------------------------------------------
@@ -2769,6 +2861,10 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
                     S.i4r_zero[blk] = best_zero;
                     S.i4mode[blk] = (int8_t)best;
                     if (lastw >= 0) S.tc[blk] = (int8_t)S.i4_tc[k][lastw];
+                    // the verification record (i4_verify): the costs used an nC
+                    // only without an exact mode and with a coded one
+                    S.ih.i4_ncls[blk] = (int8_t)(!E && W ? nc_class(k ? nC1 : nC0) : -1);
+                    S.ih.i4_lwtc[blk] = (int8_t)(lastw >= 0 ? S.i4_tc[k][lastw] : -1);
                 }
             }
             if (c.tid < 16 * nslot) {
@@ -2783,14 +2879,25 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
         HL_PROF_ADD(c, 15, ti3);  // resolution + barrier
 #endif
     }
+    int last_sct = -1;
     for (int blk = 0; blk < 16; ++blk) {  // z-order: cost sum, distortion, CBP, counter writes
         best_cost = dadd(best_cost, uni(S.i4r_dmin[blk]));
         best_dist += uni(S.i4r_dist[blk]);
         if (!uni(S.i4r_zero[blk])) cbp4 |= 1 << blk;
         const int sct = uni(S.i4r_sct[blk]);
-        if (sct >= 0) chain_write(c, sct);
+        if (sct >= 0) {
+            chain_write(c, sct);
+            last_sct = sct;
+        }
+    }
+    if (c.tid == 0) {
+        S.ih.i4_cbp = cbp4;
+        S.ih.i4_dist = best_dist;
+        S.ih.i4_sct = last_sct;
+        S.ih.i4_cost = best_cost;
     }
 #else
+    S.ih.i4_sct = -1;
     for (int blk = 0; blk < 16; ++blk) {
         const int xO = blk_x(blk), yO = blk_y(blk);
         int p[13];
@@ -2858,13 +2965,14 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
         // uniform resolution in mode order (rdo.c:1931-2014)
         double dmin = 1.7976931348623157e308;
         int best = 2, lastw = -1;
-        bool best_zero = false;
+        bool best_zero = false, exact = false;
         for (int m = 0; m < 9; ++m) {
             if (!S.i4_cost_ok[0][m]) continue;
             if (S.i4_exact[0][m]) {
                 dmin = 0.0;
                 best = m;
                 best_zero = true;
+                exact = true;
                 break;
             }
             if (S.i4_nz[0][m]) lastw = m;
@@ -2874,7 +2982,14 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
                 best_zero = !S.i4_nz[0][m];
             }
         }
-        if (lastw >= 0) chain_write(c, S.i4_sctr[0][lastw]);
+        // the verification record (i4_verify): the costs used an nC only
+        // without an exact mode and with a coded one
+        S.ih.i4_ncls[blk] = (int8_t)(!exact && lastw >= 0 ? nc_class(nC) : -1);
+        S.ih.i4_lwtc[blk] = (int8_t)(lastw >= 0 ? S.i4_tc[0][lastw] : -1);
+        if (lastw >= 0) {
+            chain_write(c, S.i4_sctr[0][lastw]);
+            S.ih.i4_sct = S.i4_sctr[0][lastw];
+        }
         best_cost = dadd(best_cost, dmin);
         best_dist += S.i4_dist[0][best];
         if (!best_zero) cbp4 |= 1 << blk;
@@ -2888,6 +3003,9 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
         }
         HL_SYNC();
     }
+    S.ih.i4_cbp = cbp4;
+    S.ih.i4_dist = best_dist;
+    S.ih.i4_cost = best_cost;
 #endif
 }
 
@@ -2930,20 +3048,114 @@ HD void pred_modes_4x4(Shared& S)  // pred_intra.c:541-615 (lane 0)
     }
 }
 
+// Intra4x4 decided by the intra helper under its guess of the live
+// TotalCoeffs (S.ih, imported): every block whose mode costs used an nC must
+// see the same nC class in the live state the MB left after its Intra16x16
+// trials (S.tc).  Inside the MB a neighbour's TotalCoeff is the one its own
+// resolution wrote, if any; by induction over the blocks' order every block
+// then saw the same neighbours and costs.  Uniform.
+HD bool i4_verify(Ctx& c)
+{
+    Shared& S = c.S;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int b = c.tid & 15, want = S.ih.i4_ncls[b];
+    bool ok = true;
+    if (want >= 0) {
+        const int nC = nc_luma_of(S, b, [&](int ni) -> int {
+            const int lw = S.ih.i4_lwtc[ni];
+            return lw >= 0 ? lw : S.tc[ni];
+        });
+        ok = nc_class(nC) == want;
+    }
+    return (__ballot(!ok) & 0xFFFFull) == 0;
+#else
+    for (int b = 0; b < 16; ++b) {
+        const int want = S.ih.i4_ncls[b];
+        if (want < 0) continue;
+        const int nC = nc_luma_of(S, b, [&](int ni) -> int {
+            const int lw = S.ih.i4_lwtc[ni];
+            return lw >= 0 ? lw : S.tc[ni];
+        });
+        if (nc_class(nC) != want) return false;
+    }
+    return true;
+#endif
+}
+
+// The helper's Intra4x4 decision, verified, applied to the live MB as
+// guess_i4 would have left it
+HD void i4_apply(Ctx& c, const IntraSpec* hin, double& c4, int& cbp4, int& d4)
+{
+    Shared& S = c.S;
+    if (c.tid == 0) {
+        S.e_type = ET_I_NXN;
+        S.flags = FL_INTRA;
+        S.pm0 = PM_I4;
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int t = c.tid;
+    if (t < 16) {
+        const int lw = S.ih.i4_lwtc[t];
+        if (lw >= 0) S.tc[t] = (int8_t)lw;
+        S.i4mode[t] = S.ih.i4_mode[t];
+        reinterpret_cast<uint4*>(S.rec)[t] = gmem(reinterpret_cast<const uint4*>(hin->i4_rec))[t];
+    }
+    else if (t < 16 + 128) {  // LumaLevel, two levels per lane
+        const int k = t - 16;
+        const uint32_t w = gmem(reinterpret_cast<const uint32_t*>(&hin->i4_lv[0][0]))[k];
+        S.luma_level[k >> 3][(k & 7) * 2] = (int16_t)(w & 0xFFFF);
+        S.luma_level[k >> 3][(k & 7) * 2 + 1] = (int16_t)(w >> 16);
+    }
+#else
+    for (int t = 0; t < 16; ++t) {
+        if (S.ih.i4_lwtc[t] >= 0) S.tc[t] = S.ih.i4_lwtc[t];
+        S.i4mode[t] = S.ih.i4_mode[t];
+    }
+    for (int t = 0; t < 256; ++t) {
+        S.rec[t] = hin->i4_rec[t];
+        S.luma_level[t >> 4][t & 15] = hin->i4_lv[t >> 4][t & 15];
+    }
+#endif
+    c4 = uni(S.ih.i4_cost);
+    cbp4 = uni(S.ih.i4_cbp);
+    d4 = uni(S.ih.i4_dist);
+    const int sct = uni(S.ih.i4_sct);
+    if (sct >= 0) chain_write(c, sct);
+    HL_SYNC();
+}
+
 // hl_codec_264_rdo_mb_guess_best_intra_pred_avc, rdo.c:99-299.  Returns the
-// best intra cost (the reference's static last_best_intra_cost).
-HD double guess_intra(Ctx& c)
+// best intra cost (the reference's static last_best_intra_cost).  hin: the
+// results of this MB's intra helper task (S.ih already imported), or null.
+HD double guess_intra(Ctx& c, const IntraSpec* hin = nullptr)
 {
     const FrameArgs& F = c.F;
     Shared& S = c.S;
     double c16, c4;
-    int cbp16, cbp4 = 0, d16 = 0, d4 = 0;
+    int cbp16, cbp4 = 0, d16 = 0, d4 = 0, m16;
     HL_PROF_T(t16);
-    guess_i16(c, c16, cbp16, d16);
+    if (!hin) i16_heavy(c);
+    i16_light(c, c16, cbp16, d16, m16, false);
+    i16_copy_best(c, m16, cbp16 != 0, hin);
     HL_PROF_ADD(c, 10, t16);
     HL_PROF_T(t4);
     if (c16 == 0.0) c4 = 1.7976931348623157e308;
-    else guess_i4(c, c4, cbp4, d4);
+    else if (hin && uni(S.ih.i4_valid) && i4_verify(c)) {
+        i4_apply(c, hin, c4, cbp4, d4);
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (c.tid == 0 && F.perr) atomicAdd(F.perr + 2, 1);  // helper's Intra4x4 kept (hl_amd_last_helper_stats)
+#else
+        if (F.perr) ++F.perr[2];
+#endif
+    }
+    else {
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (hin && c.tid == 0 && F.perr) atomicAdd(F.perr + 3, 1);  // helper's Intra4x4 rejected
+#else
+        if (hin && F.perr) ++F.perr[3];
+#endif
+        guess_i4(c, c4, cbp4, d4);
+    }
     HL_PROF_ADD(c, 11, t4);
     HL_SYNC();
     const int i16mode = S.i16mode;
@@ -3141,6 +3353,49 @@ HD int early_term_modes(Ctx& c)
 }
 
 // --------------------------------------------------------------------------
+// The MB's intra helper task (pipelined runs, FrameArgs::hstate): take the
+// task over if no workgroup has claimed it yet (the MB then decides intra
+// itself), else wait until the helper has published -- it waits on nothing,
+// so the wait ends.  use: import the helper's IntraHead into S.ih.  Returns
+// the helper's results, or null.  Called once per P macroblock, before
+// mb_end: the per-address results buffer is free again once the MB ends.
+// --------------------------------------------------------------------------
+HD const IntraSpec* helper_join(Ctx& c, bool use)
+{
+    const FrameArgs& F = c.F;
+    if (!F.hstate) return nullptr;
+#if defined(__HIP_DEVICE_COMPILE__)
+    Shared& S = c.S;
+    if (c.tid < 64) {
+        if (c.tid == 0) {
+            int s = atomicCAS(F.hstate + c.addr, HS_FREE, HS_MAIN);
+            if (s == HS_CLAIMED) {
+                const int e0 = F.perr ? ld_relaxed(F.perr) : 0;
+                spin_ge(F.hstate + c.addr, HS_DONE, F.perr);
+                s = F.perr && ld_relaxed(F.perr) != e0 ? HS_MAIN : HS_DONE;  // gave up: decide intra here
+            }
+            if (s == HS_MAIN && F.perr) atomicAdd(F.perr + 4, 1);  // helper not claimed in time
+            S.hs_x = s;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    HL_SYNC();
+    if (!use || uni(S.hs_x) != HS_DONE) return nullptr;
+    const IntraSpec* hin = F.ispec + c.addr;
+    constexpr int kHW = (int)(sizeof(IntraHead) / 16);
+    if (c.tid < kHW) reinterpret_cast<uint4*>(&S.ih)[c.tid] = gmem(reinterpret_cast<const uint4*>(&hin->h))[c.tid];
+    HL_SYNC();
+    return hin;
+#else
+    if (F.hstate[c.addr] != HS_DONE || !use) return nullptr;
+    const IntraSpec* hin = F.ispec + c.addr;
+    c.S.ih = hin->h;
+    return hin;
+#endif
+}
+
+// --------------------------------------------------------------------------
 // P macroblock decision, rdo.c:678-1271
 // --------------------------------------------------------------------------
 HD void guess_inter(Ctx& c)
@@ -3232,10 +3487,12 @@ HD void guess_inter(Ctx& c)
     }
     if (!pskip) {
         HL_PROF_T(ti);
-        const double ic = guess_intra(c);
+        const IntraSpec* hin = helper_join(c, true);
+        const double ic = guess_intra(c, hin);
         HL_PROF_ADD(c, 5, ti);
         if (ic <= best_cost) return;
     }
+    else helper_join(c, false);  // not needed: cancelled, or its results are not read
     // finalize (rdo.c:1167-1262)
     const PartDef& bp = kParts[best_part];
     HL_SYNC();
@@ -3629,6 +3886,74 @@ HD void mb_end(Ctx& c)
     HL_SYNC();
 }
 #endif
+
+#if defined(HL_EMU_BUILD) && !defined(__HIP_DEVICE_COMPILE__)
+extern int g_emu_bad_guess;
+#endif
+// The intra helper task of P macroblock addr (pipelined runs): the parts of
+// its intra fallback that do not depend on its inter search, into out --
+// every Intra16x16 mode's statistics and results (i16_heavy), and the
+// Intra4x4 decision under the live state the Intra16x16 trials leave when
+// the inter search left this address's previous TotalCoeffs and the entry
+// value s_in of rdo.Single_ctr (i16_light with spec, guess_i4).  The MB keeps
+// that decision only if i4_verify holds.  Reads what the MB's mb_begin reads
+// (all final when the MB is ready) and writes only out.
+#if defined(HL_HELPER_NOINLINE)
+__host__ __device__ __attribute__((noinline)) void intra_helper(
+#else
+HD void intra_helper(
+#endif
+    const FrameArgs& F, Shared& S, int addr, int tid, int nthr, int s_in, IntraSpec* out)
+{
+    Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0, S.lk[tid & 15]};
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (tid < 16) S.lk[tid] = make_lanek(tid, F.qp, F.qpc);
+    c.Q = make_laneq(tid, F.qp);
+#endif
+    mb_begin(c);
+#if defined(HL_EMU_BUILD) && !defined(__HIP_DEVICE_COMPILE__)
+    if (g_emu_bad_guess)  // tests: a wrong guess of the live TotalCoeffs, so that i4_verify must reject
+        for (int i = 0; i < 16; ++i) S.tc[i] = (int8_t)((i * 5 + addr) % 11);
+#endif
+    i16_heavy(c);
+    double c16, c4;
+    int cbp16, d16, m16, cbp4, d4;
+    i16_light(c, c16, cbp16, d16, m16, true);
+    guess_i4(c, c4, cbp4, d4);
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (tid < 16) S.ih.i4_mode[tid] = S.i4mode[tid];
+    if (tid == 0) S.ih.i4_valid = 1;
+    HL_SYNC();
+    // 16-byte stores: the head, the modes' bulk results, the Intra4x4 results
+    constexpr int kHW = (int)(sizeof(IntraHead) / 16);
+    const auto o = gmem(reinterpret_cast<uint4*>(out));
+    static_assert(offsetof(IntraSpec, i4_lv) == sizeof(IntraHead) + 16 * (64 + 64 + 128 + 8 + 16), "IntraSpec layout");
+    for (int k = tid; k < kHW + 64 + 64 + 128 + 8 + 16; k += nthr) {
+        uint4 v;
+        if (k < kHW) v = reinterpret_cast<const uint4*>(&S.ih)[k];
+        else if (k < kHW + 64) v = reinterpret_cast<const uint4*>(S.ih_rec)[k - kHW];
+        else if (k < kHW + 128) v = reinterpret_cast<const uint4*>(S.ih_pred)[k - kHW - 64];
+        else if (k < kHW + 256) v = reinterpret_cast<const uint4*>(S.ih_ac)[k - kHW - 128];
+        else if (k < kHW + 264) v = reinterpret_cast<const uint4*>(S.ih_dcl)[k - kHW - 256];
+        else v = reinterpret_cast<const uint4*>(S.rec)[k - kHW - 264];
+        o[k] = v;  // IntraSpec: h, rec, pred, ac, dcl, i4_rec in this order
+    }
+    if (tid < 128) {  // LumaLevel, two levels per lane
+        const uint32_t w = (uint32_t)(S.luma_level[tid >> 3][(tid & 7) * 2] & 0xFFFF) | ((uint32_t)S.luma_level[tid >> 3][(tid & 7) * 2 + 1] << 16);
+        gmem(reinterpret_cast<uint32_t*>(&out->i4_lv[0][0]))[tid] = w;
+    }
+#else
+    for (int i = 0; i < 16; ++i) S.ih.i4_mode[i] = S.i4mode[i];
+    S.ih.i4_valid = 1;
+    out->h = S.ih;
+    memcpy(out->rec, S.ih_rec, sizeof(out->rec));
+    memcpy(out->pred, S.ih_pred, sizeof(out->pred));
+    memcpy(out->ac, S.ih_ac, sizeof(out->ac));
+    memcpy(out->dcl, S.ih_dcl, sizeof(out->dcl));
+    memcpy(out->i4_rec, S.rec, sizeof(out->i4_rec));
+    for (int t = 0; t < 256; ++t) out->i4_lv[t >> 4][t & 15] = (int16_t)S.luma_level[t >> 4][t & 15];
+#endif
+}
 
 // One macroblock, start to end.  s_in = rdo.Single_ctr on entry (spec_in = 1
 // while it is a row-start speculation); (gx, gy) = reference region already

@@ -167,6 +167,21 @@ int32_t hl_amd_last_mb_launches(hl_amd_encoder_t* encoder);
  * walks.  A healthy call has [1] = [2] = [3] = 0. */
 int32_t hl_amd_last_batch_stats(hl_amd_encoder_t* encoder, int32_t* out5);
 
+/* Intra helper tasks (pipelined runs, on by default; also HL_AMD_HELPERS=0
+ * at create): a P macroblock's intra fallback (rdo.c:1161-1167) is prepared
+ * by a second workgroup beside the macroblock's inter search -- every
+ * Intra16x16 mode's transform, quantisation, CAVLC statistics and
+ * reconstruction, and the Intra4x4 decision under a guess of the live
+ * TotalCoeffs that the macroblock verifies.  Results do not
+ * depend on it.  No reference interface. */
+int32_t hl_amd_set_intra_helpers(hl_amd_encoder_t* encoder, int32_t enable);
+
+/* How the intra fallbacks of the last encode call ran -- diagnostics:
+ * out3[0] P macroblocks that kept their helper's Intra4x4 decision, [1]
+ * that rejected it (an nC class differed: decided again), [2] whose helper
+ * no workgroup had claimed in time (the macroblock decided intra itself). */
+int32_t hl_amd_last_helper_stats(hl_amd_encoder_t* encoder, int32_t* out3);
+
 /* per-phase shader-clock counters of the macroblock kernel; filled only by
  * the profiling build (make profile); out[2k] = cycles, out[2k+1] = calls
  * for k < 32, then out[64 + addr] = cycles of macroblock addr in the last
@@ -238,7 +253,10 @@ int32_t hl_amd_import_layer(hl_amd_encoder_t* encoder, int32_t layer, const void
  * results[i] = access unit i: HDR with every header set those calls signal,
  * in order, and DATA; valid until the next call.  Needs every layer coded by
  * this encoder (no layer range).  No reference interface: a throughput entry
- * point like hl_amd_encode_batch. */
+ * point like hl_amd_encode_batch.  A call that fails part-way leaves the
+ * layers of its access units inconsistent: every later call then returns
+ * HL_AMD_ERROR_INVALID_STATE, and destroying and re-creating the encoder is
+ * the only reset. */
 int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* encoder, int32_t n, int32_t layers, const uint8_t* const* planes,
                                    hl_amd_result_t* results);
 

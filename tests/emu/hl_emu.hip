@@ -4,6 +4,7 @@
 // bitstream writer.  It lets tests/ diff the gfx950 kernel logic against the
 // oracle without a GPU.  The product library never links this file; it
 // fails loudly without a GPU instead of falling back to it.
+#define HL_EMU_BUILD 1
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -21,6 +22,10 @@
 
 using namespace hl;
 
+#if !defined(__HIP_DEVICE_COMPILE__)
+int hl::g_emu_bad_guess = 0;  // intra_helper (hl_mbcore.h): HL_EMU_HELPER=2
+#endif
+
 struct EmuEnc {
     int W, H, Wc, Hc, mbw, mbh, nmb, qp, qpc, me_range, deblock, gop, early_term;
     int pstride;
@@ -33,6 +38,12 @@ struct EmuEnc {
     std::vector<uint8_t> scratch, out, hdr;
     int cur, frame_index, gop_left, pict_count, idr_pic_id, chain_end;
     Shared* S;
+    Shared* S2;                        // the intra helper's workgroup image (HL_EMU_HELPER)
+    std::vector<IntraSpec> ispec;
+    std::vector<int32_t> hstate;
+    long helper_runs = 0;
+    int helper_mode = 0;               // 0 off, 1 helpers, 2 helpers with a wrong guess (emu_set_helper, HL_EMU_HELPER)
+    int32_t perr[8] = {};              // FrameArgs::perr: [2] helper Intra4x4 kept, [3] rejected
     std::unique_ptr<RateControl> rc;  // rate control (hl_rc.h), as in the product
     int last_qp;
 };
@@ -220,6 +231,8 @@ extern "C" void* emu_create(int W, int H, int qp, int me_range, int deblock, int
     e->hdr.resize(256);
     e->hdr.resize(write_stream_headers(sp, e->hdr.data(), e->hdr.size()));
     e->S = (Shared*)calloc(1, sizeof(Shared));
+    e->S2 = (Shared*)calloc(1, sizeof(Shared));
+    e->helper_mode = getenv("HL_EMU_HELPER") ? atoi(getenv("HL_EMU_HELPER")) : 0;
     return e;
 }
 
@@ -228,8 +241,12 @@ extern "C" void emu_destroy(void* h)
     EmuEnc* e = (EmuEnc*)h;
     if (!e) return;
     free(e->S);
+    free(e->S2);
     delete e;
 }
+extern "C" long emu_helper_runs(void* h) { return ((EmuEnc*)h)->helper_runs; }
+extern "C" int emu_helper_i4(void* h, int rejected) { return ((EmuEnc*)h)->perr[rejected ? 3 : 2]; }
+extern "C" void emu_set_helper(void* h, int mode) { ((EmuEnc*)h)->helper_mode = mode; }
 
 // Writes hdr (first frame) + 00 00 01 + slice into out; returns bytes or -1.
 // rate control of the product path (hl_amd_set_rate_control)
@@ -288,6 +305,24 @@ extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, co
     F.chain = e->chain.data();
     F.spec = e->spec.data();
     F.prof = nullptr;
+    F.run_done = nullptr;
+    F.perr = e->perr;
+    // HL_EMU_HELPER=1: every P macroblock's intra helper (hl_mbcore.h
+    // intra_helper) runs first, on its own workgroup image, as a pipelined
+    // run's helper task would; the macroblock then uses its results
+    // (2: the helpers guess the live TotalCoeffs wrongly; emu_set_helper)
+    const int helper = e->helper_mode;
+#if !defined(__HIP_DEVICE_COMPILE__)
+    g_emu_bad_guess = helper == 2;
+#endif
+    F.ispec = nullptr;
+    F.hstate = nullptr;
+    if (helper && !intra) {
+        e->ispec.resize(e->nmb);
+        e->hstate.assign(e->nmb, HS_DONE);
+        F.ispec = e->ispec.data();
+        F.hstate = e->hstate.data();
+    }
     int chain = e->chain_end;
     // HL_EMU_POISON=<seed>: fill the workgroup's LDS image with pseudo-random
     // bytes before every macroblock (a GPU workgroup finds whatever the
@@ -304,6 +339,10 @@ extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, co
                 prng ^= prng << 17;
                 s[i] = (uint8_t)prng;
             }
+        }
+        if (F.hstate) {
+            intra_helper(F, *e->S2, a, 0, 1, chain, F.ispec + a);
+            ++e->helper_runs;
         }
         encode_mb(F, *e->S, a, 0, 1, chain);
         chain = e->chain[a].s_out;

@@ -48,10 +48,11 @@ def child(lib):
         kernel_ms = tm[1]
         outs += [r.annexb() for r in enc.last_batch_results()]
         exact = all(hashlib.md5(o).hexdigest() == m for o, m in zip(outs, g["frame_md5"]))
+        hs = enc.last_helper_stats() if hasattr(enc.lib, "hl_amd_last_helper_stats") else {}
         enc.close()
         print(f"{os.path.relpath(lib, ROOT)} geom {os.environ.get('HL_AB_GEOM', 'default')} warmup {warm} steps {steps}: {steps / dt:.2f} fps ({dt * 1e3:.1f} ms, kernel {kernel_ms:.1f} ms, "
               f"records copy {tm[2]:.1f} ms, slice writing {tm[3]:.1f} ms) "
-              f"bitexact {exact}", flush=True)
+              f"bitexact {exact} helpers {hs}", flush=True)
 
 
 def main():
