@@ -38,7 +38,6 @@ BYTES_PER_MB = 2752  # compulsory HBM bytes per macroblock, DESIGN.md / SURVEY Â
 # tools/pmc_summary.py; kept under tools/pmc/ (travels to the GPU box; a copy
 # in profiles/).  They describe the library whose SHA-256 they name.
 PMC_FILE = os.path.join(ROOT, "tools", "pmc", "pmc_k_pipeline.json")
-LIB_FILE = os.path.join(ROOT, "hartallo_amd", "libhartallo_amd.so")
 STAT_KEYS = ("runs", "per_picture", "fallbacks", "waits_gave_up", "chain_walks")
 MAX_RUN = 128  # pictures per pipelined launch (kMaxRun, hl_encoder.hip)
 # The synthetic stream is always generated for BENCH_CLIP_FRAMES frames (its
@@ -49,23 +48,57 @@ MAX_RUN = 128  # pictures per pipelined launch (kMaxRun, hl_encoder.hip)
 BENCH_CLIP_FRAMES = 150
 BENCH_GOLDEN = os.path.join(ROOT, "tests", "golden", "bench_golden.json")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+SHADER_CLOCK_HZ = 2.4e9  # MI355X peak engine clock (MI355X_MICROARCH.md)
 PLANES_PAD = 40  # kPad of the quarter-pel planes (hl_mbcore.h)
 
 
-def load_pmc(warmup, steps):
-    """The recorded counters when they were taken on this exact library and
-    workload, else (None, why not)."""
+def load_pmc(lib_path, warmup, steps, workgroups, streams_per_gpu):
+    """The recorded counters when they were taken on this exact library (the
+    file that was loaded) and workload -- picture size, warm-up and timed
+    pictures, k_pipeline workgroups, streams sharing the GPU -- else (None,
+    why not)."""
     import hashlib
 
     if not os.path.exists(PMC_FILE):
         return None, "no counters recorded (tools/pmc_record.sh)"
+    if not lib_path or not os.path.exists(lib_path):
+        return None, "library not found"
     pmc = json.load(open(PMC_FILE))
-    sha = hashlib.sha256(open(LIB_FILE, "rb").read()).hexdigest()
+    sha = hashlib.sha256(open(lib_path, "rb").read()).hexdigest()
     if pmc.get("lib_sha256") != sha:
         return None, f"stale: recorded on library {pmc.get('lib_sha256', '?')[:12]}, this one is {sha[:12]} (rerun tools/pmc_record.sh)"
-    if (pmc.get("warmup"), pmc.get("steps")) != (warmup, steps):
-        return None, f"recorded at --warmup {pmc.get('warmup')} --steps {pmc.get('steps')}, not this workload"
+    want = {"warmup": warmup, "steps": steps, "width": W, "height": H, "workgroups": workgroups, "streams_per_gpu": streams_per_gpu}
+    diff = {k: (pmc.get(k), v) for k, v in want.items() if pmc.get(k) != v}
+    if diff:
+        return None, "recorded on another workload: " + ", ".join(f"{k} {a} (here {b})" for k, (a, b) in diff.items())
     return pmc, f"tools/pmc/pmc_k_pipeline.json, library sha256 {sha[:12]}, recorded {pmc.get('recorded', '?')}"
+
+
+def critical_path_steps(frames, mbw, mbh, reach=2):
+    """Longest dependency chain of a pipelined run of `frames` pictures, in
+    macroblock tasks (hl_pipeline.h task_deps: (x-1, y), (x+1, y-1) -- (x,
+    y-1) in the last column -- and picture f-1's reach_task(x+R, y+R)): the
+    run's time per step of it is the macroblock latency its critical path
+    achieved."""
+    import numpy as np
+
+    prev = None
+    for _ in range(frames):
+        d = np.zeros((mbh, mbw), dtype=np.int64)
+        for y in range(mbh):
+            for x in range(mbw):
+                v = 0
+                if x > 0:
+                    v = d[y, x - 1]
+                if y > 0:
+                    v = max(v, d[y - 1, min(x + 1, mbw - 1)])
+                if prev is not None:
+                    ty = min(y + reach + 2, mbh - 1)
+                    tx = min(x + reach + (3 if ty == mbh - 1 else 2), mbw - 1)
+                    v = max(v, prev[ty, tx])
+                d[y, x] = v + 1
+        prev = d
+    return int(prev.max())
 
 
 def cpu_model():
@@ -422,9 +455,11 @@ def main():
     # execute side by side instead of taking turns for the whole device
     # (several streams per GPU fill the MB wavefront's ramp and tail)
     share = -(-int(os.environ.get("LOCAL_WORLD_SIZE", "1")) // max(1, torch.cuda.device_count()))
+    wg_used = 0  # k_pipeline workgroups (0: one per resident slot)
     if share > 1:
         cus = torch.cuda.get_device_properties(local).multi_processor_count
-        enc.set_pipeline(max(1, cus // share), 2, 64)
+        wg_used = max(1, cus // share)
+        enc.set_pipeline(wg_used, 2, 64)
     outputs = []
     warm = {k: 0 for k in STAT_KEYS}
     if args.warmup:  # same entry point as the timed frames (warms the pipelined path and its buffers)
@@ -474,7 +509,16 @@ def main():
         avg_launch_s = (mb_ms / 1e3) / mb_launches
         bytes_per_launch = BYTES_PER_MB * nmb * run_frames / mb_launches
         achieved = bytes_per_launch / avg_launch_s / 1e9
-        pmc, pmc_note = load_pmc(args.warmup, args.steps)
+        from hartallo_amd import _lib
+
+        pmc, pmc_note = load_pmc(getattr(_lib, "LOADED_PATH", None) or _lib.LIB_PATH, args.warmup, args.steps, wg_used, share)
+        # the achieved macroblock latency along the run's critical path, and
+        # VALU issue against one wave64 VALU instruction per SIMD per cycle
+        cp_steps = critical_path_steps(run_frames, W // 16, H // 16) if mb_launches == 1 else None
+        cp_us = round(avg_launch_s * 1e6 / cp_steps, 2) if cp_steps else None
+        cus = torch.cuda.get_device_properties(local).multi_processor_count
+        valu_util = (round(pmc["valu_insts_per_mb"] * nmb * run_frames / avg_launch_s / (4 * cus * SHADER_CLOCK_HZ), 4)
+                     if pmc and mb_launches == 1 else None)
         line = {
             "metric": "1080p encoded frames/sec (bit-exact) at 1/2/4/8 MI355X; macroblocks/sec/GPU",
             "value": round(fps, 4),
@@ -506,6 +550,10 @@ def main():
                          "sq_wait_frac": pmc["sq_wait_frac"] if pmc else None,
                          "sq_issue_frac": pmc["sq_issue_frac"] if pmc else None,
                          "valu_insts_per_mb": pmc["valu_insts_per_mb"] if pmc else None,
+                         "valu_util": valu_util,
+                         "valu_util_def": "VALU wave-instructions/s / (4 SIMD x CUs x 2.4 GHz)",
+                         "critical_path_steps": cp_steps,
+                         "critical_path_us_per_step": cp_us,
                          "pmc": pmc_note},
             "planes_roofline": {"kernel": "k_planes", "bound": "hbm", "achieved": round(planes_bytes / (planes_ms / 1e3) / 1e9, 1),
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(planes_bytes / (planes_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -108,6 +108,7 @@ except ImportError:  # numpy is optional for the plain ctypes binding
     MB_RECORD = None
 
 _lib = None
+LOADED_PATH = None  # the library file load_library loaded (bench.py stamps counters with its hash)
 
 
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
@@ -124,6 +125,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     except ImportError:
         pass
     lib = ctypes.CDLL(path)
+    global LOADED_PATH
+    LOADED_PATH = os.path.abspath(path)
     vp, i32 = ctypes.c_void_p, ctypes.c_int32
     lib.hl_amd_encoder_create.argtypes = [ctypes.POINTER(_Params), ctypes.POINTER(vp)]
     lib.hl_amd_encoder_create.restype = i32
@@ -159,10 +162,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_last_mb_launches.restype = i32
     lib.hl_amd_last_batch_stats.argtypes = [vp, ctypes.POINTER(i32)]
     lib.hl_amd_last_batch_stats.restype = i32
-    lib.hl_amd_set_intra_helpers.argtypes = [vp, i32]
-    lib.hl_amd_set_intra_helpers.restype = i32
-    lib.hl_amd_last_helper_stats.argtypes = [vp, ctypes.POINTER(i32)]
-    lib.hl_amd_last_helper_stats.restype = i32
+    for name, args in (("hl_amd_set_intra_helpers", [vp, i32]), ("hl_amd_last_helper_stats", [vp, ctypes.POINTER(i32)])):
+        if hasattr(lib, name):  # (absent from builds before round 4 loaded through HL_LIB)
+            getattr(lib, name).argtypes = args
+            getattr(lib, name).restype = i32
     lib.hl_amd_profile_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong), i32]
     lib.hl_amd_profile_counters.restype = i32
     # diagnostics entry points (absent from older builds loaded through HL_LIB)

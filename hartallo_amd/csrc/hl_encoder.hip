@@ -262,14 +262,18 @@ __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
         int d[3][3];
         P.cnt[i] = task_deps(f, a % mbw, a / mbw, mbw, mbh, P.reach, d);
         P.done[i] = 0;
-        P.queue[2 * f * nmb + a] = i == 0 ? 1 : (i == 1 && h0 ? 1 + nmb : 0);
-        P.queue[2 * f * nmb + nmb + a] = 0;
+        P.queue[i] = i == 0 ? 1 : 0;
         P.claim[i] = 0;
         P.hstate[i] = HS_FREE;
+        P.hq[i] = i == 0 && h0 ? 1 : 0;
     }
     if (i < P.nframes) {
         P.head[i] = 0;
-        P.tail[i] = i == 0 ? (h0 ? 2 : 1) : 0;
+        P.tail[i] = i == 0 ? 1 : 0;
+    }
+    if (i == 0) {
+        *P.hq_head = 0;
+        *P.hq_tail = h0 ? 1 : 0;
     }
     if (i == 0) {
         *P.oldest = 0;
@@ -313,10 +317,10 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh)
         else {
             // the head entries themselves (0: pushed, not yet written)
             int q = 0;
-            if (lane < w && h < t) q = ld_relaxed(P.queue + (size_t)(o + lane) * 2 * nmb + h);
+            if (lane < w && h < t) q = ld_relaxed(P.queue + (o + lane) * nmb + h);
             int key = -1;
             if (q > 0) {
-                const int a = q - 1 - (q > nmb ? nmb : 0), y = a / mbw, x = a - y * mbw;
+                const int a = q - 1, y = a / mbw, x = a - y * mbw;
                 key = (((mbw - 1 - x) + 2 * (mbh - 1 - y) - P.hop * lane + 4096) << 6) | (63 - lane);
             }
             for (int s = 1; s < 64; s <<= 1) key = max(key, __shfl_xor(key, s, 64));
@@ -334,24 +338,37 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh)
             if (lane == 0 && atomicCAS(P.head + f, hh, hh + 1) == hh) {
                 r = v;
                 // the slot is pushed right after the tail moved
-                for (unsigned k = 0; r == 0 && (r = ld_relaxed(P.queue + (size_t)f * 2 * nmb + hh)) == 0; ++k)
+                for (unsigned k = 0; r == 0 && (r = ld_relaxed(P.queue + f * nmb + hh)) == 0; ++k)
                     if (k > (1u << 26)) {
                         atomicAdd(P.err, 1);
                         r = -1;
                         break;
                     }
-                // a macroblock task: claim it (workgroup 0 may have); an intra
-                // helper: claim it unless its macroblock took it over
-                if (r > nmb) {
-                    if (atomicCAS(P.hstate + f * nmb + r - 1 - nmb, HS_FREE, HS_CLAIMED) != HS_FREE) r = 0;
-                }
-                else if (r > 0 && atomicCAS(P.claim + f * nmb + r - 1, 0, 1) != 0) r = 0;
+                if (r > 0 && atomicCAS(P.claim + f * nmb + r - 1, 0, 1) != 0) r = 0;
             }
             r = __builtin_amdgcn_readfirstlane(r);
             if (r < 0) return -1;
-            if (r > nmb) return P.nframes * nmb + f * nmb + r - 1 - nmb;  // intra helper of (f, r - 1 - nmb)
             if (r > 0) return f * nmb + r - 1;
             continue;  // another workgroup took it
+        }
+        if (P.helpers) {  // no macroblock ready: an intra helper task, unless its macroblock took it over
+            const int hh = ld_relaxed(P.hq_head), ht = ld_relaxed(P.hq_tail);
+            if (hh < ht) {
+                int r = 0;
+                if (lane == 0 && atomicCAS(P.hq_head, hh, hh + 1) == hh) {
+                    for (unsigned k = 0; (r = ld_relaxed(P.hq + hh)) == 0; ++k)
+                        if (k > (1u << 26)) {
+                            atomicAdd(P.err, 1);
+                            r = -1;
+                            break;
+                        }
+                    if (r > 0 && atomicCAS(P.hstate + r - 1, HS_FREE, HS_CLAIMED) != HS_FREE) r = 0;
+                }
+                r = __builtin_amdgcn_readfirstlane(r);
+                if (r < 0) return -1;
+                if (r > 0) return P.nframes * nmb + r - 1;
+                continue;
+            }
         }
         if (__builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 10 s at 100 MHz
             if (lane == 0) atomicAdd(P.err, 1);
@@ -397,6 +414,9 @@ __device__ int claim_next(const PipeArgs& P, int nmb, int& cursor)
 #ifndef HL_PIPE_WAVES_PER_EU
 #define HL_PIPE_WAVES_PER_EU 2
 #endif
+#ifndef HL_CONT
+#define HL_CONT 0
+#endif
 __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(PipeArgs P, int mbw, int mbh)
 {
     __shared__ Shared S;
@@ -405,6 +425,9 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
     const int nmb = mbw * mbh;
     const bool in_order = blockIdx.x == 0;  // claims tasks in run order (claim_next)
     int cursor = 0;
+    // (wave 0) the task this workgroup runs next without popping: one of the
+    // successors its last task made ready, or -1
+    int next_task = -1;
 #if defined(HL_PROFILE)
     // per-workgroup totals (profiling build): prof[40..44] = waits for a ready
     // task, decisions, filters, tasks, workgroup lifetime (shader clock)
@@ -417,7 +440,8 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         const unsigned long long pt0 = __builtin_readcyclecounter();
 #endif
         if (threadIdx.x < 64) {
-            const int t = in_order ? claim_next(P, nmb, cursor) : pop_task(P, nmb, mbw, mbh);
+            const int t = next_task >= 0 ? next_task : (in_order ? claim_next(P, nmb, cursor) : pop_task(P, nmb, mbw, mbh));
+            next_task = -1;
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
             if (threadIdx.x == 0) s_task = t;
@@ -510,17 +534,40 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
             if (tid == 0) st_relaxed(P.done + t, 1);
             int fo = 0, xo = 0, yo = 0;
             const int ns = task_succ(f, x, y, mbw, mbh, P.reach, P.nframes, -1, fo, xo, yo);
+            // every successor this task makes ready is queued (with its intra
+            // helper, in P pictures) -- except the first one, which this
+            // workgroup claims and runs next without a pop (workgroup 0 keeps
+            // claiming in run order): with hundreds of workgroups converging
+            // on the same queue head, pops were a serial bottleneck
+            int ready = -1;  // this lane's successor (one per lane: ns <= 64)
             for (int j = tid; j < ns; j += 64) {
                 task_succ(f, x, y, mbw, mbh, P.reach, P.nframes, j, fo, xo, yo);
                 const int a = yo * mbw + xo;
-                if (__hip_atomic_fetch_add(P.cnt + fo * nmb + a, -1, HL_CNT_ORDER, __HIP_MEMORY_SCOPE_AGENT) == 1) {
-                    // the macroblock, then (P pictures) its intra helper
-                    const bool hp = P.helpers && !ld_relaxed(&P.fr[fo].F.is_intra);
-                    const int pos = __hip_atomic_fetch_add(P.tail + fo, hp ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(P.queue + (size_t)fo * 2 * nmb + pos, a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                    if (hp) __hip_atomic_store(P.queue + (size_t)fo * 2 * nmb + pos + 1, a + 1 + nmb, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                if (__hip_atomic_fetch_add(P.cnt + fo * nmb + a, -1, HL_CNT_ORDER, __HIP_MEMORY_SCOPE_AGENT) == 1) ready = fo * nmb + a;
+            }
+            // (continuation: HL_CONT 0 none, 1 any successor, 2 one of this picture)
+            const unsigned long long rb = __ballot(ready >= 0 && (HL_CONT == 1 || ready / nmb == f));
+            const int keep = in_order || !rb || HL_CONT == 0 ? -1 : __ffsll((long long)rb) - 1;
+            if (ready >= 0) {
+                const int ff = ready / nmb, a = ready - ff * nmb;
+                bool main_entry = true;
+                if (tid == keep && atomicCAS(P.claim + ready, 0, 1) == 0) {
+                    main_entry = false;
+                    next_task = ready;
+                }
+                else if (tid == keep)
+                    main_entry = false;  // workgroup 0 holds it (claim_next)
+                // the macroblock, then (P pictures) its intra helper
+                if (main_entry) {
+                    const int pos = __hip_atomic_fetch_add(P.tail + ff, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(P.queue + ff * nmb + pos, a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (P.helpers && !ld_relaxed(&P.fr[ff].F.is_intra)) {
+                    const int pos = __hip_atomic_fetch_add(P.hq_tail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(P.hq + pos, ready + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
+            if (keep >= 0) next_task = __builtin_amdgcn_readlane(next_task, keep);
             // pictures finish in order: the last MB depends on every other one
             // and on the previous picture's last MB
             if (tid == 0 && addr == nmb - 1) {
@@ -986,7 +1033,7 @@ static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
         (r = hipHostMalloc(&e->h_bchain, sizeof(MbChain) * nmb * n, hipHostMallocDefault)) ||
         (r = hipHostMalloc(&e->h_pf, sizeof(PipeFrame) * n, hipHostMallocDefault)) ||
         (r = hipMalloc(&e->d_cnt, sizeof(int32_t) * 2 * nmb * n)) || (r = hipMalloc(&e->d_done, sizeof(int32_t) * nmb * n)) ||
-        (r = hipMalloc(&e->d_queue, sizeof(int32_t) * 2 * nmb * n)) || (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * n + 1))) ||
+        (r = hipMalloc(&e->d_queue, sizeof(int32_t) * 2 * nmb * n)) || (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * n + 3))) ||
         (r = hipMalloc(&e->d_hstate, sizeof(int32_t) * nmb * n)) || (r = hipMalloc(&e->d_ispec, sizeof(IntraSpec) * nmb)) ||
         (r = hipHostGetDevicePointer((void**)&e->dh_brec, e->h_brec, 0)))
         return r;
@@ -1201,6 +1248,9 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
     P.queue = e->d_queue;
     P.hstate = e->d_hstate;
     P.helpers = e->helpers ? 1 : 0;
+    P.hq = e->d_queue + nmb * m;
+    P.hq_head = e->d_head + 2 * m + 1;
+    P.hq_tail = e->d_head + 2 * m + 2;
     P.head = e->d_head;
     P.tail = e->d_head + m;
     P.oldest = e->d_head + 2 * m;

@@ -3487,7 +3487,11 @@ HD void guess_inter(Ctx& c)
     }
     if (!pskip) {
         HL_PROF_T(ti);
+        HL_PROF_T(tj);
         const IntraSpec* hin = helper_join(c, true);
+#if !defined(HL_STEP_PROF)
+        HL_PROF_ADD(c, 19, tj);  // joining the intra helper
+#endif
         const double ic = guess_intra(c, hin);
         HL_PROF_ADD(c, 5, ti);
         if (ic <= best_cost) return;

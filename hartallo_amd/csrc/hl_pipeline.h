@@ -176,9 +176,15 @@ struct PipeArgs {
     int32_t* cnt;    // [nframes][nmb] unfinished dependencies
     int32_t* claim;  // [nframes][nmb] 1 once a workgroup holds the task
     int32_t* done;   // [nframes][nmb] 1 once the task finished (reach_wait polls it)
-    int32_t* queue;  // [nframes][2 nmb] ready tasks, MB address + 1 (+ nmb: its intra helper; 0 = slot not yet written)
-    int32_t* hstate; // [nframes][nmb] intra helper task states (HS_*, hl_mbcore.h)
-    int32_t helpers; // 1 = a ready P macroblock also queues its intra helper task
+    int32_t* queue;  // [nframes][nmb] ready tasks, MB address + 1 (0 = slot not yet written)
+    // intra helper tasks (hl_mbcore.h intra_helper): a ready P macroblock also
+    // queues its helper, in one FIFO that workgroups take from only when no
+    // macroblock is ready (ramp and tail of a run, a lone picture)
+    int32_t helpers; // 1 = queue them
+    int32_t* hstate; // [nframes][nmb] helper task states (HS_*)
+    int32_t* hq;     // [nframes * nmb] FIFO of helper tasks, f * nmb + MB address + 1 (0 = slot not yet written)
+    int32_t* hq_head;
+    int32_t* hq_tail;
     int32_t* head;   // [nframes] next queue slot to pop
     int32_t* tail;   // [nframes] next queue slot to push
     int32_t* oldest; // [0] first unfinished picture of the run

@@ -48,11 +48,25 @@ def child(lib):
         kernel_ms = tm[1]
         outs += [r.annexb() for r in enc.last_batch_results()]
         exact = all(hashlib.md5(o).hexdigest() == m for o, m in zip(outs, g["frame_md5"]))
-        hs = enc.last_helper_stats() if hasattr(enc.lib, "hl_amd_last_helper_stats") else {}
+        hs = enc.last_helper_stats() if hasattr(enc.lib, "hl_amd_last_helper_stats") else "n/a"
         enc.close()
         print(f"{os.path.relpath(lib, ROOT)} geom {os.environ.get('HL_AB_GEOM', 'default')} warmup {warm} steps {steps}: {steps / dt:.2f} fps ({dt * 1e3:.1f} ms, kernel {kernel_ms:.1f} ms, "
               f"records copy {tm[2]:.1f} ms, slice writing {tm[3]:.1f} ms) "
               f"bitexact {exact} helpers {hs}", flush=True)
+    # one picture per call (the plugin's per-frame path): P pictures 2..7
+    enc = Encoder(W, H, 28, 16, 1, 30)
+    outs, ms = [], []
+    for i in range(8):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        outs.append(enc.encode_device(*ptrs[i]).annexb())
+        torch.cuda.synchronize()
+        ms.append((time.perf_counter() - t) * 1e3)
+    exact = all(hashlib.md5(o).hexdigest() == m for o, m in zip(outs, g["frame_md5"]))
+    hs = enc.last_helper_stats() if hasattr(enc.lib, "hl_amd_last_helper_stats") else "n/a"
+    enc.close()
+    print(f"{os.path.relpath(lib, ROOT)} per-picture calls: P pictures {sum(ms[2:]) / 6:.1f} ms each "
+          f"({' '.join(f'{m:.1f}' for m in ms)}) bitexact {exact} helpers (last call) {hs}", flush=True)
 
 
 def main():
@@ -61,8 +75,15 @@ def main():
         return
     libs = sys.argv[1:] or [os.path.join(ROOT, "hartallo_amd", "libhartallo_amd.so")]
     rc = 0
-    for lib in libs:
-        r = subprocess.run([sys.executable, "-u", __file__, "--child", lib])
+    for spec in libs:  # lib.so[:VAR=value,...] -- environment of that child
+        lib, _, envs = spec.partition(":")
+        env = dict(os.environ)
+        for kv in filter(None, envs.split(",")):
+            k, _, v = kv.partition("=")
+            env[k] = v
+        if envs:
+            print(f"== {lib} with {envs}", flush=True)
+        r = subprocess.run([sys.executable, "-u", __file__, "--child", lib], env=env)
         rc = rc or r.returncode
         if r.returncode in (-6, -11, 134, 139):
             break

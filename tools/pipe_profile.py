@@ -24,7 +24,7 @@ _lib.load_library(os.path.join(ROOT, "build", "prof", "hartallo_amd", "libhartal
 from hartallo_amd import Encoder, synth  # noqa: E402
 
 PHASES = ["eval:block", "eval:nC", "eval:reduce", "search_partition", "mvp", "guess_intra(P)", "mb_begin", "mb_end", "whole MB",
-          "reach_wait", "intra:i16", "intra:i4"]
+          "reach_wait", "intra:i16", "intra:i4", "", "", "", "", "step:candidates", "step:selection", "", "helper join"]
 
 
 def main():
@@ -39,6 +39,8 @@ def main():
     ptrs = [(dev[i].data_ptr(), dev[i].data_ptr() + ny, dev[i].data_ptr() + ny + nc) for i in range(n + 2)]
     enc = Encoder(W, H, 28, 16, 1, 30)
     enc.set_pipeline(*geo)
+    if os.environ.get("HL_PROF_HELPERS") == "0":
+        enc.set_intra_helpers(False)
     enc.set_timing(True)
     for i in range(2):
         enc.encode_device(*ptrs[i], collect=False)
@@ -48,17 +50,21 @@ def main():
     dt = time.perf_counter() - t
     ms = enc.timing_ms()
     cnt = enc.profile_counters(64)
-    print(f"wg,R,window={geo}: {n} P pictures in {dt * 1e3:.1f} ms (kernel {ms[1]:.1f} ms, reruns {enc.last_reruns()})")
+    print(f"wg,R,window={geo}: {n} P pictures in {dt * 1e3:.1f} ms (kernel {ms[1]:.1f} ms, reruns {enc.last_reruns()}) helpers {enc.last_helper_stats()}")
     life, wait, mb, filt, tasks = cnt[44], cnt[40], cnt[41], cnt[42], cnt[43]
     if life:
         wgs = geo[0] or 256
         print(f"   workgroups {wgs}, tasks {tasks} ({tasks / max(1, n * nmb):.2f} per MB), mean lifetime {life / wgs / 1e6:.1f} Mcycles"
               f" (~{life / wgs / (ms[1] * 1e-3) / 1e9:.2f} GHz shader clock if the kernel spans it)")
-        for name, v in (("task-start waits", wait), ("decisions", mb), ("deblock + planes", filt), ("rest", life - wait - mb - filt)):
+        hlp, hn = cnt[45], cnt[46]
+        if hn:
+            print(f"   intra helper tasks {hn} ({hn / max(1, n * nmb):.2f} per MB), {hlp / hn / 1e3:.1f} kcycles each")
+        for name, v in (("task-start waits", wait), ("decisions", mb), ("deblock + planes", filt), ("intra helpers", hlp),
+                        ("rest", life - wait - mb - filt - hlp)):
             print(f"   {name:18s} {100.0 * v / life:6.1f} %   {v / max(1, tasks) / 1e3:9.1f} kcycles/task")
     for i, name in enumerate(PHASES):
         cyc, calls = cnt[2 * i], cnt[2 * i + 1]
-        if calls:
+        if calls and name:
             print(f"   {name:18s} calls/MB {calls / (n * nmb):8.1f}  cycles/call {cyc / calls:10.0f}  kcycles/MB {cyc / (n * nmb) / 1e3:9.1f}")
     enc.close()
 

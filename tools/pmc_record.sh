@@ -24,5 +24,5 @@ for set in "${sets[@]}"; do
       python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $R/gpurun_out/pmc/p$i.log 2>&1 || exit $?
 done
 cd $R
-python3 tools/pmc_summary.py --warmup 5 --steps 20 gpurun_out/pmc/p1 gpurun_out/pmc/p2 gpurun_out/pmc/p3 gpurun_out/pmc/p4 \
+python3 tools/pmc_summary.py --warmup 5 --steps 20 --width 1920 --height 1088 --workgroups 0 --streams-per-gpu 1 gpurun_out/pmc/p1 gpurun_out/pmc/p2 gpurun_out/pmc/p3 gpurun_out/pmc/p4 \
     > gpurun_out/pmc/pmc_k_pipeline.json && cat gpurun_out/pmc/pmc_k_pipeline.json

@@ -41,6 +41,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--warmup", type=int, required=True)
     ap.add_argument("--steps", type=int, required=True)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1088)
+    ap.add_argument("--workgroups", type=int, default=0, help="k_pipeline workgroups (0: one per resident slot)")
+    ap.add_argument("--streams-per-gpu", type=int, default=1)
+    ap.add_argument("--lib", default=os.path.join(ROOT, "hartallo_amd", "libhartallo_amd.so"))
     ap.add_argument("dirs", nargs="+")
     a = ap.parse_args()
     c, launches = {}, set()
@@ -48,11 +53,12 @@ def main():
         v, n = timed_launch(d)
         c.update(v)
         launches.add(n)
-    mbs = a.steps * (1920 // 16) * (1088 // 16)  # the timed call: one launch of `steps` pictures
-    lib = os.path.join(ROOT, "hartallo_amd", "libhartallo_amd.so")
+    mbs = a.steps * (a.width // 16) * (a.height // 16)  # the timed call: one launch of `steps` pictures
     out = {
-        "kernel": "k_pipeline", "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
+        "kernel": "k_pipeline", "lib_sha256": hashlib.sha256(open(a.lib, "rb").read()).hexdigest(),
         "recorded": time.strftime("%Y-%m-%d"), "warmup": a.warmup, "steps": a.steps,
+        # the workload the counters belong to (bench.py uses them only for this one)
+        "width": a.width, "height": a.height, "workgroups": a.workgroups, "streams_per_gpu": a.streams_per_gpu,
         "k_pipeline_dispatches_per_pass": sorted(launches), "macroblocks_per_launch": mbs,
         "counters": {k: c[k] for k in sorted(c)},
     }
