@@ -423,6 +423,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=GOP)  # the first GOP (also warms the pipelined path)
     ap.add_argument("--cpu-frames", type=int, default=6)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--streams", type=int, default=1, help="streams per process, in shared pipelined runs (hl_amd_encode_streams)")
     ap.add_argument("--svc", action="store_true", help="BASELINE config 4 (spatial SVC) instead of the headline workload")
     args = ap.parse_args()
     if args.svc:
@@ -441,53 +442,79 @@ def main():
     torch.cuda.set_device(local)
 
     n_frames = args.warmup + args.steps
-    seed = dist.stream_seed(rank)
-    frames_host = synth.clip(W, H, max(n_frames, BENCH_CLIP_FRAMES), seed)[:n_frames]
+    K = max(1, args.streams)  # streams this process encodes (one encoder each, shared pipelined runs)
+    seeds = [dist.stream_seed(rank * K + si) for si in range(K)]
+    frames_host = [synth.clip(W, H, max(n_frames, BENCH_CLIP_FRAMES), sd)[:n_frames] for sd in seeds]
     # inputs resident in HBM before timing
-    dev = torch.from_numpy(frames_host).to(f"cuda:{local}")
+    devs = [torch.from_numpy(fh).to(f"cuda:{local}") for fh in frames_host]
     torch.cuda.synchronize()
     ny, nc = W * H, W * H // 4
-    ptrs = [(dev[i].data_ptr(), dev[i].data_ptr() + ny, dev[i].data_ptr() + ny + nc) for i in range(n_frames)]
+    ptrs = [[(dev[i].data_ptr(), dev[i].data_ptr() + ny, dev[i].data_ptr() + ny + nc) for i in range(n_frames)] for dev in devs]
 
-    enc = Encoder(W, H, QP, ME_RANGE, DEBLOCK, GOP, 0, local)
+    encs = [Encoder(W, H, QP, ME_RANGE, DEBLOCK, GOP, 0, local) for _ in range(K)]
+    enc = encs[0]  # launches the shared runs (its diagnostics describe them)
     # streams sharing one GPU (more ranks on this node than visible GPUs):
     # each rank's persistent run takes its share of the CUs, so the runs
     # execute side by side instead of taking turns for the whole device
-    # (several streams per GPU fill the MB wavefront's ramp and tail)
+    # (several streams per GPU fill the MB wavefront's ramp and
+    # tail).  More than two processes per GPU time-slice the device (4 of
+    # them collapsed to 3.5 frames/s, profiles/r03_streams_sharing_hw_queues.log):
+    # several streams per GPU belong in one process (--streams).
     share = -(-int(os.environ.get("LOCAL_WORLD_SIZE", "1")) // max(1, torch.cuda.device_count()))
+    warning = None
+    if share > 2:
+        warning = (f"{share} processes share each GPU: the device time-slices between processes and persistent runs stall "
+                   "each other's dependency waits; run several streams in one process instead (--streams)")
+        if rank == 0:
+            print(f"bench.py: warning: {warning}", file=sys.stderr, flush=True)
     wg_used = 0  # k_pipeline workgroups (0: one per resident slot)
     if share > 1:
         cus = torch.cuda.get_device_properties(local).multi_processor_count
         wg_used = max(1, cus // share)
         enc.set_pipeline(wg_used, 2, 64)
-    outputs = []
+
+    def encode(lo, hi, collect):
+        if K == 1:
+            return [enc.encode_batch_device(ptrs[0][lo:hi], collect=collect)]
+        return Encoder.encode_streams_device(encs, [p[lo:hi] for p in ptrs], collect=collect)
+
+    def stats_sum():  # the launches (encoder 0) and every stream's per-picture path
+        st = [e.last_batch_stats() for e in encs]
+        return {k: st[0][k] if k in ("runs", "chain_walks", "waits_gave_up") else sum(x[k] for x in st) for k in STAT_KEYS}
+
+    outputs = [[] for _ in range(K)]
     warm = {k: 0 for k in STAT_KEYS}
     if args.warmup:  # same entry point as the timed frames (warms the pipelined path and its buffers)
-        outputs += [r.annexb() for r in enc.encode_batch_device(ptrs[:args.warmup])]
-        warm = enc.last_batch_stats()
+        for si, rs in enumerate(encode(0, args.warmup, True)):
+            outputs[si] += [r.annexb() for r in rs]
+        warm = stats_sum()
     enc.set_timing(True)
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    out_bytes = enc.encode_batch_device(ptrs[args.warmup:], collect=False)
+    out_bytes = sum(encode(args.warmup, n_frames, False))
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = dist.max_over_ranks(time.perf_counter() - t0)
     ms = enc.timing_ms()
     mb_ms, mb_launches = ms[1], enc.last_mb_launches()  # the (last) pipelined launch
-    stats = enc.last_batch_stats()
+    stats = stats_sum()
     # how every rank's calls ran (fallbacks to the per-picture path would show here), summed over ranks
     tot = dist.sum_over_ranks([stats[k] for k in STAT_KEYS] + [warm["fallbacks"] + warm["waits_gave_up"] + warm["per_picture"]])
     pipeline = dict(zip(STAT_KEYS, tot[:len(STAT_KEYS)]))
     pipeline["warmup_off_pipeline"] = tot[-1]
-    pipeline["scope"] = "timed call (hl_amd_last_batch_stats), summed over ranks; warmup_off_pipeline = warm-up pictures not coded by a clean run"
+    pipeline["scope"] = ("timed call (hl_amd_last_batch_stats), summed over ranks (runs: launches); warmup_off_pipeline = "
+                         "warm-up pictures not coded by a clean run")
     # bit-exactness of everything this rank encoded, outside the timed region
-    outputs += [r.annexb() for r in enc.last_batch_results()]
-    bitexact = check_bitexact(outputs, seed)
-    # every rank joins the collective (-1: no reference MD5s cover this rank's stream)
+    bitexact = True
+    for si, e in enumerate(encs):
+        outputs[si] += [r.annexb() for r in e.last_batch_results()]
+        b = check_bitexact(outputs[si], seeds[si])
+        bitexact = None if b is None or bitexact is None else (bitexact and b)
+    # every rank joins the collective (-1: no reference MD5s cover this rank's streams)
     ex = dist.min_over_ranks(-1 if bitexact is None else (1 if bitexact else 0))
     bitexact_all = None if ex < 0 else ex
-    # pictures of the last pipelined launch: runs span GOPs, up to MAX_RUN pictures each
+    # pictures of the last pipelined launch (per stream): runs span GOPs, up to MAX_RUN pictures each
     run_frames = (args.steps - 1) % MAX_RUN + 1 if mb_launches == 1 else 1
 
     # the HBM-bound kernel of the path on its own: quarter-pel planes of a
@@ -498,26 +525,26 @@ def main():
 
     base = None
     if rank == 0 and not args.no_cpu_baseline:  # after the timed region, on rank 0 only
-        base = cpu_baseline(frames_host, min(args.cpu_frames, n_frames), args.warmup, args.steps)
+        base = cpu_baseline(frames_host[0], min(args.cpu_frames, n_frames), args.warmup, args.steps)
 
     if rank == 0:
-        total = world * args.steps
+        total = world * K * args.steps
         fps = total / elapsed
         nmb = (W // 16) * (H // 16)
         # dominant kernel: k_pipeline (one launch per run of pictures);
         # algorithmic bytes per launch = 2752 B x MBs per launch
         avg_launch_s = (mb_ms / 1e3) / mb_launches
-        bytes_per_launch = BYTES_PER_MB * nmb * run_frames / mb_launches
+        bytes_per_launch = BYTES_PER_MB * nmb * run_frames * K / mb_launches
         achieved = bytes_per_launch / avg_launch_s / 1e9
         from hartallo_amd import _lib
 
-        pmc, pmc_note = load_pmc(getattr(_lib, "LOADED_PATH", None) or _lib.LIB_PATH, args.warmup, args.steps, wg_used, share)
+        pmc, pmc_note = load_pmc(getattr(_lib, "LOADED_PATH", None) or _lib.LIB_PATH, args.warmup, args.steps, wg_used, share * K)
         # the achieved macroblock latency along the run's critical path, and
         # VALU issue against one wave64 VALU instruction per SIMD per cycle
         cp_steps = critical_path_steps(run_frames, W // 16, H // 16) if mb_launches == 1 else None
         cp_us = round(avg_launch_s * 1e6 / cp_steps, 2) if cp_steps else None
         cus = torch.cuda.get_device_properties(local).multi_processor_count
-        valu_util = (round(pmc["valu_insts_per_mb"] * nmb * run_frames / avg_launch_s / (4 * cus * SHADER_CLOCK_HZ), 4)
+        valu_util = (round(pmc["valu_insts_per_mb"] * nmb * run_frames * K / avg_launch_s / (4 * cus * SHADER_CLOCK_HZ), 4)
                      if pmc and mb_launches == 1 else None)
         line = {
             "metric": "1080p encoded frames/sec (bit-exact) at 1/2/4/8 MI355X; macroblocks/sec/GPU",
@@ -533,8 +560,10 @@ def main():
             "dtype": "u8/int32",
             "data": "synthetic (hartallo_amd.synth, seeded per rank)",
             "config": {"workload": "1920x1088 YUV420 IPPP GOP30 QP28 ME16 deblock, one stream per GPU, frame-pipelined", "width": W, "height": H,
-                       "qp": QP, "me_range": ME_RANGE, "deblock": DEBLOCK, "gop": GOP, "parallelism": f"streams{world}", "streams_per_gpu": share},
+                       "qp": QP, "me_range": ME_RANGE, "deblock": DEBLOCK, "gop": GOP, "parallelism": f"streams{world * K}",
+                       "streams_per_gpu": share * K, "streams_per_process": K},
             "mb_per_s_per_gpu": round(fps / world * share * nmb, 1),
+            "warning": warning,
             "bitexact": bitexact_all if bitexact_all is None else bool(bitexact_all),
             "bitexact_check": "every frame of every rank (warm-up and timed) vs the reference encoder's per-frame MD5s "
                               "(tests/golden/bench_golden.json, oracle/_ref/ref_enc on the same synthetic stream)",
@@ -542,7 +571,7 @@ def main():
             "bitstream_bytes_per_frame": round(out_bytes / args.steps, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": round(pmc["traffic_bytes_per_mb"] * nmb * run_frames) if pmc and mb_launches == 1 else None,
+                         "traffic": round(pmc["traffic_bytes_per_mb"] * nmb * run_frames * K) if pmc and mb_launches == 1 else None,
                          "kernel": "k_pipeline", "avg_launch_us": round(avg_launch_s * 1e6, 2),
                          "frames_per_launch": run_frames,
                          "note": "latency-bound MB wavefront, frames pipelined; achieved = 2752 B/MB x MBs per launch / launch time",
@@ -562,7 +591,8 @@ def main():
             "cpu_baseline": base,
         }
         print(json.dumps(line), flush=True)
-    enc.close()
+    for e in encs:
+        e.close()
     dist.shutdown()
 
 

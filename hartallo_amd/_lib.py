@@ -34,6 +34,7 @@ EXPORTED_SYMBOLS = (
     "hl_amd_encode",
     "hl_amd_encode_device",
     "hl_amd_encode_batch",
+    "hl_amd_encode_streams",
     "hl_amd_set_pipeline",
     "hl_amd_set_rate_control",
     "hl_amd_last_qp",
@@ -138,6 +139,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     pp = ctypes.POINTER(ctypes.c_void_p)
     lib.hl_amd_encode_batch.argtypes = [vp, i32, pp, pp, pp, ctypes.POINTER(_Result)]
     lib.hl_amd_encode_batch.restype = i32
+    if hasattr(lib, "hl_amd_encode_streams"):  # (absent from builds before round 4 loaded through HL_LIB)
+        lib.hl_amd_encode_streams.argtypes = [ctypes.POINTER(vp), i32, i32, pp, pp, pp, ctypes.POINTER(_Result)]
+        lib.hl_amd_encode_streams.restype = i32
     lib.hl_amd_set_pipeline.argtypes = [vp, i32, i32, i32]
     lib.hl_amd_set_pipeline.restype = i32
     lib.hl_amd_set_rate_control.argtypes = [vp, ctypes.c_int64, i32, i32, i32, i32, i32]
@@ -280,6 +284,29 @@ class Encoder:
             raise HlAmdError(rc, "hl_amd_encode_batch")
         self._last_batch = res  # the results stay valid until the next encode call
         return [self._result(r) for r in res] if collect else sum(r.data_size for r in res)
+
+    @staticmethod
+    def encode_streams_device(encoders, ptrs, collect: bool = True):
+        """hl_amd_encode_streams: frames of several streams in shared
+        pipelined runs; encoders[s] codes ptrs[s] (each a list of (y, u, v)
+        device pointers, the same length).  Returns per stream its results (or,
+        with collect=False, its total bitstream bytes)."""
+        S, n = len(encoders), len(ptrs[0])
+        assert len(ptrs) == S and all(len(p) == n for p in ptrs)
+        lib = encoders[0].lib
+        hs = (ctypes.c_void_p * S)(*[e._h for e in encoders])
+        flat = [f for p in ptrs for f in p]
+        arr = [(ctypes.c_void_p * (S * n))(*[f[i] for f in flat]) for i in range(3)]
+        res = (_Result * (S * n))()
+        rc = lib.hl_amd_encode_streams(hs, S, n, arr[0], arr[1], arr[2], res)
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_encode_streams")
+        out = []
+        for s, e in enumerate(encoders):
+            rs = res[s * n:(s + 1) * n]
+            e._last_batch = rs
+            out.append([e._result(r) for r in rs] if collect else sum(r.data_size for r in rs))
+        return out
 
     def last_batch_results(self):
         """The results of the last encode_batch_device call (also after

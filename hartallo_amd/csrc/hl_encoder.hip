@@ -256,27 +256,26 @@ __device__ void task_filters(const PipeFrame& PF, Shared& S, int x, int y, int m
 __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
 {
     const int nmb = mbw * mbh, i = blockIdx.x * 256 + threadIdx.x;
-    const bool h0 = P.helpers && !P.fr[0].F.is_intra;  // the first task's intra helper
     if (i < P.nframes * nmb) {
-        const int f = i / nmb, a = i - f * nmb;
+        const int f = i / nmb, a = i - f * nmb, k = f % P.spp;  // picture k of its stream
         int d[3][3];
-        P.cnt[i] = task_deps(f, a % mbw, a / mbw, mbw, mbh, P.reach, d);
+        P.cnt[i] = task_deps(k, a % mbw, a / mbw, mbw, mbh, P.reach, d);
         P.done[i] = 0;
-        P.queue[i] = i == 0 ? 1 : 0;
+        P.queue[i] = k == 0 && a == 0 ? 1 : 0;  // every stream's first task
         P.claim[i] = 0;
         P.hstate[i] = HS_FREE;
-        P.hq[i] = i == 0 && h0 ? 1 : 0;
+        P.hq[i] = 0;
     }
     if (i < P.nframes) {
         P.head[i] = 0;
-        P.tail[i] = i == 0 ? 1 : 0;
+        P.tail[i] = i % P.spp == 0 ? 1 : 0;
     }
+    if (i < P.nstreams) P.oldest[i] = 0;
     if (i == 0) {
         *P.hq_head = 0;
-        *P.hq_tail = h0 ? 1 : 0;
+        *P.hq_tail = 0;
     }
     if (i == 0) {
-        *P.oldest = 0;
         for (int k = 0; k < 5; ++k) P.err[k] = 0;  // give-ups, chain walks, helper I4 kept / rejected / taken over
     }
 }
@@ -298,17 +297,24 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh)
     const int lane = threadIdx.x & 63;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-        const int o = ld_relaxed(P.oldest);
-        if (o >= P.nframes) return -1;
-        const int w = min(P.window, P.nframes - o);
+        // lane = (stream lane % S, its picture oldest + lane / S): the window
+        // of each stream's first unfinished pictures
+        const int S = P.nstreams;
+        int ol = 0;
+        if (lane < S) ol = ld_relaxed(P.oldest + lane);
+        if (__ballot(lane < S && ol < P.spp) == 0) return -1;  // every stream finished
+        const int sj = lane % S, j = lane / S;
+        const int k = __shfl(ol, sj, 64) + j;
+        const bool in = j < max(1, P.window / S) && k < P.spp;
+        const int fl = sj * P.spp + k;
         int h = 0, t = 0;
-        if (lane < w) {
-            h = ld_relaxed(P.head + o + lane);
-            t = ld_relaxed(P.tail + o + lane);
+        if (in) {
+            h = ld_relaxed(P.head + fl);
+            t = ld_relaxed(P.tail + fl);
         }
         int i0 = -1, hh = 0, v = 0;
         if (P.hop < 0) {
-            const unsigned long long bal = __ballot(lane < w && h < t);
+            const unsigned long long bal = __ballot(in && h < t);
             if (bal) {
                 i0 = __ffsll((long long)bal) - 1;
                 hh = __builtin_amdgcn_readlane(h, i0);
@@ -317,11 +323,11 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh)
         else {
             // the head entries themselves (0: pushed, not yet written)
             int q = 0;
-            if (lane < w && h < t) q = ld_relaxed(P.queue + (o + lane) * nmb + h);
+            if (in && h < t) q = ld_relaxed(P.queue + fl * nmb + h);
             int key = -1;
             if (q > 0) {
                 const int a = q - 1, y = a / mbw, x = a - y * mbw;
-                key = (((mbw - 1 - x) + 2 * (mbh - 1 - y) - P.hop * lane + 4096) << 6) | (63 - lane);
+                key = (((mbw - 1 - x) + 2 * (mbh - 1 - y) - P.hop * j + 4096) << 6) | (63 - lane);
             }
             for (int s = 1; s < 64; s <<= 1) key = max(key, __shfl_xor(key, s, 64));
             key = __builtin_amdgcn_readfirstlane(key);
@@ -333,7 +339,7 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh)
             // else: empty, or only pushes between their tail and slot stores
         }
         if (i0 >= 0) {
-            const int f = o + i0;
+            const int f = __builtin_amdgcn_readlane(fl, i0);
             int r = 0;
             if (lane == 0 && atomicCAS(P.head + f, hh, hh + 1) == hh) {
                 r = v;
@@ -526,14 +532,15 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         __syncthreads();
         if (tid < 64) {
 #if HL_HOSTREC_SYS
-            if (P.progress) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // host-visible records (system scope)
+            if (PF.progress) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // host-visible records (system scope)
             else
 #endif
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, HL_REL_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (tid == 0) st_relaxed(P.done + t, 1);
             int fo = 0, xo = 0, yo = 0;
-            const int ns = task_succ(f, x, y, mbw, mbh, P.reach, P.nframes, -1, fo, xo, yo);
+            const int fk = f % P.spp, fb = f - fk;  // picture fk of the stream whose first slot is fb
+            const int ns = task_succ(fk, x, y, mbw, mbh, P.reach, P.spp, -1, fo, xo, yo);
             // every successor this task makes ready is queued (with its intra
             // helper, in P pictures) -- except the first one, which this
             // workgroup claims and runs next without a pop (workgroup 0 keeps
@@ -541,7 +548,8 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
             // on the same queue head, pops were a serial bottleneck
             int ready = -1;  // this lane's successor (one per lane: ns <= 64)
             for (int j = tid; j < ns; j += 64) {
-                task_succ(f, x, y, mbw, mbh, P.reach, P.nframes, j, fo, xo, yo);
+                task_succ(fk, x, y, mbw, mbh, P.reach, P.spp, j, fo, xo, yo);
+                fo += fb;
                 const int a = yo * mbw + xo;
                 if (__hip_atomic_fetch_add(P.cnt + fo * nmb + a, -1, HL_CNT_ORDER, __HIP_MEMORY_SCOPE_AGENT) == 1) ready = fo * nmb + a;
             }
@@ -568,12 +576,12 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
                 }
             }
             if (keep >= 0) next_task = __builtin_amdgcn_readlane(next_task, keep);
-            // pictures finish in order: the last MB depends on every other one
-            // and on the previous picture's last MB
+            // a stream's pictures finish in order: the last MB depends on every
+            // other one and on the previous picture's last MB
             if (tid == 0 && addr == nmb - 1) {
-                __hip_atomic_store(P.oldest, f + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                // every record of picture f is in host memory (each task released at system scope)
-                if (P.progress) __hip_atomic_store(P.progress, f + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(P.oldest + f / P.spp, fk + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                // every record of the picture is in host memory (each task released at system scope)
+                if (PF.progress) __hip_atomic_store(PF.progress, fk + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (P.pub_clock) P.pub_clock[f] = wall_clock64();
             }
         }
@@ -629,6 +637,7 @@ struct hl_amd_encoder_s {
     int pipe_wg, reach, window;  // workgroups (0: one per resident slot), R in MBs, pictures looked at
     int hop;                     // pop order (PipeArgs::hop)
     int bcap;                    // pictures the run buffers hold
+    int scap = 0;                // picture slots the scheduler state holds (ensure_sched)
     uint8_t *d_bpic, *d_bpl;     // per picture: recon (Y|U|V), quarter-pel planes
     MbRecord *d_brec, *h_brec, *dh_brec;  // dh_brec: device address of the pinned h_brec (the run writes it)
     int32_t* h_progress;                  // pinned: pictures of the running run whose records are in h_brec
@@ -980,7 +989,8 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
 // ---------------------------------------------------------------------------
 // pipelined runs of P pictures
 // ---------------------------------------------------------------------------
-constexpr int kMaxRun = 128;  // pictures per pipelined launch (bench.py MAX_RUN)
+constexpr int kMaxRun = 128;     // pictures per pipelined launch and stream (bench.py MAX_RUN)
+constexpr int kMaxStreams = 16;  // streams per launch (hl_amd_encode_streams)
 
 static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
 {
@@ -1014,28 +1024,17 @@ static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
     dfree(e->d_brec);
     dfree(e->d_bchain);
     dfree(e->d_bspec);
-    dfree(e->d_pf);
-    dfree(e->d_cnt);
-    dfree(e->d_done);
-    dfree(e->d_queue);
-    dfree(e->d_head);
-    dfree(e->d_hstate);
     dfree(e->d_ispec);
     hfree(e->h_brec);
     hfree(e->h_bchain);
-    hfree(e->h_pf);
     e->bcap = 0;
     hipError_t r;
     if ((r = hipMalloc(&e->d_bpic, pic * n)) || (r = hipMalloc(&e->d_bpl, 4 * e->plsz * n)) ||
         (drec && (r = hipMalloc(&e->d_brec, drec * nmb * n))) || (r = hipMalloc(&e->d_bchain, sizeof(MbChain) * nmb * n)) ||
-        (r = hipMalloc(&e->d_bspec, sizeof(int32_t) * e->mbh * n)) || (r = hipMalloc(&e->d_pf, sizeof(PipeFrame) * n)) ||
+        (r = hipMalloc(&e->d_bspec, sizeof(int32_t) * e->mbh * n)) ||
         (r = hipHostMalloc(&e->h_brec, sizeof(MbRecord) * nmb * n, hipHostMallocDefault)) ||
         (r = hipHostMalloc(&e->h_bchain, sizeof(MbChain) * nmb * n, hipHostMallocDefault)) ||
-        (r = hipHostMalloc(&e->h_pf, sizeof(PipeFrame) * n, hipHostMallocDefault)) ||
-        (r = hipMalloc(&e->d_cnt, sizeof(int32_t) * 2 * nmb * n)) || (r = hipMalloc(&e->d_done, sizeof(int32_t) * nmb * n)) ||
-        (r = hipMalloc(&e->d_queue, sizeof(int32_t) * 2 * nmb * n)) || (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * n + 3))) ||
-        (r = hipMalloc(&e->d_hstate, sizeof(int32_t) * nmb * n)) || (r = hipMalloc(&e->d_ispec, sizeof(IntraSpec) * nmb)) ||
-        (r = hipHostGetDevicePointer((void**)&e->dh_brec, e->h_brec, 0)))
+        (r = hipMalloc(&e->d_ispec, sizeof(IntraSpec) * nmb)) || (r = hipHostGetDevicePointer((void**)&e->dh_brec, e->h_brec, 0)))
         return r;
     if (!e->d_err && (r = hipMalloc(&e->d_err, sizeof(int32_t) * 8))) return r;
     // defined contents from the start (nothing reads a run buffer before the
@@ -1048,6 +1047,38 @@ static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
     if ((r = hipMemcpyAsync(e->d_bspec, spec.data(), sizeof(int32_t) * spec.size(), hipMemcpyHostToDevice, e->stream))) return r;
     if ((r = hipStreamSynchronize(e->stream))) return r;
     e->bcap = n;
+    return hipSuccess;
+}
+
+// The scheduler state of a pipelined launch (hl_pipeline.h) for `slots`
+// pictures (of one or several streams), owned by the encoder that launches.
+static hipError_t ensure_sched(hl_amd_encoder_t* e, int slots)
+{
+    if (slots <= e->scap) return hipSuccess;
+    const size_t nmb = e->nmb;
+    if (slots > 1) slots = std::max(slots, kMaxRun);
+    auto dfree = [](auto*& p) {
+        (void)hipFree(p);
+        p = nullptr;
+    };
+    dfree(e->d_pf);
+    dfree(e->d_cnt);
+    dfree(e->d_done);
+    dfree(e->d_queue);
+    dfree(e->d_head);
+    dfree(e->d_hstate);
+    (void)hipHostFree(e->h_pf);
+    e->h_pf = nullptr;
+    e->scap = 0;
+    hipError_t r;
+    if ((r = hipMalloc(&e->d_pf, sizeof(PipeFrame) * slots)) || (r = hipHostMalloc(&e->h_pf, sizeof(PipeFrame) * slots, hipHostMallocDefault)) ||
+        (r = hipMalloc(&e->d_cnt, sizeof(int32_t) * 2 * nmb * slots)) || (r = hipMalloc(&e->d_done, sizeof(int32_t) * nmb * slots)) ||
+        (r = hipMalloc(&e->d_queue, sizeof(int32_t) * 2 * nmb * slots)) ||
+        (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * slots + kMaxStreams + 2))) ||
+        (r = hipMalloc(&e->d_hstate, sizeof(int32_t) * nmb * slots)))
+        return r;
+    if (!e->d_err && (r = hipMalloc(&e->d_err, sizeof(int32_t) * 8))) return r;
+    e->scap = slots;
     return hipSuccess;
 }
 
@@ -1102,9 +1133,9 @@ static void store_result(hl_amd_encoder_t* e, int i, const hl_amd_result_t& src,
 // threads serialise its pictures in parallel, each with its own scratch
 // buffers, into bout[base + k].  Returns the bytes written per picture
 // (start code included; 0 = output buffer too short).
-static std::vector<size_t> write_run(hl_amd_encoder_t* e, int m, int base, const std::atomic<bool>* abort = nullptr)
+static std::vector<size_t> write_run(hl_amd_encoder_t* e, int m, int base, const std::atomic<bool>* abort = nullptr, int nw = 0)
 {
-    const int n = std::max(1, std::min(m, e->nwriters));
+    const int n = std::max(1, std::min(m, nw > 0 ? nw : e->nwriters));
     const StreamParams sp{e->W, e->H, e->p.qp, e->p.deblock};
     if ((int)e->wscratch.size() < n) {
         e->wscratch.resize(n);
@@ -1144,137 +1175,155 @@ static std::vector<size_t> write_run(hl_amd_encoder_t* e, int m, int base, const
     return size;
 }
 
-// m consecutive pictures (IDR and P, in GOP order) in one pipelined launch
-// (a single picture too: one persistent launch instead of a launch per
-// anti-diagonal); falls back to the per-picture path when a bounded wait gave
-// up or a row-start speculation turned out to matter (resolve_chain makes the
-// latter exact inside a run).  Under rate control m is 1 and the picture's QP
-// comes from the rate controller.
-static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, const uint8_t* const* U, const uint8_t* const* V,
-                          hl_amd_result_t* res, int base)
+// m consecutive pictures (IDR and P, in GOP order) of each of S streams
+// (encoders es[s], frames Y[s][k]; the same picture size) in one pipelined
+// launch (a single picture too: one persistent launch instead of a launch
+// per anti-diagonal): the streams' tasks share the device's workgroups, so
+// one stream's ramp and tail overlap the others' work.  Each stream's
+// results are those of its own run.  A stream falls back to the per-picture
+// path when a row-start speculation turned out to matter (resolve_chain
+// makes that exact inside a run), every stream when a bounded wait gave up.
+// Under rate control S and m are 1 and the picture's QP comes from the rate
+// controller.
+static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uint8_t* const* const* Y, const uint8_t* const* const* U,
+                            const uint8_t* const* const* V, hl_amd_result_t* const* res, int base)
 {
-    if (e->rc && m != 1) return HL_AMD_ERROR_INVALID_STATE;
-    HL_HIP_CHECK(ensure_batch(e, m));
-    // picture types, idr_pic_id and QP of the run, as m encode_frame calls would set them
-    e->run_intra.resize(m);
-    e->run_idr_id.resize(m);
-    e->run_qp.assign(m, e->p.qp);
-    e->run_bits.assign(m, SliceBits{});
-    for (int k = 0, gl = e->gop_left, idr = e->idr_pic_id; k < m; ++k) {
-        const bool intra = gl <= 0;
-        if (intra) gl = e->p.gop_size;
-        e->run_intra[k] = intra;
-        e->run_idr_id[k] = idr;
-        idr += intra;
-        --gl;
-    }
-    // rate control picks the picture's QP before it is coded (hl_codec_264.c:719-742)
-    if (e->rc) e->run_qp[0] = e->rc->begin_picture(e->run_intra[0] != 0);
-    e->run_fallback = false;
-    e->run_aborted.store(false, std::memory_order_release);
-    const size_t pic = (size_t)e->W * e->H * 3 / 2, nmb = e->nmb;
-    uint8_t** ref0 = e->d_pic[e->cur ^ 1];
-    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[0], e->stream));
-    {  // quarter-pel planes of the picture before the run
-        launch_planes(e, ref0[0]);
+    hl_amd_encoder_t* e0 = es[0];
+    const size_t pic = (size_t)e0->W * e0->H * 3 / 2, nmb = e0->nmb;
+    const int slots = S * m;
+    for (int si = 0; si < S; ++si) {
+        hl_amd_encoder_t* e = es[si];
+        if (e->rc && (m != 1 || S != 1)) return HL_AMD_ERROR_INVALID_STATE;
+        HL_HIP_CHECK(ensure_batch(e, m));
+        // picture types, idr_pic_id and QP of the run, as m encode_frame calls would set them
+        e->run_intra.resize(m);
+        e->run_idr_id.resize(m);
+        e->run_qp.assign(m, e->p.qp);
+        e->run_bits.assign(m, SliceBits{});
+        for (int k = 0, gl = e->gop_left, idr = e->idr_pic_id; k < m; ++k) {
+            const bool intra = gl <= 0;
+            if (intra) gl = e->p.gop_size;
+            e->run_intra[k] = intra;
+            e->run_idr_id[k] = idr;
+            idr += intra;
+            --gl;
+        }
+        // rate control picks the picture's QP before it is coded (hl_codec_264.c:719-742)
+        if (e->rc) e->run_qp[0] = e->rc->begin_picture(e->run_intra[0] != 0);
+        e->run_fallback = false;
+        e->run_aborted.store(false, std::memory_order_release);
+        if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[0], e->stream));
+        launch_planes(e, e->d_pic[e->cur ^ 1][0]);  // quarter-pel planes of the picture before the run
         HL_HIP_CHECK(hipGetLastError());
+        if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[1], e->stream));
+        HL_HIP_CHECK(hipMemcpyAsync(e->d_snap, e->d_st, sizeof(MbState) * nmb, hipMemcpyDeviceToDevice, e->stream));
     }
-    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[1], e->stream));
-    HL_HIP_CHECK(hipMemcpyAsync(e->d_snap, e->d_st, sizeof(MbState) * nmb, hipMemcpyDeviceToDevice, e->stream));
-    HL_HIP_CHECK(hipStreamSynchronize(e->stream));  // h_pf may still be read by a previous copy
-    for (int k = 0; k < m; ++k) {
-        PipeFrame& pf = e->h_pf[k];
-        pf = PipeFrame{};
-        FrameArgs& F = pf.F;
-        F = frame_args(e, e->run_intra[k] != 0, e->run_qp[k]);
-        uint8_t* cur = e->d_bpic + pic * k;
-        F.src[0] = Y[k];
-        F.src[1] = U[k];
-        F.src[2] = V[k];
-        F.cur[0] = cur;
-        F.cur[1] = cur + (size_t)e->W * e->H;
-        F.cur[2] = cur + (size_t)e->W * e->H * 5 / 4;
-        if (k == 0)
-            for (int c = 0; c < 3; ++c) F.ref[c] = ref0[c];
-        else {
-            const uint8_t* rp = e->d_bpic + pic * (k - 1);
-            F.ref[0] = rp;
-            F.ref[1] = rp + (size_t)e->W * e->H;
-            F.ref[2] = rp + (size_t)e->W * e->H * 5 / 4;
-        }
-        const uint8_t* plb = k == 0 ? e->d_pl[0] : e->d_bpl + 4 * e->plsz * (k - 1);
-        for (int i = 0; i < 4; ++i) F.pl[i] = plb + i * e->plsz;
-        F.rec = e->d_brec ? e->d_brec + nmb * k : nullptr;
-        F.hrec = e->dh_brec + nmb * k;  // the slice writers read the records from host memory during the run
+    HL_HIP_CHECK(ensure_sched(e0, slots));
+    for (int si = 0; si < S; ++si) HL_HIP_CHECK(hipStreamSynchronize(es[si]->stream));  // (h_pf may still be read by a previous copy)
+    for (int si = 0; si < S; ++si) {
+        hl_amd_encoder_t* e = es[si];
+        uint8_t** ref0 = e->d_pic[e->cur ^ 1];
+        int32_t* d_progress = nullptr;
+        HL_HIP_CHECK(hipHostGetDevicePointer((void**)&d_progress, e->h_progress, 0));
+        for (int k = 0; k < m; ++k) {
+            const int slot = si * m + k;
+            PipeFrame& pf = e0->h_pf[slot];
+            pf = PipeFrame{};
+            FrameArgs& F = pf.F;
+            F = frame_args(e, e->run_intra[k] != 0, e->run_qp[k]);
+            uint8_t* cur = e->d_bpic + pic * k;
+            F.src[0] = Y[si][k];
+            F.src[1] = U[si][k];
+            F.src[2] = V[si][k];
+            F.cur[0] = cur;
+            F.cur[1] = cur + (size_t)e->W * e->H;
+            F.cur[2] = cur + (size_t)e->W * e->H * 5 / 4;
+            if (k == 0)
+                for (int c = 0; c < 3; ++c) F.ref[c] = ref0[c];
+            else {
+                const uint8_t* rp = e->d_bpic + pic * (k - 1);
+                F.ref[0] = rp;
+                F.ref[1] = rp + (size_t)e->W * e->H;
+                F.ref[2] = rp + (size_t)e->W * e->H * 5 / 4;
+            }
+            const uint8_t* plb = k == 0 ? e->d_pl[0] : e->d_bpl + 4 * e->plsz * (k - 1);
+            for (int i = 0; i < 4; ++i) F.pl[i] = plb + i * e->plsz;
+            F.rec = e->d_brec ? e->d_brec + nmb * k : nullptr;
+            F.hrec = e->dh_brec + nmb * k;  // the slice writers read the records from host memory during the run
 #if defined(HL_DIAG_INPUTS)
-        F.rec_dev = 1;
+            F.rec_dev = 1;
 #else
-        F.rec_dev = 0;
+            F.rec_dev = 0;
 #endif
-        F.chain = e->d_bchain + nmb * k;
-        F.spec = e->d_bspec + e->mbh * k;
-        F.ref_done = k == 0 ? nullptr : e->d_done + (k - 1) * nmb;
-        F.ref_epoch = 1;
-        F.perr = e->d_err;
-        F.run_done = e->d_done;
-        F.run_chain = e->d_bchain;
-        F.run_pos = k;
-        F.carry_in = e->chain_end;
-        if (e->helpers && !e->run_intra[k]) {
-            F.ispec = e->d_ispec;
-            F.hstate = e->d_hstate + nmb * k;
+            F.chain = e->d_bchain + nmb * k;
+            F.spec = e->d_bspec + e->mbh * k;
+            F.ref_done = k == 0 ? nullptr : e0->d_done + (slot - 1) * nmb;
+            F.ref_epoch = 1;
+            F.perr = e0->d_err;
+            F.run_done = e0->d_done + (size_t)si * m * nmb;  // this stream's picture 0
+            F.run_chain = e->d_bchain;
+            F.run_pos = k;
+            F.carry_in = e->chain_end;
+            if (e0->helpers && !e->run_intra[k]) {
+                F.ispec = e->d_ispec;
+                F.hstate = e0->d_hstate + nmb * slot;
+            }
+            pf.D.W = e->W;
+            pf.D.H = e->H;
+            pf.D.Wc = e->Wc;
+            pf.D.mbw = e->mbw;
+            pf.D.qp = F.qp;
+            pf.D.qpc = F.qpc;
+            for (int c = 0; c < 3; ++c) pf.D.pic[c] = F.cur[c];
+            pf.D.st = e->d_st;
+            pf.pl_out = e->d_bpl + 4 * e->plsz * k;
+            pf.deblock = e->p.deblock;
+            pf.progress = d_progress;
         }
-        pf.D.W = e->W;
-        pf.D.H = e->H;
-        pf.D.Wc = e->Wc;
-        pf.D.mbw = e->mbw;
-        pf.D.qp = F.qp;
-        pf.D.qpc = F.qpc;
-        for (int c = 0; c < 3; ++c) pf.D.pic[c] = F.cur[c];
-        pf.D.st = e->d_st;
-        pf.pl_out = e->d_bpl + 4 * e->plsz * k;
-        pf.deblock = e->p.deblock;
+        __atomic_store_n(e->h_progress, 0, __ATOMIC_RELEASE);
+        e->run_live.store(1, std::memory_order_release);
     }
-    HL_HIP_CHECK(hipMemcpyAsync(e->d_pf, e->h_pf, sizeof(PipeFrame) * m, hipMemcpyHostToDevice, e->stream));
-    PipeArgs P;
-    P.fr = e->d_pf;
-    P.nframes = m;
-    P.reach = e->reach;
-    P.window = e->window;
-    P.hop = e->hop;
-    P.cnt = e->d_cnt;
-    P.claim = e->d_cnt + nmb * m;
-    P.done = e->d_done;
-    P.queue = e->d_queue;
-    P.hstate = e->d_hstate;
-    P.helpers = e->helpers ? 1 : 0;
-    P.hq = e->d_queue + nmb * m;
-    P.hq_head = e->d_head + 2 * m + 1;
-    P.hq_tail = e->d_head + 2 * m + 2;
-    P.head = e->d_head;
-    P.tail = e->d_head + m;
-    P.oldest = e->d_head + 2 * m;
-    P.err = e->d_err;
-    int32_t* d_progress = nullptr;
-    HL_HIP_CHECK(hipHostGetDevicePointer((void**)&d_progress, e->h_progress, 0));
-    __atomic_store_n(e->h_progress, 0, __ATOMIC_RELEASE);
-    e->run_live.store(1, std::memory_order_release);
     struct RunLive {  // cleared on every way out of the run (an error return included)
-        std::atomic<int>& r;
-        ~RunLive() { r.store(0, std::memory_order_release); }
-    } run_live_guard{e->run_live};
-    P.progress = d_progress;
+        hl_amd_encoder_t* const* es;
+        int S;
+        ~RunLive()
+        {
+            for (int si = 0; si < S; ++si) es[si]->run_live.store(0, std::memory_order_release);
+        }
+    } run_live_guard{es, S};
+    HL_HIP_CHECK(hipMemcpyAsync(e0->d_pf, e0->h_pf, sizeof(PipeFrame) * slots, hipMemcpyHostToDevice, e0->stream));
+    PipeArgs P;
+    P.fr = e0->d_pf;
+    P.nframes = slots;
+    P.spp = m;
+    P.nstreams = S;
+    P.reach = e0->reach;
+    P.window = e0->window;
+    P.hop = e0->hop;
+    P.cnt = e0->d_cnt;
+    P.claim = e0->d_cnt + nmb * slots;
+    P.done = e0->d_done;
+    P.queue = e0->d_queue;
+    P.hstate = e0->d_hstate;
+    P.helpers = e0->helpers ? 1 : 0;
+    P.hq = e0->d_queue + nmb * slots;
+    P.head = e0->d_head;
+    P.tail = e0->d_head + slots;
+    P.oldest = e0->d_head + 2 * slots;
+    P.hq_head = e0->d_head + 2 * slots + kMaxStreams;
+    P.hq_tail = e0->d_head + 2 * slots + kMaxStreams + 1;
+    P.err = e0->d_err;
     static const bool trace = getenv("HL_AMD_TRACE_WRITERS") != nullptr;
     static unsigned long long* h_clock = nullptr;
     P.pub_clock = nullptr;
-    if (trace) {
+    if (trace && slots <= 1024) {
         if (!h_clock) HL_HIP_CHECK(hipHostMalloc((void**)&h_clock, sizeof(unsigned long long) * 1024, hipHostMallocCoherent));
         HL_HIP_CHECK(hipHostGetDevicePointer((void**)&P.pub_clock, h_clock, 0));
     }
-    k_pipe_init<<<(unsigned)((nmb * m + 255) / 256), 256, 0, e->stream>>>(P, e->mbw, e->mbh);
+    k_pipe_init<<<(unsigned)((nmb * slots + 255) / 256), 256, 0, e0->stream>>>(P, e0->mbw, e0->mbh);
     HL_HIP_CHECK(hipGetLastError());
     static const int env_wg = getenv("HL_AMD_PIPE_WG") ? atoi(getenv("HL_AMD_PIPE_WG")) : 0;  // experiments
-    int wgs = e->pipe_wg > 0 ? e->pipe_wg : env_wg;
+    int wgs = e0->pipe_wg > 0 ? e0->pipe_wg : env_wg;
     if (wgs <= 0) {  // one workgroup per resident slot of the device
         int dev = 0, cus = 0, occ = 0;
         HL_HIP_CHECK(hipGetDevice(&dev));
@@ -1282,137 +1331,169 @@ static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, c
         HL_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_pipeline, kMbThreads, 0));
         wgs = std::max(1, cus * occ);
     }
-    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[4], e->stream));
-    e->run_t0 = std::chrono::steady_clock::now();
-    k_pipeline<<<wgs, kMbThreads, 0, e->stream>>>(P, e->mbw, e->mbh);
+    if (e0->timing) HL_HIP_CHECK(hipEventRecord(e0->ev[4], e0->stream));
+    for (int si = 0; si < S; ++si) es[si]->run_t0 = std::chrono::steady_clock::now();
+    k_pipeline<<<wgs, kMbThreads, 0, e0->stream>>>(P, e0->mbw, e0->mbh);
     HL_HIP_CHECK(hipGetLastError());
-    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[5], e->stream));
+    if (e0->timing) HL_HIP_CHECK(hipEventRecord(e0->ev[5], e0->stream));
     // The kernel stores every finished MB's record into pinned host memory and
-    // counts finished pictures in a host-mapped word: writer threads serialise
-    // each picture's slice as soon as it is complete, while the run goes on.
-    // The chain records and the give-up counter come back after the run.
-    // bounded waits that gave up, resolve_chain walks: pinned, so that the
-    // copy is asynchronous (a copy into pageable memory blocks the host
-    // until the kernel ends, and with it the writers)
-    int32_t* errw = e->h_progress + 4;
-    HL_HIP_CHECK(hipMemcpyAsync(e->h_bchain, e->d_bchain, sizeof(MbChain) * nmb * m, hipMemcpyDeviceToHost, e->stream));
-    HL_HIP_CHECK(hipMemcpyAsync(errw, e->d_err, 5 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
-    if (e->timing) HL_HIP_CHECK(hipEventRecord(e->ev[2], e->stream));
-    std::atomic<bool> abort{false};
-    std::vector<size_t> wsize;
-    std::thread writers([&] { wsize = write_run(e, m, base, &abort); });
-    const hipError_t serr = hipStreamSynchronize(e->stream);
-    e->run_live.store(0, std::memory_order_release);
+    // counts each stream's finished pictures in a host-mapped word: writer
+    // threads serialise each picture's slice as soon as it is complete, while
+    // the run goes on.  The chain records and the give-up counter come back
+    // after the run (pinned: the copies are asynchronous -- a copy into
+    // pageable memory blocks the host until the kernel ends, and with it the
+    // writers).
+    int32_t* errw = e0->h_progress + 4;  // bounded waits that gave up, resolve_chain walks, helper counts
+    for (int si = 0; si < S; ++si)
+        HL_HIP_CHECK(hipMemcpyAsync(es[si]->h_bchain, es[si]->d_bchain, sizeof(MbChain) * nmb * m, hipMemcpyDeviceToHost, e0->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(errw, e0->d_err, 5 * sizeof(int32_t), hipMemcpyDeviceToHost, e0->stream));
+    if (e0->timing) HL_HIP_CHECK(hipEventRecord(e0->ev[2], e0->stream));
+    std::vector<std::atomic<bool>> abort(S);
+    std::vector<std::vector<size_t>> wsize(S);
+    std::vector<std::thread> writers;
+    for (int si = 0; si < S; ++si) {
+        abort[si] = false;
+        writers.emplace_back([&, si] { wsize[si] = write_run(es[si], m, base, &abort[si], std::max(1, es[si]->nwriters / S)); });
+    }
+    const hipError_t serr = hipStreamSynchronize(e0->stream);
+    for (int si = 0; si < S; ++si) es[si]->run_live.store(0, std::memory_order_release);
     const auto tw0 = std::chrono::steady_clock::now();
-    if (serr != hipSuccess || __atomic_load_n(e->h_progress, __ATOMIC_ACQUIRE) < m) abort = true;
-    writers.join();
-    if (e->timing) e->ms[3] = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - tw0).count();
-    if (trace)
-        for (int k = 0; k < m; ++k) fprintf(stderr, "picture %d published at device clock +%.2f ms\n", k, (h_clock[k] - h_clock[0]) * 1e-5);
+    bool aborted = false;
+    for (int si = 0; si < S; ++si)
+        if (serr != hipSuccess || __atomic_load_n(es[si]->h_progress, __ATOMIC_ACQUIRE) < m) {
+            abort[si] = true;
+            aborted = true;
+        }
+    for (auto& w : writers) w.join();
+    if (e0->timing) e0->ms[3] = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - tw0).count();
+    if (trace && P.pub_clock)
+        for (int f = 0; f < slots; ++f) fprintf(stderr, "picture %d published at device clock +%.2f ms\n", f, (h_clock[f] - h_clock[0]) * 1e-5);
     HL_HIP_CHECK(serr);
-    if (abort) {
-        fprintf(stderr, "hartallo_amd: pipelined run ended with %d of %d pictures published\n", __atomic_load_n(e->h_progress, __ATOMIC_ACQUIRE), m);
+    if (aborted) {
+        fprintf(stderr, "hartallo_amd: pipelined run ended before every picture was published\n");
         return HL_AMD_ERROR_SYSTEM;
     }
-    if (e->timing) {
-        (void)hipEventElapsedTime(&e->ms[0], e->ev[0], e->ev[1]);
-        (void)hipEventElapsedTime(&e->ms[1], e->ev[4], e->ev[5]);
-        (void)hipEventElapsedTime(&e->ms[2], e->ev[5], e->ev[2]);
+    if (e0->timing) {
+        (void)hipEventElapsedTime(&e0->ms[0], e0->ev[0], e0->ev[1]);
+        (void)hipEventElapsedTime(&e0->ms[1], e0->ev[4], e0->ev[5]);
+        (void)hipEventElapsedTime(&e0->ms[2], e0->ev[5], e0->ev[2]);
     }
     const int32_t err = errw[0];
-    e->chain_walks = errw[1];
-    e->mb_launches = 1;
-    e->reruns = 0;
-    ++e->calls_runs;
-    e->calls_gave_up += err;
-    e->calls_walks += errw[1];
-    e->helper_kept += errw[2];
-    e->helper_rejected += errw[3];
-    e->helper_self += errw[4];
     if (err) fprintf(stderr, "hartallo_amd: pipelined run: %d bounded waits gave up; re-encoding the run picture by picture\n", err);
-    int32_t carry = e->chain_end;
-    bool ok = err == 0;
-    for (int k = 0; k < m && ok; ++k) ok = validate_rows(e->h_bchain + nmb * k, e->mbw, e->mbh, 9, carry);
-    {  // diagnostics: HL_AMD_FORCE_FALLBACK=1 takes the fallback below for every run (tests)
-        const char* ff = getenv("HL_AMD_FORCE_FALLBACK");
-        if (ff && atoi(ff) > 0) ok = false;
-    }
-    if (!ok) {  // a speculated row start mattered (or a wait gave up): redo the run picture by picture
-        e->run_fallback = true;
-        ++e->calls_fallbacks;
-        // an SVC batch's enhancement-layer thread may be coding from this
-        // run's pictures: stop it and drain what it queued before they are
-        // rewritten (hl_amd_encode_layers_batch re-codes those layers)
-        e->run_aborted.store(true, std::memory_order_release);
-        {
-            std::lock_guard<std::mutex> lk(e->el_mu);
-            HL_HIP_CHECK(svc_drain_el(e));
+    static const bool force_fb = getenv("HL_AMD_FORCE_FALLBACK") && atoi(getenv("HL_AMD_FORCE_FALLBACK")) > 0;
+    for (int si = 0; si < S; ++si) {
+        hl_amd_encoder_t* e = es[si];
+        // the launch's counters (shared by its streams)
+        e->chain_walks = errw[1];
+        e->mb_launches = 1;
+        e->reruns = 0;
+        ++e->calls_runs;
+        e->calls_gave_up += err;
+        e->calls_walks += errw[1];
+        e->helper_kept += errw[2];
+        e->helper_rejected += errw[3];
+        e->helper_self += errw[4];
+        if (si) {
+            e->ms[1] = e0->ms[1];
+            e->ms[3] = e0->ms[3];
         }
-        HL_HIP_CHECK(hipMemcpyAsync(e->d_st, e->d_snap, sizeof(MbState) * nmb, hipMemcpyDeviceToDevice, e->stream));
+        int32_t carry = e->chain_end;
+        bool ok = err == 0;
+        for (int k = 0; k < m && ok; ++k) ok = validate_rows(e->h_bchain + nmb * k, e->mbw, e->mbh, 9, carry);
+        if (force_fb) ok = false;  // diagnostics: HL_AMD_FORCE_FALLBACK=1 takes the fallback below for every run (tests)
+        if (!ok) {  // a speculated row start mattered (or a wait gave up): redo the stream's run picture by picture
+            e->run_fallback = true;
+            ++e->calls_fallbacks;
+            // an SVC batch's enhancement-layer thread may be coding from this
+            // run's pictures: stop it and drain what it queued before they are
+            // rewritten (hl_amd_encode_layers_batch re-codes those layers)
+            e->run_aborted.store(true, std::memory_order_release);
+            {
+                std::lock_guard<std::mutex> lk(e->el_mu);
+                HL_HIP_CHECK(svc_drain_el(e));
+            }
+            HL_HIP_CHECK(hipMemcpyAsync(e->d_st, e->d_snap, sizeof(MbState) * nmb, hipMemcpyDeviceToDevice, e->stream));
+            for (int k = 0; k < m; ++k) {
+                hl_amd_result_t rr;
+                // under rate control the run's picture already has its QP (m == 1)
+                const int32_t rc = encode_frame(e, Y[si][k], U[si][k], V[si][k], &rr, e->rc ? e->run_qp[k] : -1);
+                if (rc) return rc;
+                store_result(e, base + k, rr, &res[si][k]);
+                // keep every picture's records and reconstruction in the run
+                // buffers, as the pipelined run would (diagnostics, and the
+                // reference layer of hl_amd_encode_layers_batch)
+                memcpy(e->h_brec + nmb * k, e->h_rec, sizeof(MbRecord) * nmb);
+                memcpy(e->h_bchain + nmb * k, e->h_chain, sizeof(MbChain) * nmb);
+                uint8_t* dst = e->d_bpic + pic * k;
+                const size_t ys = (size_t)e->W * e->H, cs = ys / 4;
+                uint8_t** rp = e->d_pic[e->cur ^ 1];
+                HL_HIP_CHECK(hipMemcpyAsync(dst, rp[0], ys, hipMemcpyDeviceToDevice, e->stream));
+                HL_HIP_CHECK(hipMemcpyAsync(dst + ys, rp[1], cs, hipMemcpyDeviceToDevice, e->stream));
+                HL_HIP_CHECK(hipMemcpyAsync(dst + ys + cs, rp[2], cs, hipMemcpyDeviceToDevice, e->stream));
+                e->last_recs[base + k] = e->h_brec + nmb * k;
+                e->last_chain[base + k] = e->h_bchain + nmb * k;
+                e->last_pic[base + k] = dst;
+            }
+            e->reruns = 1;
+            continue;
+        }
         for (int k = 0; k < m; ++k) {
-            hl_amd_result_t rr;
-            // under rate control the run's picture already has its QP (m == 1)
-            const int32_t rc = encode_frame(e, Y[k], U[k], V[k], &rr, e->rc ? e->run_qp[k] : -1);
-            if (rc) return rc;
-            store_result(e, base + k, rr, &res[k]);
-            // keep every picture's records and reconstruction in the run
-            // buffers, as the pipelined run would (diagnostics, and the
-            // reference layer of hl_amd_encode_layers_batch)
-            memcpy(e->h_brec + nmb * k, e->h_rec, sizeof(MbRecord) * nmb);
-            memcpy(e->h_bchain + nmb * k, e->h_chain, sizeof(MbChain) * nmb);
-            uint8_t* dst = e->d_bpic + pic * k;
-            const size_t ys = (size_t)e->W * e->H, cs = ys / 4;
-            uint8_t** rp = e->d_pic[e->cur ^ 1];
-            HL_HIP_CHECK(hipMemcpyAsync(dst, rp[0], ys, hipMemcpyDeviceToDevice, e->stream));
-            HL_HIP_CHECK(hipMemcpyAsync(dst + ys, rp[1], cs, hipMemcpyDeviceToDevice, e->stream));
-            HL_HIP_CHECK(hipMemcpyAsync(dst + ys + cs, rp[2], cs, hipMemcpyDeviceToDevice, e->stream));
             e->last_recs[base + k] = e->h_brec + nmb * k;
             e->last_chain[base + k] = e->h_bchain + nmb * k;
-            e->last_pic[base + k] = dst;
+            e->last_pic[base + k] = e->d_bpic + pic * k;
         }
-        e->reruns = 1;
-        return HL_AMD_SUCCESS;
-    }
-    for (int k = 0; k < m; ++k) {
-        e->last_recs[base + k] = e->h_brec + nmb * k;
-        e->last_chain[base + k] = e->h_bchain + nmb * k;
-        e->last_pic[base + k] = e->d_bpic + pic * k;
-    }
-    for (int k = 0; k < m; ++k) {
-        if (!wsize[k]) return HL_AMD_ERROR_TOOSHORT;
-        hl_amd_result_t& o = res[k];
-        o.type = HL_AMD_RESULT_TYPE_DATA;
-        o.data = e->bout[base + k].data();
-        o.data_size = e->bout[base + k].size();
-        o.hdr = e->hdr.data();
-        o.hdr_size = e->hdr.size();
-        if (e->frame_index == 0) o.type |= HL_AMD_RESULT_TYPE_HDR;
-        if (e->run_intra[k]) e->gop_left = e->p.gop_size;  // encode_frame's bookkeeping, picture by picture
-        if (e->rc) {  // hl_codec_264_rc_end_frame / _end_gop, hl_codec_264.c:1018-1031
-            RcPictureStats st{};
-            const MbRecord* rr = e->h_brec + nmb * k;
-            for (size_t a = 0; a < nmb; ++a) st.mad_sum += rr[a].mad;
-            st.header_bits = e->run_bits[k].header_bits;
-            st.texture_bits = e->run_bits[k].texture_bits;
-            st.nbits = (int32_t)((wsize[k] - 3) * 8);
-            e->rc->end_picture(e->run_intra[k] != 0, st, e->gop_left - 1 <= 0);
+        for (int k = 0; k < m; ++k) {
+            if (!wsize[si][k]) return HL_AMD_ERROR_TOOSHORT;
+            hl_amd_result_t& o = res[si][k];
+            o.type = HL_AMD_RESULT_TYPE_DATA;
+            o.data = e->bout[base + k].data();
+            o.data_size = e->bout[base + k].size();
+            o.hdr = e->hdr.data();
+            o.hdr_size = e->hdr.size();
+            if (e->frame_index == 0) o.type |= HL_AMD_RESULT_TYPE_HDR;
+            if (e->run_intra[k]) e->gop_left = e->p.gop_size;  // encode_frame's bookkeeping, picture by picture
+            if (e->rc) {  // hl_codec_264_rc_end_frame / _end_gop, hl_codec_264.c:1018-1031
+                RcPictureStats st{};
+                const MbRecord* rr = e->h_brec + nmb * k;
+                for (size_t a = 0; a < nmb; ++a) st.mad_sum += rr[a].mad;
+                st.header_bits = e->run_bits[k].header_bits;
+                st.texture_bits = e->run_bits[k].texture_bits;
+                st.nbits = (int32_t)((wsize[si][k] - 3) * 8);
+                e->rc->end_picture(e->run_intra[k] != 0, st, e->gop_left - 1 <= 0);
+            }
+            e->last_qp = e->run_qp[k];
+            ++e->pict_count;
+            if (e->run_intra[k]) ++e->idr_pic_id;
+            --e->gop_left;
+            ++e->frame_index;
         }
-        e->last_qp = e->run_qp[k];
-        ++e->pict_count;
-        if (e->run_intra[k]) ++e->idr_pic_id;
-        --e->gop_left;
-        ++e->frame_index;
+        e->chain_end = carry;
+        // the last picture of the run becomes the reference
+        uint8_t** dst = e->d_pic[e->cur];
+        const uint8_t* last = e->d_bpic + pic * (m - 1);
+        HL_HIP_CHECK(hipMemcpyAsync(dst[0], last, (size_t)e->W * e->H, hipMemcpyDeviceToDevice, e->stream));
+        HL_HIP_CHECK(hipMemcpyAsync(dst[1], last + (size_t)e->W * e->H, (size_t)e->Wc * e->Hc, hipMemcpyDeviceToDevice, e->stream));
+        HL_HIP_CHECK(hipMemcpyAsync(dst[2], last + (size_t)e->W * e->H * 5 / 4, (size_t)e->Wc * e->Hc, hipMemcpyDeviceToDevice, e->stream));
+        HL_HIP_CHECK(hipStreamSynchronize(e->stream));
+        e->cur ^= 1;
     }
-    e->chain_end = carry;
-    // the last picture of the run becomes the reference
-    uint8_t** dst = e->d_pic[e->cur];
-    const uint8_t* last = e->d_bpic + pic * (m - 1);
-    HL_HIP_CHECK(hipMemcpyAsync(dst[0], last, (size_t)e->W * e->H, hipMemcpyDeviceToDevice, e->stream));
-    HL_HIP_CHECK(hipMemcpyAsync(dst[1], last + (size_t)e->W * e->H, (size_t)e->Wc * e->Hc, hipMemcpyDeviceToDevice, e->stream));
-    HL_HIP_CHECK(hipMemcpyAsync(dst[2], last + (size_t)e->W * e->H * 5 / 4, (size_t)e->Wc * e->Hc, hipMemcpyDeviceToDevice, e->stream));
-    HL_HIP_CHECK(hipStreamSynchronize(e->stream));
-    e->cur ^= 1;
     return HL_AMD_SUCCESS;
+}
+
+static int32_t encode_run(hl_amd_encoder_t* e, int m, const uint8_t* const* Y, const uint8_t* const* U, const uint8_t* const* V,
+                          hl_amd_result_t* res, int base)
+{
+    return encode_group(&e, 1, m, &Y, &U, &V, &res, base);
+}
+
+static void begin_call(hl_amd_encoder_t* e, int n)
+{
+    e->bout.resize(n);
+    e->last_recs.assign(n, nullptr);
+    e->last_chain.assign(n, nullptr);
+    e->last_pic.assign(n, nullptr);
+    e->calls_runs = e->calls_per_picture = e->calls_fallbacks = e->calls_gave_up = e->calls_walks = 0;
+    e->helper_kept = e->helper_rejected = e->helper_self = 0;
 }
 
 // n consecutive pictures of the stream, every one through a pipelined run:
@@ -1424,15 +1505,42 @@ static int32_t encode_pictures(hl_amd_encoder_t* e, int n, const uint8_t* const*
                                hl_amd_result_t* results)
 {
     if (e->broken) return HL_AMD_ERROR_INVALID_STATE;
-    e->bout.resize(n);
-    e->last_recs.assign(n, nullptr);
-    e->last_chain.assign(n, nullptr);
-    e->last_pic.assign(n, nullptr);
-    e->calls_runs = e->calls_per_picture = e->calls_fallbacks = e->calls_gave_up = e->calls_walks = 0;
-    e->helper_kept = e->helper_rejected = e->helper_self = 0;
+    begin_call(e, n);
     for (int i = 0; i < n;) {
         const int m = e->rc ? 1 : std::min(n - i, kMaxRun);
         const int32_t rc = encode_run(e, m, y + i, u + i, v + i, results + i, i);
+        if (rc) return rc;
+        i += m;
+    }
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_encode_streams(hl_amd_encoder_t* const* encoders, int32_t count, int32_t n, const uint8_t* const* y,
+                                         const uint8_t* const* u, const uint8_t* const* v, hl_amd_result_t* results)
+{
+    if (!encoders || count <= 0 || count > kMaxStreams || n <= 0 || !y || !u || !v || !results) return HL_AMD_ERROR_INVALID_PARAMETER;
+    for (int i = 0; i < count * n; ++i)
+        if (!y[i] || !u[i] || !v[i]) return HL_AMD_ERROR_INVALID_PARAMETER;
+    for (int s = 0; s < count; ++s) {
+        hl_amd_encoder_t* e = encoders[s];
+        if (!e) return HL_AMD_ERROR_INVALID_PARAMETER;
+        for (int t = 0; t < s; ++t)
+            if (encoders[t] == e) return HL_AMD_ERROR_INVALID_PARAMETER;
+        if (e->W != encoders[0]->W || e->H != encoders[0]->H || e->p.device != encoders[0]->p.device) return HL_AMD_ERROR_INVALID_FORMAT;
+        if (e->rc || e->svc || e->broken) return HL_AMD_ERROR_INVALID_STATE;
+    }
+    for (int s = 0; s < count; ++s) begin_call(encoders[s], n);
+    std::vector<const uint8_t* const*> Y(count), U(count), V(count);
+    std::vector<hl_amd_result_t*> R(count);
+    for (int i = 0; i < n;) {
+        const int m = std::min(n - i, kMaxRun);
+        for (int s = 0; s < count; ++s) {
+            Y[s] = y + (size_t)s * n + i;
+            U[s] = u + (size_t)s * n + i;
+            V[s] = v + (size_t)s * n + i;
+            R[s] = results + (size_t)s * n + i;
+        }
+        const int32_t rc = encode_group(encoders, count, m, Y.data(), U.data(), V.data(), R.data(), i);
         if (rc) return rc;
         i += m;
     }

@@ -106,8 +106,9 @@ HD void plane_block(const uint8_t* ref, int W, int H, int mbw, int mbh, uint8_t*
 struct PipeFrame {
     FrameArgs F;
     DeblockArgs D;
-    uint8_t* pl_out;  // this picture's quarter-pel planes (plane p at pl_out + p * F.plsz)
-    int32_t deblock;  // deblocking enabled (disable_deblocking_filter_idc 0)
+    uint8_t* pl_out;    // this picture's quarter-pel planes (plane p at pl_out + p * F.plsz)
+    int32_t deblock;    // deblocking enabled (disable_deblocking_filter_idc 0)
+    int32_t* progress;  // host-mapped count of its stream's published pictures, or null
 };
 
 // Dependencies of task (f, x, y) inside a run: the wavefront neighbours
@@ -166,9 +167,13 @@ HD int task_succ(int f, int X, int Y, int mbw, int mbh, int R, int nframes, int 
     return n;
 }
 
+// A run holds nstreams independent streams of spp consecutive pictures each:
+// picture k of stream s is slot s * spp + k; task_deps / task_succ apply to
+// the pictures of one stream (k), offset by the stream's first slot.
 struct PipeArgs {
     const PipeFrame* fr;
-    int32_t nframes;
+    int32_t nframes;  // slots: nstreams * spp
+    int32_t spp, nstreams;
     int32_t reach;   // guaranteed reference reach R in MBs
     int32_t window;  // pictures a workgroup looks at for ready tasks (from the oldest unfinished)
     int32_t hop;     // pop order: < 0 oldest picture first; else longest remaining path first, a picture
@@ -187,9 +192,8 @@ struct PipeArgs {
     int32_t* hq_tail;
     int32_t* head;   // [nframes] next queue slot to pop
     int32_t* tail;   // [nframes] next queue slot to push
-    int32_t* oldest; // [0] first unfinished picture of the run
+    int32_t* oldest; // [nstreams] first unfinished picture of each stream
     int32_t* err;    // [0] number of bounded waits that gave up
-    int32_t* progress;  // host-mapped: pictures whose records are all in host memory (system scope), or null
     unsigned long long* pub_clock;  // diagnostics: device wall clock at each picture's publication, or null
 };
 

@@ -102,6 +102,21 @@ int32_t hl_amd_encode_device(hl_amd_encoder_t* encoder, const uint8_t* y, const 
 int32_t hl_amd_encode_batch(hl_amd_encoder_t* encoder, int32_t n, const uint8_t* const* y, const uint8_t* const* u,
                             const uint8_t* const* v, hl_amd_result_t* results);
 
+/* n frames of each of `count` independent streams (1..16 encoders, one per
+ * stream: the same picture size and device, no rate control, no spatial
+ * layers) in shared pipelined runs: one persistent launch holds every
+ * stream's pictures, so the streams' macroblock tasks share the device's
+ * workgroups and one stream's wavefront ramp and tail overlap the others'
+ * work (several streams per GPU without processes time-slicing the device).
+ * y[s * n + i] = frame i of stream s (device memory, as hl_amd_encode_batch);
+ * results[s * n + i] its result, valid until the next call on that encoder;
+ * each stream's results are those of hl_amd_encode_batch on its encoder
+ * alone (the reference serves N streams as N hl_codec_t instances,
+ * hl_codec.c:24-150).  The diagnostics of every encoder (stats, timing)
+ * describe the shared launches.  No reference interface. */
+int32_t hl_amd_encode_streams(hl_amd_encoder_t* const* encoders, int32_t count, int32_t n, const uint8_t* const* y,
+                              const uint8_t* const* u, const uint8_t* const* v, hl_amd_result_t* results);
+
 /* rate control (hl_codec_t.rc_bitrate > 0; hl_codec_264.c:719-742, 1018-1031,
  * model hl_codec_264_rc.c): bitrate in bits/s, frame rate fps_den / fps_num
  * (hl_codec_t.fps, integer quotient), rc_basicunit (<= 0: the picture),
