@@ -251,8 +251,18 @@ __device__ void task_filters(const PipeFrame& PF, Shared& S, int x, int y, int m
     }
 }
 
+// Every picture's ready queue is split into kSubQ sub-queues (MB address %
+// kSubQ) with their own heads: a workgroup prefers its own sub-queue
+// (blockIdx % kSubQ) among tasks of similar priority, so that hundreds of
+// idle workgroups do not all race for one queue head (one head serialised
+// the pops: 19 attempts per task, 18 lost, profiles/r04_pipe_profile_pops.log).
+#ifndef HL_SUBQ
+#define HL_SUBQ 4
+#endif
+constexpr int kSubQ = HL_SUBQ;
+
 // Dependency counters and ready queues of a run (hl_pipeline.h): only task
-// (0, 0) of the first picture starts ready.
+// (0, 0) of every stream's first picture starts ready.
 __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
 {
     const int nmb = mbw * mbh, i = blockIdx.x * 256 + threadIdx.x;
@@ -261,14 +271,14 @@ __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
         int d[3][3];
         P.cnt[i] = task_deps(k, a % mbw, a / mbw, mbw, mbh, P.reach, d);
         P.done[i] = 0;
-        P.queue[i] = k == 0 && a == 0 ? 1 : 0;  // every stream's first task
+        for (int q = 0; q < kSubQ; ++q) P.queue[(f * kSubQ + q) * nmb + a] = k == 0 && a == 0 && q == 0 ? 1 : 0;  // every stream's first task
         P.claim[i] = 0;
         P.hstate[i] = HS_FREE;
         P.hq[i] = 0;
     }
-    if (i < P.nframes) {
+    if (i < P.nframes * kSubQ) {
         P.head[i] = 0;
-        P.tail[i] = i % P.spp == 0 ? 1 : 0;
+        P.tail[i] = (i / kSubQ) % P.spp == 0 && i % kSubQ == 0 ? 1 : 0;
     }
     if (i < P.nstreams) P.oldest[i] = 0;
     if (i == 0) {
@@ -292,25 +302,36 @@ __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
 // steps; each later picture adds the lag of task_deps' staircase, about
 // 3 (R+2) steps (P.hop).  The oldest-first order lets the newest pictures'
 // wavefronts start late, and the run ends on their critical path.
-__device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh)
+#if defined(HL_PROFILE)
+#define HL_POPSTAT(i) (++pst[i])
+#else
+#define HL_POPSTAT(i) ((void)0)
+#endif
+__device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh
+#if defined(HL_PROFILE)
+                        , unsigned long long* pst  // profiling: [0] attempts on a macroblock, [1] lost, [2] empty rounds
+#endif
+)
 {
     const int lane = threadIdx.x & 63;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    int empty = 0;
     for (;;) {
-        // lane = (stream lane % S, its picture oldest + lane / S): the window
-        // of each stream's first unfinished pictures
+        // lane = (sub-queue lane % kSubQ, stream r % S, its picture oldest +
+        // r / S) with r = lane / kSubQ: the window of each stream's first
+        // unfinished pictures
         const int S = P.nstreams;
         int ol = 0;
         if (lane < S) ol = ld_relaxed(P.oldest + lane);
         if (__ballot(lane < S && ol < P.spp) == 0) return -1;  // every stream finished
-        const int sj = lane % S, j = lane / S;
+        const int sq = lane % kSubQ, rr = lane / kSubQ, sj = rr % S, j = rr / S;
         const int k = __shfl(ol, sj, 64) + j;
         const bool in = j < max(1, P.window / S) && k < P.spp;
-        const int fl = sj * P.spp + k;
+        const int fl = sj * P.spp + k, ql = fl * kSubQ + sq;  // picture slot, its sub-queue
         int h = 0, t = 0;
         if (in) {
-            h = ld_relaxed(P.head + fl);
-            t = ld_relaxed(P.tail + fl);
+            h = ld_relaxed(P.head + ql);
+            t = ld_relaxed(P.tail + ql);
         }
         int i0 = -1, hh = 0, v = 0;
         if (P.hop < 0) {
@@ -323,11 +344,12 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh)
         else {
             // the head entries themselves (0: pushed, not yet written)
             int q = 0;
-            if (in && h < t) q = ld_relaxed(P.queue + fl * nmb + h);
+            if (in && h < t) q = ld_relaxed(P.queue + ql * nmb + h);
             int key = -1;
             if (q > 0) {
                 const int a = q - 1, y = a / mbw, x = a - y * mbw;
-                key = (((mbw - 1 - x) + 2 * (mbh - 1 - y) - P.hop * j + 4096) << 6) | (63 - lane);
+                const int own = sq == (int)(blockIdx.x % kSubQ) ? 12 : 0;  // preference for the workgroup's sub-queue
+                key = (((mbw - 1 - x) + 2 * (mbh - 1 - y) - P.hop * j + own + 4096) << 6) | (63 - lane);
             }
             for (int s = 1; s < 64; s <<= 1) key = max(key, __shfl_xor(key, s, 64));
             key = __builtin_amdgcn_readfirstlane(key);
@@ -339,12 +361,13 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh)
             // else: empty, or only pushes between their tail and slot stores
         }
         if (i0 >= 0) {
-            const int f = __builtin_amdgcn_readlane(fl, i0);
+            HL_POPSTAT(0);
+            const int f = __builtin_amdgcn_readlane(fl, i0), qf = __builtin_amdgcn_readlane(ql, i0);
             int r = 0;
-            if (lane == 0 && atomicCAS(P.head + f, hh, hh + 1) == hh) {
+            if (lane == 0 && atomicCAS(P.head + qf, hh, hh + 1) == hh) {
                 r = v;
                 // the slot is pushed right after the tail moved
-                for (unsigned k = 0; r == 0 && (r = ld_relaxed(P.queue + f * nmb + hh)) == 0; ++k)
+                for (unsigned k = 0; r == 0 && (r = ld_relaxed(P.queue + qf * nmb + hh)) == 0; ++k)
                     if (k > (1u << 26)) {
                         atomicAdd(P.err, 1);
                         r = -1;
@@ -355,6 +378,7 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh)
             r = __builtin_amdgcn_readfirstlane(r);
             if (r < 0) return -1;
             if (r > 0) return f * nmb + r - 1;
+            HL_POPSTAT(1);
             continue;  // another workgroup took it
         }
         if (P.helpers) {  // no macroblock ready: an intra helper task, unless its macroblock took it over
@@ -376,11 +400,14 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh)
                 continue;
             }
         }
+        HL_POPSTAT(2);
         if (__builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 10 s at 100 MHz
             if (lane == 0) atomicAdd(P.err, 1);
             return -1;
         }
-        __builtin_amdgcn_s_sleep(4);
+        // nothing ready: back off (fewer scans of the queue words while tasks run)
+        if (++empty < 4) __builtin_amdgcn_s_sleep(4);
+        else __builtin_amdgcn_s_sleep(16);
     }
 }
 
@@ -420,8 +447,8 @@ __device__ int claim_next(const PipeArgs& P, int nmb, int& cursor)
 #ifndef HL_PIPE_WAVES_PER_EU
 #define HL_PIPE_WAVES_PER_EU 2
 #endif
-#ifndef HL_CONT
-#define HL_CONT 0
+#ifndef HL_EARLY_RELEASE
+#define HL_EARLY_RELEASE 1
 #endif
 __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(PipeArgs P, int mbw, int mbh)
 {
@@ -431,13 +458,11 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
     const int nmb = mbw * mbh;
     const bool in_order = blockIdx.x == 0;  // claims tasks in run order (claim_next)
     int cursor = 0;
-    // (wave 0) the task this workgroup runs next without popping: one of the
-    // successors its last task made ready, or -1
-    int next_task = -1;
 #if defined(HL_PROFILE)
     // per-workgroup totals (profiling build): prof[40..44] = waits for a ready
     // task, decisions, filters, tasks, workgroup lifetime (shader clock)
     unsigned long long pw_wait = 0, pw_mb = 0, pw_filt = 0, pw_n = 0, pw_hlp = 0, pw_hn = 0;
+    unsigned long long pst[3] = {0, 0, 0};  // pop_task rounds (wave 0)
     const unsigned long long pw_t0 = __builtin_readcyclecounter();
     unsigned long long* prof = P.fr[0].F.prof;
 #endif
@@ -446,8 +471,11 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         const unsigned long long pt0 = __builtin_readcyclecounter();
 #endif
         if (threadIdx.x < 64) {
-            const int t = next_task >= 0 ? next_task : (in_order ? claim_next(P, nmb, cursor) : pop_task(P, nmb, mbw, mbh));
-            next_task = -1;
+            const int t = in_order ? claim_next(P, nmb, cursor) : pop_task(P, nmb, mbw, mbh
+#if defined(HL_PROFILE)
+                                                                                           , pst
+#endif
+            );
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
             if (threadIdx.x == 0) s_task = t;
@@ -469,7 +497,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         const PipeFrame& PF = P.fr[f];
         const int x = addr % mbw, y = addr / mbw;
         int gx = 1 << 20, gy = 1 << 20;
-        if (f > 0) {
+        if (f % P.spp > 0) {  // the reference is a picture of this run (of the same stream)
             gx = min(x + P.reach, mbw - 1);
             gy = min(y + P.reach, mbh - 1);
         }
@@ -514,6 +542,52 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #if defined(HL_PROFILE)
         const unsigned long long pt2 = __builtin_readcyclecounter();
 #endif
+        const int fk = f % P.spp, fb = f - fk;  // picture fk of the stream whose first slot is fb
+        // Releases successors (Guideline 16: every wave drained, barrier, ONE
+        // release whose own wait is explicit, then relaxed atomics: the L2
+        // write-back of the release fence covers the payload, and every
+        // consumer acquires after its pop): those of this picture (phase 0),
+        // of the next one (1), or all (2).  Those whose last dependency this
+        // was are queued (with their intra helpers, in P pictures).
+        auto release = [&](int phase) {
+            int fo = 0, xo = 0, yo = 0;
+            const int ns = task_succ(fk, x, y, mbw, mbh, P.reach, P.spp, -1, fo, xo, yo);
+            for (int j = tid; j < ns; j += 64) {
+                task_succ(fk, x, y, mbw, mbh, P.reach, P.spp, j, fo, xo, yo);
+                if (phase != 2 && (fo == fk) != (phase == 0)) continue;
+                fo += fb;
+                const int a = yo * mbw + xo;
+                if (__hip_atomic_fetch_add(P.cnt + fo * nmb + a, -1, HL_CNT_ORDER, __HIP_MEMORY_SCOPE_AGENT) != 1) continue;
+                const int qf = fo * kSubQ + a % kSubQ;
+                const int pos = __hip_atomic_fetch_add(P.tail + qf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(P.queue + qf * nmb + pos, a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                if (P.helpers && !ld_relaxed(&P.fr[fo].F.is_intra)) {
+                    const int hp = __hip_atomic_fetch_add(P.hq_tail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(P.hq + hp, fo * nmb + a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        };
+#if HL_EARLY_RELEASE
+        // This picture's successors need the decision (its reconstruction, MB
+        // object, chain record), not this task's deblocking and plane blocks:
+        // they are released before those.  The filters then wait for the
+        // filters of the in-picture predecessors, which keeps the deblocking
+        // in the reference's raster causality (tests/test_pipeline_schedule.py
+        // models both events); the next picture still waits for `done`, set
+        // after the filters.
+        if (tid < 64) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, HL_REL_SCOPE);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            release(0);
+            if (tid == 0) {
+                if (x > 0) spin_ge(P.done + t - 1, 1, P.err);
+                if (y > 0) spin_ge(P.done + f * nmb + (y - 1) * mbw + min(x + 1, mbw - 1), 1, P.err);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+#endif
         // deblocking, then quarter-pel planes, this decision completed
         task_filters(PF, S, x, y, mbw, mbh, tid);
 #if defined(HL_PROFILE)
@@ -522,12 +596,6 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         pw_filt += __builtin_readcyclecounter() - pt2;
         ++pw_n;
 #endif
-        // publish (Guideline 16: every wave drained, barrier, ONE release whose
-        // own wait is explicit), then release the successors with relaxed
-        // atomics: the L2 write-back of the release fence already covers the
-        // payload of this task, and every consumer acquires after its pop.
-        // Those whose last dependency this was are pushed onto their
-        // picture's ready queue.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid < 64) {
@@ -538,44 +606,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, HL_REL_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (tid == 0) st_relaxed(P.done + t, 1);
-            int fo = 0, xo = 0, yo = 0;
-            const int fk = f % P.spp, fb = f - fk;  // picture fk of the stream whose first slot is fb
-            const int ns = task_succ(fk, x, y, mbw, mbh, P.reach, P.spp, -1, fo, xo, yo);
-            // every successor this task makes ready is queued (with its intra
-            // helper, in P pictures) -- except the first one, which this
-            // workgroup claims and runs next without a pop (workgroup 0 keeps
-            // claiming in run order): with hundreds of workgroups converging
-            // on the same queue head, pops were a serial bottleneck
-            int ready = -1;  // this lane's successor (one per lane: ns <= 64)
-            for (int j = tid; j < ns; j += 64) {
-                task_succ(fk, x, y, mbw, mbh, P.reach, P.spp, j, fo, xo, yo);
-                fo += fb;
-                const int a = yo * mbw + xo;
-                if (__hip_atomic_fetch_add(P.cnt + fo * nmb + a, -1, HL_CNT_ORDER, __HIP_MEMORY_SCOPE_AGENT) == 1) ready = fo * nmb + a;
-            }
-            // (continuation: HL_CONT 0 none, 1 any successor, 2 one of this picture)
-            const unsigned long long rb = __ballot(ready >= 0 && (HL_CONT == 1 || ready / nmb == f));
-            const int keep = in_order || !rb || HL_CONT == 0 ? -1 : __ffsll((long long)rb) - 1;
-            if (ready >= 0) {
-                const int ff = ready / nmb, a = ready - ff * nmb;
-                bool main_entry = true;
-                if (tid == keep && atomicCAS(P.claim + ready, 0, 1) == 0) {
-                    main_entry = false;
-                    next_task = ready;
-                }
-                else if (tid == keep)
-                    main_entry = false;  // workgroup 0 holds it (claim_next)
-                // the macroblock, then (P pictures) its intra helper
-                if (main_entry) {
-                    const int pos = __hip_atomic_fetch_add(P.tail + ff, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(P.queue + ff * nmb + pos, a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                if (P.helpers && !ld_relaxed(&P.fr[ff].F.is_intra)) {
-                    const int pos = __hip_atomic_fetch_add(P.hq_tail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(P.hq + pos, ready + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            if (keep >= 0) next_task = __builtin_amdgcn_readlane(next_task, keep);
+            release(HL_EARLY_RELEASE ? 1 : 2);
             // a stream's pictures finish in order: the last MB depends on every
             // other one and on the previous picture's last MB
             if (tid == 0 && addr == nmb - 1) {
@@ -595,6 +626,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         atomicAdd(prof + 44, __builtin_readcyclecounter() - pw_t0);
         atomicAdd(prof + 45, pw_hlp);  // intra helper tasks: cycles, count
         atomicAdd(prof + 46, pw_hn);
+        for (int i = 0; i < 3; ++i) atomicAdd(prof + 47 + i, pst[i]);  // pops: attempts, lost, empty rounds
     }
 #endif
 }
@@ -1073,8 +1105,8 @@ static hipError_t ensure_sched(hl_amd_encoder_t* e, int slots)
     hipError_t r;
     if ((r = hipMalloc(&e->d_pf, sizeof(PipeFrame) * slots)) || (r = hipHostMalloc(&e->h_pf, sizeof(PipeFrame) * slots, hipHostMallocDefault)) ||
         (r = hipMalloc(&e->d_cnt, sizeof(int32_t) * 2 * nmb * slots)) || (r = hipMalloc(&e->d_done, sizeof(int32_t) * nmb * slots)) ||
-        (r = hipMalloc(&e->d_queue, sizeof(int32_t) * 2 * nmb * slots)) ||
-        (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * slots + kMaxStreams + 2))) ||
+        (r = hipMalloc(&e->d_queue, sizeof(int32_t) * (kSubQ + 1) * nmb * slots)) ||
+        (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * kSubQ * slots + kMaxStreams + 2))) ||
         (r = hipMalloc(&e->d_hstate, sizeof(int32_t) * nmb * slots)))
         return r;
     if (!e->d_err && (r = hipMalloc(&e->d_err, sizeof(int32_t) * 8))) return r;
@@ -1306,12 +1338,12 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
     P.queue = e0->d_queue;
     P.hstate = e0->d_hstate;
     P.helpers = e0->helpers ? 1 : 0;
-    P.hq = e0->d_queue + nmb * slots;
+    P.hq = e0->d_queue + kSubQ * nmb * slots;
     P.head = e0->d_head;
-    P.tail = e0->d_head + slots;
-    P.oldest = e0->d_head + 2 * slots;
-    P.hq_head = e0->d_head + 2 * slots + kMaxStreams;
-    P.hq_tail = e0->d_head + 2 * slots + kMaxStreams + 1;
+    P.tail = e0->d_head + kSubQ * slots;
+    P.oldest = e0->d_head + 2 * kSubQ * slots;
+    P.hq_head = e0->d_head + 2 * kSubQ * slots + kMaxStreams;
+    P.hq_tail = e0->d_head + 2 * kSubQ * slots + kMaxStreams + 1;
     P.err = e0->d_err;
     static const bool trace = getenv("HL_AMD_TRACE_WRITERS") != nullptr;
     static unsigned long long* h_clock = nullptr;

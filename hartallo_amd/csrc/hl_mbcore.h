@@ -1868,20 +1868,23 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
 #else
         auto seg_pick = [&](int j, double& m) -> int { return pick(lo[j], lo[j] + n[j], m); };
 #endif
-        // resolve the chain step by step
-        int used = 0;
-#if defined(HL_CHAIN_PROF)
-        bool brk = false;
-#endif
-#pragma unroll
-        for (int j = 0; j < kMaxSeg; ++j) {
-            if (j >= nseg) break;
-            used = lo[j] + n[j];
-            if (stage == 3) {  // MVP / (0,0) (me_ds.c:280-300)
+        // Resolve the chain (me_ds.c:280-470 applied to its steps, in closed
+        // form): the MVP/(0,0) step (stage 3, always first) may take its
+        // winner; from then on the best cost stays fixed until a step moves,
+        // so the chain moves at its first later step with a candidate below
+        // that cost, and every step before it ends its stage.  The stage's
+        // window is the one re-centred when it began (kept by a move).
+        int used;
+        {
+            int j0 = 0;
+            bool cut = false;  // the (0,0) candidate won: the continuations assumed the MVP
+            if (stage == 3) {  // MVP / (0,0)
                 double m;
-                const int bi = seg_pick(j, m);
+                const int bi = seg_pick(0, m);
                 if (m < b.cost) take(bi, m);
                 stage = 2;
+                j0 = 1;
+                cut = b.mv[0] != pmv[0] || b.mv[1] != pmv[1];
                 cx = centre_of(2, b.mv[0]);
                 cy = centre_of(2, b.mv[1]);
                 flags = 0x1FF;
@@ -1889,47 +1892,54 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
                 right = cx + range;
                 top = cy - range;
                 bottom = cy + range;
-                if (b.mv[0] != pmv[0] || b.mv[1] != pmv[1]) {
-#if defined(HL_CHAIN_PROF)
-                    if (j + 1 < nseg) HL_PROF_ADD(c, 12, __builtin_readcyclecounter() - 1);  // (0,0) won: speculation dropped
-                    brk = true;
-#endif
-                    break;  // the continuation assumed the MVP
+            }
+            unsigned mv_mask = 0;  // steps with a candidate below the best cost
+            double sj[kMaxSeg];
+            int bj[kMaxSeg];
+#pragma unroll
+            for (int j = 0; j < kMaxSeg; ++j) {
+                bj[j] = 0;
+                sj[j] = 1.7976931348623157e308;
+                if (j >= j0 && j < nseg && n[j]) {
+                    bj[j] = seg_pick(j, sj[j]);
+                    if (sj[j] < b.cost) mv_mask |= 1u << j;
                 }
-                continue;
             }
-            int best = -1;
-            if (n[j]) {
-                double m;
-                const int bi = seg_pick(j, m);
-                if (m < b.cost) best = take(bi, m);
+            if (cut) used = lo[0] + n[0];
+            else if (mv_mask) {
+                const int jm = __builtin_ctz(mv_mask);
+                if (jm > j0) {  // the steps before it ended their stages: the stage began at step jm
+                    stage -= jm - j0;
+                    const int wx = centre_of(stage, b.mv[0]), wy = centre_of(stage, b.mv[1]);
+                    left = wx - range;
+                    right = wx + range;
+                    top = wy - range;
+                    bottom = wy + range;
+                }
+                // moved: the stage goes on from the new centre (window kept, me_ds.c:309)
+                const int best = take(bj[jm], sj[jm]);
+                cx = b.mv[0] >> stage;
+                cy = b.mv[1] >> stage;
+                flags = mask_of(stage, best);  // points the move already visited
+                used = lo[jm] + n[jm];
             }
-            if (best >= 0) {  // moved: the stage goes on from the new centre (window kept, me_ds.c:309)
-                cx = b.mv[0] >> (stage == 2 ? 2 : (stage == 1 ? 1 : 0));
-                cy = b.mv[1] >> (stage == 2 ? 2 : (stage == 1 ? 1 : 0));
-                flags = mask_of(stage == 2 ? 2 : (stage == 1 ? 1 : 0), best);  // points the move already visited
-#if defined(HL_CHAIN_PROF)
-                HL_PROF_ADD(c, stage == 2 ? 13 : (stage == 1 ? 14 : 15), __builtin_readcyclecounter() - 1);  // a move ends the pass
-                brk = true;
-#endif
-                break;
+            else {  // no step moved: each ended its stage
+                stage -= nseg - j0;
+                if (stage >= 0) {
+                    cx = centre_of(stage, b.mv[0]);
+                    cy = centre_of(stage, b.mv[1]);
+                    flags = 0x1FF;
+                    left = cx - range;
+                    right = cx + range;
+                    top = cy - range;
+                    bottom = cy + range;
+                }
+                used = lo[nseg - 1] + n[nseg - 1];
             }
-            --stage;  // no better point: the next stage (the chain's next step)
-            if (stage < 0) break;
-            cx = centre_of(stage, b.mv[0]);
-            cy = centre_of(stage, b.mv[1]);
-            flags = 0x1FF;
-            left = cx - range;
-            right = cx + range;
-            top = cy - range;
-            bottom = cy + range;
         }
 #if defined(__HIP_DEVICE_COMPILE__)
 #if defined(HL_STEP_PROF)
         HL_PROF_ADD(c, 18, tres);  // the chain resolved
-#endif
-#if defined(HL_CHAIN_PROF)
-        if (!brk && stage >= 0) HL_PROF_ADD(c, 18, __builtin_readcyclecounter() - 1);  // chain resolved, search goes on: budget-limited
 #endif
         if (used) commit_candidates(c, g, used, pv_last);
 #else

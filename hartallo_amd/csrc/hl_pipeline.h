@@ -181,7 +181,7 @@ struct PipeArgs {
     int32_t* cnt;    // [nframes][nmb] unfinished dependencies
     int32_t* claim;  // [nframes][nmb] 1 once a workgroup holds the task
     int32_t* done;   // [nframes][nmb] 1 once the task finished (reach_wait polls it)
-    int32_t* queue;  // [nframes][nmb] ready tasks, MB address + 1 (0 = slot not yet written)
+    int32_t* queue;  // [nframes][kSubQ][nmb] ready tasks, MB address + 1 (0 = slot not yet written)
     // intra helper tasks (hl_mbcore.h intra_helper): a ready P macroblock also
     // queues its helper, in one FIFO that workgroups take from only when no
     // macroblock is ready (ramp and tail of a run, a lone picture)
@@ -190,8 +190,8 @@ struct PipeArgs {
     int32_t* hq;     // [nframes * nmb] FIFO of helper tasks, f * nmb + MB address + 1 (0 = slot not yet written)
     int32_t* hq_head;
     int32_t* hq_tail;
-    int32_t* head;   // [nframes] next queue slot to pop
-    int32_t* tail;   // [nframes] next queue slot to push
+    int32_t* head;   // [nframes][kSubQ] next queue slot to pop
+    int32_t* tail;   // [nframes][kSubQ] next queue slot to push
     int32_t* oldest; // [nstreams] first unfinished picture of each stream
     int32_t* err;    // [0] number of bounded waits that gave up
     unsigned long long* pub_clock;  // diagnostics: device wall clock at each picture's publication, or null

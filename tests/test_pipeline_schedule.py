@@ -100,6 +100,55 @@ def test_task_schedule(mbw, mbh):
         assert len(deblocked) == len(planed) == mbw * mbh
 
 
+@pytest.mark.parametrize("mbw,mbh", [(1, 1), (2, 1), (1, 2), (2, 2), (3, 3), (4, 2), (2, 4), (5, 7), (11, 9), (22, 18), (8, 3)])
+def test_task_schedule_early_release(mbw, mbh):
+    """k_pipeline with HL_EARLY_RELEASE: a task releases this picture's
+    successors after its decision, then runs its filters once the filters of
+    its in-picture predecessors are done.  Decisions and filter phases are
+    separate events here, interleaved in random orders the two rules allow;
+    the same checks as test_task_schedule hold at every filter event, and no
+    decision runs while a sample it reads unfiltered is being deblocked (the
+    readers of every deblocked sample are decided before it)."""
+    lib = _lib()
+    tdb = {(x, y): _blocks(lib, 0, x, y, mbw, mbh) for y in range(mbh) for x in range(mbw)}
+    tpl = {(x, y): _blocks(lib, 1, x, y, mbw, mbh) for y in range(mbh) for x in range(mbw)}
+    inside = lambda p: 0 <= p[0] < mbw and 0 <= p[1] < mbh  # noqa: E731
+    tasks = [(x, y) for y in range(mbh) for x in range(mbw)]
+    for seed in range(12):
+        rng = random.Random(seed)
+        decided, filtered, deblocked, planed = set(), set(), set(), set()
+        events = [("d", t) for t in tasks] + [("f", t) for t in tasks]
+        while events:
+            ok = []
+            for ev in events:
+                kind, t = ev
+                deps = _deps(lib, *t, mbw, mbh)
+                if kind == "d" and all(d in decided for d in deps):
+                    ok.append(ev)
+                if kind == "f" and t in decided and all(d in filtered for d in deps):
+                    ok.append(ev)
+            kind, t = ev = rng.choice(ok)
+            events.remove(ev)
+            if kind == "d":
+                decided.add(t)
+                continue
+            for (X, Y) in tdb[t]:
+                for p in [(X - 1, Y), (X, Y - 1), (X + 1, Y - 1)]:
+                    assert not inside(p) or p in deblocked, ("deblock order", (X, Y), p, t)
+                for r in [(X + 1, Y), (X - 1, Y + 1), (X, Y + 1), (X + 1, Y + 1), (X - 2, Y + 1)]:
+                    assert not inside(r) or r in decided, ("unfiltered reader pending", (X, Y), r, t)
+                assert (X, Y) not in deblocked
+                deblocked.add((X, Y))
+            for (X, Y) in tpl[t]:
+                for a in range(X - 1, X + 2):
+                    for b in range(Y - 1, Y + 2):
+                        assert not inside((a, b)) or (a, b) in deblocked, ("planes", (X, Y), (a, b), t)
+                assert (X, Y) not in planed
+                planed.add((X, Y))
+            filtered.add(t)
+        assert len(deblocked) == len(planed) == mbw * mbh
+
+
 @pytest.mark.parametrize("mbw,mbh,R,nf", [(1, 1, 0, 3), (2, 3, 0, 4), (5, 4, 2, 3), (9, 6, 1, 3), (12, 7, 3, 2), (4, 9, 4, 3), (20, 3, 2, 2)])
 def test_task_successors_invert_dependencies(mbw, mbh, R, nf):
     lib = _lib()

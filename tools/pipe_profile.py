@@ -57,6 +57,8 @@ def main():
         print(f"   workgroups {wgs}, tasks {tasks} ({tasks / max(1, n * nmb):.2f} per MB), mean lifetime {life / wgs / 1e6:.1f} Mcycles"
               f" (~{life / wgs / (ms[1] * 1e-3) / 1e9:.2f} GHz shader clock if the kernel spans it)")
         hlp, hn = cnt[45], cnt[46]
+        print(f"   pops: {cnt[47]} attempts on a macroblock ({cnt[47] / max(1, tasks):.2f} per task), {cnt[48]} lost to another "
+              f"workgroup, {cnt[49]} empty rounds ({cnt[49] / max(1, tasks):.1f} per task)")
         if hn:
             print(f"   intra helper tasks {hn} ({hn / max(1, n * nmb):.2f} per MB), {hlp / hn / 1e3:.1f} kcycles each")
         for name, v in (("task-start waits", wait), ("decisions", mb), ("deblock + planes", filt), ("intra helpers", hlp),
