@@ -613,12 +613,14 @@ HD void mb_diag_inputs(Ctx& c)
 #endif
 }
 
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && HL_MB_THREADS >= 512
 // MB start on the device: every global load of the MB start is issued in one
 // round -- the MB objects of this address and of A, B, C, D (16-byte words),
 // the source samples, the intra neighbour samples of the current picture and
 // the CAVLC length tables -- and lands in LDS; the derivations then run from
 // LDS, each on its own lanes.  Same results as the host version below.
+// The lane assignment needs 512 lanes (smaller workgroups take the generic
+// strided version below).
 __device__ __forceinline__ void mb_begin(Ctx& c)
 {
     const FrameArgs& F = c.F;
@@ -628,6 +630,7 @@ __device__ __forceinline__ void mb_begin(Ctx& c)
     const int hasA = c.mbx > 0, hasB = c.mby > 0, hasC = c.mby > 0 && c.mbx < F.mbw - 1, hasD = c.mbx > 0 && c.mby > 0;
     const int xc = c.xL >> 1, yc = c.yL >> 1;
     constexpr int kW = (int)(sizeof(MbState) / 16);  // 16-byte words per MB object
+    static_assert(5 * kW + 32 <= 448 && kMbThreads >= 464, "mb_begin lane map");
     // ---- round 1: loads (addresses clamped to valid memory, values unused there)
     uint4 q = make_uint4(0, 0, 0, 0);
     int b1 = kNA, b2 = 0, b3 = 0;
