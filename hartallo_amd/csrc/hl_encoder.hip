@@ -463,6 +463,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
     // task, decisions, filters, tasks, workgroup lifetime (shader clock)
     unsigned long long pw_wait = 0, pw_mb = 0, pw_filt = 0, pw_n = 0, pw_hlp = 0, pw_hn = 0;
     unsigned long long pst[3] = {0, 0, 0};  // pop_task rounds (wave 0)
+    unsigned long long ptail[4] = {0, 0, 0, 0};  // after the filters: barrier, release fence, successors' release; early release
     const unsigned long long pw_t0 = __builtin_readcyclecounter();
     unsigned long long* prof = P.fr[0].F.prof;
 #endif
@@ -588,16 +589,24 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         }
         __syncthreads();
 #endif
+#if defined(HL_PROFILE)
+        const unsigned long long pt2e = __builtin_readcyclecounter();
+#endif
         // deblocking, then quarter-pel planes, this decision completed
         task_filters(PF, S, x, y, mbw, mbh, tid);
 #if defined(HL_PROFILE)
         pw_wait += pt1 - pt0;
         pw_mb += pt2 - pt1;
-        pw_filt += __builtin_readcyclecounter() - pt2;
+        const unsigned long long pw_filt_last = __builtin_readcyclecounter() - pt2;
+        pw_filt += pw_filt_last;
         ++pw_n;
 #endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+#if defined(HL_PROFILE)
+        const unsigned long long pt3 = __builtin_readcyclecounter();
+        unsigned long long pt4 = pt3;
+#endif
         if (tid < 64) {
 #if HL_HOSTREC_SYS
             if (PF.progress) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // host-visible records (system scope)
@@ -605,6 +614,9 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #endif
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, HL_REL_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if defined(HL_PROFILE)
+            pt4 = __builtin_readcyclecounter();
+#endif
             if (tid == 0) st_relaxed(P.done + t, 1);
             release(HL_EARLY_RELEASE ? 1 : 2);
             // a stream's pictures finish in order: the last MB depends on every
@@ -616,6 +628,15 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
                 if (P.pub_clock) P.pub_clock[f] = wall_clock64();
             }
         }
+#if defined(HL_PROFILE)
+        {
+            const unsigned long long pt5 = __builtin_readcyclecounter();
+            ptail[0] += pt3 - pt2 - (pw_filt_last);
+            ptail[1] += pt4 - pt3;
+            ptail[2] += pt5 - pt4;
+            ptail[3] += pt2e - pt2;
+        }
+#endif
     }
 #if defined(HL_PROFILE)
     if (threadIdx.x == 0 && prof) {
@@ -627,6 +648,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         atomicAdd(prof + 45, pw_hlp);  // intra helper tasks: cycles, count
         atomicAdd(prof + 46, pw_hn);
         for (int i = 0; i < 3; ++i) atomicAdd(prof + 47 + i, pst[i]);  // pops: attempts, lost, empty rounds
+        for (int i = 0; i < 4; ++i) atomicAdd(prof + 50 + i, ptail[i]);  // filters' barrier, release fence, successors, early release
     }
 #endif
 }
@@ -1412,7 +1434,8 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
     }
     const int32_t err = errw[0];
     if (err) fprintf(stderr, "hartallo_amd: pipelined run: %d bounded waits gave up; re-encoding the run picture by picture\n", err);
-    static const bool force_fb = getenv("HL_AMD_FORCE_FALLBACK") && atoi(getenv("HL_AMD_FORCE_FALLBACK")) > 0;
+    const bool force_fb = getenv("HL_AMD_FORCE_FALLBACK")  // (read per run: tests set it per case)
+                           && atoi(getenv("HL_AMD_FORCE_FALLBACK")) > 0;
     for (int si = 0; si < S; ++si) {
         hl_amd_encoder_t* e = es[si];
         // the launch's counters (shared by its streams)

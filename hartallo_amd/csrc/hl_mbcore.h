@@ -88,7 +88,9 @@ constexpr int kMaxPass = (9 * 16 + kMbRows - 1) / kMbRows;  // rows per lane for
 #ifndef HL_QUAD_EVAL
 #define HL_QUAD_EVAL 1
 #endif
-constexpr int kQPass = 2;  // quad rounds per pass: 2 x 128 blocks
+// quad rounds per pass: 2 x 128 blocks at 512 lanes; smaller workgroups take
+// enough rounds for the largest non-speculative step (9 16x16 candidates)
+constexpr int kQPass = kMbThreads >= 512 ? 2 : (9 * 16 + (kMbThreads >> 2) - 1) / (kMbThreads >> 2);
 constexpr int kPassItems = HL_QUAD_EVAL ? kQPass * (kMbThreads >> 2) : kMaxPass * kMbRows;
 constexpr int kSpecMaxBlocks = HL_QUAD_EVAL ? HL_SPEC_MAX_BLOCKS : 8;
 
@@ -1290,8 +1292,12 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
     // sees it at this point of the sequence (residual.c:640-755 with the live
     // TotalCoeffs of quirk 1), coeff_token, candidate sums, cost.  All LDS
     // reads are issued up front.
-    if (g.nblk > 1 && c.tid < (ncand << 4)) {
-        const int wave = c.tid >> 6, ci = c.tid >> 4, k0 = c.tid & 15;
+    // (one round at 512 lanes; smaller workgroups take more)
+    constexpr int kRowRounds = (kMaxCand + kMbRows - 1) / kMbRows;
+#pragma unroll
+    for (int rr = 0; rr < kRowRounds; ++rr)
+    if (g.nblk > 1 && c.tid + rr * kMbThreads < (ncand << 4)) {
+        const int wave = c.tid >> 6, ci = (c.tid >> 4) + rr * kMbRows, k0 = c.tid & 15;
         const bool valid = k0 < g.nblk;
         const int k = valid ? k0 : 0;
         const int hx = k & (g.nbw - 1), hy = k >> g.lbw;
@@ -2756,11 +2762,14 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
     const int qbits = 15 + F.qp / 6, fq = (1 << qbits) / 3;
     // this lane's prediction taps: row = (slot, mode), lane = sample (kI4Tab)
     const uint32_t te = kI4Tab.e[row < 18 ? (row >= 9 ? row - 9 : row) : 0][c.tid & 15];
-    for (int d = 0; d < 10; ++d) {
+    // (workgroups below 288 lanes lack the 18 rows of a two-slot step: one
+    // block per step, in z-order)
+    constexpr bool kTwoSlots = kMbThreads >= 18 * 16;
+    for (int d = 0; d < (kTwoSlots ? 10 : 16); ++d) {
 #if defined(HL_I4_PROF)
         HL_PROF_T(ti0);
 #endif
-        const int b0 = kWave[d][0], b1 = kWave[d][1];
+        const int b0 = kTwoSlots ? kWave[d][0] : d, b1 = kTwoSlots ? kWave[d][1] : 255;
         const int nslot = b1 == 255 ? 1 : 2;
         if (c.tid < 32 && (c.tid >> 4) < nslot) {
             // lane i of the slot's 16-lane row: neighbour sample i (i4_neighbours,
