@@ -255,8 +255,8 @@ struct Shared {
     int16_t best_mv[4][4][2], best_mvp[4][4][2];
     // --- intra scratch
     int32_t pred[256];
-    int32_t i16_ac[16][16], i16_dcc[16];  // (i16_ac: scratch of the pipelined task's plane blocks)
-    int32_t i16_called[16], i16_bits[16], i16_dist[16], i16_distz[16];
+    int32_t i16_ac[16][16], i16_dcc[32];  // (i16_ac: scratch of the pipelined task's plane blocks)
+    int32_t i16_called[16], i16_bits[16], i16_dist[32], i16_distz[32];  // (i16_dcc / _dist / _distz: two modes' rows)
     alignas(16) int16_t i16_best_ac[16][16];
     alignas(16) int16_t i16_best_dc[16];
     alignas(16) uint8_t i16_best_rec[256];
@@ -277,7 +277,7 @@ struct Shared {
     int32_t i4r_dist[16], i4r_sct[16], i4r_zero[16];
     int32_t luma_level[16][16];
     int16_t i4nb[2][16];         // neighbours of the current 4x4 blocks (p[13] layout)
-    int32_t dcY[16];             // I16x16: scaled DC per DC-matrix position
+    int32_t dcY[32];             // I16x16: scaled DC per DC-matrix position (two modes)
     int32_t chain_x;             // resolve_chain result
     int32_t hs_x;                // intra helper state seen by the MB (HS_*)
     int32_t homo[4];             // early termination: homogeneity of the four 8x8 source quadrants
@@ -2433,53 +2433,57 @@ HD void i16_heavy(Ctx& c)
     const FrameArgs& F = c.F;
     Shared& S = c.S;
 #if defined(__HIP_DEVICE_COMPILE__)
-    // one 16-lane row per 4x4 block (rows 0-15), modes in order
-    const int row = c.tid >> 4;
+    // one 16-lane row per 4x4 block; two modes per round (rows 0-15 mode m0,
+    // rows 16-31 mode m0 + 1: waves 0-3 and 4-7) at 512 lanes
+    constexpr int kSlots = kMbThreads >= 512 ? 2 : 1;
+    const int row = c.tid >> 4, blk = row & 15, slot = row >> 4;
     const int qbits = 15 + F.qp / 6, fq = (1 << qbits) / 3;
-    const int x = blk_x(row & 15) + (c.K.p & 3), y = blk_y(row & 15) + (c.K.p >> 2);
-    for (int mode = 0; mode < 4; ++mode) {
-        if (!i16_mode_avail(S, mode)) continue;
-        int dcv, pa, pb, pc;
-        i16_params(S, mode, dcv, pa, pb, pc);
-        dcv = uni(dcv);
-        pa = uni(pa);
-        pb = uni(pb);
-        pc = uni(pc);
+    const int x = blk_x(blk) + (c.K.p & 3), y = blk_y(blk) + (c.K.p >> 2);
+    for (int m0 = 0; m0 < 4; m0 += kSlots) {
+        const int mode = m0 + slot;  // (wave-uniform)
+        const bool act = slot < kSlots && i16_mode_avail(S, mode);
         int pred = 0, sv = 0, q = 0;
-        if (row < 16) {  // blocks: transform, quant, AC statistics
+        if (act) {  // blocks: transform, quant, AC statistics
+            int dcv, pa, pb, pc;
+            i16_params(S, mode, dcv, pa, pb, pc);
+            dcv = uni(dcv);
+            pa = uni(pa);
+            pb = uni(pb);
+            pc = uni(pc);
             pred = i16_pred(S, mode, x, y, dcv, pa, pb, pc);
             sv = S.src[y * 16 + x];
             const int w = coop_fwd(c.K, sv - pred);
             q = coop_quant(w, c.K.mf, qbits, fq);
             const bool qz = row_or(q != 0) == 0;
             const CoopStat st = coop_cavlc(S.ct, q, c.K.s - 1, S.lvs[row]);
-            S.ih_ac[mode][row][c.K.s == 0 ? 15 : c.K.s - 1] = (int16_t)(c.K.s == 0 ? 0 : q);
+            S.ih_ac[mode][blk][c.K.s == 0 ? 15 : c.K.s - 1] = (int16_t)(c.K.s == 0 ? 0 : q);
             S.ih_pred[mode][y * 16 + x] = (uint8_t)pred;
             if (c.K.p == 0) {
                 S.i16_dcc[row] = w;
-                S.ih.blk[mode][row] = (qz ? 0 : 1) | (st.tc << 1) | (st.t1 << 6) | ((st.sctr + 1) << 8) | (st.rest << 16);
+                S.ih.blk[mode][blk] = (qz ? 0 : 1) | (st.tc << 1) | (st.t1 << 6) | ((st.sctr + 1) << 8) | (st.rest << 16);
             }
         }
         HL_SYNC();
-        if (c.tid < 16) {  // the DC block: Hadamard, quant, CAVLC, scaling
-            const int hh = coop_lin(c.K.had, S.i16_dcc[kDcPos[c.K.p]]) >> 1;
+        if (c.tid < 16 * kSlots && i16_mode_avail(S, m0 + (c.tid >> 4))) {  // the DC blocks: Hadamard, quant, CAVLC, scaling
+            const int ds = c.tid >> 4, dm = m0 + ds;
+            const int hh = coop_lin(c.K.had, S.i16_dcc[ds * 16 + kDcPos[c.K.p]]) >> 1;
             const int qd = quant_dc(F.qp, true, hh);
-            const CoopStat st = coop_cavlc(S.ct, qd, c.K.s, S.lvs[0]);
-            S.ih_dcl[mode][c.K.s] = (int16_t)qd;
+            const CoopStat st = coop_cavlc(S.ct, qd, c.K.s, S.lvs[ds]);
+            S.ih_dcl[dm][c.K.s] = (int16_t)qd;
             const int f = coop_lin(c.K.had, qd);
             const int scale = level_scale(F.qp % 6, 0, 0), q6 = F.qp / 6;
-            S.dcY[c.K.p] = F.qp >= 36 ? (f * scale) << (q6 - 6) : (f * scale + (1 << (5 - q6))) >> (6 - q6);
-            if (c.tid == 0) {  // block 0's nC neighbours lie outside the MB: the DC rate is fixed
+            S.dcY[ds * 16 + c.K.p] = F.qp >= 36 ? (f * scale) << (q6 - 6) : (f * scale + (1 << (5 - q6))) >> (6 - q6);
+            if ((c.tid & 15) == 0) {  // block 0's nC neighbours lie outside the MB: the DC rate is fixed
                 const int nC = nc_luma_of(S, 0, [&](int ni) -> int { return S.tc[ni]; });
-                S.ih.dcs[mode][0] = st.rest + coop_token_len(S.ct, nC, st.tc, st.t1);
-                S.ih.dcs[mode][1] = st.tc;
-                S.ih.dcs[mode][2] = st.sctr;
-                S.ih.dcs[mode][3] = 0;
+                S.ih.dcs[dm][0] = st.rest + coop_token_len(S.ct, nC, st.tc, st.t1);
+                S.ih.dcs[dm][1] = st.tc;
+                S.ih.dcs[dm][2] = st.sctr;
+                S.ih.dcs[dm][3] = 0;
             }
         }
         HL_SYNC();
-        if (row < 16) {  // reconstruction with the residual; both distortions
-            const int r = coop_idct(c.K, c.K.p == 0 ? S.dcY[kDcPos[row]] : coop_dequant(q, c.K.ls, F.qp));
+        if (act) {  // reconstruction with the residual; both distortions
+            const int r = coop_idct(c.K, c.K.p == 0 ? S.dcY[slot * 16 + kDcPos[blk]] : coop_dequant(q, c.K.ls, F.qp));
             const int rec = clip255(pred + r);
             S.ih_rec[mode][y * 16 + x] = (uint8_t)rec;
             const int df = row_sum(iabs(sv - rec)), dz = row_sum(iabs(sv - pred));
@@ -2489,9 +2493,10 @@ HD void i16_heavy(Ctx& c)
             }
         }
         HL_SYNC();
-        if (c.tid < 32) {
-            const int v = row_sum(c.tid < 16 ? S.i16_dist[c.tid] : S.i16_distz[c.tid & 15]);
-            if ((c.tid & 15) == 0) S.ih.dist[mode][c.tid >> 4] = v;
+        if (c.tid < 32 * kSlots && i16_mode_avail(S, m0 + (c.tid >> 5))) {  // lanes 32 s + 16 z + b: slot s, z = without residual
+            const int ds = c.tid >> 5, z = (c.tid >> 4) & 1, b = c.tid & 15;
+            const int v = row_sum(z ? S.i16_distz[ds * 16 + b] : S.i16_dist[ds * 16 + b]);
+            if (b == 0) S.ih.dist[m0 + ds][z] = v;
         }
     }
     HL_SYNC();
@@ -2602,37 +2607,36 @@ HD void i16_light(Ctx& c, double& best_cost, int& best_cbp, int& best_dist, int&
         S.pm0 = PM_I16;
         S.i16mode = 2;
     }
-    for (int mode = 0; mode < 4; ++mode) {
-        if (!i16_mode_avail(S, mode)) continue;
-        int single, bcbp, rate;
 #if defined(__HIP_DEVICE_COMPILE__)
-        // nC of the coded blocks' AC writes: inside the MB, blocks coded
-        // earlier in this mode show their own TotalCoeff (even 0), others the
-        // live state
-        if (c.tid < 16) {
-            const int t = c.tid, w = S.ih.blk[mode][t];
-            if (w & 1) {
-                const int nC = nc_luma_of(S, t, [&](int ni) -> int {
-                    const int wn = S.ih.blk[mode][ni];
-                    return (wn & 1) ? (wn >> 1) & 31 : S.tc[ni];
-                });
-                S.i16_bits[t] = (w >> 16) + coop_token_len(S.ct, nC, (w >> 1) & 31, (w >> 6) & 3);
-                S.tc[t] = (int8_t)((w >> 1) & 31);
-            }
-        }
-        HL_SYNC();
-        // The blocks' effects in block order (residual.c:881-897), vectorised:
-        // lane b of every 16-lane row holds block b.  rdo.Single_ctr after
-        // block b is the counter of the last coding block at or before b
-        // (the entry value if none); a block without coefficients before the
-        // first writer reads the entry value stale.
-        {
-            const int l = c.tid & 15;
-            const int w = S.ih.blk[mode][l];
-            const int called = w & 1, tcb = (w >> 1) & 31, sct = ((w >> 8) & 255) - 1, bits = S.i16_bits[l];
-            const unsigned bc = (unsigned)__ballot(called != 0) & 0xFFFFu, bw = (unsigned)__ballot(called && tcb > 0) & 0xFFFFu;
+    // The four modes at once, every wave alike (registers only): lane 16 m + t
+    // holds block t of mode m.  The modes' sequential effects -- the live
+    // TotalCoeffs (quirk 1) each mode's coded blocks leave for the nC of the
+    // next, the DC block's write of block 0, the rdo.Single_ctr chain -- are
+    // resolved in mode order as scalar work, with the results of the
+    // reference's mode loop (host version below).
+    const bool av[4] = {i16_mode_avail(S, 0), i16_mode_avail(S, 1), true, i16_mode_avail(S, 3)};
+    const int l = c.tid & 63, m = l >> 4, t = l & 15;
+    const bool avm = m == 0 ? av[0] : (m == 1 ? av[1] : (m == 2 ? true : av[3]));
+    const int w = S.ih.blk[m][t];
+    const int tc0 = S.tc[t];  // live TotalCoeff before the modes (lane t of every row)
+    const bool called = avm && (w & 1);
+    const int tcb = (w >> 1) & 31, sct = ((w >> 8) & 255) - 1;
+    const unsigned long long BC = __ballot(called), BW = __ballot(called && tcb > 0);
+    {
+        // per mode: sum over its coded blocks of the counter of the last
+        // writer at or before them (blocks before the first writer read the
+        // entry value: counted below)
+        const unsigned bwl = (unsigned)(BW >> (16 * m)) & 0xFFFFu;
+        const unsigned upto = bwl & ((2u << t) - 1u);
+        const int sv = __shfl(sct, (l & 48) | (upto ? 31 - __clz(upto) : 0), 64);
+        const int s1 = row_sum(called && upto ? sv : 0);
+        int bcbpm[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+            if (!av[mm]) continue;
+            const unsigned bc = (unsigned)(BC >> (16 * mm)) & 0xFFFFu, bw = (unsigned)(BW >> (16 * mm)) & 0xFFFFu;
             const unsigned before = bw ? (bw & (0u - bw)) - 1u : 0xFFFFu;  // blocks before the first writer
-            if (!spec && (bc & ~bw & before) && !c.fresh) {
+            if (!spec && (bc & before) && !c.fresh) {
                 // pipelined run: a speculated value is resolved here; once it
                 // is exact (resolved in this MB or to its left) the read is
                 // exact too.  The per-picture path records the stale read for
@@ -2640,16 +2644,59 @@ HD void i16_light(Ctx& c, double& best_cost, int& best_cbp, int& best_dist, int&
                 if (!F.run_done) c.dep = 1;
                 else if (c.spec) resolve_chain(c);
             }
-            const unsigned upto = bw & ((2u << l) - 1u);  // writers at or before block l
-            const int wl = upto ? 31 - __clz(upto) : 0;
-            const int sv = __shfl(sct, (c.tid & 48) | wl, 64);  // the writer's counter (same row)
-            const int ch = upto ? sv : c.chain;
-            single = uni(row_sum(called ? ch : 0));
-            rate = uni(row_sum(called ? bits : 0));
-            bcbp = (int)bc;
-            if (bw) chain_write(c, __builtin_amdgcn_readlane(sct, 31 - __clz(bw)));
+            const int single = __builtin_amdgcn_readlane(s1, 16 * mm) + __popc(bc & before) * c.chain;
+            if (bw) chain_write(c, __builtin_amdgcn_readlane(sct, 16 * mm + 31 - __clz(bw)));
+            int bcbp = (int)bc;
+            if (bcbp && single < 6) bcbp = 0;
+            if (bcbp && uni(S.ih.dcs[mm][1]) > 0) chain_write(c, uni(S.ih.dcs[mm][2]));
+            bcbpm[mm] = bcbp;
         }
+        // AC rates: nC of every coded block with the live TotalCoeffs its mode sees
+        int bits = 0;
+        if (called) {
+            const int nC = nc_luma_of(S, t, [&](int ni) -> int {
+                const int wn = S.ih.blk[m][ni];
+                if (wn & 1) return (wn >> 1) & 31;  // coded earlier in this mode
+                int v = S.tc[ni];  // (written only after the barrier below)
+#pragma unroll
+                for (int mm = 0; mm < 3; ++mm) {
+                    if (mm >= m || !av[mm]) continue;
+                    const int wp = S.ih.blk[mm][ni];
+                    if (wp & 1) v = (wp >> 1) & 31;
+                    if (ni == 0 && bcbpm[mm]) v = S.ih.dcs[mm][1];
+                }
+                return v;
+            });
+            bits = (w >> 16) + coop_token_len(S.ct, nC, tcb, (w >> 6) & 3);
+        }
+        const int rate_ac = row_sum(bits);
+        int fin = tc0;  // block t's live TotalCoeff after the modes (lanes 0-15)
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+            if (!av[mm]) continue;
+            const int bcbp = bcbpm[mm];
+            const int rate = __builtin_amdgcn_readlane(rate_ac, 16 * mm) + (bcbp ? uni(S.ih.dcs[mm][0]) : 0);
+            const int dist = uni(S.ih.dist[mm][bcbp ? 0 : 1]);
+            const double cost = dadd((double)dist, dmul(F.lambda, (double)rate));
+            if (cost < best_cost) {
+                best_cost = cost;
+                best_dist = dist;
+                best_cbp = bcbp;
+                best_mode = mm;
+            }
+            const int wf = __shfl(w, 16 * mm + t, 64);
+            if (wf & 1) fin = (wf >> 1) & 31;
+            if (t == 0 && bcbp) fin = S.ih.dcs[mm][1];
+        }
+        HL_SYNC();  // every wave's reads of S.tc are done
+        if (c.tid < 16) S.tc[c.tid] = (int8_t)fin;
+        if (c.tid == 0) S.i16mode = best_mode;
+        HL_SYNC();
+    }
 #else
+    for (int mode = 0; mode < 4; ++mode) {
+        if (!i16_mode_avail(S, mode)) continue;
+        int single, bcbp, rate;
         int bits[16];
         for (int t = 0; t < 16; ++t) {
             const int w = S.ih.blk[mode][t];
@@ -2672,7 +2719,6 @@ HD void i16_light(Ctx& c, double& best_cost, int& best_cbp, int& best_dist, int&
         }
         for (int t = 0; t < 16; ++t)
             if (S.ih.blk[mode][t] & 1) S.tc[t] = (int8_t)((S.ih.blk[mode][t] >> 1) & 31);
-#endif
         if (bcbp && single < 6) bcbp = 0;
         if (bcbp) {  // the DC block
             rate += uni(S.ih.dcs[mode][0]);
@@ -2688,8 +2734,8 @@ HD void i16_light(Ctx& c, double& best_cost, int& best_cbp, int& best_dist, int&
             best_mode = mode;
             if (c.tid == 0) S.i16mode = mode;
         }
-        HL_SYNC();
     }
+#endif
 }
 
 // The chosen Intra16x16 mode's levels and reconstruction into S.i16_best_*:
@@ -2765,10 +2811,10 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
     // (workgroups below 288 lanes lack the 18 rows of a two-slot step: one
     // block per step, in z-order)
     constexpr bool kTwoSlots = kMbThreads >= 18 * 16;
-    for (int d = 0; d < (kTwoSlots ? 10 : 16); ++d) {
-#if defined(HL_I4_PROF)
-        HL_PROF_T(ti0);
-#endif
+    constexpr int kSteps = kTwoSlots ? 10 : 16;
+    // the neighbour samples of step d's blocks into S.i4nb (rows 0-1 of wave
+    // 0; the previous step's resolution, the same lanes, wrote their S.rec)
+    auto i4_nbrs = [&](int d) {
         const int b0 = kTwoSlots ? kWave[d][0] : d, b1 = kTwoSlots ? kWave[d][1] : 255;
         const int nslot = b1 == 255 ? 1 : 2;
         if (c.tid < 32 && (c.tid >> 4) < nslot) {
@@ -2791,7 +2837,15 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
             const int dc = (xa && ya) ? (sumt + suml + 4) >> 3 : (ya ? (suml + 2) >> 2 : (xa ? (sumt + 2) >> 2 : 128));
             if (i < 14) S.i4nb[base >> 4][i] = (int16_t)(i == 13 ? dc : v);  // [13]: the DC value
         }
-        HL_SYNC();
+    };
+    i4_nbrs(0);
+    HL_SYNC();
+    for (int d = 0; d < kSteps; ++d) {
+#if defined(HL_I4_PROF)
+        HL_PROF_T(ti0);
+#endif
+        const int b0 = kTwoSlots ? kWave[d][0] : d, b1 = kTwoSlots ? kWave[d][1] : 255;
+        const int nslot = b1 == 255 ? 1 : 2;
 #if defined(HL_I4_PROF)
         HL_PROF_ADD(c, 12, ti0);  // neighbours
         HL_PROF_T(ti1);
@@ -2896,6 +2950,7 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
                 S.luma_level[blk][t] = S.i4_lv[k][best][t];
             }
         }
+        if (d + 1 < kSteps) i4_nbrs(d + 1);
         HL_SYNC();
 #if defined(HL_I4_PROF)
         HL_PROF_ADD(c, 15, ti3);  // resolution + barrier
@@ -3438,7 +3493,15 @@ HD void guess_inter(Ctx& c)
         for (int j = fam_first(fam); j < fam_first(fam + 1); ++j) {
             const PartDef& pd = kParts[j];
             if (!((1 << (j + 1)) & mode_flags)) continue;
-            if (F.early_term && j == 0) mode_flags = early_term_modes(c);
+            if (F.early_term && j == 0) {
+#if !defined(HL_STEP_PROF) && !defined(HL_I4_PROF) && !defined(HL_NBLK_PROF)
+                HL_PROF_T(tet);
+#endif
+                mode_flags = early_term_modes(c);
+#if !defined(HL_STEP_PROF) && !defined(HL_I4_PROF) && !defined(HL_NBLK_PROF)
+                HL_PROF_ADD(c, 12, tet);  // early termination's homogeneity
+#endif
+            }
             HL_SYNC();
             if (c.tid == 0) {
                 S.e_type = fam_type(fam);
@@ -3520,6 +3583,9 @@ HD void guess_inter(Ctx& c)
     }
     else helper_join(c, false);  // not needed: cancelled, or its results are not read
     // finalize (rdo.c:1167-1262)
+#if !defined(HL_STEP_PROF) && !defined(HL_I4_PROF) && !defined(HL_NBLK_PROF)
+    HL_PROF_T(tfin);
+#endif
     const PartDef& bp = kParts[best_part];
     HL_SYNC();
     if (c.tid == 0) {
@@ -3584,6 +3650,9 @@ HD void guess_inter(Ctx& c)
             HL_SYNC();
         }
     }
+#if !defined(HL_STEP_PROF) && !defined(HL_I4_PROF) && !defined(HL_NBLK_PROF)
+    HL_PROF_ADD(c, 13, tfin);  // the inter finalize (prediction, reconstruction, CBP, skip check)
+#endif
 }
 
 // --------------------------------------------------------------------------

@@ -24,7 +24,7 @@ _lib.load_library(os.path.join(ROOT, "build", "prof", "hartallo_amd", "libhartal
 from hartallo_amd import Encoder, synth  # noqa: E402
 
 PHASES = ["eval:block", "eval:nC", "eval:reduce", "search_partition", "mvp", "guess_intra(P)", "mb_begin", "mb_end", "whole MB",
-          "reach_wait", "intra:i16", "intra:i4", "", "", "", "", "step:candidates", "step:selection", "", "helper join"]
+          "reach_wait", "intra:i16", "intra:i4", "early-term modes", "inter finalize", "", "", "step:candidates", "step:selection", "", "helper join"]
 
 
 def main():
