@@ -484,6 +484,9 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         __syncthreads();
         int t = __builtin_amdgcn_readfirstlane(s_task);
         if (t < 0) break;
+#if defined(HL_PROFILE)
+        const unsigned long long pw_start = wall_clock64();  // (the task's timeline, below)
+#endif
         const bool helper = t >= P.nframes * nmb;  // an intra helper task (hl_mbcore.h intra_helper)
         if (helper) t -= P.nframes * nmb;
 #if defined(HL_DIAG) && HL_DIAG == 1
@@ -539,6 +542,12 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         encode_mb(sF, S, addr, tid, kMbThreads, s_in, gx, gy, spec_in);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+#if defined(HL_PROFILE)
+        if (f == 0 && tid == 0 && prof) {
+            prof[64 + nmb + 3 * addr] = pw_start;
+            prof[64 + nmb + 3 * addr + 1] = wall_clock64();
+        }
+#endif
         // (encode_mb stored the record into host memory, PF.F.hrec; the publish fence below is system scope)
 #if defined(HL_PROFILE)
         const unsigned long long pt2 = __builtin_readcyclecounter();
@@ -580,6 +589,9 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, HL_REL_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             release(0);
+#if defined(HL_PROFILE)
+            if (f == 0 && tid == 0 && prof) prof[64 + nmb + 3 * addr + 2] = wall_clock64();
+#endif
             if (tid == 0) {
                 if (x > 0) spin_ge(P.done + t - 1, 1, P.err);
                 if (y > 0) spin_ge(P.done + f * nmb + (y - 1) * mbw + min(x + 1, mbw - 1), 1, P.err);
@@ -821,9 +833,11 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
     // the per-address MB objects start zeroed (calloc'd by the reference, mb.c)
     ok = ok && hipMemsetAsync(e->d_st, 0, sizeof(MbState) * e->nmb, e->stream) == hipSuccess;
 #if defined(HL_PROFILE)
-    // 64 phase counters, then the cycles of every macroblock of the last frame
-    ok = ok && hipMalloc(&e->d_prof, (64 + e->nmb) * sizeof(unsigned long long)) == hipSuccess &&
-         hipMemsetAsync(e->d_prof, 0, (64 + e->nmb) * sizeof(unsigned long long), e->stream) == hipSuccess;
+    // 64 phase counters, the cycles of every macroblock of the last frame,
+    // then the timeline of the first picture of the last pipelined run (per
+    // MB: task start, decision end, in-picture successors released; wall clock)
+    ok = ok && hipMalloc(&e->d_prof, (64 + 4 * e->nmb) * sizeof(unsigned long long)) == hipSuccess &&
+         hipMemsetAsync(e->d_prof, 0, (64 + 4 * e->nmb) * sizeof(unsigned long long), e->stream) == hipSuccess;
 #endif
     ok = ok && hipStreamSynchronize(e->stream) == hipSuccess;
     for (int i = 0; i < 6 && ok; ++i) ok = hipEventCreate(&e->ev[i]) == hipSuccess;
@@ -1751,7 +1765,7 @@ extern "C" int32_t hl_amd_last_mb_launches(hl_amd_encoder_t* e) { return e ? e->
 // counters, then (n > 64) the cycles of each macroblock of the last frame.
 extern "C" int32_t hl_amd_profile_counters(hl_amd_encoder_t* e, unsigned long long* out, int32_t n)
 {
-    if (!e || !out || n < 0 || n > 64 + e->nmb) return HL_AMD_ERROR_INVALID_PARAMETER;
+    if (!e || !out || n < 0 || n > 64 + 4 * e->nmb) return HL_AMD_ERROR_INVALID_PARAMETER;
     memset(out, 0, sizeof(unsigned long long) * n);
     if (!e->d_prof) return HL_AMD_SUCCESS;
     HL_HIP_CHECK(hipMemcpy(out, e->d_prof, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));

@@ -254,7 +254,7 @@ struct Shared {
     // --- best inter decision
     int16_t best_mv[4][4][2], best_mvp[4][4][2];
     // --- intra scratch
-    int32_t pred[256];
+    alignas(16) int32_t pred[256];
     int32_t i16_ac[16][16], i16_dcc[32];  // (i16_ac: scratch of the pipelined task's plane blocks)
     int32_t i16_called[16], i16_bits[16], i16_dist[32], i16_distz[32];  // (i16_dcc / _dist / _distz: two modes' rows)
     alignas(16) int16_t i16_best_ac[16][16];
@@ -545,6 +545,68 @@ HD int nc_luma_of(const Shared& S, int bi, F inside)
         const int ni = blk_idx(bx, by - 4);
         aB = true;
         nB = (S.cbp_l & (1 << (ni >> 2))) ? inside(ni) : 0;
+    }
+    if (aA && aB) return (nA + nB + 1) >> 1;
+    if (aA) return nA;
+    if (aB) return nB;
+    return 0;
+}
+
+// The entry-value bookkeeping of a speculated 8x8-family search (fam3 helper
+// tasks): v of block b, read from the live TotalCoeffs the search started
+// from, keeps every nC class it took part in while v stays in [lo[b], hi[b]].
+HD void iv_tighten(int8_t* lo, int8_t* hi, int b, int l, int h)
+{
+    if (lo[b] < l) lo[b] = (int8_t)l;
+    if (hi[b] > h) hi[b] = (int8_t)(h > 127 ? 127 : h);
+}
+// nC (as nc_luma_of) where inside(ni, entry) also tells whether the value is
+// an entry value; each such read tightens [lo, hi] of its block; a read of
+// both neighbours of block bi at once, [lo[16 + bi], hi[16 + bi]] of their sum
+template <typename F>
+HD int nc_luma_iv(const Shared& S, int bi, F inside, int8_t* lo, int8_t* hi)
+{
+    const int bx = blk_x(bi), by = blk_y(bi);
+    int nA = 0, nB = 0, ia = -1, ib = -1;
+    bool aA, aB;
+    if (bx == 0) {
+        aA = S.extA[bi] >= 0;
+        nA = aA ? S.extA[bi] : 0;
+    }
+    else {
+        const int ni = blk_idx(bx - 4, by);
+        aA = true;
+        if (S.cbp_l & (1 << (ni >> 2))) {
+            bool e = false;
+            nA = inside(ni, e);
+            if (e) ia = ni;
+        }
+    }
+    if (by == 0) {
+        aB = S.extB[bi] >= 0;
+        nB = aB ? S.extB[bi] : 0;
+    }
+    else {
+        const int ni = blk_idx(bx, by - 4);
+        aB = true;
+        if (S.cbp_l & (1 << (ni >> 2))) {
+            bool e = false;
+            nB = inside(ni, e);
+            if (e) ib = ni;
+        }
+    }
+    if (ia >= 0 || ib >= 0) {
+        if (aA && aB) {
+            const int sm = nA + nB;  // classes of (sm + 1) >> 1: sm <= 2, 3..6, 7..14, >= 15
+            const int slo = sm <= 2 ? 0 : (sm <= 6 ? 3 : (sm <= 14 ? 7 : 15)), shi = sm <= 2 ? 2 : (sm <= 6 ? 6 : (sm <= 14 ? 14 : 127));
+            if (ia >= 0 && ib >= 0) iv_tighten(lo + 16, hi + 16, bi, slo, shi);  // both entry values: their sum
+            else if (ia >= 0) iv_tighten(lo, hi, ia, slo - nB, shi - nB);
+            else iv_tighten(lo, hi, ib, slo - nA, shi - nA);
+        }
+        else {
+            const int v = ia >= 0 ? nA : nB, b = ia >= 0 ? ia : ib;
+            iv_tighten(lo, hi, b, v < 2 ? 0 : (v < 4 ? 2 : (v < 8 ? 4 : 8)), v < 2 ? 1 : (v < 4 ? 3 : (v < 8 ? 7 : 127)));
+        }
     }
     if (aA && aB) return (nA + nB + 1) >> 1;
     if (aA) return nA;
@@ -1027,6 +1089,19 @@ HD double mv_cost(const FrameArgs& F, int dist, int bits, int mvx, int mvy, cons
 #if defined(HL_STATS) && !defined(__HIP_DEVICE_COMPILE__)
 extern long long g_hl_stats[8];
 #endif
+#if defined(HL_EMU_BUILD) && !defined(__HIP_DEVICE_COMPILE__)
+// emu-only probe of the 8x8 family's dependence on the live TotalCoeffs it
+// starts from (tests/emu: emu_fam3_stats)
+extern long g_emu_f3[8];
+extern int g_emu_f3_on, g_emu_f3_wr, g_emu_f3_rd;
+extern int g_f3p_on, g_f3p_w, g_f3p_enable;
+extern int8_t g_f3p_lo[32], g_f3p_hi[32];
+#define HL_EMU_F3_READ(ni) (void)(g_emu_f3_on && !((g_emu_f3_wr >> (ni)) & 1) ? (g_emu_f3_rd |= 1 << (ni)) : 0)
+#define HL_EMU_F3_WRITE(bi) (void)(g_emu_f3_on ? (g_emu_f3_wr |= 1 << (bi)) : 0, g_f3p_on ? (g_f3p_w |= 1 << (bi)) : 0)
+#else
+#define HL_EMU_F3_READ(ni) ((void)0)
+#define HL_EMU_F3_WRITE(bi) ((void)0)
+#endif
 
 #if defined(__HIP_DEVICE_COMPILE__)
 // bit i set iff byte i of w is non-zero
@@ -1410,7 +1485,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         if (!S.be_nz[ci][k]) continue;
         const int hx = k % g.nbw, hy = k / g.nbw;
         const int bi = blk_idx(g.px + (hx << 2), g.py + (hy << 2));
-        const int nC = nc_luma_of(S, bi, [&](int ni) -> int {
+        auto inside = [&](int ni, bool& entry) -> int {
             const int nx = blk_x(ni) - g.px, ny = blk_y(ni) - g.py;
             if (nx >= 0 && ny >= 0 && nx < g.pw && ny < g.ph) {
                 const int kk = (ny >> 2) * g.nbw + (nx >> 2);
@@ -1418,8 +1493,21 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                 for (int cj = ci - 1; cj >= 0; --cj)
                     if (S.be_nz[cj][kk]) return S.be_tc[cj][kk];
             }
+            HL_EMU_F3_READ(ni);
+#if defined(HL_EMU_BUILD)
+            entry = g_f3p_on && !((g_f3p_w >> ni) & 1);
+#endif
             return S.tc[ni];
+        };
+#if defined(HL_EMU_BUILD)
+        int8_t dlo[32], dhi[32];
+        const int nC = nc_luma_iv(S, bi, inside, g_f3p_on ? g_f3p_lo : dlo, g_f3p_on ? g_f3p_hi : dhi);
+#else
+        const int nC = nc_luma_of(S, bi, [&](int ni) -> int {
+            bool e;
+            return inside(ni, e);
         });
+#endif
         S.be_bits[ci][k] += token_len(nC, S.be_tc[ci][k], S.be_t1[ci][k]);
     }
     // phase 3: per-candidate sums
@@ -1478,6 +1566,7 @@ HD void commit_candidates(Ctx& c, const PartGeo& g, int n, int last_l = -2)
         for (int cj = n - 1; cj >= 0; --cj)
             if (S.be_nz[cj][k]) {
                 S.tc[bi] = (int8_t)S.be_tc[cj][k];
+                HL_EMU_F3_WRITE(bi);
                 break;
             }
     }
@@ -2902,6 +2991,7 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
             const bool ex = ok && S.i4_exact[sl][l], nz = ok && S.i4_nz[sl][l];
             const unsigned long long bex = __ballot(ex), bnz = __ballot(nz);
             const int sct = ok ? S.i4_sctr[sl][l] : 0;
+            const int dl = ok ? S.i4_dist[sl][l] : 0, tl = ok ? S.i4_tc[sl][l] : 0;
             const double v = ok ? S.i4_cost[sl][l] : 1.7976931348623157e308;
             const double mn = row_min_f64(v);
             const unsigned long long bmin = __ballot(ok && v == mn);
@@ -2930,17 +3020,21 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
                 }
                 bests[k] = best;
                 lastws[k] = lastw;
+                // (every value from registers: the stores carry no dependent load)
+                const int bdist = __builtin_amdgcn_readlane(dl, 16 * k + best);  // d_min_dist4x4 (rdo.c:2011, 2023); 0 for an exact mode
+                const int lwsct = lastw >= 0 ? __builtin_amdgcn_readlane(sct, 16 * k + lastw) : -1;
+                const int lwtc = lastw >= 0 ? __builtin_amdgcn_readlane(tl, 16 * k + lastw) : -1;
                 if (c.tid == 0) {
                     S.i4r_dmin[blk] = dmin;
-                    S.i4r_dist[blk] = S.i4_dist[k][best];  // d_min_dist4x4 (rdo.c:2011, 2023); 0 for an exact mode
-                    S.i4r_sct[blk] = lastw >= 0 ? __builtin_amdgcn_readlane(sct, 16 * k + lastw) : -1;
+                    S.i4r_dist[blk] = bdist;
+                    S.i4r_sct[blk] = lwsct;
                     S.i4r_zero[blk] = best_zero;
                     S.i4mode[blk] = (int8_t)best;
-                    if (lastw >= 0) S.tc[blk] = (int8_t)S.i4_tc[k][lastw];
+                    if (lastw >= 0) S.tc[blk] = (int8_t)lwtc;
                     // the verification record (i4_verify): the costs used an nC
                     // only without an exact mode and with a coded one
                     S.ih.i4_ncls[blk] = (int8_t)(!E && W ? nc_class(k ? nC1 : nC0) : -1);
-                    S.ih.i4_lwtc[blk] = (int8_t)(lastw >= 0 ? S.i4_tc[k][lastw] : -1);
+                    S.ih.i4_lwtc[blk] = (int8_t)lwtc;
                 }
             }
             if (c.tid < 16 * nslot) {
@@ -3299,6 +3393,32 @@ HD void inter_pred_mb(Ctx& c, bool chroma_only_16x16, bool luma)
     const FrameArgs& F = c.F;
     Shared& S = c.S;
     if (luma) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        // one 4-lane quad per 4x4 block, lane r = row r: the quarter-pel
+        // sample pairs of the search (put_cand / eval_candidates)
+        if (c.tid < 64) {
+            const int t = c.tid >> 2, r = c.tid & 3, bx = blk_x(t), by = blk_y(t);
+            int pi, spi;
+            part_of(S, bx, by, pi, spi);
+            const NbInfo& n = S.nb[0];
+            const int xP = (pi % (16 / n.part_w)) * n.part_w, yP = (pi / (16 / n.part_w)) * n.part_h;
+            int xS = 0, yS = 0;
+            if (is8x8(n.e_type)) {
+                xS = (spi % (8 / n.sub_w[pi])) * n.sub_w[pi];
+                yS = (spi / (8 / n.sub_w[pi])) * n.sub_h[pi];
+            }
+            const int mvx = n.mv[pi][spi][0], mvy = n.mv[pi][spi][1];
+            const int X = clip3(-17, F.W + 17, c.xL + xP + xS + (mvx >> 2)) + kPad + bx - xP - xS;
+            const int Y = clip3(-17, F.H + 17, c.yL + yP + yS + (mvy >> 2)) + kPad + by - yP - yS + r;
+            const uint32_t e = S.qtab[((mvy & 3) << 2) | (mvx & 3)];
+            const int o1 = (int)(e & 3) * F.plsz + (Y + (int)((e >> 3) & 1)) * F.pstride + X + (int)((e >> 2) & 1);
+            const int o2 = (e & 16) ? (int)((e >> 5) & 3) * F.plsz + (Y + (int)((e >> 8) & 1)) * F.pstride + X + (int)((e >> 7) & 1) : o1;
+            const auto base = gmem(F.pl[0]);
+            const uint32_t pr = avg_u8x4(ld_u8x4(base, o1), ld_u8x4(base, o2));
+            *reinterpret_cast<int4*>(&S.pred[(by + r) * 16 + bx]) =
+                make_int4((int)(pr & 255), (int)((pr >> 8) & 255), (int)((pr >> 16) & 255), (int)(pr >> 24));
+        }
+#else
         for (int t = c.tid; t < 16; t += c.nthr) {
             const int bx = blk_x(t), by = blk_y(t);
             int pi, spi;
@@ -3317,6 +3437,7 @@ HD void inter_pred_mb(Ctx& c, bool chroma_only_16x16, bool luma)
             pred_luma4x4(F, X, Y, mvx & 3, mvy & 3, p);
             for (int i = 0; i < 16; ++i) S.pred[(by + (i >> 2)) * 16 + bx + (i & 3)] = p[i];
         }
+#endif
     }
     for (int t = c.tid; t < 64; t += c.nthr) {
         const int cx = t & 7, cy = t >> 3;
@@ -3341,6 +3462,47 @@ HD void reconstruct_inter_luma(Ctx& c, int single_luma)
 {
     const FrameArgs& F = c.F;
     Shared& S = c.S;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // one 4-lane quad per 4x4 block (hl_quad.h, as the search evaluated it)
+    if (c.tid < 64) {
+        const int t = c.tid >> 2, r = c.tid & 3, bx = blk_x(t), by = blk_y(t);
+        const LaneQ& Q = c.Q;
+        const int4 pv = *reinterpret_cast<const int4*>(&S.pred[(by + r) * 16 + bx]);
+        const int pr[4] = {pv.x, pv.y, pv.z, pv.w};
+        const uint32_t sv = *reinterpret_cast<const uint32_t*>(&S.src[(by + r) * 16 + bx]);
+        int q[4] = {0, 0, 0, 0};
+        bool coded = false;
+        if (single_luma >= 6) {
+            const int qbits = 15 + F.qp / 6, f = (1 << qbits) / 6;
+            int x[4], y[4];
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) x[cc] = (int)((sv >> (8 * cc)) & 255) - pr[cc];
+            quad_fwd(Q, x, y);
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) q[cc] = quad_q1(y[cc], (cc & 1) ? Q.mfO : Q.mfE, qbits, f);
+            coded = quad_or(q[0] | q[1] | q[2] | q[3]) != 0;
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) S.luma_level[t][(Q.zz >> (4 * cc)) & 15] = coded ? q[cc] : 0;
+        }
+        uint32_t rec = 0;
+        if (coded) {
+            int rr[4];
+            quad_idct(Q, q, F.qp, rr);
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) rec |= (uint32_t)clip255(pr[cc] + rr[cc]) << (8 * cc);
+        }
+        else rec = (uint32_t)pr[0] | ((uint32_t)pr[1] << 8) | ((uint32_t)pr[2] << 16) | ((uint32_t)pr[3] << 24);
+        *reinterpret_cast<uint32_t*>(&S.rec[(by + r) * 16 + bx]) = rec;
+        const unsigned long long bal = __ballot(coded && r == 0);
+        if (c.tid == 0) {
+            int cbp = 0;
+#pragma unroll
+            for (int b = 0; b < 16; ++b) cbp |= (int)((bal >> (4 * b)) & 1) << b;
+            S.cbp_l4x4 = cbp;
+        }
+    }
+    HL_SYNC();
+#else
     for (int t = c.tid; t < 16; t += c.nthr) {
         const int xO = blk_x(t), yO = blk_y(t);
         int res[16], pred[16];
@@ -3379,6 +3541,7 @@ HD void reconstruct_inter_luma(Ctx& c, int single_luma)
         S.cbp_l4x4 = cbp;
     }
     HL_SYNC();
+#endif
 }
 
 // --------------------------------------------------------------------------
@@ -3489,7 +3652,87 @@ HD void guess_inter(Ctx& c)
     bool probably = false;
     int mode_flags = 0xFFFF;  // rdo.c:874
     if (c.tid == 0) S.flags = FL_INTER;
+    // one partitioning j of family fam searched: the partition mode's best
+    // cost, its Single_ctr sum and distortion; returns the P_Skip probe's
+    // outcome (16x16 only)
+    auto run_part = [&](Ctx& cc, int j, int fam, double& cost_sum, int& single_sum, int& dist_sum) -> bool {
+        Shared& SS = cc.S;
+        const PartDef& pd = kParts[j];
+        HL_SYNC();
+        if (cc.tid == 0) {
+            SS.e_type = fam_type(fam);
+            SS.nb[0].e_type = fam_type(fam);
+            SS.nb[0].part_w = pd.part_w;
+            SS.nb[0].part_h = pd.part_h;
+            for (int i = 0; i < 4; ++i) {
+                SS.nb[0].sub_w[i] = pd.sub_w;
+                SS.nb[0].sub_h[i] = pd.sub_h;
+            }
+            grid_reset_inside(SS);
+        }
+        HL_SYNC();
+        bool prob = false;
+        for (int pi = 0; pi < pd.num_part; ++pi)
+            for (int spi = 0; spi < pd.num_sub; ++spi) {
+                const bool p = search_partition(cc, pd, pi, spi, j == 0 && pi == 0 && spi == 0);
+                if (j == 0 && pi == 0 && spi == 0) prob = p;
+            }
+        for (int pi = 0; pi < pd.num_part; ++pi)
+            for (int spi = 0; spi < pd.num_sub; ++spi) {
+                cost_sum = dadd(cost_sum, uni(SS.bcost[pi][spi]));
+                single_sum += uni(SS.bsingle[pi][spi]);
+                dist_sum += uni(SS.bdist[pi][spi]);
+            }
+        return prob;
+    };
+#if defined(HL_EMU_BUILD) && !defined(__HIP_DEVICE_COMPILE__)
+    // emu probe: the 8x8 family searched a second time from the MB-start
+    // live TotalCoeffs (what a concurrent helper would have to assume)
+    struct F3 {
+        Shared S2;
+        double cs[7];
+        int ss[7], ds[7];
+        int16_t bmv[7][4][4][2], bmvp[7][4][4][2];
+    };
+    int8_t f3_mbstart[16], f3_start[16];
+    for (int i = 0; i < 16; ++i) f3_mbstart[i] = S.tc[i];
+    F3* f3 = nullptr;
+    bool f3_same = true;
+    Ctx* c2 = nullptr;
+#endif
     for (int fam = 0; fam < 4 && !best_found; ++fam) {
+#if defined(HL_EMU_BUILD) && !defined(__HIP_DEVICE_COMPILE__)
+        if (fam == 3 && g_f3p_enable) {
+            f3 = new F3;
+            f3->S2 = S;
+            for (int i = 0; i < 16; ++i) f3->S2.tc[i] = f3_mbstart[i];
+            c2 = new Ctx{c.F, f3->S2, c.tid, c.nthr, c.addr, c.mbx, c.mby, c.xL, c.yL, c.chain, c.fresh, c.dep, c.K};
+            c2->gx = c.gx;
+            c2->gy = c.gy;
+            c2->wux = c.wux;
+            c2->wuy = c.wuy;
+            c2->spec = c.spec;
+            c2->par = c.par;
+            g_f3p_on = 1;
+            g_f3p_w = 0;
+            for (int i = 0; i < 32; ++i) {
+                g_f3p_lo[i] = 0;
+                g_f3p_hi[i] = 127;
+            }
+            for (int j = 3; j < 7; ++j) {
+                f3->cs[j] = 0.0;
+                f3->ss[j] = f3->ds[j] = 0;
+                if (!((1 << (j + 1)) & mode_flags)) continue;
+                run_part(*c2, j, 3, f3->cs[j], f3->ss[j], f3->ds[j]);
+                memcpy(f3->bmv[j], f3->S2.bmv, sizeof(f3->S2.bmv));
+                memcpy(f3->bmvp[j], f3->S2.bmvp, sizeof(f3->S2.bmvp));
+            }
+            g_f3p_on = 0;
+            g_emu_f3_on = 1;
+            g_emu_f3_wr = g_emu_f3_rd = 0;
+            for (int i = 0; i < 16; ++i) f3_start[i] = S.tc[i];
+        }
+#endif
         for (int j = fam_first(fam); j < fam_first(fam + 1); ++j) {
             const PartDef& pd = kParts[j];
             if (!((1 << (j + 1)) & mode_flags)) continue;
@@ -3502,34 +3745,15 @@ HD void guess_inter(Ctx& c)
                 HL_PROF_ADD(c, 12, tet);  // early termination's homogeneity
 #endif
             }
-            HL_SYNC();
-            if (c.tid == 0) {
-                S.e_type = fam_type(fam);
-                S.nb[0].e_type = fam_type(fam);
-                S.nb[0].part_w = pd.part_w;
-                S.nb[0].part_h = pd.part_h;
-                for (int i = 0; i < 4; ++i) {
-                    S.nb[0].sub_w[i] = pd.sub_w;
-                    S.nb[0].sub_h[i] = pd.sub_h;
-                }
-                grid_reset_inside(S);
-            }
-            HL_SYNC();
-            bool prob = false;
-            for (int pi = 0; pi < pd.num_part; ++pi)
-                for (int spi = 0; spi < pd.num_sub; ++spi) {
-                    const bool p = search_partition(c, pd, pi, spi, j == 0 && pi == 0 && spi == 0);
-                    if (j == 0 && pi == 0 && spi == 0) prob = p;
-                }
-            probably = prob;
             double cost_sum = 0.0;
             int single_sum = 0, dist_sum = 0;
-            for (int pi = 0; pi < pd.num_part; ++pi)
-                for (int spi = 0; spi < pd.num_sub; ++spi) {
-                    cost_sum = dadd(cost_sum, uni(S.bcost[pi][spi]));
-                    single_sum += uni(S.bsingle[pi][spi]);
-                    dist_sum += uni(S.bdist[pi][spi]);
-                }
+            probably = run_part(c, j, fam, cost_sum, single_sum, dist_sum);
+#if defined(HL_EMU_BUILD) && !defined(__HIP_DEVICE_COMPILE__)
+            if (fam == 3 && f3 && j < 7) {
+                f3_same = f3_same && f3->cs[j] == cost_sum && f3->ss[j] == single_sum && f3->ds[j] == dist_sum &&
+                          memcmp(f3->bmv[j], S.bmv, sizeof(S.bmv)) == 0 && memcmp(f3->bmvp[j], S.bmvp, sizeof(S.bmvp)) == 0;
+            }
+#endif
             if (!probably && cost_sum != 0.0 && single_sum < 6 && fam == 0) {
                 int smv[2];
                 skip_mv(S, smv);
@@ -3569,6 +3793,39 @@ HD void guess_inter(Ctx& c)
             pskip = !uni(S.cbp_cac[0]) && !uni(S.cbp_cac[1]) && !uni(S.cbp_cdc[0]) && !uni(S.cbp_cdc[1]);
         }
         best_found = best_found || best_cost == 0.0 || pskip;
+#if defined(HL_EMU_BUILD) && !defined(__HIP_DEVICE_COMPILE__)
+        if (fam == 3 && f3) {
+            g_emu_f3_on = 0;
+            int diff = 0, diffc = 0;
+            for (int i = 0; i < 16; ++i)
+                if ((g_emu_f3_rd >> i) & 1) {
+                    diff += f3_mbstart[i] != f3_start[i];
+                    diffc += nc_class(f3_mbstart[i]) != nc_class(f3_start[i]);
+                }
+            ++g_emu_f3[0];                                  // MBs that searched the 8x8 family
+            g_emu_f3[1] += g_emu_f3_rd == 0;                // ... reading no entry TotalCoeff
+            g_emu_f3[2] += diff == 0;                       // ... whose reads the MB-start values match
+            g_emu_f3[3] += __builtin_popcount(g_emu_f3_rd);  // entry values read
+            g_emu_f3[4] += diffc == 0;                      // ... matching in nC class
+            const bool same = f3_same && memcmp(f3->S2.tc, S.tc, 16) == 0 && c2->chain == c.chain && c2->fresh == c.fresh;
+            g_emu_f3[5] += same;                            // ... whose search from the MB-start values ends identically
+            g_emu_f3[6] += f3_same;                         // ... (same partition results, any end state)
+            bool ver = true;
+            for (int i = 0; i < 16; ++i) {
+                ver = ver && f3_start[i] >= g_f3p_lo[i] && f3_start[i] <= g_f3p_hi[i];
+                if (blk_x(i) > 0 && blk_y(i) > 0) {
+                    const int sm = f3_start[blk_idx(blk_x(i) - 4, blk_y(i))] + f3_start[blk_idx(blk_x(i), blk_y(i) - 4)];
+                    ver = ver && sm >= g_f3p_lo[16 + i] && sm <= g_f3p_hi[16 + i];
+                }
+            }
+            g_emu_f3[7] += ver;                             // ... verified by the entry-value intervals
+            if (ver && !f3_same) fprintf(stderr, "fam3 probe: verified but different (MB %d)\n", c.addr);
+            delete c2;
+            delete f3;
+            c2 = nullptr;
+            f3 = nullptr;
+        }
+#endif
     }
     if (!pskip) {
         HL_PROF_T(ti);

@@ -24,6 +24,10 @@ using namespace hl;
 
 #if !defined(__HIP_DEVICE_COMPILE__)
 int hl::g_emu_bad_guess = 0;  // intra_helper (hl_mbcore.h): HL_EMU_HELPER=2
+long hl::g_emu_f3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+int hl::g_emu_f3_on = 0, hl::g_emu_f3_wr = 0, hl::g_emu_f3_rd = 0;
+int hl::g_f3p_on = 0, hl::g_f3p_w = 0, hl::g_f3p_enable = 0;
+int8_t hl::g_f3p_lo[32], hl::g_f3p_hi[32];
 #endif
 
 struct EmuEnc {
@@ -247,6 +251,10 @@ extern "C" void emu_destroy(void* h)
 extern "C" long emu_helper_runs(void* h) { return ((EmuEnc*)h)->helper_runs; }
 extern "C" int emu_helper_i4(void* h, int rejected) { return ((EmuEnc*)h)->perr[rejected ? 3 : 2]; }
 extern "C" void emu_set_helper(void* h, int mode) { ((EmuEnc*)h)->helper_mode = mode; }
+#if !defined(__HIP_DEVICE_COMPILE__)
+extern "C" void emu_fam3_stats(long* out) { for (int i = 0; i < 8; ++i) out[i] = g_emu_f3[i]; }  // (development probe)
+extern "C" void emu_fam3_enable(int on) { g_f3p_enable = on; }
+#endif
 
 // Writes hdr (first frame) + 00 00 01 + slice into out; returns bytes or -1.
 // rate control of the product path (hl_amd_set_rate_control)

@@ -20,7 +20,7 @@ import torch  # noqa: E402
 
 from hartallo_amd import _lib  # noqa: E402
 
-_lib.load_library(os.path.join(ROOT, "build", "prof", "hartallo_amd", "libhartallo_amd.so"))
+_lib.load_library(os.environ.get("HL_LIB") or os.path.join(ROOT, "build", "prof", "hartallo_amd", "libhartallo_amd.so"))
 from hartallo_amd import Encoder, synth  # noqa: E402
 
 PHASES = ["eval:block", "eval:nC", "eval:reduce", "search_partition", "mvp", "guess_intra(P)", "mb_begin", "mb_end", "whole MB",
