@@ -260,6 +260,8 @@ __device__ void task_filters(const PipeFrame& PF, Shared& S, int x, int y, int m
 #define HL_SUBQ 4
 #endif
 constexpr int kSubQ = HL_SUBQ;
+// head entries each lane of pop_task examines: kScan * 64 / kSubQ pictures in view
+constexpr int kScan = 4;
 
 // Dependency counters and ready queues of a run (hl_pipeline.h): only task
 // (0, 0) of every stream's first picture starts ready.
@@ -317,52 +319,86 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     int empty = 0;
     for (;;) {
-        // lane = (sub-queue lane % kSubQ, stream r % S, its picture oldest +
-        // r / S) with r = lane / kSubQ: the window of each stream's first
-        // unfinished pictures
+        // entry e = lane + 64 i (kScan per lane) = (sub-queue e % kSubQ,
+        // stream r % S, its picture oldest + r / S) with r = e / kSubQ: the
+        // window of each stream's first unfinished pictures
         const int S = P.nstreams;
         int ol = 0;
         if (lane < S) ol = ld_relaxed(P.oldest + lane);
         if (__ballot(lane < S && ol < P.spp) == 0) return -1;  // every stream finished
-        const int sq = lane % kSubQ, rr = lane / kSubQ, sj = rr % S, j = rr / S;
-        const int k = __shfl(ol, sj, 64) + j;
-        const bool in = j < max(1, P.window / S) && k < P.spp;
-        const int fl = sj * P.spp + k, ql = fl * kSubQ + sq;  // picture slot, its sub-queue
-        int h = 0, t = 0;
-        if (in) {
-            h = ld_relaxed(P.head + ql);
-            t = ld_relaxed(P.tail + ql);
-        }
-        int i0 = -1, hh = 0, v = 0;
-        if (P.hop < 0) {
-            const unsigned long long bal = __ballot(in && h < t);
-            if (bal) {
-                i0 = __ffsll((long long)bal) - 1;
-                hh = __builtin_amdgcn_readlane(h, i0);
+        int fl[kScan], ql[kScan], hs[kScan], ts[kScan], js[kScan], sqs[kScan];
+        bool ins[kScan];
+#pragma unroll
+        for (int i = 0; i < kScan; ++i) {
+            const int e = lane + 64 * i, sq = e % kSubQ, rr = e / kSubQ, sj = rr % S, j = rr / S;
+            const int k = __shfl(ol, sj, 64) + j;
+            ins[i] = j < max(1, P.window / S) && k < P.spp;
+            fl[i] = sj * P.spp + k;  // picture slot, its sub-queue
+            ql[i] = fl[i] * kSubQ + sq;
+            js[i] = j;
+            sqs[i] = sq;
+            hs[i] = ts[i] = 0;
+            if (ins[i]) {
+                hs[i] = ld_relaxed(P.head + ql[i]);
+                ts[i] = ld_relaxed(P.tail + ql[i]);
             }
+        }
+        int i0 = -1, hh = 0, v = 0, bfl = 0, bql = 0;
+        if (P.hop < 0) {
+            // oldest first: the first non-empty entry
+            unsigned long long bal = 0;
+            int bh = 0;
+#pragma unroll
+            for (int i = 0; i < kScan && !bal; ++i) {
+                bal = __ballot(ins[i] && hs[i] < ts[i]);
+                if (bal) {
+                    i0 = __ffsll((long long)bal) - 1;
+                    bh = __builtin_amdgcn_readlane(hs[i], i0);
+                    bfl = __builtin_amdgcn_readlane(fl[i], i0);
+                    bql = __builtin_amdgcn_readlane(ql[i], i0);
+                }
+            }
+            hh = bh;
         }
         else {
-            // the head entries themselves (0: pushed, not yet written)
-            int q = 0;
-            if (in && h < t) q = ld_relaxed(P.queue + ql * nmb + h);
-            int key = -1;
-            if (q > 0) {
-                const int a = q - 1, y = a / mbw, x = a - y * mbw;
-                const int own = sq == (int)(blockIdx.x % kSubQ) ? 12 : 0;  // preference for the workgroup's sub-queue
-                key = (((mbw - 1 - x) + 2 * (mbh - 1 - y) - P.hop * j + own + 4096) << 6) | (63 - lane);
+            // the head entries themselves (0: pushed, not yet written); each
+            // lane keeps its best, then the wave's best
+            int qv[kScan];
+#pragma unroll
+            for (int i = 0; i < kScan; ++i) {
+                qv[i] = 0;
+                if (ins[i] && hs[i] < ts[i]) qv[i] = ld_relaxed(P.queue + ql[i] * nmb + hs[i]);
             }
-            for (int s = 1; s < 64; s <<= 1) key = max(key, __shfl_xor(key, s, 64));
+            int key = -1, lh = 0, lq = 0, lfl = 0, lql = 0;
+#pragma unroll
+            for (int i = 0; i < kScan; ++i) {
+                if (qv[i] > 0) {
+                    const int a = qv[i] - 1, y = a / mbw, x = a - y * mbw;
+                    const int own = sqs[i] == (int)(blockIdx.x % kSubQ) ? 12 : 0;  // preference for the workgroup's sub-queue
+                    const int kk = (((mbw - 1 - x) + 2 * (mbh - 1 - y) - P.hop * js[i] + own + 4096) << 6) | (63 - lane);
+                    if (kk > key) {
+                        key = kk;
+                        lh = hs[i];
+                        lq = qv[i];
+                        lfl = fl[i];
+                        lql = ql[i];
+                    }
+                }
+            }
+            for (int s2 = 1; s2 < 64; s2 <<= 1) key = max(key, __shfl_xor(key, s2, 64));
             key = __builtin_amdgcn_readfirstlane(key);
             if (key >= 0) {
                 i0 = 63 - (key & 63);
-                hh = __builtin_amdgcn_readlane(h, i0);
-                v = __builtin_amdgcn_readlane(q, i0);
+                hh = __builtin_amdgcn_readlane(lh, i0);
+                v = __builtin_amdgcn_readlane(lq, i0);
+                bfl = __builtin_amdgcn_readlane(lfl, i0);
+                bql = __builtin_amdgcn_readlane(lql, i0);
             }
             // else: empty, or only pushes between their tail and slot stores
         }
         if (i0 >= 0) {
             HL_POPSTAT(0);
-            const int f = __builtin_amdgcn_readlane(fl, i0), qf = __builtin_amdgcn_readlane(ql, i0);
+            const int f = bfl, qf = bql;
             int r = 0;
             if (lane == 0 && atomicCAS(P.head + qf, hh, hh + 1) == hh) {
                 r = v;
