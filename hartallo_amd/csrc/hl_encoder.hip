@@ -261,7 +261,10 @@ __device__ void task_filters(const PipeFrame& PF, Shared& S, int x, int y, int m
 #endif
 constexpr int kSubQ = HL_SUBQ;
 // head entries each lane of pop_task examines: kScan * 64 / kSubQ pictures in view
-constexpr int kScan = 4;
+#ifndef HL_SCAN
+#define HL_SCAN 4
+#endif
+constexpr int kScan = HL_SCAN;
 
 // Dependency counters and ready queues of a run (hl_pipeline.h): only task
 // (0, 0) of every stream's first picture starts ready.

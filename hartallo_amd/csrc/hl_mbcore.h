@@ -301,6 +301,26 @@ struct Shared {
 #endif
 };
 
+// A fresh, opaque copy of the lane index at the entry of each phase: the
+// compiler cannot compute the phase's lane-dependent addresses earlier and
+// hold them (spilled) across the partition searches.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define HL_FRESH_TID(c) \
+    do { \
+        int t_ = (c).tid; \
+        asm volatile("" : "+v"(t_)); \
+        (c).tid = t_; \
+    } while (0)
+#else
+#define HL_FRESH_TID(c) ((void)0)
+#endif
+#ifndef HL_FRESH_MASK
+#define HL_FRESH_MASK 0xFFE
+#endif
+#define HL_FRESH_TID_K(c, k) \
+    do { \
+        if ((HL_FRESH_MASK >> (k)) & 1) HL_FRESH_TID(c); \
+    } while (0)
 struct Ctx {
     const FrameArgs& F;
     Shared& S;
@@ -1669,6 +1689,7 @@ HD void reach_wait(Ctx& c, const PartGeo& g, const int pmv[2])
 // the P_Skip probe fired (16x16 only).
 HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
 {
+    // (no HL_FRESH_TID here: ROCm 7.2's greedy register allocator crashes on it)
     Shared& S = c.S;
     HL_PROF_T(tsp);
     const int xP = (pi % (16 / pd.part_w)) * pd.part_w, yP = (pi / (16 / pd.part_w)) * pd.part_h;
@@ -2264,6 +2285,7 @@ HD void i16_params(const Shared& S, int mode, int& dcv, int& pa, int& pb, int& p
 // S.predc holds the chroma prediction; writes recon to the picture.
 HD void reconstruct_chroma(Ctx& c, bool intra_flag)
 {
+    HL_FRESH_TID_K(c, 1);
     const FrameArgs& F = c.F;
     Shared& S = c.S;
     for (int t = c.tid; t < 8; t += c.nthr) {
@@ -2466,6 +2488,7 @@ HD void intra_chroma_pred(Ctx& c, int mode)
 // per 1088p I picture, none in the P pictures of the test content.
 HD void resolve_chain(Ctx& c)
 {
+    HL_FRESH_TID_K(c, 2);
 #if defined(__HIP_DEVICE_COMPILE__)
     const FrameArgs& F = c.F;
     Shared& S = c.S;
@@ -2519,6 +2542,7 @@ HD int nc_class(int nC) { return nC < 2 ? 0 : (nC < 4 ? 1 : (nC < 8 ? 2 : 3)); }
 // it.  Into S.ih (blk, dcs, dist) and S.ih_rec / ih_pred / ih_ac / ih_dcl.
 HD void i16_heavy(Ctx& c)
 {
+    HL_FRESH_TID_K(c, 3);
     const FrameArgs& F = c.F;
     Shared& S = c.S;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -2684,6 +2708,7 @@ HD void i16_heavy(Ctx& c)
 // coded-block mask, distortion and index.
 HD void i16_light(Ctx& c, double& best_cost, int& best_cbp, int& best_dist, int& best_mode, bool spec)
 {
+    HL_FRESH_TID_K(c, 4);
     const FrameArgs& F = c.F;
     Shared& S = c.S;
     best_dist = 0;
@@ -2832,6 +2857,7 @@ HD void i16_light(Ctx& c, double& best_cost, int& best_cbp, int& best_dist, int&
 // global memory (hin)
 HD void i16_copy_best(Ctx& c, int mode, bool coded, const IntraSpec* hin)
 {
+    HL_FRESH_TID_K(c, 5);
     Shared& S = c.S;
 #if defined(__HIP_DEVICE_COMPILE__)
     const int t = c.tid;
@@ -2875,6 +2901,7 @@ HD void guess_i16(Ctx& c, double& best_cost, int& best_cbp, int& best_dist)
 // --------------------------------------------------------------------------
 HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
 {
+    HL_FRESH_TID_K(c, 6);
     best_dist = 0;
     const FrameArgs& F = c.F;
     Shared& S = c.S;
@@ -3257,6 +3284,7 @@ HD bool i4_verify(Ctx& c)
 // guess_i4 would have left it
 HD void i4_apply(Ctx& c, const IntraSpec* hin, double& c4, int& cbp4, int& d4)
 {
+    HL_FRESH_TID_K(c, 7);
     Shared& S = c.S;
     if (c.tid == 0) {
         S.e_type = ET_I_NXN;
@@ -3300,6 +3328,7 @@ HD void i4_apply(Ctx& c, const IntraSpec* hin, double& c4, int& cbp4, int& d4)
 // results of this MB's intra helper task (S.ih already imported), or null.
 HD double guess_intra(Ctx& c, const IntraSpec* hin = nullptr)
 {
+    HL_FRESH_TID_K(c, 8);
     const FrameArgs& F = c.F;
     Shared& S = c.S;
     double c16, c4;
@@ -3390,6 +3419,7 @@ HD void part_of(const Shared& S, int lx, int ly, int& pi, int& spi)
 // luma prediction of the MB into S.pred, chroma into S.predc; mv from S.nb[0].mv
 HD void inter_pred_mb(Ctx& c, bool chroma_only_16x16, bool luma)
 {
+    HL_FRESH_TID_K(c, 9);
     const FrameArgs& F = c.F;
     Shared& S = c.S;
     if (luma) {
@@ -3460,6 +3490,7 @@ HD void inter_pred_mb(Ctx& c, bool chroma_only_16x16, bool luma)
 // rdo.c:2274-2500 luma part (chroma via reconstruct_chroma)
 HD void reconstruct_inter_luma(Ctx& c, int single_luma)
 {
+    HL_FRESH_TID_K(c, 10);
     const FrameArgs& F = c.F;
     Shared& S = c.S;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -3991,6 +4022,7 @@ __device__ __forceinline__ int count_nz(const T* v, int n)
 // and / or device memory).  Same results as the host version below.
 __device__ __forceinline__ void mb_end(Ctx& c)
 {
+    HL_FRESH_TID_K(c, 11);
     const FrameArgs& F = c.F;
     Shared& S = c.S;
     const int tid = c.tid;
