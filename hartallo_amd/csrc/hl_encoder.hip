@@ -489,6 +489,11 @@ __device__ int claim_next(const PipeArgs& P, int nmb, int& cursor)
 #ifndef HL_EARLY_RELEASE
 #define HL_EARLY_RELEASE 1
 #endif
+// 1: successor-counter decrements relaxed behind the task's release fence,
+// an acquire fence only before a push (0: acq_rel decrements)
+#ifndef HL_CNT_SPLIT
+#define HL_CNT_SPLIT 1
+#endif
 __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(PipeArgs P, int mbw, int mbh)
 {
     __shared__ Shared S;
@@ -502,7 +507,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
     // task, decisions, filters, tasks, workgroup lifetime (shader clock)
     unsigned long long pw_wait = 0, pw_mb = 0, pw_filt = 0, pw_n = 0, pw_hlp = 0, pw_hn = 0;
     unsigned long long pst[3] = {0, 0, 0};  // pop_task rounds (wave 0)
-    unsigned long long ptail[4] = {0, 0, 0, 0};  // after the filters: barrier, release fence, successors' release; early release
+    unsigned long long ptail[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // after the filters: barrier, release fence, successors' release; early release; its fence, release, spin, acquire
     const unsigned long long pw_t0 = __builtin_readcyclecounter();
     unsigned long long* prof = P.fr[0].F.prof;
 #endif
@@ -598,22 +603,32 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         // consumer acquires after its pop): those of this picture (phase 0),
         // of the next one (1), or all (2).  Those whose last dependency this
         // was are queued (with their intra helpers, in P pictures).
+        // (two dependent round trips per successor: its counter, then the
+        // queue and helper FIFO tails together; the successor picture's kind
+        // is read before them)
         auto release = [&](int phase) {
             int fo = 0, xo = 0, yo = 0;
             const int ns = task_succ(fk, x, y, mbw, mbh, P.reach, P.spp, -1, fo, xo, yo);
             for (int j = tid; j < ns; j += 64) {
                 task_succ(fk, x, y, mbw, mbh, P.reach, P.spp, j, fo, xo, yo);
                 if (phase != 2 && (fo == fk) != (phase == 0)) continue;
+                const bool hlp = P.helpers && !(fo == fk ? sF.is_intra : ld_relaxed(&P.fr[fo + fb].F.is_intra));
                 fo += fb;
                 const int a = yo * mbw + xo;
+#if HL_CNT_SPLIT
+                // the release half is the fence before release(); the acquire
+                // half (the other dependencies' writes happen before the push)
+                // only where this decrement was the last
+                if (__hip_atomic_fetch_add(P.cnt + fo * nmb + a, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1) continue;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
+#else
                 if (__hip_atomic_fetch_add(P.cnt + fo * nmb + a, -1, HL_CNT_ORDER, __HIP_MEMORY_SCOPE_AGENT) != 1) continue;
+#endif
                 const int qf = fo * kSubQ + a % kSubQ;
                 const int pos = __hip_atomic_fetch_add(P.tail + qf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int hp = hlp ? __hip_atomic_fetch_add(P.hq_tail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
                 __hip_atomic_store(P.queue + qf * nmb + pos, a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                if (P.helpers && !ld_relaxed(&P.fr[fo].F.is_intra)) {
-                    const int hp = __hip_atomic_fetch_add(P.hq_tail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(P.hq + hp, fo * nmb + a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                }
+                if (hlp) __hip_atomic_store(P.hq + hp, fo * nmb + a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             }
         };
 #if HL_EARLY_RELEASE
@@ -625,18 +640,35 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         // models both events); the next picture still waits for `done`, set
         // after the filters.
         if (tid < 64) {
+#if defined(HL_PROFILE)
+            const unsigned long long pe0 = __builtin_readcyclecounter();
+#endif
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, HL_REL_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if defined(HL_PROFILE)
+            const unsigned long long pe1 = __builtin_readcyclecounter();
+#endif
             release(0);
 #if defined(HL_PROFILE)
             if (f == 0 && tid == 0 && prof) prof[64 + nmb + 3 * addr + 2] = wall_clock64();
+            const unsigned long long pe2 = __builtin_readcyclecounter();
 #endif
             if (tid == 0) {
                 if (x > 0) spin_ge(P.done + t - 1, 1, P.err);
                 if (y > 0) spin_ge(P.done + f * nmb + (y - 1) * mbw + min(x + 1, mbw - 1), 1, P.err);
             }
+#if defined(HL_PROFILE)
+            const unsigned long long pe3 = __builtin_readcyclecounter();
+#endif
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if defined(HL_PROFILE)
+            const unsigned long long pe4 = __builtin_readcyclecounter();
+            ptail[4] += pe1 - pe0;
+            ptail[5] += pe2 - pe1;
+            ptail[6] += pe3 - pe2;
+            ptail[7] += pe4 - pe3;
+#endif
         }
         __syncthreads();
 #endif
@@ -699,7 +731,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         atomicAdd(prof + 45, pw_hlp);  // intra helper tasks: cycles, count
         atomicAdd(prof + 46, pw_hn);
         for (int i = 0; i < 3; ++i) atomicAdd(prof + 47 + i, pst[i]);  // pops: attempts, lost, empty rounds
-        for (int i = 0; i < 4; ++i) atomicAdd(prof + 50 + i, ptail[i]);  // filters' barrier, release fence, successors, early release
+        for (int i = 0; i < 8; ++i) atomicAdd(prof + 50 + i, ptail[i]);  // filters' barrier, release fence, successors, early release (fence, release, spin, acquire)
     }
 #endif
 }

@@ -62,7 +62,9 @@ def main():
         if hn:
             print(f"   intra helper tasks {hn} ({hn / max(1, n * nmb):.2f} per MB), {hlp / hn / 1e3:.1f} kcycles each")
         print(f"   after the filters: barrier {cnt[50] / max(1, tasks) / 1e3:.1f}, release fence {cnt[51] / max(1, tasks) / 1e3:.1f}, "
-              f"successors {cnt[52] / max(1, tasks) / 1e3:.1f} kcycles/task; early release block (in the filters) {cnt[53] / max(1, tasks) / 1e3:.1f}")
+              f"successors {cnt[52] / max(1, tasks) / 1e3:.1f} kcycles/task; early release block (in the filters) {cnt[53] / max(1, tasks) / 1e3:.1f} "
+              f"(fence {cnt[54] / max(1, tasks) / 1e3:.1f}, release {cnt[55] / max(1, tasks) / 1e3:.1f}, spin {cnt[56] / max(1, tasks) / 1e3:.1f}, "
+              f"acquire {cnt[57] / max(1, tasks) / 1e3:.1f})")
         for name, v in (("task-start waits", wait), ("decisions", mb), ("deblock + planes", filt), ("intra helpers", hlp),
                         ("rest", life - wait - mb - filt - hlp)):
             print(f"   {name:18s} {100.0 * v / life:6.1f} %   {v / max(1, tasks) / 1e3:9.1f} kcycles/task")
