@@ -26,7 +26,7 @@ hartallo_amd/libhartallo_amd.so: $(CSRC)/hl_encoder.hip $(HOSTSRC) $(HDRS)
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) $(DEVFLAGS) -shared -o $@ $(CSRC)/hl_encoder.hip $(HOSTSRC)
 
 tests/emu/libhl_emu.so: tests/emu/hl_emu.hip $(HOSTSRC) $(HDRS)
-	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -O2 -shared -o $@ tests/emu/hl_emu.hip $(HOSTSRC)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -O2 -DHL_FAM3=1 -shared -o $@ tests/emu/hl_emu.hip $(HOSTSRC)
 
 tests/gpu_unit/libhl_unit.so: tests/gpu_unit/hl_unit.hip $(HDRS)
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -shared -o $@ tests/gpu_unit/hl_unit.hip

@@ -49,6 +49,7 @@ EXPORTED_SYMBOLS = (
     "hl_amd_last_batch_stats",
     "hl_amd_set_intra_helpers",
     "hl_amd_last_helper_stats",
+    "hl_amd_last_fam3_stats",
     "hl_amd_profile_counters",
     "hl_amd_debug_records",
     "hl_amd_record_size",
@@ -166,7 +167,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_last_mb_launches.restype = i32
     lib.hl_amd_last_batch_stats.argtypes = [vp, ctypes.POINTER(i32)]
     lib.hl_amd_last_batch_stats.restype = i32
-    for name, args in (("hl_amd_set_intra_helpers", [vp, i32]), ("hl_amd_last_helper_stats", [vp, ctypes.POINTER(i32)])):
+    for name, args in (("hl_amd_set_intra_helpers", [vp, i32]), ("hl_amd_last_helper_stats", [vp, ctypes.POINTER(i32)]),
+                       ("hl_amd_last_fam3_stats", [vp, ctypes.POINTER(i32)])):
         if hasattr(lib, name):  # (absent from builds before round 4 loaded through HL_LIB)
             getattr(lib, name).argtypes = args
             getattr(lib, name).restype = i32
@@ -448,7 +450,12 @@ class Encoder:
         rc = self.lib.hl_amd_last_helper_stats(self._h, a)
         if rc != HL_AMD_SUCCESS:
             raise HlAmdError(rc, "hl_amd_last_helper_stats")
-        return dict(zip(("i4_kept", "i4_rejected", "taken_over"), list(a)))
+        r = dict(zip(("i4_kept", "i4_rejected", "taken_over"), list(a)))
+        if hasattr(self.lib, "hl_amd_last_fam3_stats"):
+            b = (ctypes.c_int32 * 2)()
+            if self.lib.hl_amd_last_fam3_stats(self._h, b) == HL_AMD_SUCCESS:
+                r["fam3_kept"], r["fam3_rejected"] = b[0], b[1]
+        return r
 
 
 class SvcEncoder(Encoder):

@@ -279,7 +279,9 @@ __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
         for (int q = 0; q < kSubQ; ++q) P.queue[(f * kSubQ + q) * nmb + a] = k == 0 && a == 0 && q == 0 ? 1 : 0;  // every stream's first task
         P.claim[i] = 0;
         P.hstate[i] = HS_FREE;
+        P.hstate3[i] = HS_FREE;
         P.hq[i] = 0;
+        P.hq[P.nframes * nmb + i] = 0;
     }
     if (i < P.nframes * kSubQ) {
         P.head[i] = 0;
@@ -291,7 +293,7 @@ __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
         *P.hq_tail = 0;
     }
     if (i == 0) {
-        for (int k = 0; k < 5; ++k) P.err[k] = 0;  // give-ups, chain walks, helper I4 kept / rejected / taken over
+        for (int k = 0; k < 8; ++k) P.err[k] = 0;  // give-ups, chain walks, helper I4 kept / rejected / taken over, -, 8x8 family kept / rejected
     }
 }
 
@@ -424,6 +426,7 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh
             const int hh = ld_relaxed(P.hq_head), ht = ld_relaxed(P.hq_tail);
             if (hh < ht) {
                 int r = 0;
+                int kind = 0;
                 if (lane == 0 && atomicCAS(P.hq_head, hh, hh + 1) == hh) {
                     for (unsigned k = 0; (r = ld_relaxed(P.hq + hh)) == 0; ++k)
                         if (k > (1u << 26)) {
@@ -431,11 +434,16 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh
                             r = -1;
                             break;
                         }
-                    if (r > 0 && atomicCAS(P.hstate + r - 1, HS_FREE, HS_CLAIMED) != HS_FREE) r = 0;
+                    if (r > 0) {
+                        kind = r >> 30;
+                        r &= (1 << 30) - 1;
+                        if (atomicCAS((kind ? P.hstate3 : P.hstate) + r - 1, HS_FREE, HS_CLAIMED) != HS_FREE) r = 0;
+                    }
                 }
                 r = __builtin_amdgcn_readfirstlane(r);
+                kind = __builtin_amdgcn_readfirstlane(kind);
                 if (r < 0) return -1;
-                if (r > 0) return P.nframes * nmb + r - 1;
+                if (r > 0) return (1 + kind) * P.nframes * nmb + r - 1;  // intra helpers, then 8x8-family helpers
                 continue;
             }
         }
@@ -531,8 +539,10 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #if defined(HL_PROFILE)
         const unsigned long long pw_start = wall_clock64();  // (the task's timeline, below)
 #endif
-        const bool helper = t >= P.nframes * nmb;  // an intra helper task (hl_mbcore.h intra_helper)
-        if (helper) t -= P.nframes * nmb;
+        // helper tasks (hl_mbcore.h): 1 = intra_helper, 2 = fam3_helper
+        const int hk = t >= 2 * P.nframes * nmb ? 2 : (t >= P.nframes * nmb ? 1 : 0);
+        const bool helper = hk > 0;
+        t -= hk * P.nframes * nmb;
 #if defined(HL_DIAG) && HL_DIAG == 1
         __syncthreads();
 #endif
@@ -567,15 +577,18 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         if (threadIdx.x < 64) __builtin_amdgcn_s_sleep(20);
 #endif
         frame_args_to_lds(sF, PF.F, tid);
+        // (one call site of encode_mb: the macroblock and its 8x8-family helper
+        // share the inlined search)
+        if (hk == 1) intra_helper(sF, S, addr, tid, kMbThreads, s_in, PF.F.ispec + addr);
+        else encode_mb(sF, S, addr, tid, kMbThreads, s_in, gx, gy, spec_in, hk == 2 ? PF.F.f3 + addr : nullptr);
         if (helper) {
             // results, every wave's stores drained, barrier, one release, the state
-            intra_helper(sF, S, addr, tid, kMbThreads, s_in, PF.F.ispec + addr);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (tid < 64) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, HL_REL_SCOPE);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (tid == 0) st_relaxed(P.hstate + t, HS_DONE);
+                if (tid == 0) st_relaxed((hk == 1 ? P.hstate : P.hstate3) + t, HS_DONE);
             }
 #if defined(HL_PROFILE)
             pw_hlp += __builtin_readcyclecounter() - pt1;
@@ -583,7 +596,6 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #endif
             continue;
         }
-        encode_mb(sF, S, addr, tid, kMbThreads, s_in, gx, gy, spec_in);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
 #if defined(HL_PROFILE)
@@ -626,9 +638,12 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #endif
                 const int qf = fo * kSubQ + a % kSubQ;
                 const int pos = __hip_atomic_fetch_add(P.tail + qf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const int hp = hlp ? __hip_atomic_fetch_add(P.hq_tail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+                const int hp = hlp ? __hip_atomic_fetch_add(P.hq_tail, 1 + P.fam3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
                 __hip_atomic_store(P.queue + qf * nmb + pos, a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                if (hlp) __hip_atomic_store(P.hq + hp, fo * nmb + a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                if (hlp) {  // the 8x8-family helper first (the longer one), then the intra helper
+                    if (P.fam3) __hip_atomic_store(P.hq + hp, (1 << 30) | (fo * nmb + a + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(P.hq + hp + P.fam3, fo * nmb + a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
         };
 #if HL_EARLY_RELEASE
@@ -787,6 +802,9 @@ struct hl_amd_encoder_s {
     IntraSpec* d_ispec = nullptr;                // intra helper results, per MB address
     bool helpers = true;                         // P macroblocks of pipelined runs get intra helper tasks
     int32_t helper_kept = 0, helper_rejected = 0, helper_self = 0;  // hl_amd_last_helper_stats
+    bool fam3 = true;                            // ... and 8x8-family helper tasks (HL_AMD_FAM3=0: off)
+    int32_t fam3_kept = 0, fam3_rejected = 0;    // hl_amd_last_fam3_stats
+    Fam3Out* d_f3 = nullptr;                     // 8x8-family helper results [slot][MB]
     PipeFrame *d_pf, *h_pf;
     std::vector<std::vector<uint8_t>> bout;  // bitstreams of the last hl_amd_encode_batch
     int nwriters;                            // host slice writer threads of a run
@@ -843,6 +861,7 @@ static void free_all(hl_amd_encoder_t* e)
     (void)hipFree(e->d_queue);
     (void)hipFree(e->d_head);
     (void)hipFree(e->d_hstate);
+    (void)hipFree(e->d_f3);
     (void)hipFree(e->d_ispec);
     (void)hipFree(e->d_pf);
     (void)hipHostFree(e->h_brec);
@@ -926,6 +945,8 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
     {
         const char* h = getenv("HL_AMD_HELPERS");  // A/B knob (hl_amd_set_intra_helpers)
         e->helpers = !(h && atoi(h) == 0);
+        const char* h3 = getenv("HL_AMD_FAM3");  // A/B knob
+        e->fam3 = !(h3 && atoi(h3) == 0);
     }
     e->reach = 2;
     e->window = 64;
@@ -1206,15 +1227,18 @@ static hipError_t ensure_sched(hl_amd_encoder_t* e, int slots)
     dfree(e->d_queue);
     dfree(e->d_head);
     dfree(e->d_hstate);
+    dfree(e->d_f3);
     (void)hipHostFree(e->h_pf);
     e->h_pf = nullptr;
     e->scap = 0;
     hipError_t r;
+    // (helper states: intra [slot][MB], then 8x8 family; the helper FIFO sits
+    // after the ready queues, two entries per MB)
     if ((r = hipMalloc(&e->d_pf, sizeof(PipeFrame) * slots)) || (r = hipHostMalloc(&e->h_pf, sizeof(PipeFrame) * slots, hipHostMallocDefault)) ||
         (r = hipMalloc(&e->d_cnt, sizeof(int32_t) * 2 * nmb * slots)) || (r = hipMalloc(&e->d_done, sizeof(int32_t) * nmb * slots)) ||
-        (r = hipMalloc(&e->d_queue, sizeof(int32_t) * (kSubQ + 1) * nmb * slots)) ||
+        (r = hipMalloc(&e->d_queue, sizeof(int32_t) * (kSubQ + 2) * nmb * slots)) ||
         (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * kSubQ * slots + kMaxStreams + 2))) ||
-        (r = hipMalloc(&e->d_hstate, sizeof(int32_t) * nmb * slots)))
+        (r = hipMalloc(&e->d_hstate, sizeof(int32_t) * 2 * nmb * slots)) || (r = hipMalloc(&e->d_f3, sizeof(Fam3Out) * nmb * slots)))
         return r;
     if (!e->d_err && (r = hipMalloc(&e->d_err, sizeof(int32_t) * 8))) return r;
     e->scap = slots;
@@ -1406,6 +1430,10 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
             if (e0->helpers && !e->run_intra[k]) {
                 F.ispec = e->d_ispec;
                 F.hstate = e0->d_hstate + nmb * slot;
+                if (HL_FAM3 && e0->fam3) {
+                    F.f3 = e0->d_f3 + (size_t)nmb * slot;
+                    F.hstate3 = e0->d_hstate + (size_t)nmb * (slots + slot);
+                }
             }
             pf.D.W = e->W;
             pf.D.H = e->H;
@@ -1444,7 +1472,9 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
     P.done = e0->d_done;
     P.queue = e0->d_queue;
     P.hstate = e0->d_hstate;
+    P.hstate3 = e0->d_hstate + (size_t)nmb * slots;
     P.helpers = e0->helpers ? 1 : 0;
+    P.fam3 = HL_FAM3 && e0->helpers && e0->fam3 ? 1 : 0;
     P.hq = e0->d_queue + kSubQ * nmb * slots;
     P.head = e0->d_head;
     P.tail = e0->d_head + kSubQ * slots;
@@ -1485,7 +1515,7 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
     int32_t* errw = e0->h_progress + 4;  // bounded waits that gave up, resolve_chain walks, helper counts
     for (int si = 0; si < S; ++si)
         HL_HIP_CHECK(hipMemcpyAsync(es[si]->h_bchain, es[si]->d_bchain, sizeof(MbChain) * nmb * m, hipMemcpyDeviceToHost, e0->stream));
-    HL_HIP_CHECK(hipMemcpyAsync(errw, e0->d_err, 5 * sizeof(int32_t), hipMemcpyDeviceToHost, e0->stream));
+    HL_HIP_CHECK(hipMemcpyAsync(errw, e0->d_err, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, e0->stream));
     if (e0->timing) HL_HIP_CHECK(hipEventRecord(e0->ev[2], e0->stream));
     std::vector<std::atomic<bool>> abort(S);
     std::vector<std::vector<size_t>> wsize(S);
@@ -1533,6 +1563,8 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
         e->helper_kept += errw[2];
         e->helper_rejected += errw[3];
         e->helper_self += errw[4];
+        e->fam3_kept += errw[5];
+        e->fam3_rejected += errw[6];
         if (si) {
             e->ms[1] = e0->ms[1];
             e->ms[3] = e0->ms[3];
@@ -1634,6 +1666,7 @@ static void begin_call(hl_amd_encoder_t* e, int n)
     e->last_pic.assign(n, nullptr);
     e->calls_runs = e->calls_per_picture = e->calls_fallbacks = e->calls_gave_up = e->calls_walks = 0;
     e->helper_kept = e->helper_rejected = e->helper_self = 0;
+    e->fam3_kept = e->fam3_rejected = 0;
 }
 
 // n consecutive pictures of the stream, every one through a pipelined run:
@@ -1695,6 +1728,14 @@ extern "C" int32_t hl_amd_last_batch_stats(hl_amd_encoder_t* e, int32_t* out5)
     out5[2] = e->calls_fallbacks;
     out5[3] = e->calls_gave_up;
     out5[4] = e->calls_walks;
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_last_fam3_stats(hl_amd_encoder_t* e, int32_t* out2)
+{
+    if (!e || !out2) return HL_AMD_ERROR_INVALID_PARAMETER;
+    out2[0] = e->fam3_kept;
+    out2[1] = e->fam3_rejected;
     return HL_AMD_SUCCESS;
 }
 

@@ -156,6 +156,29 @@ static_assert(sizeof(IntraSpec) % 16 == 0, "IntraSpec in whole 16-byte words");
 // helper task state (FrameArgs::hstate[addr])
 enum : int32_t { HS_FREE = 0, HS_CLAIMED = 1, HS_MAIN = 2, HS_DONE = 3 };
 
+// An 8x8-family helper task's results (fam3_helper, FrameArgs::f3[addr]): the
+// P8x8 partitionings (kParts[3..6], rdo.c:745-760) searched from the MB-start
+// live TotalCoeffs while the macroblock searches 16x16 / 16x8 / 8x16, with the
+// intervals of the entry values under which every nC class it used holds
+// (f3_verify), and the state the family leaves behind.
+struct Fam3Out {
+    double cost[4];               // partitioning j = 3..6: sum of the partitions' best costs (header bits not added)
+    int32_t single[4], dist[4];
+    int32_t done_mask;            // bit j - 3: partitioning j searched (mode_flags)
+    int32_t wmask;                // blocks whose live TotalCoeff the family wrote
+    int32_t chain, fresh;         // rdo.Single_ctr after the family; fresh = the family wrote it
+    int32_t e_last;               // the last partitioning searched
+    int32_t pad0[3];
+    int8_t tc[16];                // live TotalCoeffs after the family (blocks in wmask)
+    int8_t lo[32], hi[32];        // [b]: entry value of block b; [16 + b]: sum of block b's inside neighbours' entry values
+    int16_t bmv[4][4][4][2], bmvp[4][4][4][2];  // per partitioning: best MVs and MVPs
+    int16_t nbmv[4][4][2];        // MvL0 of the partitions (Shared::nb[0].mv) after the family
+    int32_t mvg[6][6];            // motion grid after the family
+    int8_t mvs[6][6];
+    int8_t pad1[12];
+};
+static_assert(sizeof(Fam3Out) % 16 == 0, "Fam3Out in whole 16-byte words");
+
 struct FrameArgs {
     int32_t W, H, Wc, Hc, mbw, mbh;
     int32_t qp, qpc, is_intra, me_range;
@@ -188,6 +211,9 @@ struct FrameArgs {
     // per-address results and this picture's task states (HS_*)
     IntraSpec* ispec;
     int32_t* hstate;
+    // 8x8-family helper tasks (the same pictures): this picture's results and states
+    Fam3Out* f3;
+    int32_t* hstate3;
 };
 
 struct NbInfo {
@@ -280,6 +306,13 @@ struct Shared {
     int32_t dcY[32];             // I16x16: scaled DC per DC-matrix position (two modes)
     int32_t chain_x;             // resolve_chain result
     int32_t hs_x;                // intra helper state seen by the MB (HS_*)
+    int32_t hs3_x;               // 8x8-family helper state seen by the MB
+    int32_t f3lo[32], f3hi[32];  // fam3_helper: entry-value intervals being recorded (see Fam3Out)
+    int32_t f3w;                 // fam3_helper: blocks whose live TotalCoeff the family wrote so far
+    int8_t f3entry[16];          // the MB's live TotalCoeffs entering the family
+    int16_t f3best_mv[4][4][2], f3best_mvp[4][4][2];  // best_mv / best_mvp entering the family
+    double f3b_cost;             // the best so far entering the family, and rdo.Single_ctr (LDS: nothing
+    int32_t f3b[8];              // extra stays live in registers across the family's searches)
     int32_t homo[4];             // early termination: homogeneity of the four 8x8 source quadrants
     int32_t predc[2][64];
     int32_t cres_dc[2][4], cres_cac[2][4], cres_cdc[2][4], cres_tc[2][4], cres_sctr[2][4];
@@ -301,6 +334,18 @@ struct Shared {
 #endif
 };
 
+// 8x8-family helper tasks (guess_inter): 1 = built in.  Off
+// in the product: the recording in the search's hot loop and the import
+// path cost the macroblock decision more registers (VGPR spills 19 -> 34)
+// than the helpers win in the ramp and tail (profiles/r04_ab_fam3_helpers.log);
+// the CPU emulator builds it (tests/emu) and `make variant` can.
+#ifndef HL_FAM3
+#define HL_FAM3 0
+#endif
+#ifndef HL_F3REC_ON
+#define HL_F3REC_ON 1
+#endif
+#define HL_F3REC(c) (HL_FAM3 && HL_F3REC_ON && (c).f3rec)
 // A fresh, opaque copy of the lane index at the entry of each phase: the
 // compiler cannot compute the phase's lane-dependent addresses earlier and
 // hold them (spilled) across the partition searches.
@@ -335,6 +380,7 @@ struct Ctx {
     int wux = 0, wuy = 0;   // usable columns / rows of the LDS search window (0: none)
     int spec = 0;           // 1 = chain is still a row-start speculation (uniform)
     int par = 0;            // buffer parity of the last candidate step (Shared::cd, be_tcb)
+    int f3rec = 0;          // 1 = fam3_helper: record entry-value intervals and written blocks (Shared::f3*)
 #if defined(HL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
     unsigned long long pacc[kProfSlots] = {};
     unsigned pcnt[kProfSlots] = {};
@@ -575,16 +621,30 @@ HD int nc_luma_of(const Shared& S, int bi, F inside)
 // The entry-value bookkeeping of a speculated 8x8-family search (fam3 helper
 // tasks): v of block b, read from the live TotalCoeffs the search started
 // from, keeps every nC class it took part in while v stays in [lo[b], hi[b]].
-HD void iv_tighten(int8_t* lo, int8_t* hi, int b, int l, int h)
+template <typename T>
+HD void iv_tighten(T* lo, T* hi, int b, int l, int h)
 {
-    if (lo[b] < l) lo[b] = (int8_t)l;
-    if (hi[b] > h) hi[b] = (int8_t)(h > 127 ? 127 : h);
+    if (lo[b] < l) lo[b] = (T)l;
+    if (hi[b] > h) hi[b] = (T)(h > 127 ? 127 : h);
+}
+// the interval of an entry value v (or of a sum of two) that keeps the nC
+// class of a read: both neighbours available -> nC = (nA + nB + 1) >> 1, else
+// the one available value.  sum: nA + nB (both), else v.
+HD void iv_of_sum(int sm, int& l, int& h)  // classes of (sm + 1) >> 1: sm <= 2, 3..6, 7..14, >= 15
+{
+    l = sm <= 2 ? 0 : (sm <= 6 ? 3 : (sm <= 14 ? 7 : 15));
+    h = sm <= 2 ? 2 : (sm <= 6 ? 6 : (sm <= 14 ? 14 : 127));
+}
+HD void iv_of_one(int v, int& l, int& h)  // classes of v: 0-1, 2-3, 4-7, >= 8
+{
+    l = v < 2 ? 0 : (v < 4 ? 2 : (v < 8 ? 4 : 8));
+    h = v < 2 ? 1 : (v < 4 ? 3 : (v < 8 ? 7 : 127));
 }
 // nC (as nc_luma_of) where inside(ni, entry) also tells whether the value is
 // an entry value; each such read tightens [lo, hi] of its block; a read of
 // both neighbours of block bi at once, [lo[16 + bi], hi[16 + bi]] of their sum
-template <typename F>
-HD int nc_luma_iv(const Shared& S, int bi, F inside, int8_t* lo, int8_t* hi)
+template <typename F, typename T>
+HD int nc_luma_iv(const Shared& S, int bi, F inside, T* lo, T* hi)
 {
     const int bx = blk_x(bi), by = blk_y(bi);
     int nA = 0, nB = 0, ia = -1, ib = -1;
@@ -616,16 +676,16 @@ HD int nc_luma_iv(const Shared& S, int bi, F inside, int8_t* lo, int8_t* hi)
         }
     }
     if (ia >= 0 || ib >= 0) {
+        int l, h;
         if (aA && aB) {
-            const int sm = nA + nB;  // classes of (sm + 1) >> 1: sm <= 2, 3..6, 7..14, >= 15
-            const int slo = sm <= 2 ? 0 : (sm <= 6 ? 3 : (sm <= 14 ? 7 : 15)), shi = sm <= 2 ? 2 : (sm <= 6 ? 6 : (sm <= 14 ? 14 : 127));
-            if (ia >= 0 && ib >= 0) iv_tighten(lo + 16, hi + 16, bi, slo, shi);  // both entry values: their sum
-            else if (ia >= 0) iv_tighten(lo, hi, ia, slo - nB, shi - nB);
-            else iv_tighten(lo, hi, ib, slo - nA, shi - nA);
+            iv_of_sum(nA + nB, l, h);
+            if (ia >= 0 && ib >= 0) iv_tighten(lo + 16, hi + 16, bi, l, h);  // both entry values: their sum
+            else if (ia >= 0) iv_tighten(lo, hi, ia, l - nB, h - nB);
+            else iv_tighten(lo, hi, ib, l - nA, h - nA);
         }
         else {
-            const int v = ia >= 0 ? nA : nB, b = ia >= 0 ? ia : ib;
-            iv_tighten(lo, hi, b, v < 2 ? 0 : (v < 4 ? 2 : (v < 8 ? 4 : 8)), v < 2 ? 1 : (v < 4 ? 3 : (v < 8 ? 7 : 127)));
+            iv_of_one(ia >= 0 ? nA : nB, l, h);
+            iv_tighten(lo, hi, ia >= 0 ? ia : ib, l, h);
         }
     }
     if (aA && aB) return (nA + nB + 1) >> 1;
@@ -1109,19 +1169,6 @@ HD double mv_cost(const FrameArgs& F, int dist, int bits, int mvx, int mvy, cons
 #if defined(HL_STATS) && !defined(__HIP_DEVICE_COMPILE__)
 extern long long g_hl_stats[8];
 #endif
-#if defined(HL_EMU_BUILD) && !defined(__HIP_DEVICE_COMPILE__)
-// emu-only probe of the 8x8 family's dependence on the live TotalCoeffs it
-// starts from (tests/emu: emu_fam3_stats)
-extern long g_emu_f3[8];
-extern int g_emu_f3_on, g_emu_f3_wr, g_emu_f3_rd;
-extern int g_f3p_on, g_f3p_w, g_f3p_enable;
-extern int8_t g_f3p_lo[32], g_f3p_hi[32];
-#define HL_EMU_F3_READ(ni) (void)(g_emu_f3_on && !((g_emu_f3_wr >> (ni)) & 1) ? (g_emu_f3_rd |= 1 << (ni)) : 0)
-#define HL_EMU_F3_WRITE(bi) (void)(g_emu_f3_on ? (g_emu_f3_wr |= 1 << (bi)) : 0, g_f3p_on ? (g_f3p_w |= 1 << (bi)) : 0)
-#else
-#define HL_EMU_F3_READ(ni) ((void)0)
-#define HL_EMU_F3_WRITE(bi) ((void)0)
-#endif
 
 #if defined(__HIP_DEVICE_COMPILE__)
 // bit i set iff byte i of w is non-zero
@@ -1179,6 +1226,11 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         // single-block partitions: both nC neighbours lie outside the partition,
         // so nC is fixed for its whole search (read here, beside the loads)
         const int nc1 = g.nblk == 1 ? nc_luma_of(S, blk_idx(g.px, g.py), [&](int ni) -> int { return S.tc[ni]; }) : 0;
+        if (HL_F3REC(c) && g.nblk == 1 && c.tid == 0)  // fam3_helper: its entry reads (lane 0; phase 2 does not run)
+            nc_luma_iv(S, blk_idx(g.px, g.py), [&](int ni, bool& e) -> int {
+                e = !((S.f3w >> ni) & 1);
+                return S.tc[ni];
+            }, S.f3lo, S.f3hi);
         int o1[kQPass], o2[kQPass];
         uint32_t sv[kQPass], pr[kQPass];
 #if HL_LDS_WINDOW
@@ -1289,6 +1341,11 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         // single-block partitions: both nC neighbours lie outside the partition,
         // so nC is fixed for its whole search (read here, beside the loads)
         const int nc1 = g.nblk == 1 ? nc_luma_of(S, blk_idx(g.px, g.py), [&](int ni) -> int { return S.tc[ni]; }) : 0;
+        if (HL_F3REC(c) && g.nblk == 1 && c.tid == 0)  // fam3_helper: its entry reads (lane 0; phase 2 does not run)
+            nc_luma_iv(S, blk_idx(g.px, g.py), [&](int ni, bool& e) -> int {
+                e = !((S.f3w >> ni) & 1);
+                return S.tc[ni];
+            }, S.f3lo, S.f3hi);
         // slots and source samples first (one LDS round trip), then all loads
         int o1[kMaxPass], o2[kMaxPass];
         HL_PROF_T(ta0);
@@ -1403,6 +1460,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         const int kkA = inA ? ((hy << g.lbw) + hx - 1) : 0, kkB = inB ? (((hy - 1) << g.lbw) + hx) : 0;
         const int w0 = S.be_w0[ci][k], w1 = S.be_w1[ci][k], w2 = S.be_w2[ci][k];
         const int eA = S.extA[bi], eB = S.extB[bi], cbp = S.cbp_l, tA = S.tc[niA], tB = S.tc[niB];
+        const int f3w = HL_F3REC(c) ? S.f3w : 0;
         const uint8_t *rA = tcb[kkA], *rB = tcb[kkB];
         const CandSlot cs = S.wc[wave][ci];
         int bits = 0, dist = 0, cs_sum = 0, last = 0;
@@ -1412,7 +1470,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
             if (tc) {
                 const uint32_t allow = ci == 31 ? ~0u : (2u << ci) - 1u;  // candidates 0..ci
                 int nA = 0, nB = 0;
-                bool aA = true, aB = true;
+                bool aA = true, aB = true, enA = false, enB = false;  // en: an entry value of the family (fam3_helper)
                 if (bx == 0) {
                     aA = eA >= 0;
                     nA = aA ? eA : 0;
@@ -1420,6 +1478,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                 else if (cbp & (1 << (niA >> 2))) {
                     const int v = inA ? tcb_last(rA, allow) : -1;
                     nA = v >= 0 ? v : tA;
+                    enA = HL_F3REC(c) && v < 0 && !((f3w >> niA) & 1);
                 }
                 if (by == 0) {
                     aB = eB >= 0;
@@ -1428,8 +1487,32 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                 else if (cbp & (1 << (niB >> 2))) {
                     const int v = inB ? tcb_last(rB, allow) : -1;
                     nB = v >= 0 ? v : tB;
+                    enB = HL_F3REC(c) && v < 0 && !((f3w >> niB) & 1);
                 }
                 const int nC = (aA && aB) ? (nA + nB + 1) >> 1 : (aA ? nA : (aB ? nB : 0));
+                if (enA || enB) {  // the interval of the entry value(s) keeping this nC's class
+                    int l, h, ix;
+                    if (aA && aB) {
+                        iv_of_sum(nA + nB, l, h);
+                        if (enA && enB) ix = 16 + bi;
+                        else if (enA) {
+                            ix = niA;
+                            l -= nB;
+                            h -= nB;
+                        }
+                        else {
+                            ix = niB;
+                            l -= nA;
+                            h -= nA;
+                        }
+                    }
+                    else {
+                        iv_of_one(enA ? nA : nB, l, h);
+                        ix = enA ? niA : niB;
+                    }
+                    atomicMax(&S.f3lo[ix], l);
+                    atomicMin(&S.f3hi[ix], min(h, 127));
+                }
                 const int cls = nC < 2 ? 0 : (nC < 4 ? 1 : (nC < 8 ? 2 : 3));
                 const int sctr = ((w0 >> 8) & 15) - 1;
                 bits = (w1 & 0xFFFF) + ((w2 >> (5 * cls)) & 31);
@@ -1513,21 +1596,10 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                 for (int cj = ci - 1; cj >= 0; --cj)
                     if (S.be_nz[cj][kk]) return S.be_tc[cj][kk];
             }
-            HL_EMU_F3_READ(ni);
-#if defined(HL_EMU_BUILD)
-            entry = g_f3p_on && !((g_f3p_w >> ni) & 1);
-#endif
+            entry = c.f3rec && !((S.f3w >> ni) & 1);
             return S.tc[ni];
         };
-#if defined(HL_EMU_BUILD)
-        int8_t dlo[32], dhi[32];
-        const int nC = nc_luma_iv(S, bi, inside, g_f3p_on ? g_f3p_lo : dlo, g_f3p_on ? g_f3p_hi : dhi);
-#else
-        const int nC = nc_luma_of(S, bi, [&](int ni) -> int {
-            bool e;
-            return inside(ni, e);
-        });
-#endif
+        const int nC = nc_luma_iv(S, bi, inside, S.f3lo, S.f3hi);
         S.be_bits[ci][k] += token_len(nC, S.be_tc[ci][k], S.be_t1[ci][k]);
     }
     // phase 3: per-candidate sums
@@ -1570,7 +1642,11 @@ HD void commit_candidates(Ctx& c, const PartGeo& g, int n, int last_l = -2)
     if (c.tid < g.nblk) {
         const int k = c.tid;
         const int v = tcb_last(tcb[k], n >= 32 ? ~0u : (1u << n) - 1u);
-        if (v >= 0) S.tc[blk_idx(g.px + ((k & (g.nbw - 1)) << 2), g.py + ((k >> g.lbw) << 2))] = (int8_t)v;
+        const int bi = blk_idx(g.px + ((k & (g.nbw - 1)) << 2), g.py + ((k >> g.lbw) << 2));
+        if (v >= 0) {
+            S.tc[bi] = (int8_t)v;
+            if (HL_F3REC(c)) atomicOr(&S.f3w, 1 << bi);
+        }
     }
     {  // last candidate that wrote the counter (vectorised over the pass)
         const int l = c.tid & 31;
@@ -1586,7 +1662,7 @@ HD void commit_candidates(Ctx& c, const PartGeo& g, int n, int last_l = -2)
         for (int cj = n - 1; cj >= 0; --cj)
             if (S.be_nz[cj][k]) {
                 S.tc[bi] = (int8_t)S.be_tc[cj][k];
-                HL_EMU_F3_WRITE(bi);
+                if (c.f3rec) S.f3w |= 1 << bi;
                 break;
             }
     }
@@ -3669,12 +3745,86 @@ HD const IntraSpec* helper_join(Ctx& c, bool use)
 // --------------------------------------------------------------------------
 // P macroblock decision, rdo.c:678-1271
 // --------------------------------------------------------------------------
-HD void guess_inter(Ctx& c)
+HD int32_t fam_etype(int f) { return f < 3 ? ET_P16x16 + f : ET_P8x8REF0; }
+
+// One partitioning j of family fam searched (rdo.c:731-760): the partition
+// mode's best cost (header bits not added), its Single_ctr sum and
+// distortion; returns the P_Skip probe's outcome (16x16 only).  abort() is
+// asked before every partition search; when it says so the search stops
+// (aborted = true) and the results are meaningless.
+template <typename A>
+HD bool search_family_part(Ctx& c, int j, int fam, double& cost_sum, int& single_sum, int& dist_sum, A abort, bool& aborted)
+{
+    Shared& S = c.S;
+    const PartDef& pd = kParts[j];
+    aborted = false;
+    HL_SYNC();
+    if (c.tid == 0) {
+        S.e_type = fam_etype(fam);
+        S.nb[0].e_type = fam_etype(fam);
+        S.nb[0].part_w = pd.part_w;
+        S.nb[0].part_h = pd.part_h;
+        for (int i = 0; i < 4; ++i) {
+            S.nb[0].sub_w[i] = pd.sub_w;
+            S.nb[0].sub_h[i] = pd.sub_h;
+        }
+        grid_reset_inside(S);
+    }
+    HL_SYNC();
+    bool prob = false;
+    for (int pi = 0; pi < pd.num_part; ++pi)
+        for (int spi = 0; spi < pd.num_sub; ++spi) {
+            if (abort()) {
+                aborted = true;
+                return false;
+            }
+            const bool p = search_partition(c, pd, pi, spi, j == 0 && pi == 0 && spi == 0);
+            if (j == 0 && pi == 0 && spi == 0) prob = p;
+        }
+    for (int pi = 0; pi < pd.num_part; ++pi)
+        for (int spi = 0; spi < pd.num_sub; ++spi) {
+            cost_sum = dadd(cost_sum, uni(S.bcost[pi][spi]));
+            single_sum += uni(S.bsingle[pi][spi]);
+            dist_sum += uni(S.bdist[pi][spi]);
+        }
+    return prob;
+}
+
+// --------------------------------------------------------------------------
+// 8x8-family helper tasks (pipelined runs): while a P macroblock searches
+// 16x16 / 16x8 / 8x16, an idle workgroup searches the P8x8 partitionings
+// (kParts[3..6]) from the MB-start live TotalCoeffs.  The family reads the
+// live TotalCoeffs it starts from only through nC classes, and only until the
+// family itself overwrites a block; fam3_helper records, for every such read,
+// the interval of the entry value (or of the sum of two) that keeps the class
+// (Shared::f3lo / f3hi).  The family never reads rdo.Single_ctr.  So if the
+// macroblock's real entry values lie in every interval, the family's every
+// cost, decision and write is the same, and the macroblock takes them
+// (f3_import); otherwise it searches the family itself.
+// --------------------------------------------------------------------------
+// The macroblock's real entry values (S.f3entry) against the helper's intervals
+template <typename P>
+HD bool f3_verify(const Shared& S, P h)
+{
+    bool ok = true;
+    for (int i = 0; i < 16; ++i) {
+        const int v = S.f3entry[i];
+        ok = ok && v >= h->lo[i] && v <= h->hi[i];
+        if (blk_x(i) > 0 && blk_y(i) > 0) {
+            const int sm = S.f3entry[blk_idx(blk_x(i) - 4, blk_y(i))] + S.f3entry[blk_idx(blk_x(i), blk_y(i) - 4)];
+            ok = ok && sm >= h->lo[16 + i] && sm <= h->hi[16 + i];
+        }
+    }
+    return ok;
+}
+
+// f3out: run as the macroblock's 8x8-family helper task instead (the family
+// only, recorded for f3_verify, into f3out; see above)
+HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr)
 {
     const FrameArgs& F = c.F;
     Shared& S = c.S;
     auto fam_first = [](int f) -> int { return f < 4 ? f : 7; };  // {0, 1, 2, 3, 7}
-    auto fam_type = [](int f) -> int32_t { return f < 3 ? ET_P16x16 + f : ET_P8x8REF0; };
     double best_cost = 1.7976931348623157e308;
     int best_single = 9, best_part = -1, best_fam = -1, best_dist = 0;
     bool best_found = false, pskip = false;
@@ -3683,88 +3833,183 @@ HD void guess_inter(Ctx& c)
     bool probably = false;
     int mode_flags = 0xFFFF;  // rdo.c:874
     if (c.tid == 0) S.flags = FL_INTER;
-    // one partitioning j of family fam searched: the partition mode's best
-    // cost, its Single_ctr sum and distortion; returns the P_Skip probe's
-    // outcome (16x16 only)
-    auto run_part = [&](Ctx& cc, int j, int fam, double& cost_sum, int& single_sum, int& dist_sum) -> bool {
-        Shared& SS = cc.S;
+    // a partitioning's results against the best so far (rdo.c:1148-1160)
+    auto take_part = [&](int j, int fam, double cost_sum, int single_sum, int dist_sum, auto bmv, auto bmvp) {
         const PartDef& pd = kParts[j];
-        HL_SYNC();
-        if (cc.tid == 0) {
-            SS.e_type = fam_type(fam);
-            SS.nb[0].e_type = fam_type(fam);
-            SS.nb[0].part_w = pd.part_w;
-            SS.nb[0].part_h = pd.part_h;
-            for (int i = 0; i < 4; ++i) {
-                SS.nb[0].sub_w[i] = pd.sub_w;
-                SS.nb[0].sub_h[i] = pd.sub_h;
+        cost_sum = dadd(cost_sum, dmul(F.lambda, (double)pd.hdr_bits));
+        if (cost_sum < best_cost) {
+            best_cost = cost_sum;
+            best_single = single_sum;
+            best_dist = dist_sum;
+            best_part = j;
+            best_fam = fam;
+            HL_SYNC();
+            if (c.tid == 0) {
+                for (int pi = 0; pi < pd.num_part; ++pi)
+                    for (int spi = 0; spi < pd.num_sub; ++spi) {
+                        const int o = (pi * 4 + spi) * 2;
+                        S.best_mv[pi][spi][0] = bmv[o];
+                        S.best_mv[pi][spi][1] = bmv[o + 1];
+                        S.best_mvp[pi][spi][0] = bmvp[o];
+                        S.best_mvp[pi][spi][1] = bmvp[o + 1];
+                    }
             }
-            grid_reset_inside(SS);
+            HL_SYNC();
+        }
+    };
+    // the helper: the MB-start state, the recording on
+    if (HL_FAM3 && f3out) {
+        if (F.early_term) mode_flags = early_term_modes(c);
+        for (int i = c.tid; i < 32; i += c.nthr) {
+            S.f3lo[i] = 0;
+            S.f3hi[i] = 127;
+        }
+        if (c.tid == 0) {
+            S.f3w = 0;
+            S.f3b[0] = 0;  // partitionings searched
+            S.f3b[1] = 3;  // the last one
         }
         HL_SYNC();
-        bool prob = false;
-        for (int pi = 0; pi < pd.num_part; ++pi)
-            for (int spi = 0; spi < pd.num_sub; ++spi) {
-                const bool p = search_partition(cc, pd, pi, spi, j == 0 && pi == 0 && spi == 0);
-                if (j == 0 && pi == 0 && spi == 0) prob = p;
-            }
-        for (int pi = 0; pi < pd.num_part; ++pi)
-            for (int spi = 0; spi < pd.num_sub; ++spi) {
-                cost_sum = dadd(cost_sum, uni(SS.bcost[pi][spi]));
-                single_sum += uni(SS.bsingle[pi][spi]);
-                dist_sum += uni(SS.bdist[pi][spi]);
-            }
-        return prob;
-    };
-#if defined(HL_EMU_BUILD) && !defined(__HIP_DEVICE_COMPILE__)
-    // emu probe: the 8x8 family searched a second time from the MB-start
-    // live TotalCoeffs (what a concurrent helper would have to assume)
-    struct F3 {
-        Shared S2;
-        double cs[7];
-        int ss[7], ds[7];
-        int16_t bmv[7][4][4][2], bmvp[7][4][4][2];
-    };
-    int8_t f3_mbstart[16], f3_start[16];
-    for (int i = 0; i < 16; ++i) f3_mbstart[i] = S.tc[i];
-    F3* f3 = nullptr;
-    bool f3_same = true;
-    Ctx* c2 = nullptr;
+        c.f3rec = 1;
+        c.fresh = 0;
+    }
+    for (int fam = HL_FAM3 && f3out ? 3 : 0; fam < 4 && !best_found; ++fam) {
+        // the 8x8 family's helper (pipelined runs): taken over if no workgroup
+        // claimed it, else polled between partition searches
+        int h3 = HS_MAIN;
+        if (HL_FAM3 && fam == 3 && F.hstate3 && !f3out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+            if (c.tid == 0) S.hs3_x = atomicCAS(F.hstate3 + c.addr, HS_FREE, HS_MAIN);
+            HL_SYNC();
+            h3 = uni(S.hs3_x);
+#else
+            h3 = F.hstate3[c.addr] == HS_FREE ? HS_MAIN : F.hstate3[c.addr];
+            if (h3 == HS_MAIN) F.hstate3[c.addr] = HS_MAIN;
 #endif
-    for (int fam = 0; fam < 4 && !best_found; ++fam) {
-#if defined(HL_EMU_BUILD) && !defined(__HIP_DEVICE_COMPILE__)
-        if (fam == 3 && g_f3p_enable) {
-            f3 = new F3;
-            f3->S2 = S;
-            for (int i = 0; i < 16; ++i) f3->S2.tc[i] = f3_mbstart[i];
-            c2 = new Ctx{c.F, f3->S2, c.tid, c.nthr, c.addr, c.mbx, c.mby, c.xL, c.yL, c.chain, c.fresh, c.dep, c.K};
-            c2->gx = c.gx;
-            c2->gy = c.gy;
-            c2->wux = c.wux;
-            c2->wuy = c.wuy;
-            c2->spec = c.spec;
-            c2->par = c.par;
-            g_f3p_on = 1;
-            g_f3p_w = 0;
-            for (int i = 0; i < 32; ++i) {
-                g_f3p_lo[i] = 0;
-                g_f3p_hi[i] = 127;
+            if (h3 == HS_FREE) h3 = HS_MAIN;
+            if (h3 != HS_MAIN) {  // the state the family starts from, and the best so far
+                for (int i = c.tid; i < 16; i += c.nthr) S.f3entry[i] = S.tc[i];
+                for (int i = c.tid; i < 32; i += c.nthr) {
+                    (&S.f3best_mv[0][0][0])[i] = (&S.best_mv[0][0][0])[i];
+                    (&S.f3best_mvp[0][0][0])[i] = (&S.best_mvp[0][0][0])[i];
+                }
+                if (c.tid == 0) {
+                    S.f3b_cost = best_cost;
+                    S.f3b[0] = best_single;
+                    S.f3b[1] = best_part;
+                    S.f3b[2] = best_fam;
+                    S.f3b[3] = best_dist;
+                    S.f3b[4] = c.chain;
+                    S.f3b[5] = c.fresh;
+                    S.f3b[6] = c.spec;
+                }
+                HL_SYNC();
             }
-            for (int j = 3; j < 7; ++j) {
-                f3->cs[j] = 0.0;
-                f3->ss[j] = f3->ds[j] = 0;
-                if (!((1 << (j + 1)) & mode_flags)) continue;
-                run_part(*c2, j, 3, f3->cs[j], f3->ss[j], f3->ds[j]);
-                memcpy(f3->bmv[j], f3->S2.bmv, sizeof(f3->S2.bmv));
-                memcpy(f3->bmvp[j], f3->S2.bmvp, sizeof(f3->S2.bmvp));
-            }
-            g_f3p_on = 0;
-            g_emu_f3_on = 1;
-            g_emu_f3_wr = g_emu_f3_rd = 0;
-            for (int i = 0; i < 16; ++i) f3_start[i] = S.tc[i];
         }
+        // a claimed helper: has it finished?  (the first check at once, then
+        // between partition searches)
+        auto h3_done = [&]() -> bool {
+            if (h3 != HS_CLAIMED) return h3 == HS_DONE;
+#if defined(__HIP_DEVICE_COMPILE__)
+            if (c.tid == 0) S.hs3_x = ld_relaxed(F.hstate3 + c.addr);
+            HL_SYNC();
+            if (uni(S.hs3_x) == HS_DONE) h3 = HS_DONE;
+#else
+            if (F.hstate3[c.addr] == HS_DONE) h3 = HS_DONE;
 #endif
-        for (int j = fam_first(fam); j < fam_first(fam + 1); ++j) {
+            return h3 == HS_DONE;
+        };
+        // the helper finished, and its family is proven for this MB's entry state?
+        // (asked at the family's start and before each partition search while
+        // the helper runs; a helper found unproven is not asked again)
+        auto f3_ready = [&]() -> bool {
+            if (h3 == HS_MAIN) return false;
+            if (!h3_done()) return false;
+#if defined(__HIP_DEVICE_COMPILE__)
+            if (c.tid < 64) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            HL_SYNC();
+            const bool ok = f3_verify(S, gmem(F.f3 + c.addr));
+#else
+            const bool ok = f3_verify(S, F.f3 + c.addr);
+#endif
+            if (!ok) {
+                h3 = HS_MAIN;  // (decided once)
+#if defined(__HIP_DEVICE_COMPILE__)
+                if (c.tid == 0 && F.perr) atomicAdd(F.perr + 6, 1);
+#else
+                if (F.perr) ++F.perr[6];
+#endif
+            }
+            return ok;
+        };
+        // the helper's family from the entry state: the best so far, the live
+        // TotalCoeffs, rdo.Single_ctr and the partition state it leaves
+        auto f3_import = [&]() {
+#if defined(__HIP_DEVICE_COMPILE__)
+            const auto h = gmem(F.f3 + c.addr);
+#else
+            const Fam3Out* h = F.f3 + c.addr;
+#endif
+            HL_SYNC();
+            best_cost = uni(S.f3b_cost);
+            best_single = uni(S.f3b[0]);
+            best_part = uni(S.f3b[1]);
+            best_fam = uni(S.f3b[2]);
+            best_dist = uni(S.f3b[3]);
+            for (int i = c.tid; i < 32; i += c.nthr) {
+                (&S.best_mv[0][0][0])[i] = (&S.f3best_mv[0][0][0])[i];
+                (&S.best_mvp[0][0][0])[i] = (&S.f3best_mvp[0][0][0])[i];
+            }
+            const int done = uni((int)h->done_mask), wm = uni((int)h->wmask), last = uni((int)h->e_last);
+#pragma unroll
+            for (int j = 3; j < 7; ++j)
+                if ((done >> (j - 3)) & 1)
+                    take_part(j, 3, uni((double)h->cost[j - 3]), uni((int)h->single[j - 3]), uni((int)h->dist[j - 3]), &h->bmv[j - 3][0][0][0],
+                              &h->bmvp[j - 3][0][0][0]);
+            HL_SYNC();
+            for (int i = c.tid; i < 16; i += c.nthr) S.tc[i] = ((wm >> i) & 1) ? h->tc[i] : S.f3entry[i];
+            for (int i = c.tid; i < 32; i += c.nthr) {
+                (&S.nb[0].mv[0][0][0])[i] = (&h->nbmv[0][0][0])[i];
+                (&S.bmv[0][0][0])[i] = (&h->bmv[last - 3][0][0][0])[i];
+                (&S.bmvp[0][0][0])[i] = (&h->bmvp[last - 3][0][0][0])[i];
+            }
+            for (int i = c.tid; i < 36; i += c.nthr) {
+                (&S.mvg[0][0])[i] = (&h->mvg[0][0])[i];
+                (&S.mvs[0][0])[i] = (&h->mvs[0][0])[i];
+            }
+            if (c.tid == 0) {
+                const PartDef& pd = kParts[last];
+                S.e_type = fam_etype(3);
+                S.nb[0].e_type = fam_etype(3);
+                S.nb[0].part_w = pd.part_w;
+                S.nb[0].part_h = pd.part_h;
+                for (int i = 0; i < 4; ++i) {
+                    S.nb[0].sub_w[i] = pd.sub_w;
+                    S.nb[0].sub_h[i] = pd.sub_h;
+                }
+            }
+            if (uni((int)h->fresh)) chain_write(c, uni((int)h->chain));
+            else {
+                c.chain = uni(S.f3b[4]);
+                c.fresh = uni(S.f3b[5]);
+                c.spec = uni(S.f3b[6]);
+            }
+            HL_SYNC();
+#if defined(__HIP_DEVICE_COMPILE__)
+            if (c.tid == 0 && F.perr) atomicAdd(F.perr + 5, 1);
+#else
+            if (F.perr) ++F.perr[5];
+#endif
+        };
+        bool imported = false;
+        if (HL_FAM3 && h3 != HS_MAIN && f3_ready()) {
+            f3_import();
+            imported = true;
+        }
+        for (int j = fam_first(fam); j < fam_first(fam + 1) && !imported; ++j) {
             const PartDef& pd = kParts[j];
             if (!((1 << (j + 1)) & mode_flags)) continue;
             if (F.early_term && j == 0) {
@@ -3778,39 +4023,42 @@ HD void guess_inter(Ctx& c)
             }
             double cost_sum = 0.0;
             int single_sum = 0, dist_sum = 0;
-            probably = run_part(c, j, fam, cost_sum, single_sum, dist_sum);
-#if defined(HL_EMU_BUILD) && !defined(__HIP_DEVICE_COMPILE__)
-            if (fam == 3 && f3 && j < 7) {
-                f3_same = f3_same && f3->cs[j] == cost_sum && f3->ss[j] == single_sum && f3->ds[j] == dist_sum &&
-                          memcmp(f3->bmv[j], S.bmv, sizeof(S.bmv)) == 0 && memcmp(f3->bmvp[j], S.bmvp, sizeof(S.bmvp)) == 0;
+            bool aborted = false;
+            // (one call site: every copy of the search is inlined)
+            probably = search_family_part(c, j, fam, cost_sum, single_sum, dist_sum, [&] { return HL_FAM3 && h3 == HS_CLAIMED && f3_ready(); }, aborted);
+            if (HL_FAM3 && aborted) {  // the helper's family is ready and proven: taken instead
+                f3_import();
+                imported = true;
+                break;
             }
+            if (HL_FAM3 && f3out) {  // the helper: this partitioning's results
+                HL_SYNC();
+#if defined(__HIP_DEVICE_COMPILE__)
+                auto o = gmem(f3out);
+#else
+                Fam3Out* o = f3out;
 #endif
+                if (c.tid == 0) {
+                    o->cost[j - 3] = cost_sum;
+                    o->single[j - 3] = single_sum;
+                    o->dist[j - 3] = dist_sum;
+                    S.f3b[0] |= 1 << (j - 3);
+                    S.f3b[1] = j;
+                }
+                for (int i = c.tid; i < 32; i += c.nthr)  // best MVs and MVPs, 16 words each
+                    (i < 16 ? reinterpret_cast<int32_t*>(&o->bmv[j - 3][0][0][0]) : reinterpret_cast<int32_t*>(&o->bmvp[j - 3][0][0][0]))[i & 15] =
+                        reinterpret_cast<const int32_t*>(i < 16 ? &S.bmv[0][0][0] : &S.bmvp[0][0][0])[i & 15];
+                continue;
+            }
             if (!probably && cost_sum != 0.0 && single_sum < 6 && fam == 0) {
                 int smv[2];
                 skip_mv(S, smv);
                 probably = uni(smv[0]) == uni(S.bmvp[0][0][0]) && uni(smv[1]) == uni(S.bmvp[0][0][1]) &&
                            uni(S.bmv[0][0][0]) == uni(S.bmvp[0][0][0]) && uni(S.bmv[0][0][1]) == uni(S.bmvp[0][0][1]);
             }
-            cost_sum = dadd(cost_sum, dmul(F.lambda, (double)pd.hdr_bits));
-            if (cost_sum < best_cost) {
-                best_cost = cost_sum;
-                best_single = single_sum;
-                best_dist = dist_sum;
-                best_part = j;
-                best_fam = fam;
-                HL_SYNC();
-                if (c.tid == 0) {
-                    for (int pi = 0; pi < pd.num_part; ++pi)
-                        for (int spi = 0; spi < pd.num_sub; ++spi) {
-                            S.best_mv[pi][spi][0] = S.bmv[pi][spi][0];
-                            S.best_mv[pi][spi][1] = S.bmv[pi][spi][1];
-                            S.best_mvp[pi][spi][0] = S.bmvp[pi][spi][0];
-                            S.best_mvp[pi][spi][1] = S.bmvp[pi][spi][1];
-                        }
-                }
-                HL_SYNC();
-            }
+            take_part(j, fam, cost_sum, single_sum, dist_sum, &S.bmv[0][0][0], &S.bmvp[0][0][0]);
         }
+        if (imported) probably = false;  // (the probe is 16x16's)
         pskip = probably;
         if (pskip) {  // _is_zeros_inter16x16_chroma, rdo.c:2140-2215
             HL_SYNC();
@@ -3824,39 +4072,32 @@ HD void guess_inter(Ctx& c)
             pskip = !uni(S.cbp_cac[0]) && !uni(S.cbp_cac[1]) && !uni(S.cbp_cdc[0]) && !uni(S.cbp_cdc[1]);
         }
         best_found = best_found || best_cost == 0.0 || pskip;
-#if defined(HL_EMU_BUILD) && !defined(__HIP_DEVICE_COMPILE__)
-        if (fam == 3 && f3) {
-            g_emu_f3_on = 0;
-            int diff = 0, diffc = 0;
-            for (int i = 0; i < 16; ++i)
-                if ((g_emu_f3_rd >> i) & 1) {
-                    diff += f3_mbstart[i] != f3_start[i];
-                    diffc += nc_class(f3_mbstart[i]) != nc_class(f3_start[i]);
-                }
-            ++g_emu_f3[0];                                  // MBs that searched the 8x8 family
-            g_emu_f3[1] += g_emu_f3_rd == 0;                // ... reading no entry TotalCoeff
-            g_emu_f3[2] += diff == 0;                       // ... whose reads the MB-start values match
-            g_emu_f3[3] += __builtin_popcount(g_emu_f3_rd);  // entry values read
-            g_emu_f3[4] += diffc == 0;                      // ... matching in nC class
-            const bool same = f3_same && memcmp(f3->S2.tc, S.tc, 16) == 0 && c2->chain == c.chain && c2->fresh == c.fresh;
-            g_emu_f3[5] += same;                            // ... whose search from the MB-start values ends identically
-            g_emu_f3[6] += f3_same;                         // ... (same partition results, any end state)
-            bool ver = true;
-            for (int i = 0; i < 16; ++i) {
-                ver = ver && f3_start[i] >= g_f3p_lo[i] && f3_start[i] <= g_f3p_hi[i];
-                if (blk_x(i) > 0 && blk_y(i) > 0) {
-                    const int sm = f3_start[blk_idx(blk_x(i) - 4, blk_y(i))] + f3_start[blk_idx(blk_x(i), blk_y(i) - 4)];
-                    ver = ver && sm >= g_f3p_lo[16 + i] && sm <= g_f3p_hi[16 + i];
-                }
-            }
-            g_emu_f3[7] += ver;                             // ... verified by the entry-value intervals
-            if (ver && !f3_same) fprintf(stderr, "fam3 probe: verified but different (MB %d)\n", c.addr);
-            delete c2;
-            delete f3;
-            c2 = nullptr;
-            f3 = nullptr;
-        }
+    }
+    if (HL_FAM3 && f3out) {  // the helper: the family's end state (the task publishes it with its release)
+        HL_SYNC();
+#if defined(__HIP_DEVICE_COMPILE__)
+        auto o = gmem(f3out);
+#else
+        Fam3Out* o = f3out;
 #endif
+        if (c.tid == 0) {
+            o->done_mask = S.f3b[0];
+            o->wmask = S.f3w;
+            o->chain = c.chain;
+            o->fresh = c.fresh;
+            o->e_last = S.f3b[1];
+        }
+        for (int i = c.tid; i < 16; i += c.nthr) o->tc[i] = S.tc[i];
+        for (int i = c.tid; i < 32; i += c.nthr) {
+            o->lo[i] = (int8_t)S.f3lo[i];
+            o->hi[i] = (int8_t)S.f3hi[i];
+            (&o->nbmv[0][0][0])[i] = (&S.nb[0].mv[0][0][0])[i];
+        }
+        for (int i = c.tid; i < 36; i += c.nthr) {
+            (&o->mvg[0][0])[i] = (&S.mvg[0][0])[i];
+            (&o->mvs[0][0])[i] = (&S.mvs[0][0])[i];
+        }
+        return;
     }
     if (!pskip) {
         HL_PROF_T(ti);
@@ -3880,7 +4121,7 @@ HD void guess_inter(Ctx& c)
         S.mad = best_dist;
         S.flags = FL_INTER;
         S.pm0 = PM_L0;
-        S.e_type = fam_type(best_fam);
+        S.e_type = fam_etype(best_fam);
         S.mb_type = S.e_type - 301;
         S.num_part = bp.num_part;
         S.nb[0].intra = 0;
@@ -4273,6 +4514,7 @@ HD void mb_end(Ctx& c)
 
 #if defined(HL_EMU_BUILD) && !defined(__HIP_DEVICE_COMPILE__)
 extern int g_emu_bad_guess;
+extern int g_emu_bad_guess3;
 #endif
 // The intra helper task of P macroblock addr (pipelined runs): the parts of
 // its intra fallback that do not depend on its inter search, into out --
@@ -4342,8 +4584,9 @@ HD void intra_helper(
 // One macroblock, start to end.  s_in = rdo.Single_ctr on entry (spec_in = 1
 // while it is a row-start speculation); (gx, gy) = reference region already
 // known complete (pipelined runs; see reach_wait).
+// f3out: the macroblock's 8x8-family helper task instead (guess_inter)
 HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, int s_in, int gx = 1 << 20, int gy = 1 << 20,
-               int spec_in = 1)
+               int spec_in = 1, Fam3Out* f3out = nullptr)
 {
     Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0, S.lk[tid & 15]};
     c.gx = gx;
@@ -4354,7 +4597,7 @@ HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, in
     if (tid < 16) S.lk[tid] = make_lanek(tid, F.qp, F.qpc);
     c.Q = make_laneq(tid, F.qp);
 #endif
-    if (tid == 0) gmem(F.chain + addr)->s_in = s_in;
+    if (tid == 0 && !f3out) gmem(F.chain + addr)->s_in = s_in;
     HL_PROF_T(t0);
 #if defined(__HIP_DEVICE_COMPILE__) && HL_LDS_WINDOW
     // the LDS search window: loads issued here, stored after mb_begin's load
@@ -4384,6 +4627,14 @@ HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, in
     }
 #endif
     HL_PROF_ADD(c, 6, t0);
+    if (f3out) {
+#if defined(HL_EMU_BUILD) && !defined(__HIP_DEVICE_COMPILE__)
+        if (g_emu_bad_guess3)  // tests: a wrong guess of the entry values, so that f3_verify must reject
+            for (int i = 0; i < 16; ++i) S.tc[i] = (int8_t)((i * 5 + addr) % 11);
+#endif
+        if (HL_FAM3) guess_inter(c, f3out);
+        return;
+    }
     if (F.is_intra) guess_intra(c);
     else guess_inter(c);
     HL_PROF_T(t1);

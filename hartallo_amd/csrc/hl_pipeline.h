@@ -187,7 +187,9 @@ struct PipeArgs {
     // macroblock is ready (ramp and tail of a run, a lone picture)
     int32_t helpers; // 1 = queue them
     int32_t* hstate; // [nframes][nmb] helper task states (HS_*)
-    int32_t* hq;     // [nframes * nmb] FIFO of helper tasks, f * nmb + MB address + 1 (0 = slot not yet written)
+    int32_t* hstate3; // [nframes][nmb] 8x8-family helper task states
+    int32_t fam3;    // 1 = queue 8x8-family helpers too
+    int32_t* hq;     // [2 * nframes * nmb] FIFO of helper tasks, kind << 30 | (f * nmb + MB address + 1) (0 = slot not yet written)
     int32_t* hq_head;
     int32_t* hq_tail;
     int32_t* head;   // [nframes][kSubQ] next queue slot to pop

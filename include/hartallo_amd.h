@@ -187,7 +187,11 @@ int32_t hl_amd_last_batch_stats(hl_amd_encoder_t* encoder, int32_t* out5);
  * by a second workgroup beside the macroblock's inter search -- every
  * Intra16x16 mode's transform, quantisation, CAVLC statistics and
  * reconstruction, and the Intra4x4 decision under a guess of the live
- * TotalCoeffs that the macroblock verifies.  Results do not
+ * TotalCoeffs that the macroblock verifies; and a third
+ * workgroup searches the macroblock's P8x8 partitionings from its MB-start
+ * live TotalCoeffs while the macroblock searches the larger ones, proven by
+ * nC-class intervals before the macroblock takes them (DESIGN.md §6.6;
+ * HL_AMD_FAM3=0 at create turns that part off).  Results do not
  * depend on it.  No reference interface. */
 int32_t hl_amd_set_intra_helpers(hl_amd_encoder_t* encoder, int32_t enable);
 
@@ -196,6 +200,11 @@ int32_t hl_amd_set_intra_helpers(hl_amd_encoder_t* encoder, int32_t enable);
  * that rejected it (an nC class differed: decided again), [2] whose helper
  * no workgroup had claimed in time (the macroblock decided intra itself). */
 int32_t hl_amd_last_helper_stats(hl_amd_encoder_t* encoder, int32_t* out3);
+
+/* How the 8x8-family helpers of the last encode call ran -- diagnostics:
+ * out2[0] P macroblocks that took their helper's P8x8 searches, [1] that
+ * found them unproven for their entry state (searched again). */
+int32_t hl_amd_last_fam3_stats(hl_amd_encoder_t* encoder, int32_t* out2);
 
 /* per-phase shader-clock counters of the macroblock kernel; filled only by
  * the profiling build (make profile); out[2k] = cycles, out[2k+1] = calls

@@ -24,10 +24,7 @@ using namespace hl;
 
 #if !defined(__HIP_DEVICE_COMPILE__)
 int hl::g_emu_bad_guess = 0;  // intra_helper (hl_mbcore.h): HL_EMU_HELPER=2
-long hl::g_emu_f3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-int hl::g_emu_f3_on = 0, hl::g_emu_f3_wr = 0, hl::g_emu_f3_rd = 0;
-int hl::g_f3p_on = 0, hl::g_f3p_w = 0, hl::g_f3p_enable = 0;
-int8_t hl::g_f3p_lo[32], hl::g_f3p_hi[32];
+int hl::g_emu_bad_guess3 = 0;  // fam3_helper: HL_EMU_HELPER bit 8
 #endif
 
 struct EmuEnc {
@@ -45,9 +42,14 @@ struct EmuEnc {
     Shared* S2;                        // the intra helper's workgroup image (HL_EMU_HELPER)
     std::vector<IntraSpec> ispec;
     std::vector<int32_t> hstate;
-    long helper_runs = 0;
-    int helper_mode = 0;               // 0 off, 1 helpers, 2 helpers with a wrong guess (emu_set_helper, HL_EMU_HELPER)
-    int32_t perr[8] = {};              // FrameArgs::perr: [2] helper Intra4x4 kept, [3] rejected
+    std::vector<Fam3Out> f3;
+    std::vector<int32_t> hstate3;
+    long helper_runs = 0, helper3_runs = 0;
+    // bits (emu_set_helper, HL_EMU_HELPER): 1 intra helpers, 2 intra helpers
+    // with a wrong guess, 4 8x8-family helpers, 8 8x8-family helpers with a
+    // wrong guess
+    int helper_mode = 0;
+    int32_t perr[8] = {};              // FrameArgs::perr: [2] helper Intra4x4 kept, [3] rejected; [5] 8x8 family kept, [6] rejected
     std::unique_ptr<RateControl> rc;  // rate control (hl_rc.h), as in the product
     int last_qp;
 };
@@ -250,11 +252,9 @@ extern "C" void emu_destroy(void* h)
 }
 extern "C" long emu_helper_runs(void* h) { return ((EmuEnc*)h)->helper_runs; }
 extern "C" int emu_helper_i4(void* h, int rejected) { return ((EmuEnc*)h)->perr[rejected ? 3 : 2]; }
+extern "C" int emu_helper_fam3(void* h, int rejected) { return ((EmuEnc*)h)->perr[rejected ? 6 : 5]; }
+extern "C" long emu_helper3_runs(void* h) { return ((EmuEnc*)h)->helper3_runs; }
 extern "C" void emu_set_helper(void* h, int mode) { ((EmuEnc*)h)->helper_mode = mode; }
-#if !defined(__HIP_DEVICE_COMPILE__)
-extern "C" void emu_fam3_stats(long* out) { for (int i = 0; i < 8; ++i) out[i] = g_emu_f3[i]; }  // (development probe)
-extern "C" void emu_fam3_enable(int on) { g_f3p_enable = on; }
-#endif
 
 // Writes hdr (first frame) + 00 00 01 + slice into out; returns bytes or -1.
 // rate control of the product path (hl_amd_set_rate_control)
@@ -319,17 +319,28 @@ extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, co
     // intra_helper) runs first, on its own workgroup image, as a pipelined
     // run's helper task would; the macroblock then uses its results
     // (2: the helpers guess the live TotalCoeffs wrongly; emu_set_helper)
+    // (4: every P macroblock's 8x8-family helper, fam3_helper, likewise;
+    // 8: with a wrong guess of the entry values)
     const int helper = e->helper_mode;
 #if !defined(__HIP_DEVICE_COMPILE__)
-    g_emu_bad_guess = helper == 2;
+    g_emu_bad_guess = (helper & 2) != 0;
+    g_emu_bad_guess3 = (helper & 8) != 0;
 #endif
     F.ispec = nullptr;
     F.hstate = nullptr;
-    if (helper && !intra) {
+    F.f3 = nullptr;
+    F.hstate3 = nullptr;
+    if ((helper & 3) && !intra) {
         e->ispec.resize(e->nmb);
         e->hstate.assign(e->nmb, HS_DONE);
         F.ispec = e->ispec.data();
         F.hstate = e->hstate.data();
+    }
+    if ((helper & 12) && !intra) {
+        e->f3.resize(e->nmb);
+        e->hstate3.assign(e->nmb, HS_DONE);
+        F.f3 = e->f3.data();
+        F.hstate3 = e->hstate3.data();
     }
     int chain = e->chain_end;
     // HL_EMU_POISON=<seed>: fill the workgroup's LDS image with pseudo-random
@@ -351,6 +362,10 @@ extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, co
         if (F.hstate) {
             intra_helper(F, *e->S2, a, 0, 1, chain, F.ispec + a);
             ++e->helper_runs;
+        }
+        if (F.hstate3) {
+            encode_mb(F, *e->S2, a, 0, 1, chain, 1 << 20, 1 << 20, 1, F.f3 + a);  // as the 8x8-family helper task
+            ++e->helper3_runs;
         }
         encode_mb(F, *e->S, a, 0, 1, chain);
         chain = e->chain[a].s_out;

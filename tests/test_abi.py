@@ -15,7 +15,7 @@ HEADER = os.path.join(ROOT, "include", "hartallo_amd.h")
 def declared_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(hl_amd_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(hl_amd_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_header_declares_the_boundary():

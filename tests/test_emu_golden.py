@@ -123,3 +123,30 @@ def test_i4_prediction_table():
     lib = ctypes.CDLL(EMU_LIB)
     lib.emu_i4_table_check.restype = ctypes.c_long
     assert lib.emu_i4_table_check(7, 20000) == 0
+
+
+@pytest.mark.parametrize("mode", [4, 12, 5], ids=["fam3", "fam3_bad_guess", "intra_and_fam3"])
+@pytest.mark.parametrize("cfg", ALL, ids=[c[0] for c in ALL])
+def test_fam3_helpers_match_reference(cfg, mode):
+    """Every P macroblock's 8x8-family helper task (hl_mbcore.h guess_inter
+    with f3out: the P8x8 partitionings searched from the MB-start live
+    TotalCoeffs, with the nC-class intervals of the entry values it read) run
+    first; the macroblock takes the helper's family when its real entry state
+    lies in every interval (f3_verify), else searches the family itself: the
+    same streams.  mode 12 makes the helper start from wrong entry values, so
+    both the rejection and the acceptance of an unread wrong value are
+    exercised; mode 5 runs both kinds of helper."""
+    name, w, h, n, qp, mer, db, gop, seed = cfg
+    clip = golden_input(cfg)
+    ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()
+    enc = EmuEncoder(w, h, qp, mer, db, gop, GOLD[name].get("early_term", 0))
+    enc.lib.emu_set_helper(ctypes.c_void_p(enc.h_), mode)
+    out = b""
+    for f in range(n):
+        out += enc.encode(clip[f])
+        assert md5(enc.recon()) == GOLD[name]["recon_md5"][f], f"{name}: recon of frame {f}"
+    assert out == ref, f"{name}: first differing byte {first_diff(out, ref)}"
+    kept = enc.lib.emu_helper_fam3(ctypes.c_void_p(enc.h_), 0)
+    rejected = enc.lib.emu_helper_fam3(ctypes.c_void_p(enc.h_), 1)
+    if any(f % gop for f in range(n)) and w * h >= 64 * 48:
+        assert kept + rejected > 0
