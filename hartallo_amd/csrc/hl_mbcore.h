@@ -345,7 +345,7 @@ struct Shared {
 #ifndef HL_F3REC_ON
 #define HL_F3REC_ON 1
 #endif
-#define HL_F3REC(c) (HL_FAM3 && HL_F3REC_ON && (c).f3rec)
+#define HL_F3REC(c) (HL_FAM3 && HL_F3REC_ON && REC && (c).f3rec)  // (REC: the search's template argument)
 // A fresh, opaque copy of the lane index at the entry of each phase: the
 // compiler cannot compute the phase's lane-dependent addresses earlier and
 // hold them (spilled) across the partition searches.
@@ -1197,6 +1197,8 @@ __device__ __forceinline__ int tcb_last(const uint8_t* row, uint32_t allow)
 // Evaluates the candidates S.wc[wave][0..ncand) of partition g in order.
 // Leaves per-candidate cost/rbc/dist/single/cbp in S.cd_*, updates the live
 // TotalCoeffsLuma S.tc (last writer) and the Single_ctr chain.
+// REC: the 8x8-family helper's instantiation (entry-value intervals recorded)
+template <bool REC = false>
 HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
 {
 #if defined(HL_STATS) && !defined(__HIP_DEVICE_COMPILE__)
@@ -1632,6 +1634,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
 // S.tc is behind a barrier.
 // last_l: candidate (tid & 31)'s R.last when the caller has it in a register
 // (device; -2 = read it here)
+template <bool REC = false>
 HD void commit_candidates(Ctx& c, const PartGeo& g, int n, int last_l = -2)
 {
     Shared& S = c.S;
@@ -1763,6 +1766,7 @@ HD void reach_wait(Ctx& c, const PartGeo& g, const int pmv[2])
 
 // Diamond search of one (sub)partition, me_ds.c:104-477.  Returns true when
 // the P_Skip probe fired (16x16 only).
+template <bool REC = false>
 HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
 {
     // (no HL_FRESH_TID here: ROCm 7.2's greedy register allocator crashes on it)
@@ -1807,8 +1811,8 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         smv[1] = uni(smv[1]);
         if (pmv[0] == smv[0] && pmv[1] == smv[1]) {
             put_cand(c, g.px, g.py, g.pw, g.ph, 0, pmv[0], pmv[1], 0, (c.tid & 63) == 0);
-            eval_candidates(c, g, 1, pmv);
-            commit_candidates(c, g, 1);
+            eval_candidates<REC>(c, g, 1, pmv);
+            commit_candidates<REC>(c, g, 1);
             if (uni(S.cd[c.par].bits[0]) == 0 || uni(S.cd[c.par].single[0]) < 6) {
                 probably = true;
                 b.cost = 0.0;
@@ -2007,7 +2011,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         const int total = lo[nseg - 1] + n[nseg - 1];
         if (total) {
             HL_PROF_ADD(c, 16, tgap);
-            eval_candidates(c, g, total, pmv);
+            eval_candidates<REC>(c, g, total, pmv);
         }
         HL_PROF_T(tsel);
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -2136,9 +2140,9 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
 #if defined(HL_STEP_PROF)
         HL_PROF_ADD(c, 18, tres);  // the chain resolved
 #endif
-        if (used) commit_candidates(c, g, used, pv_last);
+        if (used) commit_candidates<REC>(c, g, used, pv_last);
 #else
-        if (used) commit_candidates(c, g, used);
+        if (used) commit_candidates<REC>(c, g, used);
 #endif
         HL_PROF_ADD(c, 17, tsel);
     }
@@ -3752,7 +3756,7 @@ HD int32_t fam_etype(int f) { return f < 3 ? ET_P16x16 + f : ET_P8x8REF0; }
 // distortion; returns the P_Skip probe's outcome (16x16 only).  abort() is
 // asked before every partition search; when it says so the search stops
 // (aborted = true) and the results are meaningless.
-template <typename A>
+template <bool REC, typename A>
 HD bool search_family_part(Ctx& c, int j, int fam, double& cost_sum, int& single_sum, int& dist_sum, A abort, bool& aborted)
 {
     Shared& S = c.S;
@@ -3778,7 +3782,7 @@ HD bool search_family_part(Ctx& c, int j, int fam, double& cost_sum, int& single
                 aborted = true;
                 return false;
             }
-            const bool p = search_partition(c, pd, pi, spi, j == 0 && pi == 0 && spi == 0);
+            const bool p = search_partition<REC>(c, pd, pi, spi, j == 0 && pi == 0 && spi == 0);
             if (j == 0 && pi == 0 && spi == 0) prob = p;
         }
     for (int pi = 0; pi < pd.num_part; ++pi)
@@ -4025,7 +4029,9 @@ HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr)
             int single_sum = 0, dist_sum = 0;
             bool aborted = false;
             // (one call site: every copy of the search is inlined)
-            probably = search_family_part(c, j, fam, cost_sum, single_sum, dist_sum, [&] { return HL_FAM3 && h3 == HS_CLAIMED && f3_ready(); }, aborted);
+            // (the helper runs its own instantiation, with the recording)
+            if (HL_FAM3 && f3out) probably = search_family_part<true>(c, j, fam, cost_sum, single_sum, dist_sum, [] { return false; }, aborted);
+            else probably = search_family_part<false>(c, j, fam, cost_sum, single_sum, dist_sum, [&] { return HL_FAM3 && h3 == HS_CLAIMED && f3_ready(); }, aborted);
             if (HL_FAM3 && aborted) {  // the helper's family is ready and proven: taken instead
                 f3_import();
                 imported = true;
