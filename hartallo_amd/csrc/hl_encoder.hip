@@ -721,7 +721,14 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #if defined(HL_PROFILE)
             pt4 = __builtin_readcyclecounter();
 #endif
-            if (tid == 0) st_relaxed(P.done + t, 1);
+            if (tid == 0) {
+                st_relaxed(P.done + t, 1);
+                // the row's records are in host memory: every MB of rows <= y
+                // set its done flag after its system-scope release, and this
+                // task's filters waited for (x-1, y) and (x, y-1) (the slice
+                // writers consume the picture row by row)
+                if (x == mbw - 1 && PF.rows) __hip_atomic_store(PF.rows, y + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             release(HL_EARLY_RELEASE ? 1 : 2);
             // a stream's pictures finish in order: the last MB depends on every
             // other one and on the previous picture's last MB
@@ -767,6 +774,9 @@ static int diag_count(int mbw, int rows, int diag)
 // ---------------------------------------------------------------------------
 // encoder context
 // ---------------------------------------------------------------------------
+constexpr int kMaxRun = 128;  // pictures per pipelined launch and stream (bench.py MAX_RUN)
+constexpr int kRowsAt = 16;   // h_progress word of picture 0's row count
+
 struct hl_amd_encoder_s {
     hl_amd_params_t p;
     int W, H, Wc, Hc, mbw, mbh, nmb, qpc, pstride;
@@ -798,7 +808,8 @@ struct hl_amd_encoder_s {
     int scap = 0;                // picture slots the scheduler state holds (ensure_sched)
     uint8_t *d_bpic, *d_bpl;     // per picture: recon (Y|U|V), quarter-pel planes
     MbRecord *d_brec, *h_brec, *dh_brec;  // dh_brec: device address of the pinned h_brec (the run writes it)
-    int32_t* h_progress;                  // pinned: pictures of the running run whose records are in h_brec
+    int32_t* h_progress;                  // pinned: pictures of the running run whose records are in h_brec;
+                                          // [4, 12) the run's error words; [kRowsAt + k] MB rows of picture k
     std::atomic<int> run_live{0};         // 1 while a pipelined run is on the GPU (h_progress counts its pictures)
     std::chrono::steady_clock::time_point run_t0;  // launch time of the running run (writer tracing)
     MbChain *d_bchain, *h_bchain;
@@ -923,7 +934,7 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
          hipHostMalloc(&e->h_rec, sizeof(MbRecord) * e->nmb, hipHostMallocDefault) == hipSuccess &&
          hipHostMalloc(&e->h_chain, sizeof(MbChain) * e->nmb, hipHostMallocDefault) == hipSuccess &&
          hipHostMalloc(&e->h_spec, sizeof(int32_t) * e->mbh, hipHostMallocDefault) == hipSuccess &&
-         hipHostMalloc(&e->h_progress, 64, hipHostMallocCoherent) == hipSuccess;
+         hipHostMalloc(&e->h_progress, sizeof(int32_t) * (kRowsAt + kMaxRun), hipHostMallocCoherent) == hipSuccess;
     ok = ok && hipMalloc(&e->d_rows, sizeof(int32_t) * (e->mbh + 1)) == hipSuccess &&
          hipMemsetAsync(e->d_rows, 0, sizeof(int32_t) * (e->mbh + 1), e->stream) == hipSuccess;
     // the per-address MB objects start zeroed (calloc'd by the reference, mb.c)
@@ -1155,7 +1166,6 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
 // ---------------------------------------------------------------------------
 // pipelined runs of P pictures
 // ---------------------------------------------------------------------------
-constexpr int kMaxRun = 128;     // pictures per pipelined launch and stream (bench.py MAX_RUN)
 constexpr int kMaxStreams = 16;  // streams per launch (hl_amd_encode_streams)
 
 static hipError_t ensure_batch(hl_amd_encoder_t* e, int n)
@@ -1316,19 +1326,33 @@ static std::vector<size_t> write_run(hl_amd_encoder_t* e, int m, int base, const
     }
     std::vector<size_t> size(m, 0);
     std::atomic<int> next{0};
+    // during a run: a row of picture k is read once the kernel has put its
+    // records in host memory (h_progress[kRowsAt + k] counts the rows)
+    struct Gate {
+        const int32_t* rows;
+        const std::atomic<bool>* abort;
+        static bool wait(void* ctx, int r)
+        {
+            const Gate* g = (const Gate*)ctx;
+            while (__atomic_load_n(g->rows, __ATOMIC_ACQUIRE) <= r) {
+                if (g->abort->load()) return false;
+                std::this_thread::sleep_for(std::chrono::microseconds(20));
+            }
+            return true;
+        }
+    };
     auto work = [&](int w) {
         for (int k; (k = next.fetch_add(1)) < m;) {
-            // during a run: wait until the kernel has put picture k's records in host memory
-            while (abort && __atomic_load_n(e->h_progress, __ATOMIC_ACQUIRE) <= k) {
-                if (abort->load()) return;
-                std::this_thread::sleep_for(std::chrono::microseconds(50));
-            }
+            Gate g{e->h_progress + kRowsAt + k, abort};
+            const RowGate gate{&Gate::wait, &g};
+            if (abort && !Gate::wait(&g, 0)) return;
             const SliceState ss{e->run_intra[k], e->pict_count + k, e->run_idr_id[k], e->run_qp[k]};
             uint8_t* out = e->wout[w].data();
             static const bool trace = getenv("HL_AMD_TRACE_WRITERS") != nullptr;
             const auto tk = std::chrono::steady_clock::now();
             const size_t nb = write_slice(sp, ss, e->h_brec + (size_t)e->nmb * k, e->wscratch[w].data(), out, e->wout[w].size(),
-                                          &e->run_bits[k]);
+                                          &e->run_bits[k], abort ? &gate : nullptr);
+            if (!nb && abort && abort->load()) return;
             if (trace)
                 fprintf(stderr, "writer %d picture %d: start %.2f ms, write %.2f ms\n", w, k,
                         std::chrono::duration<double, std::milli>(tk - e->run_t0).count(),
@@ -1452,6 +1476,8 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
             pf.pl_out = e->d_bpl + 4 * e->plsz * k;
             pf.deblock = e->p.deblock;
             pf.progress = d_progress;
+            pf.rows = d_progress + kRowsAt + k;
+            __atomic_store_n(e->h_progress + kRowsAt + k, 0, __ATOMIC_RELAXED);
         }
         __atomic_store_n(e->h_progress, 0, __ATOMIC_RELEASE);
         e->run_live.store(1, std::memory_order_release);

@@ -109,6 +109,7 @@ struct PipeFrame {
     uint8_t* pl_out;    // this picture's quarter-pel planes (plane p at pl_out + p * F.plsz)
     int32_t deblock;    // deblocking enabled (disable_deblocking_filter_idc 0)
     int32_t* progress;  // host-mapped count of its stream's published pictures, or null
+    int32_t* rows;      // host-mapped count of this picture's published MB rows, or null
 };
 
 // Dependencies of task (f, x, y) inside a run: the wavefront neighbours

@@ -282,7 +282,7 @@ size_t slice_scratch_bytes(const StreamParams& p)
 }
 
 size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap,
-                   SliceBits* bits)
+                   SliceBits* bits, const RowGate* gate)
 {
     static const int16_t kZeros[16] = {0};
     const size_t scap = slice_scratch_bytes(p);
@@ -320,7 +320,9 @@ size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* r
     // slice_data, mb.c:543-892
     int skip_run = 0;
     int64_t texture = 0;
+    const int mbw = p.width / 16;
     for (int a = 0; a < nmb; ++a) {
+        if (gate && a % mbw == 0 && !gate->wait(gate->ctx, a / mbw)) return 0;
         const MbRecord& m = recs[a];
         if (!s.idr) {
             if (m.e_type == ET_PSKIP) {

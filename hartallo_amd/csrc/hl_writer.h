@@ -64,8 +64,15 @@ size_t slice_scratch_bytes(const StreamParams& p);
 // writer serialises with; the GPU bit counter (hl_prims.h level_code_len)
 // must agree with it for every (suffixLength, levelCode).
 int level_code_bits(int suffix_length, int level_code);
+// gate (optional): wait(ctx, r) returns once the records of MB row r may be
+// read, or false to give up (write_slice then returns 0) -- a pipelined run
+// publishes a picture's records row by row while it is still coding it.
+struct RowGate {
+    bool (*wait)(void* ctx, int row);
+    void* ctx;
+};
 size_t write_slice(const StreamParams& p, const SliceState& s, const MbRecord* recs, uint8_t* scratch, uint8_t* out, size_t cap,
-                   SliceBits* bits = nullptr);
+                   SliceBits* bits = nullptr, const RowGate* gate = nullptr);
 
 // ---------------------------------------------------------------------------
 // Spatial SVC (Annex G), the reference's encoder syntax (hl_codec_264.c:
