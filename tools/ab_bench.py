@@ -35,8 +35,8 @@ def child(lib):
     ptrs = [(dev[i].data_ptr(), dev[i].data_ptr() + ny, dev[i].data_ptr() + ny + ny // 4) for i in range(150)]
     for warm, steps in ((5, 20), (30, 120)):
         enc = Encoder(W, H, 28, 16, 1, 30)
-        if os.environ.get("HL_AB_GEOM"):  # "workgroups,reach,window" (hl_amd_set_pipeline)
-            enc.set_pipeline(*[int(v) for v in os.environ["HL_AB_GEOM"].split(",")])
+        if os.environ.get("HL_AB_GEOM"):  # "workgroups,reach,window" or with "/" (hl_amd_set_pipeline)
+            enc.set_pipeline(*[int(v) for v in os.environ["HL_AB_GEOM"].replace("/", ",").split(",")])
         enc.set_timing(True)
         outs = [r.annexb() for r in enc.encode_batch_device(ptrs[:warm])]
         torch.cuda.synchronize()

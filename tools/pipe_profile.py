@@ -25,6 +25,10 @@ from hartallo_amd import Encoder, synth  # noqa: E402
 
 PHASES = ["eval:block", "eval:nC", "eval:reduce", "search_partition", "mvp", "guess_intra(P)", "mb_begin", "mb_end", "whole MB",
           "reach_wait", "intra:i16", "intra:i4", "early-term modes", "inter finalize", "", "", "step:candidates", "step:selection", "", "helper join"]
+if os.environ.get("HL_STEP_NAMES"):  # a build with -DHL_STEP_PROF: slots 12..15, 18, 19 time the steps' sub-phases
+    PHASES[12:16] = ["step:loads", "step:quad work", "step:eval barrier", "step:results+minima"]
+    PHASES[18] = "step:chain resolved"
+    PHASES[19] = "step:cands generated"
 
 
 def main():
