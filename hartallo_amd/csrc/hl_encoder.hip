@@ -26,12 +26,16 @@
 #include <thread>
 #include <vector>
 
+#if !defined(HL_KERNELS_ONLY)
 #include "../../include/hartallo_amd.h"
 #include "hl_rc.h"
+#endif
 #include "hl_pipeline.h"
+#if !defined(HL_KERNELS_ONLY)
 #include "hl_svc.h"
 #include "hl_cavlc.h"
 #include "hl_writer.h"
+#endif
 
 using namespace hl;
 
@@ -48,7 +52,9 @@ using namespace hl;
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
+#if !defined(HL_KERNELS_ONLY)
 static void launch_planes(hl_amd_encoder_t* e, const uint8_t* ref_y);
+#endif
 
 #if defined(HL_POISON_LDS)
 // Debug builds (-DHL_POISON_LDS=<salt>): the workgroup's LDS image (bytes
@@ -100,6 +106,7 @@ __device__ __forceinline__ void frame_args_to_lds(FrameArgs& dst, const FrameArg
     __syncthreads();
 }
 
+#if !defined(HL_KERNELS_ONLY)
 __global__ __launch_bounds__(kMbThreads, 2) void k_mb_diag(FrameArgs F, int diag, int row0)
 {
     __shared__ Shared S;
@@ -113,7 +120,9 @@ __global__ __launch_bounds__(kMbThreads, 2) void k_mb_diag(FrameArgs F, int diag
     __syncthreads();
     encode_mb(sF, S, addr, threadIdx.x, kMbThreads, s_in);
 }
+#endif
 
+#if !defined(HL_KERNELS_ONLY)
 // Deblocking of a whole picture in one launch: one 64-lane workgroup per MB
 // row, its MBs left to right; MB (x, y) waits until row y - 1 has finished
 // MB x + 1 -- the order of the anti-diagonal launches d = x + 2y, so every
@@ -163,6 +172,7 @@ __global__ __launch_bounds__(64) void k_deblock_rows(DeblockArgs D, int32_t* row
         if (tid == 0) st_relaxed(row_done + y, x + 1);
     }
 }
+#endif
 
 // Deblocking and plane blocks of task (x, y) (hl_pipeline.h).
 // The deblocking of one MB in the LDS tile (DbMbTile, hl_filters.h) that
@@ -266,6 +276,7 @@ constexpr int kSubQ = HL_SUBQ;
 #endif
 constexpr int kScan = HL_SCAN;
 
+#if !defined(HL_KERNELS_ONLY)
 // Dependency counters and ready queues of a run (hl_pipeline.h): only task
 // (0, 0) of every stream's first picture starts ready.
 __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
@@ -296,6 +307,7 @@ __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
         for (int k = 0; k < 8; ++k) P.err[k] = 0;  // give-ups, chain walks, helper I4 kept / rejected / taken over, -, 8x8 family kept / rejected
     }
 }
+#endif
 
 // Wave 0 takes the next ready task and claims it: f * nmb + addr, or -1 once
 // the run has finished (or after ~10 s without a task: a wait gave up
@@ -764,6 +776,8 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #endif
 }
 
+#if !defined(HL_KERNELS_ONLY)  // (hl_encoder_fam3.hip compiles the kernels above again, with HL_FAM3=1)
+extern "C" hipError_t hl_fam3_launch_pipeline(const void* args, size_t psz, int mbw, int mbh, int workgroups, hipStream_t stream);
 static int diag_count(int mbw, int rows, int diag)
 {
     const int ylo = std::max(0, (diag - mbw + 2) / 2);
@@ -1384,6 +1398,9 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
     hl_amd_encoder_t* e0 = es[0];
     const size_t pic = (size_t)e0->W * e0->H * 3 / 2, nmb = e0->nmb;
     const int slots = S * m;
+    // a lone picture runs the kernel built with the 8x8-family helper tasks
+    // (hl_encoder_fam3.hip): most workgroups would idle beside its wavefront
+    const bool fam3 = slots == 1 && e0->helpers && e0->fam3;
     for (int si = 0; si < S; ++si) {
         hl_amd_encoder_t* e = es[si];
         if (e->rc && (m != 1 || S != 1)) return HL_AMD_ERROR_INVALID_STATE;
@@ -1460,7 +1477,7 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
             if (e0->helpers && !e->run_intra[k]) {
                 F.ispec = e->d_ispec;
                 F.hstate = e0->d_hstate + nmb * slot;
-                if (HL_FAM3 && e0->fam3) {
+                if (fam3) {
                     F.f3 = e0->d_f3 + (size_t)nmb * slot;
                     F.hstate3 = e0->d_hstate + (size_t)nmb * (slots + slot);
                 }
@@ -1506,7 +1523,7 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
     P.hstate = e0->d_hstate;
     P.hstate3 = e0->d_hstate + (size_t)nmb * slots;
     P.helpers = e0->helpers ? 1 : 0;
-    P.fam3 = HL_FAM3 && e0->helpers && e0->fam3 ? 1 : 0;
+    P.fam3 = fam3 ? 1 : 0;
     P.hq = e0->d_queue + kSubQ * nmb * slots;
     P.head = e0->d_head;
     P.tail = e0->d_head + kSubQ * slots;
@@ -1534,7 +1551,8 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
     }
     if (e0->timing) HL_HIP_CHECK(hipEventRecord(e0->ev[4], e0->stream));
     for (int si = 0; si < S; ++si) es[si]->run_t0 = std::chrono::steady_clock::now();
-    k_pipeline<<<wgs, kMbThreads, 0, e0->stream>>>(P, e0->mbw, e0->mbh);
+    if (fam3) HL_HIP_CHECK(hl_fam3_launch_pipeline(&P, sizeof(P), e0->mbw, e0->mbh, wgs, e0->stream));
+    else k_pipeline<<<wgs, kMbThreads, 0, e0->stream>>>(P, e0->mbw, e0->mbh);
     HL_HIP_CHECK(hipGetLastError());
     if (e0->timing) HL_HIP_CHECK(hipEventRecord(e0->ev[5], e0->stream));
     // The kernel stores every finished MB's record into pinned host memory and
@@ -2807,3 +2825,4 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
     restore.ok = rc == HL_AMD_SUCCESS;
     return rc;
 }
+#endif  // !HL_KERNELS_ONLY
