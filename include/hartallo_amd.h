@@ -187,12 +187,13 @@ int32_t hl_amd_last_batch_stats(hl_amd_encoder_t* encoder, int32_t* out5);
  * by a second workgroup beside the macroblock's inter search -- every
  * Intra16x16 mode's transform, quantisation, CAVLC statistics and
  * reconstruction, and the Intra4x4 decision under a guess of the live
- * TotalCoeffs that the macroblock verifies; and a third
- * workgroup searches the macroblock's P8x8 partitionings from its MB-start
- * live TotalCoeffs while the macroblock searches the larger ones, proven by
- * nC-class intervals before the macroblock takes them (DESIGN.md §6.6;
- * HL_AMD_FAM3=0 at create turns that part off).  Results do not
- * depend on it.  No reference interface. */
+ * TotalCoeffs that the macroblock verifies; and, in a run
+ * of one picture (the per-frame path), a third workgroup searches the
+ * macroblock's P8x8 partitionings from its MB-start live TotalCoeffs while
+ * the macroblock searches the larger ones, proven by nC-class intervals
+ * before the macroblock takes them (HL_AMD_FAM3=0 at create
+ * turns that part off).  Results do not depend on it.  No reference
+ * interface. */
 int32_t hl_amd_set_intra_helpers(hl_amd_encoder_t* encoder, int32_t enable);
 
 /* How the intra fallbacks of the last encode call ran -- diagnostics:
