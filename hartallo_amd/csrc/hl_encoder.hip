@@ -326,7 +326,11 @@ __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
 #else
 #define HL_POPSTAT(i) ((void)0)
 #endif
-__device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh
+// olc: lane s < S holds stream s's oldest unfinished picture as the previous
+// call read it (-1: none yet); the scan uses it while this call's read is in
+// flight (a stale value only shifts the window late: its first pictures are
+// finished ones, with empty queues)
+__device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc
 #if defined(HL_PROFILE)
                         , unsigned long long* pst  // profiling: [0] attempts on a macroblock, [1] lost, [2] empty rounds
 #endif
@@ -340,9 +344,9 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh
         // stream r % S, its picture oldest + r / S) with r = e / kSubQ: the
         // window of each stream's first unfinished pictures
         const int S = P.nstreams;
-        int ol = 0;
-        if (lane < S) ol = ld_relaxed(P.oldest + lane);
-        if (__ballot(lane < S && ol < P.spp) == 0) return -1;  // every stream finished
+        int oln = 0;
+        if (lane < S) oln = ld_relaxed(P.oldest + lane);
+        const int ol = P.nframes > 1 && olc >= 0 ? olc : oln;  // (a lone picture: idle workgroups poll at the read's pace)
         int fl[kScan], ql[kScan], hs[kScan], ts[kScan], js[kScan], sqs[kScan];
         bool ins[kScan];
 #pragma unroll
@@ -360,6 +364,8 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh
                 ts[i] = ld_relaxed(P.tail + ql[i]);
             }
         }
+        olc = oln;
+        if (__ballot(lane < S && oln < P.spp) == 0) return -1;  // every stream finished
         int i0 = -1, hh = 0, v = 0, bfl = 0, bql = 0;
         if (P.hop < 0) {
             // oldest first: the first non-empty entry
@@ -465,8 +471,11 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh
             return -1;
         }
         // nothing ready: back off (fewer scans of the queue words while tasks run)
+#ifndef HL_IDLE_SLEEP
+#define HL_IDLE_SLEEP 16
+#endif
         if (++empty < 4) __builtin_amdgcn_s_sleep(4);
-        else __builtin_amdgcn_s_sleep(16);
+        else __builtin_amdgcn_s_sleep(HL_IDLE_SLEEP);
     }
 }
 
@@ -522,6 +531,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
     const int nmb = mbw * mbh;
     const bool in_order = blockIdx.x == 0;  // claims tasks in run order (claim_next)
     int cursor = 0;
+    int olc = -1;  // wave 0: pop_task's oldest pictures of the previous call
 #if defined(HL_PRIO_YOUNG)
     // the second-dispatched half of the workgroup (waves 4-7) loses every VALU
     // arbitration to its SIMD partner at equal priority (MI355X_MICROARCH.md,
@@ -542,7 +552,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         const unsigned long long pt0 = __builtin_readcyclecounter();
 #endif
         if (threadIdx.x < 64) {
-            const int t = in_order ? claim_next(P, nmb, cursor) : pop_task(P, nmb, mbw, mbh
+            const int t = in_order ? claim_next(P, nmb, cursor) : pop_task(P, nmb, mbw, mbh, olc
 #if defined(HL_PROFILE)
                                                                                            , pst
 #endif
@@ -681,14 +691,23 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #if defined(HL_PROFILE)
             const unsigned long long pe1 = __builtin_readcyclecounter();
 #endif
+            // the predecessors' flags are read before the release's atomics
+            // return (their round trips overlap); polled after it if unset
+            const int32_t* dA = P.done + t - 1;
+            const int32_t* dB = P.done + f * nmb + (y - 1) * mbw + min(x + 1, mbw - 1);
+            int vA = 1, vB = 1;
+            if (tid == 0) {
+                if (x > 0) vA = ld_relaxed(dA);
+                if (y > 0) vB = ld_relaxed(dB);
+            }
             release(0);
 #if defined(HL_PROFILE)
             if (f == 0 && tid == 0 && prof) prof[64 + nmb + 3 * addr + 2] = wall_clock64();
             const unsigned long long pe2 = __builtin_readcyclecounter();
 #endif
             if (tid == 0) {
-                if (x > 0) spin_ge(P.done + t - 1, 1, P.err);
-                if (y > 0) spin_ge(P.done + f * nmb + (y - 1) * mbw + min(x + 1, mbw - 1), 1, P.err);
+                if (vA < 1) spin_ge(dA, 1, P.err);
+                if (vB < 1) spin_ge(dB, 1, P.err);
             }
 #if defined(HL_PROFILE)
             const unsigned long long pe3 = __builtin_readcyclecounter();
