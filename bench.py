@@ -14,9 +14,16 @@ encoding them one call at a time (tests/test_gpu_pipeline.py).
 Multi-GPU: one independent stream per GPU (frame-sharded throughput mode,
 SURVEY §8(e) c5) -- weak scaling, no data-path collective; torch.distributed
 (gloo) carries only the barrier and the max-over-ranks of the elapsed time.
+Each rank is one independent encoder, as the reference's one hl_codec_t per
+stream (hl_codec.c:22-61).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...
+
+Without torchrun (WORLD_SIZE unset) and N > 1, this process only launches N
+rank processes (one per GPU, LOCAL_RANK = device) and returns their exit
+status; it never touches the GPU itself.  Under torchrun, --gpus must equal
+WORLD_SIZE.
 """
 import argparse
 import json
@@ -416,9 +423,86 @@ def run_svc(args):
         tdist.destroy_process_group()
 
 
+def spawn_ranks(n, argv, script=None):
+    """Runs this script as n rank processes (RANK = LOCAL_RANK = r,
+    WORLD_SIZE = LOCAL_WORLD_SIZE = n, a free rendezvous port on 127.0.0.1)
+    and returns the first non-zero exit status, else 0.  The caller has not
+    touched the GPU and does not afterwards: it only launches and waits.
+    Ranks inherit stdout/stderr (rank 0 prints the line).  When one rank
+    fails the others are terminated: they would wait forever at the next
+    collective."""
+    import signal
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HL_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    live = list(procs)
+    try:
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c and not rc:
+                    rc = c if c > 0 else 128 - c
+                    print(f"bench.py: rank {procs.index(p)} exited with status {c}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    for q in live:
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        for p in live:
+            p.send_signal(signal.SIGTERM)
+        raise
+    return rc
+
+
+def resolve_world(gpus):
+    """(world, launch): the number of ranks and whether this process must
+    launch them.  WORLD_SIZE set (torchrun, or spawn_ranks) fixes the world;
+    an explicit --gpus that disagrees with it is an error, not a silent
+    one-GPU run."""
+    env = os.environ.get("WORLD_SIZE")
+    if env is not None:
+        world = int(env)
+        if gpus is not None and gpus != world:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: launch {gpus} ranks "
+                             f"(torchrun --nproc-per-node {gpus}) or run without torchrun")
+        return world, False
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus {n}: need at least one GPU")
+    return n, n > 1
+
+
+def rank_devices(local):
+    """[(rank, device index, PCI bus id)] of every rank, gathered on every
+    rank (gloo), so the line shows which physical GPUs ran."""
+    import torch
+    import torch.distributed as tdist
+
+    p = torch.cuda.get_device_properties(local)
+    mine = {"rank": tdist.get_rank() if tdist.is_initialized() else 0, "device": local,
+            "pci_bus_id": f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:"
+                          f"{getattr(p, 'pci_device_id', 0):02x}"}
+    if not tdist.is_initialized():
+        return [mine]
+    allr = [None] * tdist.get_world_size()
+    tdist.all_gather_object(allr, mine)
+    return allr
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks, one per GPU (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=4 * GOP)  # four whole GOPs (IDR + 29 P pictures each), one pipelined launch
     ap.add_argument("--warmup", type=int, default=GOP)  # the first GOP (also warms the pipelined path)
     ap.add_argument("--cpu-frames", type=int, default=6)
@@ -426,6 +510,9 @@ def main():
     ap.add_argument("--streams", type=int, default=1, help="streams per process, in shared pipelined runs (hl_amd_encode_streams)")
     ap.add_argument("--svc", action="store_true", help="BASELINE config 4 (spatial SVC) instead of the headline workload")
     args = ap.parse_args()
+    world_req, launch = resolve_world(args.gpus)
+    if launch:  # before anything imports torch or touches a GPU
+        sys.exit(spawn_ranks(world_req, sys.argv[1:]))
     if args.svc:
         if "--steps" not in sys.argv:
             args.steps = 30
@@ -438,8 +525,12 @@ def main():
     from hartallo_amd import Encoder, dist, synth
 
     rank, world, local = dist.init_from_env()
+    if world != world_req:
+        raise SystemExit(f"bench.py: process group of {world} ranks, expected {world_req}")
     local %= max(1, torch.cuda.device_count())  # ranks beyond the visible GPUs share them (rehearsals on a one-GPU box)
     torch.cuda.set_device(local)
+    ranks = rank_devices(local)
+    pg_world = dist.world_size()
 
     n_frames = args.warmup + args.steps
     K = max(1, args.streams)  # streams this process encodes (one encoder each, shared pipelined runs)
@@ -563,6 +654,10 @@ def main():
                        "qp": QP, "me_range": ME_RANGE, "deblock": DEBLOCK, "gop": GOP, "parallelism": f"streams{world * K}",
                        "streams_per_gpu": share * K, "streams_per_process": K},
             "mb_per_s_per_gpu": round(fps / world * share * nmb, 1),
+            # which physical GPUs ran: the process group's size and every rank's device
+            "process_group_world_size": pg_world,
+            "ranks": ranks,
+            "distinct_gpus": len({r["pci_bus_id"] for r in ranks}),
             "warning": warning,
             "bitexact": bitexact_all if bitexact_all is None else bool(bitexact_all),
             "bitexact_check": "every frame of every rank (warm-up and timed) vs the reference encoder's per-frame MD5s "

@@ -21,6 +21,13 @@ def init_from_env():
     return rank, world, local
 
 
+def world_size() -> int:
+    """The process group's size (1 without a group)."""
+    import torch.distributed as dist
+
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
 def barrier():
     import torch.distributed as dist
 
