@@ -37,6 +37,7 @@ EXPORTED_SYMBOLS = (
     "hl_amd_encode_streams",
     "hl_amd_set_pipeline",
     "hl_amd_set_rate_control",
+    "hl_amd_set_max_ref_frame",
     "hl_amd_last_qp",
     "hl_amd_pipeline_occupancy",
     "hl_amd_bench_planes",
@@ -147,6 +148,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_set_pipeline.restype = i32
     lib.hl_amd_set_rate_control.argtypes = [vp, ctypes.c_int64, i32, i32, i32, i32, i32]
     lib.hl_amd_set_rate_control.restype = i32
+    lib.hl_amd_set_max_ref_frame.argtypes = [vp, i32]
+    lib.hl_amd_set_max_ref_frame.restype = i32
     lib.hl_amd_last_qp.argtypes = [vp]
     lib.hl_amd_last_qp.restype = i32
     lib.hl_amd_pipeline_occupancy.argtypes = []
@@ -322,6 +325,12 @@ class Encoder:
         rc = self.lib.hl_amd_set_rate_control(self._h, bitrate, fps_num, fps_den, basicunit, qp_min, qp_max)
         if rc != HL_AMD_SUCCESS:
             raise HlAmdError(rc, "hl_amd_set_rate_control")
+
+    def set_max_ref_frame(self, max_ref_frame: int):
+        """hl_codec_t.max_ref_frame: SPS/PPS fields only (hl_codec_264_sps.c:620-636); before the first frame."""
+        rc = self.lib.hl_amd_set_max_ref_frame(self._h, max_ref_frame)
+        if rc:
+            raise HlAmdError(rc, "hl_amd_set_max_ref_frame")
 
     def last_qp(self) -> int:
         """SliceQPY of the last encoded picture."""

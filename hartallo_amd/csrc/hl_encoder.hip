@@ -797,6 +797,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 
 #if !defined(HL_KERNELS_ONLY)  // (hl_encoder_fam3.hip compiles the kernels above again, with HL_FAM3=1)
 extern "C" hipError_t hl_fam3_launch_pipeline(const void* args, size_t psz, int mbw, int mbh, int workgroups, hipStream_t stream);
+extern "C" hipError_t hl_fam3_pipeline_occupancy(int* per_cu);
 static int diag_count(int mbw, int rows, int diag)
 {
     const int ylo = std::max(0, (diag - mbw + 2) / 2);
@@ -854,10 +855,11 @@ struct hl_amd_encoder_s {
     int32_t helper_kept = 0, helper_rejected = 0, helper_self = 0;  // hl_amd_last_helper_stats
     bool fam3 = true;                            // ... and 8x8-family helper tasks (HL_AMD_FAM3=0: off)
     int32_t fam3_kept = 0, fam3_rejected = 0;    // hl_amd_last_fam3_stats
-    Fam3Out* d_f3 = nullptr;                     // 8x8-family helper results [slot][MB]
+    Fam3Out* d_f3 = nullptr;                     // 8x8-family helper results [MB] (only runs of one picture use them)
     PipeFrame *d_pf, *h_pf;
     std::vector<std::vector<uint8_t>> bout;  // bitstreams of the last hl_amd_encode_batch
     int nwriters;                            // host slice writer threads of a run
+    int32_t max_ref_frame = 1;               // hl_codec_t.max_ref_frame: SPS/PPS fields only (hl_amd_set_max_ref_frame)
     std::vector<std::vector<uint8_t>> wscratch, wout;
     std::vector<int32_t> run_intra, run_idr_id;  // per picture of the run: IDR, idr_pic_id
     std::vector<int32_t> run_qp;                 // per picture of the run: SliceQPY (rate control: one picture per run)
@@ -883,6 +885,7 @@ struct hl_amd_encoder_s {
 
 static void svc_free(hl_amd_encoder_t* e);
 static hipError_t svc_drain_el(hl_amd_encoder_t* e);
+static bool svc_started(const hl_amd_encoder_t* e);
 
 static void free_all(hl_amd_encoder_t* e)
 {
@@ -1004,7 +1007,7 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
         const char* h = getenv("HL_AMD_PIPE_HOP");  // A/B knob of the pop order
         e->hop = h ? atoi(h) : 3 * (e->reach + 2) + 6;  // the staircase lag plus two MB rows (tools/gpu_hop.sh)
     }
-    const StreamParams sp{e->W, e->H, p->qp, p->deblock};
+    const StreamParams sp{e->W, e->H, p->qp, p->deblock, e->max_ref_frame};
     e->scratch.resize(slice_scratch_bytes(sp));
     e->out.resize(slice_scratch_bytes(sp) + 64);
     e->hdr.resize(256);
@@ -1287,7 +1290,7 @@ static hipError_t ensure_sched(hl_amd_encoder_t* e, int slots)
         (r = hipMalloc(&e->d_cnt, sizeof(int32_t) * 2 * nmb * slots)) || (r = hipMalloc(&e->d_done, sizeof(int32_t) * nmb * slots)) ||
         (r = hipMalloc(&e->d_queue, sizeof(int32_t) * (kSubQ + 2) * nmb * slots)) ||
         (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * kSubQ * slots + kMaxStreams + 2))) ||
-        (r = hipMalloc(&e->d_hstate, sizeof(int32_t) * 2 * nmb * slots)) || (r = hipMalloc(&e->d_f3, sizeof(Fam3Out) * nmb * slots)))
+        (r = hipMalloc(&e->d_hstate, sizeof(int32_t) * 2 * nmb * slots)) || (r = hipMalloc(&e->d_f3, sizeof(Fam3Out) * nmb)))
         return r;
     if (!e->d_err && (r = hipMalloc(&e->d_err, sizeof(int32_t) * 8))) return r;
     e->scap = slots;
@@ -1449,6 +1452,15 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
     }
     HL_HIP_CHECK(ensure_sched(e0, slots));
     for (int si = 0; si < S; ++si) HL_HIP_CHECK(hipStreamSynchronize(es[si]->stream));  // (h_pf may still be read by a previous copy)
+    struct RunLive {  // cleared on every way out of the run (an error return included),
+                      // built before any stream's run_live is set
+        hl_amd_encoder_t* const* es;
+        int S;
+        ~RunLive()
+        {
+            for (int si = 0; si < S; ++si) es[si]->run_live.store(0, std::memory_order_release);
+        }
+    } run_live_guard{es, S};
     for (int si = 0; si < S; ++si) {
         hl_amd_encoder_t* e = es[si];
         uint8_t** ref0 = e->d_pic[e->cur ^ 1];
@@ -1497,7 +1509,7 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
                 F.ispec = e->d_ispec;
                 F.hstate = e0->d_hstate + nmb * slot;
                 if (fam3) {
-                    F.f3 = e0->d_f3 + (size_t)nmb * slot;
+                    F.f3 = e0->d_f3;  // fam3 runs hold one picture (slot 0)
                     F.hstate3 = e0->d_hstate + (size_t)nmb * (slots + slot);
                 }
             }
@@ -1518,14 +1530,6 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
         __atomic_store_n(e->h_progress, 0, __ATOMIC_RELEASE);
         e->run_live.store(1, std::memory_order_release);
     }
-    struct RunLive {  // cleared on every way out of the run (an error return included)
-        hl_amd_encoder_t* const* es;
-        int S;
-        ~RunLive()
-        {
-            for (int si = 0; si < S; ++si) es[si]->run_live.store(0, std::memory_order_release);
-        }
-    } run_live_guard{es, S};
     HL_HIP_CHECK(hipMemcpyAsync(e0->d_pf, e0->h_pf, sizeof(PipeFrame) * slots, hipMemcpyHostToDevice, e0->stream));
     PipeArgs P;
     P.fr = e0->d_pf;
@@ -1557,7 +1561,11 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
         if (!h_clock) HL_HIP_CHECK(hipHostMalloc((void**)&h_clock, sizeof(unsigned long long) * 1024, hipHostMallocCoherent));
         HL_HIP_CHECK(hipHostGetDevicePointer((void**)&P.pub_clock, h_clock, 0));
     }
-    k_pipe_init<<<(unsigned)((nmb * slots + 255) / 256), 256, 0, e0->stream>>>(P, e0->mbw, e0->mbh);
+    // one thread per task, and at least one per sub-queue head / tail and
+    // stream word: pictures of fewer than kSubQ macroblocks have more heads
+    // than tasks
+    const size_t init_threads = std::max({nmb * slots, (size_t)kSubQ * slots, (size_t)kMaxStreams});
+    k_pipe_init<<<(unsigned)((init_threads + 255) / 256), 256, 0, e0->stream>>>(P, e0->mbw, e0->mbh);
     HL_HIP_CHECK(hipGetLastError());
     static const int env_wg = getenv("HL_AMD_PIPE_WG") ? atoi(getenv("HL_AMD_PIPE_WG")) : 0;  // experiments
     int wgs = e0->pipe_wg > 0 ? e0->pipe_wg : env_wg;
@@ -1565,7 +1573,8 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
         int dev = 0, cus = 0, occ = 0;
         HL_HIP_CHECK(hipGetDevice(&dev));
         HL_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        HL_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_pipeline, kMbThreads, 0));
+        if (fam3) HL_HIP_CHECK(hl_fam3_pipeline_occupancy(&occ));  // the build that is launched
+        else HL_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_pipeline, kMbThreads, 0));
         wgs = std::max(1, cus * occ);
     }
     if (e0->timing) HL_HIP_CHECK(hipEventRecord(e0->ev[4], e0->stream));
@@ -1620,6 +1629,33 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
     if (err) fprintf(stderr, "hartallo_amd: pipelined run: %d bounded waits gave up; re-encoding the run picture by picture\n", err);
     const bool force_fb = getenv("HL_AMD_FORCE_FALLBACK")  // (read per run: tests set it per case)
                            && atoi(getenv("HL_AMD_FORCE_FALLBACK")) > 0;
+    // which streams keep their run (else they are re-coded picture by
+    // picture below), and every kept stream's slices fit, before any stream
+    // commits: the streams of a group advance together or not at all
+    std::vector<char> keep(S);
+    std::vector<int32_t> carry_out(S);
+    for (int si = 0; si < S; ++si) {
+        int32_t carry = es[si]->chain_end;
+        bool ok = err == 0;
+        for (int k = 0; k < m && ok; ++k) ok = validate_rows(es[si]->h_bchain + nmb * k, es[si]->mbw, es[si]->mbh, 9, carry);
+        if (force_fb) ok = false;  // diagnostics: HL_AMD_FORCE_FALLBACK=1 takes the fallback below for every run (tests)
+        keep[si] = ok;
+        carry_out[si] = carry;
+        for (int k = 0; k < m && ok; ++k)
+            if (!wsize[si][k]) return HL_AMD_ERROR_TOOSHORT;
+    }
+    // a stream whose fallback fails after earlier streams committed leaves
+    // the group out of step: every encoder of the group is then unusable
+    struct GroupGuard {
+        hl_amd_encoder_t* const* es;
+        int S;
+        bool done = false;
+        ~GroupGuard()
+        {
+            if (!done && S > 1)
+                for (int si = 0; si < S; ++si) es[si]->broken = true;
+        }
+    } group_guard{es, S};
     for (int si = 0; si < S; ++si) {
         hl_amd_encoder_t* e = es[si];
         // the launch's counters (shared by its streams)
@@ -1638,11 +1674,8 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
             e->ms[1] = e0->ms[1];
             e->ms[3] = e0->ms[3];
         }
-        int32_t carry = e->chain_end;
-        bool ok = err == 0;
-        for (int k = 0; k < m && ok; ++k) ok = validate_rows(e->h_bchain + nmb * k, e->mbw, e->mbh, 9, carry);
-        if (force_fb) ok = false;  // diagnostics: HL_AMD_FORCE_FALLBACK=1 takes the fallback below for every run (tests)
-        if (!ok) {  // a speculated row start mattered (or a wait gave up): redo the stream's run picture by picture
+        const int32_t carry = carry_out[si];
+        if (!keep[si]) {  // a speculated row start mattered (or a wait gave up): redo the stream's run picture by picture
             e->run_fallback = true;
             ++e->calls_fallbacks;
             // an SVC batch's enhancement-layer thread may be coding from this
@@ -1684,7 +1717,6 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
             e->last_pic[base + k] = e->d_bpic + pic * k;
         }
         for (int k = 0; k < m; ++k) {
-            if (!wsize[si][k]) return HL_AMD_ERROR_TOOSHORT;
             hl_amd_result_t& o = res[si][k];
             o.type = HL_AMD_RESULT_TYPE_DATA;
             o.data = e->bout[base + k].data();
@@ -1718,6 +1750,7 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
         HL_HIP_CHECK(hipStreamSynchronize(e->stream));
         e->cur ^= 1;
     }
+    group_guard.done = true;
     return HL_AMD_SUCCESS;
 }
 
@@ -1831,6 +1864,18 @@ extern "C" int32_t hl_amd_encode_batch(hl_amd_encoder_t* e, int32_t n, const uin
     for (int i = 0; i < n; ++i)
         if (!y[i] || !u[i] || !v[i]) return HL_AMD_ERROR_INVALID_PARAMETER;
     return encode_pictures(e, n, y, u, v, results);
+}
+
+extern "C" int32_t hl_amd_set_max_ref_frame(hl_amd_encoder_t* e, int32_t max_ref_frame)
+{
+    if (!e || max_ref_frame < 0 || max_ref_frame > 16) return HL_AMD_ERROR_INVALID_PARAMETER;
+    // the reference reads it once, when it builds the first SPS (sps.c:620-636)
+    if (e->frame_index != 0 || svc_started(e)) return HL_AMD_ERROR_INVALID_STATE;
+    e->max_ref_frame = max_ref_frame;
+    const StreamParams sp{e->W, e->H, e->p.qp, e->p.deblock, e->max_ref_frame};
+    e->hdr.resize(256);
+    e->hdr.resize(write_stream_headers(sp, e->hdr.data(), e->hdr.size()));
+    return HL_AMD_SUCCESS;
 }
 
 extern "C" int32_t hl_amd_set_rate_control(hl_amd_encoder_t* e, int64_t bitrate, int32_t fps_num, int32_t fps_den,
@@ -2109,6 +2154,8 @@ struct SvcState {
     bool linked = true;
     int pipe_wg = 128;  // workgroups of a batch's base run: the rest of the device codes the enhancement layers
 };
+
+static bool svc_started(const hl_amd_encoder_t* e) { return e->svc && e->svc->started; }
 
 static void svc_free(hl_amd_encoder_t* e)
 {
@@ -2470,7 +2517,7 @@ extern "C" int32_t hl_amd_encode_layer(hl_amd_encoder_t* e, int32_t width, int32
         if (rc != HL_AMD_SUCCESS) return rc;
         if (l >= s->hdr_layers) {  // hl_codec_264.c:577-687: a new (subset) SPS and PPS
             s->hdr.resize(1024);
-            const StreamParams bp{s->w[0], s->h[0], e->p.qp, e->p.deblock};
+            const StreamParams bp{s->w[0], s->h[0], e->p.qp, e->p.deblock, e->max_ref_frame};
             s->hdr.resize(write_svc_headers(bp, s->w.data(), s->h.data(), l + 1, s->hdr.data(), s->hdr.size()));
             s->hdr_layers = l + 1;
             r->type |= HL_AMD_RESULT_TYPE_HDR;
@@ -2670,12 +2717,15 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
     // single-call state: the run geometry, the stream linking, the reference
     // layer pointers into this batch, and the order of the two streams.  A
     // batch that fails part-way has advanced the enhancement layers for
-    // access units whose base picture did not finish: the encoder is then
-    // marked unusable (INVALID_STATE from then on).
+    // access units whose base picture did not finish: only then is the
+    // encoder marked unusable (INVALID_STATE from then on); an error before
+    // any enhancement layer of an unfinished chunk was coded leaves it usable.
+    std::atomic<bool> el_ahead{false};  // enhancement layers coded for a chunk that has not completed
     struct Restore {
         hl_amd_encoder_t* e;
         SvcState* s;
         int saved_wg;
+        std::atomic<bool>& el_ahead;
         bool ok = false;
         ~Restore()
         {
@@ -2684,10 +2734,10 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
             s->ref0_st = nullptr;
             for (int c = 0; c < 3; ++c) s->ref0_pic[c] = nullptr;
             // what is queued on the encoder's stream next sees the enhancement layers
-            if (hipEventRecord(s->ev_join, s->est) != hipSuccess || hipStreamWaitEvent(e->stream, s->ev_join, 0) != hipSuccess) ok = false;
-            if (!ok) e->broken = true;
+            bool joined = hipEventRecord(s->ev_join, s->est) == hipSuccess && hipStreamWaitEvent(e->stream, s->ev_join, 0) == hipSuccess;
+            if (!joined || (!ok && el_ahead.load())) e->broken = true;
         }
-    } restore{e, s, e->pipe_wg};
+    } restore{e, s, e->pipe_wg, el_ahead};
     std::atomic<bool> base_done{false};
     constexpr int32_t kAborted = -1;  // the run fell back while the thread coded from it
     // the enhancement layers of access units [i0, i0 + m) (base pictures
@@ -2737,12 +2787,13 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
             s->ms_el = 0.f;
             std::vector<uint8_t>& hdr = s->elhdr[i];
             hdr.clear();
+            el_ahead.store(true);
             for (int l = 1; l < layers && r == HL_AMD_SUCCESS; ++l) {
                 const uint8_t* const* p = planes + ((size_t)l * n + i) * 3;
                 r = svc_encode_el(e, l, p[0], p[1], p[2]);
                 if (r == HL_AMD_SUCCESS && l >= s->hdr_layers) {  // hl_codec_264.c:577-687: a new (subset) SPS and PPS
                     std::vector<uint8_t> h(1024);
-                    const StreamParams bp0{s->w[0], s->h[0], e->p.qp, e->p.deblock};
+                    const StreamParams bp0{s->w[0], s->h[0], e->p.qp, e->p.deblock, e->max_ref_frame};
                     h.resize(write_svc_headers(bp0, s->w.data(), s->h.data(), l + 1, h.data(), h.size()));
                     hdr.insert(hdr.end(), h.begin(), h.end());
                     s->hdr_layers = l + 1;
@@ -2840,6 +2891,7 @@ extern "C" int32_t hl_amd_encode_layers_batch(hl_amd_encoder_t* e, int32_t n, in
             results[i].data = au.data();
             results[i].data_size = au.size();
         }
+        if (rc == HL_AMD_SUCCESS) el_ahead.store(false);  // this chunk's base and enhancement layers are consistent
     }
     restore.ok = rc == HL_AMD_SUCCESS;
     return rc;

@@ -45,3 +45,11 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t hl_fam3_launch_pipel
     hl_fam3::k_pipeline<<<workgroups, hl_fam3::hl::kMbThreads, 0, stream>>>(P, mbw, mbh);
     return hipGetLastError();
 }
+
+// Resident workgroups per CU of this build's k_pipeline (its register use
+// differs from the HL_FAM3=0 build's); the persistent launch must not hold
+// more workgroups than fit at once.
+extern "C" __attribute__((visibility("hidden"))) hipError_t hl_fam3_pipeline_occupancy(int* per_cu)
+{
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, hl_fam3::k_pipeline, hl_fam3::hl::kMbThreads, 0);
+}

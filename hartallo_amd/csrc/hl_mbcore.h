@@ -62,10 +62,11 @@ constexpr int kProfSlots = 20;  // prof[2 * slot], prof[2 * slot + 1] (< 40: the
 
 constexpr int kPad = 40;  // padding of the luma reference planes (origin clip is +-17, block 16, tap 3)
 constexpr int kMaxWaves = 8;   // waves of the macroblock workgroup
-// lanes of the macroblock workgroup: 512 is the only size whose output has
-// been checked against the reference.  A 256-lane build (two workgroups per
-// CU, 512 macroblocks in flight) measured only +4 % on the pipelined bench and
-// its 720p output differs from the oracle, so it is not pursued.
+// lanes of the macroblock workgroup.  512 (one workgroup per CU) is the
+// product.  The 256-lane build (two workgroups per CU) is bit-exact too
+// (every parity case, round 4), but gains only 4 % where the device is full
+// and loses 35 % of macroblock latency, which the ramp, the tail and lone
+// pictures pay (profiles/r04_ab_256_lanes_two_wg_per_cu.log).
 #ifndef HL_MB_THREADS
 #define HL_MB_THREADS 512
 #endif

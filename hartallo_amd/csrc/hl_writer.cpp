@@ -187,15 +187,21 @@ void write_block(BitWriter& bw, const T* coeffLevel, int endIdx, int maxNumCoef,
     }
 }
 
-int guess_level(int w, int h)  // utils.c:14-58
+// levels in the reference's guess order (utils.c:14-58); the position is
+// also the level's zero-based index into the Table A-1 arrays
+// (HL_CODEC_264_LEVEL_TO_ZERO_BASED_INDEX, tables.h:151: 10 -> 0, 9 -> 1, ...)
+const int kLevels[16][3] = {{10, 128, 96},   {9, 128, 96},    {11, 176, 144},  {12, 320, 240},  {13, 352, 288},  {20, 352, 288},
+                            {21, 352, 480},  {22, 352, 480},  {30, 720, 480},  {31, 1280, 720}, {32, 1280, 720}, {40, 2048, 1024},
+                            {41, 2048, 1024}, {42, 2048, 1080}, {50, 2560, 1920}, {51, 3840, 2160}};
+
+int guess_level_index(int w, int h)
 {
-    static const int L[16][3] = {{10, 128, 96},   {9, 128, 96},    {11, 176, 144},  {12, 320, 240},  {13, 352, 288},  {20, 352, 288},
-                                 {21, 352, 480},  {22, 352, 480},  {30, 720, 480},  {31, 1280, 720}, {32, 1280, 720}, {40, 2048, 1024},
-                                 {41, 2048, 1024}, {42, 2048, 1080}, {50, 2560, 1920}, {51, 3840, 2160}};
     for (int i = 0; i < 16; ++i)
-        if (L[i][1] >= w && L[i][2] >= h) return L[i][0];
-    return 51;
+        if (kLevels[i][1] >= w && kLevels[i][2] >= h) return i;
+    return 15;  // 51
 }
+
+int guess_level(int w, int h) { return kLevels[guess_level_index(w, h)][0]; }  // utils.c:14-58
 
 size_t put_nal(uint8_t* out, size_t cap, const uint8_t* rbsp, size_t n)
 {
@@ -209,6 +215,13 @@ size_t put_nal(uint8_t* out, size_t cap, const uint8_t* rbsp, size_t n)
 
 }  // namespace
 
+int sps_max_num_ref_frames(int width, int height, int max_ref_frame)
+{
+    static const int kMaxDpbMbs[16] = {396, 396, 900, 2376, 2376, 2376, 4752, 8100, 8100, 18000, 20480, 32768, 32768, 34816, 110400, 184320};
+    const int dpb = kMaxDpbMbs[guess_level_index(width, height)] / ((width / 16) * (height / 16));
+    return dpb < max_ref_frame ? dpb : max_ref_frame;
+}
+
 int level_code_bits(int suffix_length, int code)
 {
     const LevelCode& L = level_code(suffix_length, code);
@@ -219,6 +232,7 @@ size_t write_stream_headers(const StreamParams& p, uint8_t* out, size_t cap)
 {
     uint8_t buf[64];
     size_t n = 0;
+    const int nref = sps_max_num_ref_frames(p.width, p.height, p.max_ref_frame);
     {
         memset(buf, 0, sizeof(buf));
         BitWriter bw(buf, sizeof(buf));
@@ -237,7 +251,7 @@ size_t write_stream_headers(const StreamParams& p, uint8_t* out, size_t cap)
         bw.ue(0);  // seq_parameter_set_id
         bw.ue(4);  // log2_max_frame_num_minus4
         bw.ue(2);  // pic_order_cnt_type
-        bw.ue(1);  // max_num_ref_frames
+        bw.ue((uint32_t)nref);  // max_num_ref_frames (sps.c:620-636)
         bw.u1(0);
         bw.ue((uint32_t)(p.width / 16 - 1));
         bw.ue((uint32_t)(p.height / 16 - 1));
@@ -259,7 +273,7 @@ size_t write_stream_headers(const StreamParams& p, uint8_t* out, size_t cap)
         bw.u1(0);    // entropy_coding_mode_flag (CAVLC)
         bw.u1(0);
         bw.ue(0);    // num_slice_groups_minus1
-        bw.ue(0);
+        bw.ue((uint32_t)(nref > 0 ? nref - 1 : 0));  // num_ref_idx_l0_default_active_minus1 (pps.c:291)
         bw.ue(0);
         bw.u1(0);
         bw.u(0, 2);
@@ -410,7 +424,7 @@ namespace {
 
 // pps.c:265-400 as write_stream_headers writes it, for pic_parameter_set_id =
 // seq_parameter_set_id = id (hl_codec_264.c:607-617)
-size_t put_pps(int id, int qp, uint8_t* out, size_t cap)
+size_t put_pps(int id, int qp, int nref, uint8_t* out, size_t cap)
 {
     uint8_t buf[64];
     memset(buf, 0, sizeof(buf));
@@ -423,7 +437,7 @@ size_t put_pps(int id, int qp, uint8_t* out, size_t cap)
     bw.u1(0);
     bw.u1(0);
     bw.ue(0);
-    bw.ue(0);
+    bw.ue((uint32_t)(nref > 0 ? nref - 1 : 0));  // num_ref_idx_l0_default_active_minus1 of SPS id (pps.c:291)
     bw.ue(0);
     bw.u1(0);
     bw.u(0, 2);
@@ -440,7 +454,7 @@ size_t put_pps(int id, int qp, uint8_t* out, size_t cap)
 // subset_seq_parameter_set_rbsp of an enhancement layer (sps.c:535-860):
 // Scalable Baseline (83) with constraint_set0 only, the High-profile fields
 // profile 83 carries, and the SVC extension the encoder sets (sps.c:799-851)
-size_t put_subset_sps(int id, int w, int h, uint8_t* out, size_t cap)
+size_t put_subset_sps(int id, int w, int h, int nref, uint8_t* out, size_t cap)
 {
     uint8_t buf[64];
     memset(buf, 0, sizeof(buf));
@@ -460,7 +474,7 @@ size_t put_subset_sps(int id, int w, int h, uint8_t* out, size_t cap)
     bw.u1(0);       // seq_scaling_matrix_present_flag
     bw.ue(4);       // log2_max_frame_num_minus4
     bw.ue(2);       // pic_order_cnt_type
-    bw.ue(1);       // max_num_ref_frames
+    bw.ue((uint32_t)nref);  // max_num_ref_frames (sps.c:620-636)
     bw.u1(0);
     bw.ue((uint32_t)(w / 16 - 1));
     bw.ue((uint32_t)(h / 16 - 1));
@@ -507,7 +521,7 @@ size_t write_svc_headers(const StreamParams& base, const int32_t* widths, const 
 {
     // SPS 0 and PPS 0 are write_stream_headers' two NAL units
     uint8_t avc[256];
-    const StreamParams b0{widths[0], heights[0], base.qp, base.deblock};
+    const StreamParams b0{widths[0], heights[0], base.qp, base.deblock, base.max_ref_frame};
     const size_t na = write_stream_headers(b0, avc, sizeof(avc));
     size_t sps0 = 3;
     while (sps0 + 2 < na && !(avc[sps0] == 0 && avc[sps0 + 1] == 0 && avc[sps0 + 2] == 1)) ++sps0;
@@ -516,12 +530,13 @@ size_t write_svc_headers(const StreamParams& base, const int32_t* widths, const 
     memcpy(out, avc, sps0);
     k = sps0;
     for (int l = 1; l < n; ++l) {
-        const size_t m = put_subset_sps(l, widths[l], heights[l], out + k, cap - k);
+        const size_t m = put_subset_sps(l, widths[l], heights[l], sps_max_num_ref_frames(widths[l], heights[l], base.max_ref_frame),
+                                        out + k, cap - k);
         if (!m) return 0;
         k += m;
     }
     for (int l = 0; l < n; ++l) {
-        const size_t m = put_pps(l, base.qp, out + k, cap - k);
+        const size_t m = put_pps(l, base.qp, sps_max_num_ref_frames(widths[l], heights[l], base.max_ref_frame), out + k, cap - k);
         if (!m) return 0;
         k += m;
     }

@@ -15,7 +15,13 @@ namespace hl {
 
 struct StreamParams {
     int32_t width, height, qp, deblock;
+    int32_t max_ref_frame = 1;  // hl_codec_t.max_ref_frame (hl_codec.c:36 default 1): SPS/PPS only
 };
+
+// max_num_ref_frames the reference writes in a SPS of this picture size:
+// min(MaxDpbMbs / PicSizeInMbs, max_ref_frame) (sps.c:620-636, the level
+// from utils.c:14-58, MaxDpbMbs from tables.h:143-151)
+int sps_max_num_ref_frames(int width, int height, int max_ref_frame);
 
 class BitWriter {
 public:
@@ -40,6 +46,9 @@ private:
 };
 
 // Writes the 00 00 01-prefixed SPS and PPS NAL units; returns bytes written.
+// The PPS's num_ref_idx_l0_default_active_minus1 follows the SPS's
+// max_num_ref_frames (pps.c:291); P slices still override it to one active
+// reference (slice.c:289, encode.c:269).
 size_t write_stream_headers(const StreamParams& p, uint8_t* out, size_t cap);
 
 struct SliceState {

@@ -130,11 +130,12 @@ def hl_codec_encode(codec: hl_codec_t, frame: hl_frame_video_t, result: hl_codec
     if frame.width % 16 or frame.height % 16:
         return HL_ERROR_INVALID_FORMAT  # hl_codec_264.c:437-438
     if codec._enc is None or (codec.width, codec.height) != (frame.width, frame.height):
-        if codec.threads_count != 1 or codec.max_ref_frame != 1:
+        if codec.threads_count != 1:  # threads_count slices per picture (hl_codec_264.c:571): one slice here
             return HL_ERROR_NOT_IMPLEMENTED
         try:
             codec._enc = Encoder(frame.width, frame.height, codec.qp, codec.me_range, codec.deblock_flag, codec.gop_size,
                                  codec.me_early_term_flag, codec.device)
+            codec._enc.set_max_ref_frame(codec.max_ref_frame)  # SPS/PPS fields (hl_codec_264_sps.c:620-636)
             if codec.rc_bitrate > 0:  # hl_codec_264.c:719-742
                 codec._enc.set_rate_control(codec.rc_bitrate, codec.fps_num, codec.fps_den, codec.rc_basicunit, codec.rc_qp_min,
                                             codec.rc_qp_max)

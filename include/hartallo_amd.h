@@ -17,7 +17,9 @@
  * Semantics follow the reference:
  *   - parameters are the hl_codec_t fields the encoder reads
  *     (hl_codec.h:33-80): qp, gop_size, me_range, deblock_flag,
- *     me_early_term_flag; threads_count is 1 and max_ref_frame is 1;
+ *     me_early_term_flag; max_ref_frame through hl_amd_set_max_ref_frame;
+ *     threads_count is 1 (the reference cuts a picture into threads_count
+ *     slices, hl_codec_264.c:571; one slice per picture here);
  *   - width and height must be multiples of 16 (1088, not 1080 -- the
  *     reference rejects cropping, hl_codec_264.c:430-438);
  *   - result.type carries HL_CODEC_RESULT_TYPE_DATA / _HDR bits
@@ -113,7 +115,12 @@ int32_t hl_amd_encode_batch(hl_amd_encoder_t* encoder, int32_t n, const uint8_t*
  * each stream's results are those of hl_amd_encode_batch on its encoder
  * alone (the reference serves N streams as N hl_codec_t instances,
  * hl_codec.c:24-150).  The diagnostics of every encoder (stats, timing)
- * describe the shared launches.  No reference interface. */
+ * describe the shared launches, and encoder 0's pipeline settings
+ * (hl_amd_set_pipeline, hl_amd_set_intra_helpers, hl_amd_set_timing) govern
+ * them.  The streams advance together: an error before any stream commits
+ * leaves every encoder as it was; a stream whose picture-by-picture fallback
+ * fails after others committed leaves every encoder of the call unusable
+ * (HL_AMD_ERROR_INVALID_STATE from then on).  No reference interface. */
 int32_t hl_amd_encode_streams(hl_amd_encoder_t* const* encoders, int32_t count, int32_t n, const uint8_t* const* y,
                               const uint8_t* const* u, const uint8_t* const* v, hl_amd_result_t* results);
 
@@ -125,6 +132,16 @@ int32_t hl_amd_encode_streams(hl_amd_encoder_t* const* encoders, int32_t count, 
  * pictures' bits, so hl_amd_encode_batch codes the pictures one by one. */
 int32_t hl_amd_set_rate_control(hl_amd_encoder_t* encoder, int64_t bitrate, int32_t fps_num, int32_t fps_den,
                                 int32_t basicunit, int32_t qp_min, int32_t qp_max);
+
+/* hl_codec_t.max_ref_frame (hl_codec.c:36, default 1): the SPS's
+ * max_num_ref_frames = min(MaxDpbMbs / PicSizeInMbs, max_ref_frame)
+ * (hl_codec_264_sps.c:620-636) and the PPS's
+ * num_ref_idx_l0_default_active_minus1 (hl_codec_264_pps.c:291), for every
+ * (subset) SPS / PPS of the stream.  The reference's P slices override the
+ * active references to one (slice.c:289, encode.c:269), so only the headers
+ * change.  0..16; call before the first frame (the reference reads it when
+ * it builds the first SPS), else HL_AMD_ERROR_INVALID_STATE. */
+int32_t hl_amd_set_max_ref_frame(hl_amd_encoder_t* encoder, int32_t max_ref_frame);
 
 /* SliceQPY of the last encoded picture (the rate-controlled QP), or -1 */
 int32_t hl_amd_last_qp(hl_amd_encoder_t* encoder);

@@ -23,11 +23,17 @@
 
 extern const hl_codec_plugin_def_t* hl_codec_264_plugin_def_t; /* the stock plugin (hl_codec_264.c:1186) */
 
+/* what a codec object has been used for: the stock plugin refuses to switch
+ * between encoding and decoding (hl_codec_264.c:100-109, 447-457) */
+enum { GFX950_UNUSED = 0, GFX950_ENCODING, GFX950_DECODING };
+
 typedef struct hl_codec_264_gfx950_s {
     HL_DECLARE_CODEC; /* first member (hl_codec.h:171) */
     hl_amd_encoder_t* enc;
     hl_size_t width, height; /* the encoder's (base layer's) size */
     hl_size_t layers;        /* spatial layers the encoder was opened with (0: AVC) */
+    int input_type;          /* GFX950_* */
+    hl_codec_t* dec;         /* stock H.264 codec that decodes for this object (created on the first decode) */
 } hl_codec_264_gfx950_t;
 
 static hl_object_t* gfx950_ctor(hl_object_t* self, va_list* app)
@@ -43,6 +49,7 @@ static hl_object_t* gfx950_dtor(hl_object_t* self)
         hl_amd_encoder_destroy(p->enc);
         p->enc = NULL;
     }
+    if (p) HL_OBJECT_SAFE_FREE(p->dec);
     return self;
 }
 
@@ -69,6 +76,10 @@ static HL_ERROR_T gfx950_open(hl_codec_264_gfx950_t* self, hl_codec_t* base, hl_
     p.me_early_term = base->me_early_term_flag;
     p.device = 0; /* one process per GPU (HIP_VISIBLE_DEVICES) */
     if ((err = hl_amd_encoder_create(&p, &self->enc))) return (HL_ERROR_T)err; /* HL_ERROR_T values (hl_types.h:101-122) */
+    /* SPS max_num_ref_frames / PPS num_ref_idx_l0_default_active_minus1
+     * (hl_codec_264_sps.c:620-636, hl_codec_264_pps.c:291) */
+    if ((err = hl_amd_set_max_ref_frame(self->enc, base->max_ref_frame))) return (HL_ERROR_T)err;
+
     /* rate control: the hl_codec_t fields hl_codec_264.c:719-742 reads */
     if (base->rc_bitrate > 0 &&
         (err = hl_amd_set_rate_control(self->enc, base->rc_bitrate, base->fps.num, base->fps.den, base->rc_basicunit,
@@ -94,6 +105,17 @@ static HL_ERROR_T gfx950_encode(hl_codec_t* base, const hl_frame_t* frame, hl_co
     int32_t err;
     hl_size_t l, L;
     if (!self || !f || !result) return HL_ERROR_INVALID_PARAMETER;
+    if (self->input_type == GFX950_DECODING) return HL_ERROR_INVALID_OPERATION; /* hl_codec_264.c:447-452 */
+    if (base->threads_count > 1) {
+        /* the stock plugin cuts every picture into threads_count slices
+         * (hl_codec_264.c:571, encode.c:488-495); hl_codec_create defaults
+         * threads_count to the core count (hl_codec.c:33).  This plugin codes
+         * one slice per picture: refused rather than a different stream. */
+        fprintf(stderr, "hl_codec_264_gfx950: threads_count %d (%d slices per picture) is not implemented; set threads_count = 1\n",
+                (int)base->threads_count, (int)base->threads_count);
+        return HL_ERROR_NOT_IMPLEMENTED;
+    }
+    self->input_type = GFX950_ENCODING;
     L = base->layers_active_count;
     if (L > 1) {
         if (base->rc_bitrate > 0) {
@@ -141,13 +163,26 @@ static HL_ERROR_T gfx950_set_option(hl_codec_t* base, const struct hl_option_s* 
     return hl_codec_264_plugin_def_t->set_option(base, opt);
 }
 
+/* plugin decode(): decoding stays on the CPU, in the stock H.264 plugin
+ * (hl_codec_264.c:79-402).  install() takes the stock plugin out of the
+ * registry, so hl_codec_decode on a codec created after install lands here;
+ * it is forwarded to a stock codec this object owns, created on the first
+ * call with this object's settings.  Like the stock plugin, an object that
+ * has encoded does not decode (hl_codec_264.c:100-106). */
 static HL_ERROR_T gfx950_decode(hl_codec_t* base, const void* data, hl_size_t size, hl_codec_result_t* result)
 {
-    (void)base;
-    (void)data;
-    (void)size;
-    (void)result;
-    return HL_ERROR_NOT_IMPLEMENTED; /* non-NULL: hl_codec_encode checks plugin->decode (hl_codec.c:154) */
+    hl_codec_264_gfx950_t* self = (hl_codec_264_gfx950_t*)base;
+    HL_ERROR_T err;
+    if (!self) return HL_ERROR_INVALID_PARAMETER;
+    if (self->input_type == GFX950_ENCODING) return HL_ERROR_INVALID_OPERATION;
+    if (!self->dec) {
+        if ((err = hl_codec_create(hl_codec_264_plugin_def_t, &self->dec))) return err;
+        self->dec->threads_count = base->threads_count;
+        self->dec->dqid_min = base->dqid_min;
+        self->dec->dqid_max = base->dqid_max;
+    }
+    self->input_type = GFX950_DECODING;
+    return hl_codec_decode(self->dec, data, size, result);
 }
 
 const hl_codec_plugin_def_t hl_codec_264_gfx950_plugin_def_s = {

@@ -9,6 +9,13 @@
  * as test_encoder.c:220-236 writes it.
  *
  * usage: drop_in_enc W H N qp me_range deblock gop early_term in.yuv out.264
+ * decoding after install: drop_in_dec dec in.264 out.yuv
+ *   hl_codec_decode through the installed plugin (it forwards to a stock
+ *   codec it owns), driven like source/test_decoder.c:43-115 and
+ *   oracle/ref_decode.c; then one hl_codec_encode on the same object, which
+ *   the stock plugin refuses (hl_codec_264.c:447-452).  drop_in_dec is this
+ *   file linked with the reference library whose bit reader works
+ *   (oracle/Makefile, libhl_dec.a)
  *   early_term -1 keeps the hl_codec_create default (hl_types.h:67)
  * spatial SVC: drop_in_enc svc L W0 H0 N qp me_range deblock gop early_term out_prefix in0.yuv .. in{L-1}.yuv
  *   hl_codec_add_layer per layer (W0 << l, H0 << l), then per frame one
@@ -18,6 +25,7 @@
  */
 #include <hartallo/hl_api.h>
 #include <hartallo/hl_codec.h>
+#include <hartallo/hl_cpu.h>
 #include <hartallo/hl_debug.h>
 #include <hartallo/hl_frame.h>
 #include <hartallo/hl_object.h>
@@ -30,10 +38,12 @@ extern const hl_codec_plugin_def_t hl_codec_264_gfx950_plugin_def_s;
 HL_ERROR_T hl_codec_264_gfx950_install(void);
 
 static int run_svc(int argc, char** argv);
+static int run_dec(int argc, char** argv);
 
 int main(int argc, char** argv)
 {
     if (argc > 1 && !strcmp(argv[1], "svc")) return run_svc(argc - 1, argv + 1);
+    if (argc > 1 && !strcmp(argv[1], "dec")) return run_dec(argc - 1, argv + 1);
     if (argc < 11) {
         fprintf(stderr, "usage: %s W H N qp me_range deblock gop early_term in.yuv out.264\n", argv[0]);
         return 1;
@@ -56,6 +66,7 @@ int main(int argc, char** argv)
     hl_frame_video_create(&f);
     c->gop_size = gop; c->me_range = mer; c->qp = qp; c->fps.num = 1; c->fps.den = 15;
     c->rc_bitrate = -1; c->deblock_flag = db; c->threads_count = 1; c->max_ref_frame = 1;
+    if (getenv("HL_REF_MAX_REF_FRAME")) c->max_ref_frame = atoi(getenv("HL_REF_MAX_REF_FRAME")); /* SPS/PPS only */
     c->distortion_mesure_type = HL_VIDEO_DISTORTION_MESURE_TYPE_SAD;
     if (et >= 0) c->me_early_term_flag = et;
     /* rate control set on the hl_codec_t as a hartallo caller would */
@@ -126,6 +137,7 @@ static int run_svc(int argc, char** argv)
     hl_frame_video_create(&f);
     c->gop_size = gop; c->me_range = mer; c->qp = qp; c->fps.num = 1; c->fps.den = 15;
     c->rc_bitrate = -1; c->deblock_flag = db; c->threads_count = 1; c->max_ref_frame = 1;
+    if (getenv("HL_REF_MAX_REF_FRAME")) c->max_ref_frame = atoi(getenv("HL_REF_MAX_REF_FRAME")); /* SPS/PPS only */
     c->distortion_mesure_type = HL_VIDEO_DISTORTION_MESURE_TYPE_SAD;
     if (et >= 0) c->me_early_term_flag = et;
     for (int l = 0; l < L; ++l)
@@ -176,5 +188,69 @@ static int run_svc(int argc, char** argv)
     hl_object_unref(c);
     hl_object_unref(f);
     printf("{\"frames\": %d, \"layers\": %d}\n", n, L);
+    return 0;
+}
+
+/* argv: dec in.264 out.yuv; prints {"frames", "width", "height", "errors",
+ * "plugin_is_gfx950", "encode_after_decode"} */
+static int run_dec(int argc, char** argv)
+{
+    if (argc < 3) {
+        fprintf(stderr, "usage: drop_in_dec dec in.264 out.yuv\n");
+        return 1;
+    }
+    FILE* fi = fopen(argv[1], "rb");
+    FILE* fo = fopen(argv[2], "wb");
+    if (!fi || !fo) return 1;
+    fseek(fi, 0, SEEK_END);
+    const long n = ftell(fi);
+    fseek(fi, 0, SEEK_SET);
+    uint8_t* buf = (uint8_t*)calloc((size_t)n + 16, 1); /* the parser reads one byte past the last NAL */
+    if (!buf || fread(buf, 1, (size_t)n, fi) != (size_t)n) return 1;
+    fclose(fi);
+    hl_debug_set_level(HL_DEBUG_LEVEL_ERROR);
+    hl_engine_set_cpu_flags(kCpuFlagAll); /* as oracle/ref_decode.c */
+    if (hl_engine_init()) return 2;
+    if (hl_codec_264_gfx950_install()) return 3;
+    const struct hl_parser_plugin_def_s* ppl = 0;
+    struct hl_parser_s* parser = 0;
+    const struct hl_codec_plugin_def_s* cpl = 0;
+    struct hl_codec_s* codec = 0;
+    struct hl_codec_result_s* res = 0;
+    if (hl_parser_plugin_find(HL_CODEC_TYPE_H264_SVC, &ppl) || hl_parser_create(ppl, &parser) || hl_codec_result_create(&res) ||
+        hl_codec_plugin_find(HL_CODEC_TYPE_H264_SVC, &cpl) || hl_codec_create(cpl, &codec))
+        return 4;
+    codec->threads_count = 1;
+    int frames = 0, errors = 0, w = 0, h = 0;
+    hl_size_t start, end, count = (hl_size_t)n;
+    const uint8_t* p = buf;
+    while (count && hl_parser_find_bounds(parser, p, count, &start, &end) == HL_ERROR_SUCCESS) {
+        res->type = HL_CODEC_RESULT_TYPE_NONE;
+        if (hl_codec_decode(codec, &p[start], end - start + 1, res) != HL_ERROR_SUCCESS) ++errors;
+        if (res->type & HL_CODEC_RESULT_TYPE_DATA) {
+            fwrite(res->data_ptr, 1, res->data_size, fo);
+            w = (int)res->width;
+            h = (int)res->height;
+            ++frames;
+        }
+        p += end;
+        count -= end;
+    }
+    fclose(fo);
+    /* the object has decoded: encoding on it is refused, as by the stock plugin */
+    hl_frame_video_t* f = 0;
+    hl_frame_video_create(&f);
+    uint8_t* pic = (uint8_t*)calloc(16 * 16 * 3 / 2, 1);
+    hl_frame_video_fill(f, HL_VIDEO_CHROMA_YUV420, 16, 16, pic, 16 * 16 * 3 / 2);
+    const int enc_err = hl_codec_encode(codec, (hl_frame_t*)f, res);
+    printf("{\"frames\": %d, \"width\": %d, \"height\": %d, \"errors\": %d, \"plugin_is_gfx950\": %d, "
+           "\"encode_after_decode\": %d, \"invalid_operation\": %d}\n",
+           frames, w, h, errors, cpl == &hl_codec_264_gfx950_plugin_def_s, enc_err, (int)HL_ERROR_INVALID_OPERATION);
+    HL_OBJECT_SAFE_FREE(f);
+    HL_OBJECT_SAFE_FREE(parser);
+    HL_OBJECT_SAFE_FREE(codec);
+    HL_OBJECT_SAFE_FREE(res);
+    free(pic);
+    free(buf);
     return 0;
 }

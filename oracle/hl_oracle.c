@@ -272,6 +272,7 @@ struct hlo_enc_s {
     uint8_t* ref[3];   /* RefPicList0[0]                                      */
     const uint8_t* src[3];
     int32_t frame_index, gop_left, pict_count, idr_pic_id;
+    int32_t max_ref_frame; /* hl_codec_t.max_ref_frame (hl_codec.c:36, default 1) */
     int32_t is_intra_slice, qp;
     double lambda_mode, last_best_intra_cost;
     int32_t rdo_single_ctr; /* pc_esd->rdo.Single_ctr (persists, residual.c:883) */
@@ -2209,8 +2210,24 @@ static int guess_level(int w, int h) /* utils.c:14-58 */
     return 51;
 }
 
+/* max_num_ref_frames = min(MaxDpbMbs[level] / PicSizeInMbs, max_ref_frame),
+ * sps.c:620-636; MaxDpbMbs is Table A-1 (tables.h:143) indexed as
+ * HL_CODEC_264_LEVEL_TO_ZERO_BASED_INDEX (tables.h:151) maps level_idc */
+static int max_num_ref_frames(const hlo_enc_t* e)
+{
+    static const int lv[16] = {10, 9, 11, 12, 13, 20, 21, 22, 30, 31, 32, 40, 41, 42, 50, 51};
+    static const int dpb[16] = {396, 396, 900, 2376, 2376, 2376, 4752, 8100, 8100, 18000, 20480, 32768, 32768, 34816, 110400, 184320};
+    const int level = guess_level(e->W, e->H);
+    int i, n;
+    for (i = 0; i < 15 && lv[i] != level; ++i) {
+    }
+    n = dpb[i] / (e->mbw * e->mbh);
+    return n < e->max_ref_frame ? n : e->max_ref_frame;
+}
+
 static size_t write_headers(const hlo_enc_t* e, uint8_t* out)
 {
+    const int nref = max_num_ref_frames(e);
     uint8_t buf[256];
     bw_t bw;
     size_t n = 0;
@@ -2232,7 +2249,7 @@ static size_t write_headers(const hlo_enc_t* e, uint8_t* out)
     bw_ue(&bw, 0);
     bw_ue(&bw, 4); /* log2_max_frame_num_minus4 */
     bw_ue(&bw, 2); /* pic_order_cnt_type */
-    bw_ue(&bw, 1); /* max_num_ref_frames = min(MaxDpbMbs/PicSizeInMbs, max_ref_frame=1) */
+    bw_ue(&bw, (uint32_t)nref); /* max_num_ref_frames (sps.c:620-636) */
     bw_u1(&bw, 0);
     bw_ue(&bw, (uint32_t)(e->mbw - 1));
     bw_ue(&bw, (uint32_t)(e->mbh - 1));
@@ -2257,7 +2274,7 @@ static size_t write_headers(const hlo_enc_t* e, uint8_t* out)
     bw_u1(&bw, 0);
     bw_u1(&bw, 0);
     bw_ue(&bw, 0); /* num_slice_groups_minus1 */
-    bw_ue(&bw, 0);
+    bw_ue(&bw, (uint32_t)(nref > 0 ? nref - 1 : 0)); /* num_ref_idx_l0_default_active_minus1, pps.c:291 */
     bw_ue(&bw, 0);
     bw_u1(&bw, 0);
     bw_u(&bw, 0, 2);
@@ -2339,6 +2356,7 @@ hlo_enc_t* hlo_create(const hlo_params_t* p)
     init_level_table();
     e = (hlo_enc_t*)calloc(1, sizeof(*e));
     e->p = *p;
+    e->max_ref_frame = 1;
     e->W = p->width;
     e->H = p->height;
     e->Wc = e->W / 2;
@@ -2491,4 +2509,12 @@ void hlo_dump_mbs(const hlo_enc_t* e, int32_t* recs)
             }
         r[MBR_ETYPE] = m->e_type;
     }
+}
+
+/* hl_codec_t.max_ref_frame, before the first frame (only the SPS / PPS read it) */
+int hlo_set_max_ref_frame(hlo_enc_t* e, int max_ref_frame)
+{
+    if (!e || max_ref_frame < 0 || max_ref_frame > 16 || e->frame_index) return -1;
+    e->max_ref_frame = max_ref_frame;
+    return 0;
 }

@@ -37,6 +37,11 @@ typedef struct hlo_enc_s hlo_enc_t;
 hlo_enc_t* hlo_create(const hlo_params_t* params);
 void hlo_destroy(hlo_enc_t* enc);
 
+/* hl_codec_t.max_ref_frame (default 1), before the first frame: the SPS's
+ * max_num_ref_frames and the PPS's num_ref_idx_l0_default_active_minus1
+ * (sps.c:620-636, pps.c:291).  0 on success. */
+int hlo_set_max_ref_frame(hlo_enc_t* enc, int max_ref_frame);
+
 /* Encodes one planar YUV420 frame.  Writes into out exactly the bytes the
  * reference harness writes for that frame: the SPS/PPS header bytes on the
  * first frame, then 00 00 01 + the (escaped) slice NAL.  Returns 0 on

@@ -59,6 +59,7 @@ int main(int argc, char** argv)
     hl_frame_video_create(&f);
     c->gop_size = gop; c->me_range = mer; c->qp = qp; c->fps.num = 1; c->fps.den = 15;
     c->rc_bitrate = -1; c->deblock_flag = db; c->threads_count = 1; c->max_ref_frame = 1;
+    if (getenv("HL_REF_MAX_REF_FRAME")) c->max_ref_frame = atoi(getenv("HL_REF_MAX_REF_FRAME")); /* SPS/PPS only */
     c->distortion_mesure_type = HL_VIDEO_DISTORTION_MESURE_TYPE_SAD;
     c->me_type = (HL_VIDEO_ME_TYPE_INTEGER | HL_VIDEO_ME_TYPE_HALF | HL_VIDEO_ME_TYPE_QUATER);
     c->me_part_types = HL_VIDEO_ME_PART_TYPE_ALL;

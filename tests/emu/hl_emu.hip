@@ -30,6 +30,7 @@ int hl::g_emu_bad_guess3 = 0;  // fam3_helper: HL_EMU_HELPER bit 8
 struct EmuEnc {
     int W, H, Wc, Hc, mbw, mbh, nmb, qp, qpc, me_range, deblock, gop, early_term;
     int pstride;
+    int max_ref_frame = 1;
     std::vector<uint8_t> pic[2][3];
     std::vector<uint8_t> pl[4];
     std::vector<MbState> st;
@@ -240,6 +241,18 @@ extern "C" void* emu_create(int W, int H, int qp, int me_range, int deblock, int
     e->S2 = (Shared*)calloc(1, sizeof(Shared));
     e->helper_mode = getenv("HL_EMU_HELPER") ? atoi(getenv("HL_EMU_HELPER")) : 0;
     return e;
+}
+
+// hl_codec_t.max_ref_frame before the first frame: the SPS / PPS fields only
+// (hl_amd_set_max_ref_frame)
+extern "C" int emu_set_max_ref_frame(void* h, int max_ref_frame)
+{
+    EmuEnc* e = (EmuEnc*)h;
+    e->max_ref_frame = max_ref_frame;
+    const StreamParams sp{e->W, e->H, e->qp, e->deblock, max_ref_frame};
+    e->hdr.resize(256);
+    e->hdr.resize(write_stream_headers(sp, e->hdr.data(), e->hdr.size()));
+    return 0;
 }
 
 extern "C" void emu_destroy(void* h)
@@ -584,6 +597,7 @@ extern "C" void emu_svc_destroy(void* h)
 }
 
 extern "C" int emu_svc_unpinned(void* h) { return ((EmuSvc*)h)->unpinned; }
+extern "C" int emu_svc_set_max_ref_frame(void* h, int max_ref_frame) { return emu_set_max_ref_frame(((EmuSvc*)h)->base, max_ref_frame); }
 
 extern "C" long emu_svc_encode(void* h, int layer, const uint8_t* y, const uint8_t* u, const uint8_t* v, uint8_t* out, long cap)
 {
@@ -626,7 +640,7 @@ extern "C" long emu_svc_encode(void* h, int layer, const uint8_t* y, const uint8
     const bool intra = s->au_intra != 0;
     if (layer == s->first) s->au.clear();
     if (layer >= s->hdr_layers) {
-        const StreamParams bp{s->ws[0], s->hs[0], s->qp, s->deblock};
+        const StreamParams bp{s->ws[0], s->hs[0], s->qp, s->deblock, s->base->max_ref_frame};
         n = write_svc_headers(bp, s->ws.data(), s->hs.data(), layer + 1, out, (size_t)cap);
         s->hdr_layers = layer + 1;
         s->last_hdr = (long)n;

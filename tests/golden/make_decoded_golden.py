@@ -71,8 +71,10 @@ def main():
             sys.exit(f"{tool} missing: run `make -C oracle ref` where /root/reference exists")
     gpath, bpath = os.path.join(HERE, "golden.json"), os.path.join(HERE, "bench_golden.json")
     gold, bgold = json.load(open(gpath)), json.load(open(bpath))
+    only = set(sys.argv[1:])  # names: only those entries are (re)made
     with ThreadPoolExecutor(max_workers=8) as ex:
-        jobs = [ex.submit(small, k, v) for k, v in gold.items()] + [ex.submit(bench, k, bgold[k]) for k in DECODED_FRAMES]
+        jobs = ([ex.submit(small, k, v) for k, v in gold.items() if not only or k in only] +
+                [ex.submit(bench, k, bgold[k]) for k in DECODED_FRAMES if not only or k in only])
         for j in jobs:
             name, md5s, why = j.result()
             table = gold if name in gold else bgold

@@ -1,7 +1,8 @@
 """Regenerates tests/golden/ from the reference encoder itself.
 
 Each configuration in tests/hl_testlib.GOLDEN_CONFIGS (and GOLDEN_ET_CONFIGS,
-encoded with me_early_term_flag = 1) is synthesised with
+encoded with me_early_term_flag = 1, GOLDEN_RC_CONFIGS with rate control,
+GOLDEN_MRF_CONFIGS with hl_codec_t.max_ref_frame > 1) is synthesised with
 hartallo_amd.synth (seeded), encoded by oracle/_ref/ref_enc (the reference's
 own C sources compiled by oracle/Makefile, driven through hl_codec_encode as
 source/test_encoder.c does), and stored as:
@@ -9,7 +10,9 @@ source/test_encoder.c does), and stored as:
   golden.json       per-config parameters, stream MD5 and per-frame MD5 of
                     the reference's reconstructed (deblocked) pictures
 
-Run in the build container (needs /root/reference):  python tests/golden/make_golden.py
+Run in the build container (needs /root/reference):  python tests/golden/make_golden.py [name ...]
+With names, only those entries are (re)made and the rest of golden.json --
+including make_decoded_golden.py's decoded_md5 fields -- is kept.
 """
 import json
 import os
@@ -22,20 +25,26 @@ sys.path.insert(0, os.path.dirname(HERE))
 
 import numpy as np  # noqa: E402
 
-from hl_testlib import GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, GOLDEN_RC_CONFIGS, REF_ENC, golden_input, md5, slice_qps  # noqa: E402
+from hl_testlib import GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, GOLDEN_MRF_CONFIGS, GOLDEN_RC_CONFIGS, REF_ENC, golden_input, md5, slice_qps  # noqa: E402
 
 
 def main():
     if not os.path.exists(REF_ENC):
         sys.exit(f"{REF_ENC} missing: run `make -C oracle ref` where /root/reference exists")
-    table = {}
+    only = set(sys.argv[1:])
+    gpath = os.path.join(HERE, "golden.json")
+    table = json.load(open(gpath)) if only else {}
     with tempfile.TemporaryDirectory() as td:
-        for cfg in GOLDEN_CONFIGS + GOLDEN_ET_CONFIGS + GOLDEN_RC_CONFIGS:
+        for cfg in GOLDEN_CONFIGS + GOLDEN_ET_CONFIGS + GOLDEN_RC_CONFIGS + GOLDEN_MRF_CONFIGS:
             name, w, h, n, qp, mer, db, gop, seed = cfg[:9]
+            if only and name not in only:
+                continue
             et = 1 if cfg in GOLDEN_ET_CONFIGS else 0
             env = dict(os.environ)
-            for k in ("HL_REF_RC_BITRATE", "HL_REF_RC_BASICUNIT", "HL_REF_RC_QP_MIN", "HL_REF_RC_QP_MAX"):
+            for k in ("HL_REF_RC_BITRATE", "HL_REF_RC_BASICUNIT", "HL_REF_RC_QP_MIN", "HL_REF_RC_QP_MAX", "HL_REF_MAX_REF_FRAME"):
                 env.pop(k, None)
+            if cfg in GOLDEN_MRF_CONFIGS:  # hl_codec_t.max_ref_frame (ref_harness.c)
+                env["HL_REF_MAX_REF_FRAME"] = str(cfg[9])
             if cfg in GOLDEN_RC_CONFIGS:  # rate control: bitrate, basic unit, QP range (ref_harness.c)
                 env.update(HL_REF_RC_BITRATE=str(cfg[9]), HL_REF_RC_BASICUNIT=str(cfg[10]), HL_REF_RC_QP_MIN=str(cfg[11]),
                            HL_REF_RC_QP_MAX=str(cfg[12]))
@@ -54,11 +63,12 @@ def main():
                 "early_term": et,
                 **({"rc_bitrate": cfg[9], "rc_basicunit": cfg[10], "rc_qp_min": cfg[11], "rc_qp_max": cfg[12],
                     "fps_num": 1, "fps_den": 15} if cfg in GOLDEN_RC_CONFIGS else {}),
+                **({"max_ref_frame": cfg[9]} if cfg in GOLDEN_MRF_CONFIGS else {}),
                 "stream_md5": md5(stream), "stream_bytes": len(stream), "slice_qp": slice_qps(stream, qp),
                 "recon_md5": [md5(r) for r in rec],
             }
             print(f"{name}: {len(stream)} bytes")
-    with open(os.path.join(HERE, "golden.json"), "w") as f:
+    with open(gpath, "w") as f:
         json.dump(table, f, indent=1, sort_keys=True)
 
 

@@ -45,6 +45,7 @@ def oracle_lib():
         lib.hlo_recon.restype = ctypes.c_void_p
         lib.hlo_rdo_overflows.argtypes = [ctypes.c_void_p]
         lib.hlo_rdo_overflows.restype = ctypes.c_int64
+        lib.hlo_set_max_ref_frame.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _oracle = lib
     return _oracle
 
@@ -62,6 +63,7 @@ def emu_lib():
         lib.emu_recon.argtypes = [ctypes.c_void_p, ctypes.c_int]
         lib.emu_set_rc.argtypes = [ctypes.c_void_p, ctypes.c_longlong] + [ctypes.c_int] * 5
         lib.emu_last_qp.argtypes = [ctypes.c_void_p]
+        lib.emu_set_max_ref_frame.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _emu = lib
     return _emu
 
@@ -82,13 +84,15 @@ def _recon(ptr_fn, w: int, h: int) -> np.ndarray:
 class OracleEncoder:
     """CPU restatement of the reference encoder (oracle/hl_oracle.c)."""
 
-    def __init__(self, w, h, qp=28, me_range=16, deblock=1, gop=30, early_term=0):
+    def __init__(self, w, h, qp=28, me_range=16, deblock=1, gop=30, early_term=0, max_ref_frame=1):
         self.lib = oracle_lib()
         self.w, self.h = w, h
         p = _OParams(w, h, qp, me_range, deblock, gop, early_term)
         self.h_ = self.lib.hlo_create(ctypes.byref(p))
         if not self.h_:
             raise ValueError("oracle rejected parameters")
+        if max_ref_frame != 1:
+            assert self.lib.hlo_set_max_ref_frame(ctypes.c_void_p(self.h_), max_ref_frame) == 0
         self.out = np.zeros(w * h * 4 + (1 << 20), np.uint8)
 
     def encode(self, frame: np.ndarray) -> bytes:
@@ -113,10 +117,12 @@ class OracleEncoder:
 class EmuEncoder:
     """Host build of the gfx950 kernel logic (tests/emu/hl_emu.hip)."""
 
-    def __init__(self, w, h, qp=28, me_range=16, deblock=1, gop=30, early_term=0):
+    def __init__(self, w, h, qp=28, me_range=16, deblock=1, gop=30, early_term=0, max_ref_frame=1):
         self.lib = emu_lib()
         self.w, self.h = w, h
         self.h_ = self.lib.emu_create(w, h, qp, me_range, deblock, gop, early_term)
+        if max_ref_frame != 1:
+            self.lib.emu_set_max_ref_frame(ctypes.c_void_p(self.h_), max_ref_frame)
         self.out = np.zeros(w * h * 4 + (1 << 20), np.uint8)
 
     def set_rate_control(self, bitrate, fps_num=1, fps_den=15, basicunit=-1, qp_min=-1, qp_max=-1):
@@ -213,10 +219,12 @@ class EmuSvcEncoder:
 class GpuEncoder:
     """The product (libhartallo_amd.so) with the same encode() shape."""
 
-    def __init__(self, w, h, qp=28, me_range=16, deblock=1, gop=30, early_term=0):
+    def __init__(self, w, h, qp=28, me_range=16, deblock=1, gop=30, early_term=0, max_ref_frame=1):
         from hartallo_amd import Encoder
 
         self.enc = Encoder(w, h, qp, me_range, deblock, gop, early_term)
+        if max_ref_frame != 1:
+            self.enc.set_max_ref_frame(max_ref_frame)
         self.w, self.h = w, h
 
     def encode(self, frame: np.ndarray) -> bytes:
@@ -350,6 +358,21 @@ GOLDEN_RC_CONFIGS = [
     ("rc_cif_200k_gop4_nodb", 352, 288, 9, 28, 8, 0, 4, 54, 200000, -1, -1, -1),
     ("rc_qcif_1m5_gop6", 176, 144, 13, 28, 16, 1, 6, 55, 1500000, -1, -1, -1),
     ("rc_qcif_60k_qp20_36", 176, 144, 12, 28, 8, 1, 5, 56, 60000, -1, 20, 36),
+]
+
+
+# max_ref_frame goldens (hl_codec_t.max_ref_frame > 1, the SPS's
+# max_num_ref_frames = min(MaxDpbMbs / PicSizeInMbs, max_ref_frame) and the
+# PPS's num_ref_idx_l0_default_active_minus1, hl_codec_264_sps.c:620-636,
+# hl_codec_264_pps.c:291): (name, W, H, frames, qp, me_range, deblock, gop,
+# seed, max_ref_frame).  CIF allows 6 reference frames at its level 1.3
+# (2376 / 396), so 8 is clipped; 720p allows 5 (18000 / 3600).
+GOLDEN_MRF_CONFIGS = [
+    ("mrf2_cif_qp28_gop3", 352, 288, 5, 28, 8, 1, 3, 61, 2),
+    ("mrf4_cif_qp31_nodb", 352, 288, 4, 31, 8, 0, 30, 62, 4),
+    ("mrf8_cif_qp26", 352, 288, 3, 26, 16, 1, 400, 63, 8),
+    ("mrf2_720p_qp28", 1280, 720, 3, 28, 16, 1, 30, 64, 2),
+    ("mrf4_720p_qp32", 1280, 720, 3, 32, 16, 1, 30, 65, 4),
 ]
 
 

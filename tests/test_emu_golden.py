@@ -9,7 +9,7 @@ import os
 
 import pytest
 
-from hl_testlib import (EMU_LIB, GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, GOLDEN_RC_CONFIGS, EmuEncoder, OracleEncoder, first_diff,
+from hl_testlib import (EMU_LIB, GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, GOLDEN_MRF_CONFIGS, GOLDEN_RC_CONFIGS, EmuEncoder, OracleEncoder, first_diff,
                         golden_input, md5)
 from hartallo_amd import synth
 
@@ -25,6 +25,21 @@ def test_kernel_logic_matches_reference(cfg):
     clip = golden_input(cfg)
     ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()
     enc = EmuEncoder(w, h, qp, mer, db, gop, GOLD[name].get("early_term", 0))
+    out = b""
+    for f in range(n):
+        out += enc.encode(clip[f])
+        assert md5(enc.recon()) == GOLD[name]["recon_md5"][f], f"{name}: recon of frame {f}"
+    assert out == ref, f"{name}: first differing byte {first_diff(out, ref)}"
+
+
+@pytest.mark.parametrize("cfg", GOLDEN_MRF_CONFIGS, ids=[c[0] for c in GOLDEN_MRF_CONFIGS])
+def test_max_ref_frame_matches_reference(cfg):
+    """hl_codec_t.max_ref_frame > 1 through the product's writer
+    (sps_max_num_ref_frames, hl_writer.cpp)."""
+    name, w, h, n, qp, mer, db, gop, seed, mrf = cfg
+    clip = golden_input(cfg)
+    ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()
+    enc = EmuEncoder(w, h, qp, mer, db, gop, 0, mrf)
     out = b""
     for f in range(n):
         out += enc.encode(clip[f])

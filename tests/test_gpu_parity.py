@@ -16,7 +16,7 @@ import os
 import numpy as np
 import pytest
 
-from hl_testlib import GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, GOLDEN_RC_CONFIGS, GpuEncoder, OracleEncoder, first_diff, golden_input, md5
+from hl_testlib import GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, GOLDEN_MRF_CONFIGS, GOLDEN_RC_CONFIGS, GpuEncoder, OracleEncoder, first_diff, golden_input, md5
 
 pytestmark = pytest.mark.gpu
 
@@ -37,6 +37,35 @@ def test_golden_streams(gpu, cfg):
         out += enc.encode(clip[f])
         assert md5(enc.recon()) == GOLD[name]["recon_md5"][f], f"{name}: recon of frame {f} differs"
     assert out == ref, f"{name}: first differing byte {first_diff(out, ref)}"
+
+
+@pytest.mark.parametrize("cfg", GOLDEN_MRF_CONFIGS, ids=[c[0] for c in GOLDEN_MRF_CONFIGS])
+def test_max_ref_frame_golden_streams(gpu, cfg):
+    """hl_codec_t.max_ref_frame > 1 (hl_amd_set_max_ref_frame): per call and
+    as one batch (the pipelined runs), both equal to the reference's stream."""
+    import torch
+
+    from hartallo_amd import Encoder
+
+    name, w, h, n, qp, mer, db, gop, seed, mrf = cfg
+    clip = golden_input(cfg)
+    ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()
+    enc = GpuEncoder(w, h, qp, mer, db, gop, 0, mrf)
+    out = b""
+    for f in range(n):
+        out += enc.encode(clip[f])
+        assert md5(enc.recon()) == GOLD[name]["recon_md5"][f], f"{name}: recon of frame {f} differs"
+    assert out == ref, f"{name}: first differing byte {first_diff(out, ref)}"
+    dev = torch.from_numpy(np.ascontiguousarray(clip)).cuda()
+    torch.cuda.synchronize()
+    ptrs = [(dev[i].data_ptr(), dev[i].data_ptr() + w * h, dev[i].data_ptr() + w * h * 5 // 4) for i in range(n)]
+    b = Encoder(w, h, qp, mer, db, gop)
+    b.set_max_ref_frame(mrf)
+    got = b"".join(r.annexb() for r in b.encode_batch_device(ptrs))
+    with pytest.raises(Exception):
+        b.set_max_ref_frame(1)  # after the first frame: the headers are out (INVALID_STATE)
+    b.close()
+    assert got == ref, f"{name} (batch): first differing byte {first_diff(got, ref)}"
 
 
 @pytest.mark.parametrize("cfg", GOLDEN_RC_CONFIGS, ids=[c[0] for c in GOLDEN_RC_CONFIGS])

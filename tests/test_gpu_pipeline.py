@@ -86,6 +86,22 @@ def test_batch_golden_streams(gpu, cfg):
     assert md5(rec) == GOLD[name]["recon_md5"][n - 1]
 
 
+@pytest.mark.parametrize("w,h", [(16, 16), (32, 16), (48, 16)], ids=["16x16", "32x16", "48x16"])
+def test_batch_tiny_pictures_long_run(gpu, w, h):
+    """Pictures of fewer macroblocks than ready sub-queues in a run of more
+    than 64 pictures: every sub-queue head / tail of every picture slot is
+    initialised (k_pipe_init), and the 130 pictures (two runs: 128 + 2,
+    across GOPs of 40) equal the reference-pinned oracle's."""
+    n = 130
+    clip = synth.clip(w, h, n, 71 + w)
+    got, rec = _batch(w, h, 28, 8, 1, 40, clip)
+    o = OracleEncoder(w, h, 28, 8, 1, 40)
+    for f in range(n):
+        want = o.encode(clip[f])
+        assert got[f] == want, f"{w}x{h} picture {f}: first differing byte {first_diff(got[f], want)}"
+    assert np.array_equal(rec, o.recon())
+
+
 @pytest.mark.parametrize("geometry", [(240, 2, 4), (8, 0, 2), (5, 1, 3), (2, 0, 6), (16, 2, 1), (1, 0, 8), (3, 0, 64)], ids=lambda g: "x".join(map(str, g)))
 def test_batch_equals_single_calls(gpu, geometry):
     w, h, n = 320, 240, 9

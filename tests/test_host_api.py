@@ -26,8 +26,13 @@ def test_frame_fill_and_format_errors():
     f2 = hc.hl_frame_video_create()
     hc.hl_frame_video_fill(f2, 1920, 1080, np.zeros(1920 * 1080 * 3 // 2, np.uint8))
     assert hc.hl_codec_encode(c, f2, hc.hl_codec_result_create()) == hc.HL_ERROR_INVALID_FORMAT
-    c.threads_count = 2
+    c.threads_count = 2  # the reference codes threads_count slices per picture (hl_codec_264.c:571): refused
     assert hc.hl_codec_encode(c, f, hc.hl_codec_result_create()) == hc.HL_ERROR_NOT_IMPLEMENTED
+    import torch
+
+    if not torch.cuda.is_available():  # max_ref_frame is forwarded; without a GPU the encoder refuses loudly
+        c.threads_count, c.max_ref_frame = 1, 4
+        assert hc.hl_codec_encode(c, f, hc.hl_codec_result_create()) not in (hc.HL_ERROR_SUCCESS, hc.HL_ERROR_NOT_IMPLEMENTED)
 
 
 def test_synth_is_deterministic():

@@ -7,7 +7,7 @@ import os
 
 import pytest
 
-from hl_testlib import GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, OracleEncoder, first_diff, golden_input, md5
+from hl_testlib import GOLDEN, GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, GOLDEN_MRF_CONFIGS, OracleEncoder, first_diff, golden_input, md5
 
 GOLD = json.load(open(os.path.join(GOLDEN, "golden.json")))
 
@@ -28,6 +28,22 @@ def test_oracle_matches_reference(cfg):
         assert md5(enc.recon()) == GOLD[name]["recon_md5"][f], f"{name}: recon of frame {f}"
     assert out == ref, f"{name}: first differing byte {first_diff(out, ref)}"
     assert enc.rdo_overflows() == 0
+
+
+@pytest.mark.parametrize("cfg", GOLDEN_MRF_CONFIGS, ids=[c[0] for c in GOLDEN_MRF_CONFIGS])
+def test_oracle_max_ref_frame_matches_reference(cfg):
+    """hl_codec_t.max_ref_frame > 1: the SPS / PPS fields (sps.c:620-636,
+    pps.c:291) and nothing else change; CIF clips 8 to its level's 6."""
+    name, w, h, n, qp, mer, db, gop, seed, mrf = cfg
+    clip = golden_input(cfg)
+    ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()
+    assert md5(ref) == GOLD[name]["stream_md5"] and GOLD[name]["max_ref_frame"] == mrf
+    enc = OracleEncoder(w, h, qp, mer, db, gop, 0, mrf)
+    out = b""
+    for f in range(n):
+        out += enc.encode(clip[f])
+        assert md5(enc.recon()) == GOLD[name]["recon_md5"][f], f"{name}: recon of frame {f}"
+    assert out == ref, f"{name}: first differing byte {first_diff(out, ref)}"
 
 
 def test_oracle_rejects_unsupported():

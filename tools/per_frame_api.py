@@ -39,10 +39,14 @@ def main():
         frames_ok = frames_ok and hashlib.md5(stream[pos:pos + nb]).hexdigest() == md5
         pos += nb
     ms = info["encode_ms"]
-    p_ms = [m for i, m in enumerate(ms) if i % g["gop"] and i > 1]  # P pictures after the first (warm) one
+    p_all = [m for i, m in enumerate(ms) if i % g["gop"]]  # every P picture
+    p_warm = p_all[1:]  # without the first P picture (its call also allocates the run buffers)
     print(json.dumps({"name": name, "width": w, "height": h, "frames": n, "bitexact": frames_ok and pos == len(stream),
-                      "encode_ms": ms, "mean_p_ms": round(sum(p_ms) / max(1, len(p_ms)), 2),
-                      "p_fps": round(1e3 * len(p_ms) / max(1e-9, sum(p_ms)), 3),
+                      "encode_ms": ms,
+                      "mean_p_ms": round(sum(p_all) / max(1, len(p_all)), 2),
+                      "mean_p_ms_rule": "mean over every P picture of the call sequence, the first one included",
+                      "mean_p_ms_after_first": round(sum(p_warm) / max(1, len(p_warm)), 2),
+                      "p_fps": round(1e3 * len(p_all) / max(1e-9, sum(p_all)), 3),
                       "path": "hl_codec_encode (reference API) -> gfx950 plugin -> hl_amd_encode, one frame per call"}), flush=True)
 
 
