@@ -321,6 +321,11 @@ __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
 // steps; each later picture adds the lag of task_deps' staircase, about
 // 3 (R+2) steps (P.hop).  The oldest-first order lets the newest pictures'
 // wavefronts start late, and the run ends on their critical path.
+// 1: pop_task acquires as soon as it has observed the task's queue entry,
+// before its claim (0: after the pop)
+#ifndef HL_EARLY_ACQ
+#define HL_EARLY_ACQ 0
+#endif
 #if defined(HL_PROFILE)
 #define HL_POPSTAT(i) (++pst[i])
 #else
@@ -422,6 +427,11 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc
         if (i0 >= 0) {
             HL_POPSTAT(0);
             const int f = bfl, qf = bql;
+#if HL_EARLY_ACQ
+            // the entry that made the task ready is observed: acquire now, so
+            // that the L1 invalidate overlaps the claim's round trips
+            if (v > 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
+#endif
             int r = 0;
             if (lane == 0 && atomicCAS(P.head + qf, hh, hh + 1) == hh) {
                 r = v;
@@ -436,7 +446,12 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc
             }
             r = __builtin_amdgcn_readfirstlane(r);
             if (r < 0) return -1;
-            if (r > 0) return f * nmb + r - 1;
+            if (r > 0) {
+#if HL_EARLY_ACQ
+                if (v <= 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
+#endif
+                return f * nmb + r - 1;
+            }
             HL_POPSTAT(1);
             continue;  // another workgroup took it
         }
@@ -461,7 +476,12 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc
                 r = __builtin_amdgcn_readfirstlane(r);
                 kind = __builtin_amdgcn_readfirstlane(kind);
                 if (r < 0) return -1;
-                if (r > 0) return (1 + kind) * P.nframes * nmb + r - 1;  // intra helpers, then 8x8-family helpers
+                if (r > 0) {
+#if HL_EARLY_ACQ
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
+#endif
+                    return (1 + kind) * P.nframes * nmb + r - 1;  // intra helpers, then 8x8-family helpers
+                }
                 continue;
             }
         }
@@ -557,7 +577,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
                                                                                            , pst
 #endif
             );
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
+            if (!HL_EARLY_ACQ || in_order) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);  // (pop_task acquires itself)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
             if (threadIdx.x == 0) s_task = t;
         }
@@ -809,6 +829,11 @@ static int diag_count(int mbw, int rows, int diag)
 // encoder context
 // ---------------------------------------------------------------------------
 constexpr int kMaxRun = 128;  // pictures per pipelined launch and stream (bench.py MAX_RUN)
+#if defined(HL_PROFILE) && defined(HL_BAR_PROF) && HL_BAR_PROF >= 2
+constexpr int kProfExtra = 2 * kBarSites;  // per barrier site after the timeline (hl_mbcore.h)
+#else
+constexpr int kProfExtra = 0;
+#endif
 constexpr int kRowsAt = 16;   // h_progress word of picture 0's row count
 
 struct hl_amd_encoder_s {
@@ -979,8 +1004,8 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
     // 64 phase counters, the cycles of every macroblock of the last frame,
     // then the timeline of the first picture of the last pipelined run (per
     // MB: task start, decision end, in-picture successors released; wall clock)
-    ok = ok && hipMalloc(&e->d_prof, (64 + 4 * e->nmb) * sizeof(unsigned long long)) == hipSuccess &&
-         hipMemsetAsync(e->d_prof, 0, (64 + 4 * e->nmb) * sizeof(unsigned long long), e->stream) == hipSuccess;
+    ok = ok && hipMalloc(&e->d_prof, (64 + 4 * e->nmb + kProfExtra) * sizeof(unsigned long long)) == hipSuccess &&
+         hipMemsetAsync(e->d_prof, 0, (64 + 4 * e->nmb + kProfExtra) * sizeof(unsigned long long), e->stream) == hipSuccess;
 #endif
     ok = ok && hipStreamSynchronize(e->stream) == hipSuccess;
     for (int i = 0; i < 6 && ok; ++i) ok = hipEventCreate(&e->ev[i]) == hipSuccess;
@@ -1991,11 +2016,12 @@ extern "C" int32_t hl_amd_last_mb_launches(hl_amd_encoder_t* e) { return e ? e->
 // counters, then (n > 64) the cycles of each macroblock of the last frame.
 extern "C" int32_t hl_amd_profile_counters(hl_amd_encoder_t* e, unsigned long long* out, int32_t n)
 {
-    if (!e || !out || n < 0 || n > 64 + 4 * e->nmb) return HL_AMD_ERROR_INVALID_PARAMETER;
+    if (!e || !out || n < 0 || n > 64 + 4 * e->nmb + kProfExtra) return HL_AMD_ERROR_INVALID_PARAMETER;
     memset(out, 0, sizeof(unsigned long long) * n);
     if (!e->d_prof) return HL_AMD_SUCCESS;
     HL_HIP_CHECK(hipMemcpy(out, e->d_prof, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
     HL_HIP_CHECK(hipMemset(e->d_prof, 0, sizeof(unsigned long long) * 64));
+    if (kProfExtra) HL_HIP_CHECK(hipMemset(e->d_prof + 64 + 4 * e->nmb, 0, sizeof(unsigned long long) * kProfExtra));
     return HL_AMD_SUCCESS;
 }
 

@@ -38,7 +38,34 @@
 
 namespace hl {
 
-#if defined(__HIP_DEVICE_COMPILE__)
+constexpr int kBarSites = 2560;  // HL_BAR_PROF=2: barrier sites (source line / 2)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(HL_PROFILE) && defined(HL_BAR_PROF)
+// profiling build: every wave's cycles inside the macroblock's barriers
+// (lane 0 of each wave adds to its own word; encode_mb reports them)
+__shared__ unsigned long long g_bar_acc[8][2];
+#if HL_BAR_PROF >= 2
+// HL_BAR_PROF=2: per barrier site (source line / 2): wait cycles summed over
+// the waves, and wave 0's count; added to FrameArgs::prof after the timeline
+__shared__ unsigned long long g_bar_site[kBarSites];
+__shared__ unsigned g_bar_cnt[kBarSites];
+#endif
+__device__ __forceinline__ void hl_sync_prof(int line)
+{
+    const unsigned long long t0 = __builtin_readcyclecounter();
+    __syncthreads();
+    const unsigned long long dt = __builtin_readcyclecounter() - t0;
+    if ((threadIdx.x & 63) == 0) {
+        g_bar_acc[threadIdx.x >> 6][0] += dt;
+        g_bar_acc[threadIdx.x >> 6][1] += 1;
+#if HL_BAR_PROF >= 2
+        const int k = min(line >> 1, kBarSites - 1);
+        atomicAdd(&g_bar_site[k], dt);
+        if (threadIdx.x == 0) g_bar_cnt[k] += 1;
+#endif
+    }
+}
+#define HL_SYNC() hl_sync_prof(__LINE__)
+#elif defined(__HIP_DEVICE_COMPILE__)
 #define HL_SYNC() __syncthreads()
 #else
 #define HL_SYNC() ((void)0)
@@ -573,18 +600,20 @@ HD void skip_mv(const Shared& S, int out[2])
 }
 
 // marks the 4x4 blocks of the luma rectangle as decided with motion mv
-HD void grid_set(Shared& S, int x, int y, int w, int h, int mvx, int mvy)
+// (lane-parallel: lane k of the first wave writes 4x4 block k; the host
+// build's one lane loops)
+HD void grid_set(Shared& S, int tid, int nthr, int x, int y, int w, int h, int mvx, int mvy)
 {
-    for (int by = y >> 2; by < (y + h) >> 2; ++by)
-        for (int bx = x >> 2; bx < (x + w) >> 2; ++bx) {
-            S.mvs[by + 1][bx + 1] = 2;
-            S.mvg[by + 1][bx + 1] = (mvx & 0xFFFF) | (mvy << 16);
-        }
+    const int nbw = w >> 2, n = nbw * (h >> 2);
+    for (int k = tid; k < n; k += nthr) {
+        const int bx = (x >> 2) + k % nbw, by = (y >> 2) + k / nbw;
+        S.mvs[by + 1][bx + 1] = 2;
+        S.mvg[by + 1][bx + 1] = (mvx & 0xFFFF) | (mvy << 16);
+    }
 }
-HD void grid_reset_inside(Shared& S)
+HD void grid_reset_inside(Shared& S, int tid, int nthr)
 {
-    for (int by = 0; by < 4; ++by)
-        for (int bx = 0; bx < 4; ++bx) S.mvs[by + 1][bx + 1] = 0;
+    for (int k = tid; k < 16; k += nthr) S.mvs[(k >> 2) + 1][(k & 3) + 1] = 0;
 }
 
 // nC of a luma-type block (residual.c:640-755): neighbour values are taken
@@ -2161,8 +2190,8 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         S.bmvp[pi][spi][1] = (int16_t)pmv[1];
         S.nb[0].mv[pi][spi][0] = (int16_t)b.mv[0];  // MvL0 feeds the MVP of later partitions
         S.nb[0].mv[pi][spi][1] = (int16_t)b.mv[1];
-        grid_set(S, g.px, g.py, g.pw, g.ph, b.mv[0], b.mv[1]);
     }
+    if (c.tid < 16) grid_set(S, c.tid, min(c.nthr, 16), g.px, g.py, g.pw, g.ph, b.mv[0], b.mv[1]);
     HL_SYNC();
     HL_PROF_ADD(c, 3, tsp);
     return probably;
@@ -3769,12 +3798,12 @@ HD bool search_family_part(Ctx& c, int j, int fam, double& cost_sum, int& single
         S.nb[0].e_type = fam_etype(fam);
         S.nb[0].part_w = pd.part_w;
         S.nb[0].part_h = pd.part_h;
-        for (int i = 0; i < 4; ++i) {
-            S.nb[0].sub_w[i] = pd.sub_w;
-            S.nb[0].sub_h[i] = pd.sub_h;
-        }
-        grid_reset_inside(S);
     }
+    for (int i = c.tid; i < 4; i += c.nthr) {
+        S.nb[0].sub_w[i] = pd.sub_w;
+        S.nb[0].sub_h[i] = pd.sub_h;
+    }
+    if (c.tid < 16) grid_reset_inside(S, c.tid, min(c.nthr, 16));
     HL_SYNC();
     bool prob = false;
     for (int pi = 0; pi < pd.num_part; ++pi)
@@ -3849,15 +3878,12 @@ HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr)
             best_part = j;
             best_fam = fam;
             HL_SYNC();
-            if (c.tid == 0) {
-                for (int pi = 0; pi < pd.num_part; ++pi)
-                    for (int spi = 0; spi < pd.num_sub; ++spi) {
-                        const int o = (pi * 4 + spi) * 2;
-                        S.best_mv[pi][spi][0] = bmv[o];
-                        S.best_mv[pi][spi][1] = bmv[o + 1];
-                        S.best_mvp[pi][spi][0] = bmvp[o];
-                        S.best_mvp[pi][spi][1] = bmvp[o + 1];
-                    }
+            for (int k = c.tid; k < pd.num_part * pd.num_sub; k += c.nthr) {
+                const int pi = k / pd.num_sub, spi = k - pi * pd.num_sub, o = (pi * 4 + spi) * 2;
+                S.best_mv[pi][spi][0] = bmv[o];
+                S.best_mv[pi][spi][1] = bmv[o + 1];
+                S.best_mvp[pi][spi][0] = bmvp[o];
+                S.best_mvp[pi][spi][1] = bmvp[o + 1];
             }
             HL_SYNC();
         }
@@ -4605,6 +4631,16 @@ HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, in
     c.Q = make_laneq(tid, F.qp);
 #endif
     if (tid == 0 && !f3out) gmem(F.chain + addr)->s_in = s_in;
+#if defined(__HIP_DEVICE_COMPILE__) && defined(HL_PROFILE) && defined(HL_BAR_PROF)
+    if ((tid & 63) == 0) g_bar_acc[tid >> 6][0] = g_bar_acc[tid >> 6][1] = 0;
+#if HL_BAR_PROF >= 2
+    for (int k = tid; k < kBarSites; k += nthr) {
+        g_bar_site[k] = 0;
+        g_bar_cnt[k] = 0;
+    }
+    __syncthreads();
+#endif
+#endif
     HL_PROF_T(t0);
 #if defined(__HIP_DEVICE_COMPILE__) && HL_LDS_WINDOW
     // the LDS search window: loads issued here, stored after mb_begin's load
@@ -4649,6 +4685,35 @@ HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, in
     HL_PROF_ADD(c, 7, t1);
     HL_PROF_ADD(c, 8, t0);
 #if defined(HL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+#if defined(HL_BAR_PROF)
+    // slot 14: barrier cycles summed over the waves (count: barriers of wave
+    // 0); slot 15: the most waiting wave's, slot 18: the least waiting wave's
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long sum = 0, mx = 0, mn = ~0ull;
+        for (int w = 0; w < nthr / 64; ++w) {
+            sum += g_bar_acc[w][0];
+            mx = max(mx, g_bar_acc[w][0]);
+            mn = min(mn, g_bar_acc[w][0]);
+        }
+        c.pacc[14] = sum;
+        c.pcnt[14] = (int)g_bar_acc[0][1];
+        c.pacc[15] = mx;
+        c.pcnt[15] = 1;
+        c.pacc[18] = mn;
+        c.pcnt[18] = 1;
+    }
+#if HL_BAR_PROF >= 2
+    if (F.prof) {
+        unsigned long long* site = F.prof + 64 + 4 * F.mbw * F.mbh;
+        for (int k = tid; k < kBarSites; k += nthr)
+            if (g_bar_cnt[k]) {
+                atomicAdd(site + 2 * k, g_bar_site[k]);
+                atomicAdd(site + 2 * k + 1, (unsigned long long)g_bar_cnt[k]);
+            }
+    }
+#endif
+#endif
     if (tid == 0 && F.prof) {
         for (int i = 0; i < kProfSlots; ++i) {
             atomicAdd(&F.prof[2 * i], c.pacc[i]);

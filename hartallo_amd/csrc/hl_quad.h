@@ -97,11 +97,20 @@ __device__ __forceinline__ LaneQ make_laneq(int tid, int qp)
 //   stage 2, partner r ^ 1: y0 = (a+d) + (b+e), y2 = (a+d) - (b+e),
 //                           y1 = 2 (a-d) + (b-e), y3 = (a-d) - 2 (b-e)
 // |values| <= 9180 (8-bit residuals), so the 24-bit multiplies are exact.
+// A per-lane weight the compiler must treat as unknown: it otherwise turns
+// each multiply by a +-1 select into a negate and a select (two instructions
+// per use instead of one multiply-add).
+__device__ __forceinline__ int opaque_w(int w)
+{
+    asm volatile("" : "+v"(w));
+    return w;
+}
+
 __device__ __forceinline__ void quad_fwd(const LaneQ& Q, const int x[4], int y[4])
 {
     const int s03 = x[0] + x[3], d03 = x[0] - x[3], s12 = x[1] + x[2], d12 = x[1] - x[2];
     const int h[4] = {s03 + s12, (d03 << 1) + d12, s03 - s12, d03 - (d12 << 1)};
-    const int s1 = Q.r < 2 ? 1 : -1, kx = Q.r == 1 ? -1 : 1, kp = Q.r < 2 ? 1 : (Q.r == 2 ? 2 : -2);
+    const int s1 = opaque_w(Q.r < 2 ? 1 : -1), kx = opaque_w(Q.r == 1 ? -1 : 1), kp = opaque_w(Q.r < 2 ? 1 : (Q.r == 2 ? 2 : -2));
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int t = __mul24(h[c], s1) + dpp_x<kQX3>(h[c]);
@@ -139,7 +148,7 @@ __device__ __forceinline__ void quad_idct(const LaneQ& Q, const int q[4], int qP
     }
     const int e0 = d[0] + d[2], e1 = d[0] - d[2], e2 = (d[1] >> 1) - d[3], e3 = d[1] + (d[3] >> 1);
     const int f[4] = {e0 + e3, e1 + e2, e1 - e2, e0 - e3};
-    const int kx = Q.r == 1 ? -1 : 1, sh = Q.r >> 1, kp = Q.r == 2 ? -1 : 1, s1 = Q.r < 2 ? 1 : -1;
+    const int kx = opaque_w(Q.r == 1 ? -1 : 1), sh = Q.r >> 1, kp = opaque_w(Q.r == 2 ? -1 : 1), s1 = opaque_w(Q.r < 2 ? 1 : -1);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int g = __mul24(f[c] >> sh, kx) + __mul24(dpp_x<kQX1>(f[c]), kp);

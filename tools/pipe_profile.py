@@ -25,6 +25,10 @@ from hartallo_amd import Encoder, synth  # noqa: E402
 
 PHASES = ["eval:block", "eval:nC", "eval:reduce", "search_partition", "mvp", "guess_intra(P)", "mb_begin", "mb_end", "whole MB",
           "reach_wait", "intra:i16", "intra:i4", "early-term modes", "inter finalize", "", "", "step:candidates", "step:selection", "", "helper join"]
+if os.environ.get("HL_BAR_NAMES"):  # a build with -DHL_BAR_PROF: barrier cycles per MB (all waves / most / least waiting wave)
+    PHASES[14] = "barriers:all waves"
+    PHASES[15] = "barriers:max wave"
+    PHASES[18] = "barriers:min wave"
 if os.environ.get("HL_STEP_NAMES"):  # a build with -DHL_STEP_PROF: slots 12..15, 18, 19 time the steps' sub-phases
     PHASES[12:16] = ["step:loads", "step:quad work", "step:eval barrier", "step:results+minima"]
     PHASES[18] = "step:chain resolved"
@@ -53,7 +57,9 @@ def main():
     enc.encode_batch_device(ptrs[2:], collect=False)
     dt = time.perf_counter() - t
     ms = enc.timing_ms()
-    cnt = enc.profile_counters(64)
+    nmb_ = nmb
+    nsites = int(os.environ.get("HL_BAR_SITES", "0"))  # an HL_BAR_PROF=2 build: 2560 barrier sites after the timeline
+    cnt = enc.profile_counters(64 + 4 * nmb_ + 2 * nsites) if nsites else enc.profile_counters(64)
     print(f"wg,R,window={geo}: {n} P pictures in {dt * 1e3:.1f} ms (kernel {ms[1]:.1f} ms, reruns {enc.last_reruns()}) helpers {enc.last_helper_stats()}")
     life, wait, mb, filt, tasks = cnt[44], cnt[40], cnt[41], cnt[42], cnt[43]
     if life:
@@ -76,6 +82,14 @@ def main():
         cyc, calls = cnt[2 * i], cnt[2 * i + 1]
         if calls and name:
             print(f"   {name:18s} calls/MB {calls / (n * nmb):8.1f}  cycles/call {cyc / calls:10.0f}  kcycles/MB {cyc / (n * nmb) / 1e3:9.1f}")
+    if nsites:  # barrier sites by their wait (source line = 2 * site or 2 * site + 1, any header)
+        base = 64 + 4 * nmb
+        sites = [(cnt[base + 2 * k], cnt[base + 2 * k + 1], k) for k in range(nsites) if cnt[base + 2 * k + 1]]
+        tot = sum(w for w, _, _ in sites)
+        print(f"   barrier sites: {len(sites)}, wait summed over the waves {tot / (n * nmb) / 1e3:.1f} kcycles/MB")
+        for w, c_, k in sorted(sites, reverse=True)[:30]:
+            print(f"     line {2 * k:5d}-{2 * k + 1:<5d} calls/MB {c_ / (n * nmb):7.2f}  wait/call (all waves) {w / c_:8.0f}  "
+                  f"kcycles/MB {w / (n * nmb) / 1e3:8.1f}  ({100.0 * w / max(1, tot):4.1f} %)")
     enc.close()
 
 
