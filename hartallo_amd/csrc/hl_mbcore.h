@@ -127,6 +127,9 @@ constexpr int kSpecMaxBlocks = HL_QUAD_EVAL ? HL_SPEC_MAX_BLOCKS : 8;
 #ifndef HL_LDS_WINDOW
 #define HL_LDS_WINDOW 0
 #endif
+#ifndef HL_LDS_WINDOW_DMA  // 1: the window filled by LDS-DMA (with HL_LDS_WINDOW=1)
+#define HL_LDS_WINDOW_DMA 0
+#endif
 struct alignas(16) CandSlot {
     int32_t off1, off2;
     int16_t mvx, mvy;
@@ -600,20 +603,20 @@ HD void skip_mv(const Shared& S, int out[2])
 }
 
 // marks the 4x4 blocks of the luma rectangle as decided with motion mv
-// (lane-parallel: lane k of the first wave writes 4x4 block k; the host
-// build's one lane loops)
-HD void grid_set(Shared& S, int tid, int nthr, int x, int y, int w, int h, int mvx, int mvy)
+// (one lane: spreading these stores over 16 lanes measured slower, the
+// extra SALU address arithmetic outweighing the stores)
+HD void grid_set(Shared& S, int x, int y, int w, int h, int mvx, int mvy)
 {
-    const int nbw = w >> 2, n = nbw * (h >> 2);
-    for (int k = tid; k < n; k += nthr) {
-        const int bx = (x >> 2) + k % nbw, by = (y >> 2) + k / nbw;
-        S.mvs[by + 1][bx + 1] = 2;
-        S.mvg[by + 1][bx + 1] = (mvx & 0xFFFF) | (mvy << 16);
-    }
+    for (int by = y >> 2; by < (y + h) >> 2; ++by)
+        for (int bx = x >> 2; bx < (x + w) >> 2; ++bx) {
+            S.mvs[by + 1][bx + 1] = 2;
+            S.mvg[by + 1][bx + 1] = (mvx & 0xFFFF) | (mvy << 16);
+        }
 }
-HD void grid_reset_inside(Shared& S, int tid, int nthr)
+HD void grid_reset_inside(Shared& S)
 {
-    for (int k = tid; k < 16; k += nthr) S.mvs[(k >> 2) + 1][(k & 3) + 1] = 0;
+    for (int by = 0; by < 4; ++by)
+        for (int bx = 0; bx < 4; ++bx) S.mvs[by + 1][bx + 1] = 0;
 }
 
 // nC of a luma-type block (residual.c:640-755): neighbour values are taken
@@ -1310,6 +1313,10 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         for (int j = 0; j < kQPass; ++j) {
             const int item = qg + j * nq;
             if (item < n) {
+#if defined(HL_NOP_PROBE)  // timing experiment: HL_NOP_PROBE x 8 independent VALU issue slots per quad round
+#pragma unroll
+                for (int np = 0; np < HL_NOP_PROBE; ++np) asm volatile("v_nop\n v_nop\n v_nop\n v_nop\n v_nop\n v_nop\n v_nop\n v_nop");
+#endif
                 const int ci = item >> g.lnb, k = item & (g.nblk - 1);
                 int x[4], y[4], q[4];
 #pragma unroll
@@ -2190,8 +2197,8 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         S.bmvp[pi][spi][1] = (int16_t)pmv[1];
         S.nb[0].mv[pi][spi][0] = (int16_t)b.mv[0];  // MvL0 feeds the MVP of later partitions
         S.nb[0].mv[pi][spi][1] = (int16_t)b.mv[1];
+        grid_set(S, g.px, g.py, g.pw, g.ph, b.mv[0], b.mv[1]);
     }
-    if (c.tid < 16) grid_set(S, c.tid, min(c.nthr, 16), g.px, g.py, g.pw, g.ph, b.mv[0], b.mv[1]);
     HL_SYNC();
     HL_PROF_ADD(c, 3, tsp);
     return probably;
@@ -3798,12 +3805,12 @@ HD bool search_family_part(Ctx& c, int j, int fam, double& cost_sum, int& single
         S.nb[0].e_type = fam_etype(fam);
         S.nb[0].part_w = pd.part_w;
         S.nb[0].part_h = pd.part_h;
+        for (int i = 0; i < 4; ++i) {
+            S.nb[0].sub_w[i] = pd.sub_w;
+            S.nb[0].sub_h[i] = pd.sub_h;
+        }
+        grid_reset_inside(S);
     }
-    for (int i = c.tid; i < 4; i += c.nthr) {
-        S.nb[0].sub_w[i] = pd.sub_w;
-        S.nb[0].sub_h[i] = pd.sub_h;
-    }
-    if (c.tid < 16) grid_reset_inside(S, c.tid, min(c.nthr, 16));
     HL_SYNC();
     bool prob = false;
     for (int pi = 0; pi < pd.num_part; ++pi)
@@ -3878,12 +3885,15 @@ HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr)
             best_part = j;
             best_fam = fam;
             HL_SYNC();
-            for (int k = c.tid; k < pd.num_part * pd.num_sub; k += c.nthr) {
-                const int pi = k / pd.num_sub, spi = k - pi * pd.num_sub, o = (pi * 4 + spi) * 2;
-                S.best_mv[pi][spi][0] = bmv[o];
-                S.best_mv[pi][spi][1] = bmv[o + 1];
-                S.best_mvp[pi][spi][0] = bmvp[o];
-                S.best_mvp[pi][spi][1] = bmvp[o + 1];
+            if (c.tid == 0) {
+                for (int pi = 0; pi < pd.num_part; ++pi)
+                    for (int spi = 0; spi < pd.num_sub; ++spi) {
+                        const int o = (pi * 4 + spi) * 2;
+                        S.best_mv[pi][spi][0] = bmv[o];
+                        S.best_mv[pi][spi][1] = bmv[o + 1];
+                        S.best_mvp[pi][spi][0] = bmvp[o];
+                        S.best_mvp[pi][spi][1] = bmvp[o + 1];
+                    }
             }
             HL_SYNC();
         }
@@ -4139,7 +4149,12 @@ HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr)
 #if !defined(HL_STEP_PROF)
         HL_PROF_ADD(c, 19, tj);  // joining the intra helper
 #endif
+#if defined(HL_SKIP_INTRA_P)  // timing experiment only (not bit-exact): the P macroblocks' intra fallback skipped
+        const double ic = 1.7976931348623157e308;
+        (void)hin;
+#else
         const double ic = guess_intra(c, hin);
+#endif
         HL_PROF_ADD(c, 5, ti);
         if (ic <= best_cost) return;
     }
@@ -4646,6 +4661,31 @@ HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, in
     // the LDS search window: loads issued here, stored after mb_begin's load
     // round (their latency overlaps it); read after guess_inter's barriers
     constexpr int kWinChunks = 4 * kWinPlane / 16, kWinRounds = (kWinChunks + kMbThreads - 1) / kMbThreads;
+#if HL_LDS_WINDOW_DMA
+    // LDS-DMA form: global_load_lds_dwordx4, no VGPR staging; every wave
+    // writes 1 KiB of the window per instruction (lane-linear), drained by
+    // the compiler's vmcnt(0) at mb_begin's first barrier
+    static_assert(kWinChunks % 64 == 0, "whole waves of 16-byte window chunks");
+    if (!F.is_intra) {
+        const int bx = c.gx >= F.mbw - 1 ? F.W + 2 * kPad : 16 * (c.gx + 1) + kPad;
+        const int by = c.gy >= F.mbh - 1 ? F.H + 2 * kPad : 16 * (c.gy + 1) + kPad;
+        c.wux = min(kWinW, bx - c.xL);
+        c.wuy = min(kWinH, by - c.yL);
+        const auto pl = gmem(F.pl[0]);
+        const int wbase = tid & ~63;
+#pragma unroll
+        for (int k = 0; k < kWinRounds; ++k) {
+            const int i0 = wbase + k * kMbThreads;  // the wave's first chunk (uniform)
+            if (i0 < kWinChunks) {
+                const int i = i0 + (tid & 63);
+                const int p = i / (kWinPlane / 16), rem = i - p * (kWinPlane / 16), r = rem / (kWinW / 16), cc = rem - r * (kWinW / 16);
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(pl + (size_t)p * F.plsz + (size_t)(c.yL + r) * F.pstride + c.xL + cc * 16),
+                    (__attribute__((address_space(3))) void*)(S.win + 16 * i0), 16, 0, 0);
+            }
+        }
+    }
+#else
     uint4 wv[kWinRounds];
     if (!F.is_intra) {
         const int bx = c.gx >= F.mbw - 1 ? F.W + 2 * kPad : 16 * (c.gx + 1) + kPad;
@@ -4661,8 +4701,9 @@ HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, in
         }
     }
 #endif
+#endif
     mb_begin(c);
-#if defined(__HIP_DEVICE_COMPILE__) && HL_LDS_WINDOW
+#if defined(__HIP_DEVICE_COMPILE__) && HL_LDS_WINDOW && !HL_LDS_WINDOW_DMA
     if (!F.is_intra) {
 #pragma unroll
         for (int k = 0; k < kWinRounds; ++k)
