@@ -3035,163 +3035,134 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
     // available top-right neighbours lie on earlier steps, and so do the
     // blocks whose TotalCoeffs its nC reads; the z-order effects (cost sum,
     // counter writes, CBP) are applied in z-order after the wavefront.
-    // One 16-lane row per (slot, mode): rows 0-8 slot 0, rows 9-17 slot 1.
+    // Wave s runs slot s of every step on its own: the block's neighbour
+    // samples (lanes 0-13), its nine modes as nine 4-lane quads (hl_quad.h:
+    // lane r = block row r), the resolution from the quads' registers and the
+    // chosen quad's reconstruction and levels; one workgroup barrier per step
+    // orders the two slots' writes before the next step reads them.
     constexpr uint8_t kWave[10][2] = {{0, 255}, {1, 255}, {2, 4}, {3, 5}, {6, 8}, {7, 9}, {10, 12}, {11, 13}, {14, 255}, {15, 255}};
-    const int row = c.tid >> 4;
-    const int qbits = 15 + F.qp / 6, fq = (1 << qbits) / 3;
-    // this lane's prediction taps: row = (slot, mode), lane = sample (kI4Tab)
-    const uint32_t te = kI4Tab.e[row < 18 ? (row >= 9 ? row - 9 : row) : 0][c.tid & 15];
-    // (workgroups below 288 lanes lack the 18 rows of a two-slot step: one
-    // block per step, in z-order)
-    constexpr bool kTwoSlots = kMbThreads >= 18 * 16;
-    constexpr int kSteps = kTwoSlots ? 10 : 16;
-    // the neighbour samples of step d's blocks into S.i4nb (rows 0-1 of wave
-    // 0; the previous step's resolution, the same lanes, wrote their S.rec)
-    auto i4_nbrs = [&](int d) {
-        const int b0 = kTwoSlots ? kWave[d][0] : d, b1 = kTwoSlots ? kWave[d][1] : 255;
-        const int nslot = b1 == 255 ? 1 : 2;
-        if (c.tid < 32 && (c.tid >> 4) < nslot) {
-            // lane i of the slot's 16-lane row: neighbour sample i (i4_neighbours,
-            // one sample per lane); lane 13: the DC value (mode 2 of i4_pred_px)
-            const int i = c.tid & 15, base = c.tid & 16, blk = base ? b1 : b0;
-            const int xO = blk_x(blk), yO = blk_y(blk);
-            const int X = i < 5 ? -1 : i - 5, Y = i < 5 ? i - 1 : -1;
-            const int x = xO + X, y = yO + Y;
-            const bool na = i >= 13 || (x > 15 && y >= 0) || (X > 3 && (blk == 3 || blk == 11));
-            const int vl = S.left[y < 0 ? 0 : y], vt = S.top[min(max(x + 1, 0), 24)], vr = S.rec[(y < 0 ? 0 : y) * 16 + min(max(x, 0), 15)];
-            int v = na ? kNA : ((x < 0 && y >= 0) ? vl : (y < 0 ? vt : vr));
-            const int s8 = base ? __builtin_amdgcn_readlane(v, 24) : __builtin_amdgcn_readlane(v, 8);
-            const int s9 = base ? __builtin_amdgcn_readlane(v, 25) : __builtin_amdgcn_readlane(v, 9);
-            if (i >= 9 && i <= 12 && s9 == kNA && s8 != kNA) v = s8;
-            const bool isl = i >= 1 && i <= 4, ist = i >= 5 && i <= 8;
-            const int suml = row_sum(isl ? v : 0), sumt = row_sum(ist ? v : 0);
-            const unsigned al = (unsigned)(__ballot(isl && v != kNA) >> base) & 0xFFFFu, at = (unsigned)(__ballot(ist && v != kNA) >> base) & 0xFFFFu;
-            const bool ya = al == 0x1Eu, xa = at == 0x1E0u;
-            const int dc = (xa && ya) ? (sumt + suml + 4) >> 3 : (ya ? (suml + 2) >> 2 : (xa ? (sumt + 2) >> 2 : 128));
-            if (i < 14) S.i4nb[base >> 4][i] = (int16_t)(i == 13 ? dc : v);  // [13]: the DC value
-        }
-    };
-    i4_nbrs(0);
-    HL_SYNC();
-    for (int d = 0; d < kSteps; ++d) {
+    static_assert(kMbThreads >= 128, "one wave per wavefront slot");
+    const int lane = c.tid & 63, sl = c.tid >> 6;
+    const int qp = uni(F.qp), qbits = 15 + qp / 6, fq = (1 << qbits) / 3;
+    const int m = min(lane >> 2, 8), rr = lane & 3;  // this quad's mode, this lane's block row
+    const LaneQ& Q = c.Q;
+    uint32_t te[4];  // the prediction taps of the lane's four samples (kI4Tab)
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) te[cc] = kI4Tab.e[m][rr * 4 + cc];
+    for (int d = 0; d < 10; ++d) {
 #if defined(HL_I4_PROF)
-        HL_PROF_T(ti0);
-#endif
-        const int b0 = kTwoSlots ? kWave[d][0] : d, b1 = kTwoSlots ? kWave[d][1] : 255;
-        const int nslot = b1 == 255 ? 1 : 2;
-#if defined(HL_I4_PROF)
-        HL_PROF_ADD(c, 12, ti0);  // neighbours
         HL_PROF_T(ti1);
 #endif
-        // nC is the same for all nine modes of a block: they only rewrite it
-        const int nC0 = uni(nc_luma_of(S, b0, [&](int ni) -> int { return S.tc[ni]; }));
-        const int nC1 = nslot == 2 ? uni(nc_luma_of(S, b1, [&](int ni) -> int { return S.tc[ni]; })) : 0;
-        if (row < 9 * nslot) {
-            const int sl = row >= 9, m = row - 9 * sl, blk = sl ? b1 : b0;
+        const int blk = sl == 0 ? kWave[d][0] : (sl == 1 ? kWave[d][1] : 255);
+        if (blk != 255) {  // (wave-uniform)
             const int xO = blk_x(blk), yO = blk_y(blk);
-            const bool ok = i4_avail(m, S.i4nb[sl]);
-            if (ok) {
-                const int x = c.K.p & 3, y = c.K.p >> 2;
-                const int16_t* nb = S.i4nb[sl];
-                const int pred = i4_tab_pred(te, nb[te & 15], nb[(te >> 4) & 15], nb[(te >> 8) & 15]);
-                const int sv = S.src[(yO + y) * 16 + xO + x];
-                const int res = sv - pred;
-                const bool exact = row_or(res != 0) == 0;
-                const int q = coop_quant(coop_fwd(c.K, res), c.K.mf, qbits, fq);
-                // reconstruction before the CAVLC chain: the two interleave
-                const int r = coop_idct(c.K, coop_dequant(q, c.K.ls, F.qp));
-                const int rec = clip255(pred + r);
-                const int dd = row_sum(iabs(sv - rec));
-                const CoopStat st = coop_cavlc(S.ct, q, c.K.s, S.lvs[row]);
-                S.i4_rec[sl][m][c.K.p] = (uint8_t)rec;
-                S.i4_lv[sl][m][c.K.s] = (int16_t)q;
-                if (c.K.p == 0) {
-                    const int bits = st.tc ? st.rest + coop_token_len(S.ct, sl ? nC1 : nC0, st.tc, st.t1) : 0;
-                    S.i4_exact[sl][m] = exact;
-                    S.i4_nz[sl][m] = st.tc > 0;
-                    S.i4_tc[sl][m] = st.tc;
-                    S.i4_sctr[sl][m] = st.sctr;
-                    S.i4_dist[sl][m] = dd;
-                    S.i4_cost[sl][m] = exact ? 0.0 : dadd((double)dd, dmul(F.lambda, (double)bits));
-                }
+            if (lane < 16) {
+                // lane i: neighbour sample i (i4_neighbours, one sample per
+                // lane); lane 13: the DC value (mode 2 of i4_pred_px)
+                const int i = lane;
+                const int X = i < 5 ? -1 : i - 5, Y = i < 5 ? i - 1 : -1;
+                const int x = xO + X, y = yO + Y;
+                const bool na = i >= 13 || (x > 15 && y >= 0) || (X > 3 && (blk == 3 || blk == 11));
+                const int vl = S.left[y < 0 ? 0 : y], vt = S.top[min(max(x + 1, 0), 24)], vr = S.rec[(y < 0 ? 0 : y) * 16 + min(max(x, 0), 15)];
+                int v = na ? kNA : ((x < 0 && y >= 0) ? vl : (y < 0 ? vt : vr));
+                const int s8 = __builtin_amdgcn_readlane(v, 8), s9 = __builtin_amdgcn_readlane(v, 9);
+                if (i >= 9 && i <= 12 && s9 == kNA && s8 != kNA) v = s8;
+                const bool isl = i >= 1 && i <= 4, ist = i >= 5 && i <= 8;
+                const int suml = row_sum(isl ? v : 0), sumt = row_sum(ist ? v : 0);
+                const unsigned al = (unsigned)__ballot(isl && v != kNA) & 0xFFFFu, at = (unsigned)__ballot(ist && v != kNA) & 0xFFFFu;
+                const bool ya = al == 0x1Eu, xa = at == 0x1E0u;
+                const int dc = (xa && ya) ? (sumt + suml + 4) >> 3 : (ya ? (suml + 2) >> 2 : (xa ? (sumt + 2) >> 2 : 128));
+                if (i < 14) S.i4nb[sl][i] = (int16_t)(i == 13 ? dc : v);  // [13]: the DC value
             }
-            if (c.K.p == 0) S.i4_cost_ok[sl][m] = ok;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // nC is the same for all nine modes of a block: they only rewrite it
+            const int nC = uni(nc_luma_of(S, blk, [&](int ni) -> int { return S.tc[ni]; }));
+            const int16_t* nb = S.i4nb[sl];
+            const bool ok = (lane >> 2) < 9 && i4_avail(m, nb);
+            const uint32_t sv4 = *reinterpret_cast<const uint32_t*>(&S.src[(yO + rr) * 16 + xO]);
+            int x[4], y[4], q[4], r[4];
+            uint32_t pr4 = 0;
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+                const uint32_t e = te[cc];
+                const int pred = i4_tab_pred(e, nb[e & 15], nb[(e >> 4) & 15], nb[(e >> 8) & 15]);
+                x[cc] = (int)((sv4 >> (8 * cc)) & 255) - pred;
+                pr4 |= (uint32_t)pred << (8 * cc);
+            }
+            const bool exact = quad_or(x[0] | x[1] | x[2] | x[3]) == 0;
+            quad_fwd(Q, x, y);
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) q[cc] = quad_q1(y[cc], (cc & 1) ? Q.mfO : Q.mfE, qbits, fq);
+            // reconstruction before the CAVLC chain: the two interleave
+            quad_idct(Q, q, qp, r);
+            uint32_t rec4 = 0;
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) rec4 |= (uint32_t)clip255((int)((pr4 >> (8 * cc)) & 255) + r[cc]) << (8 * cc);
+            const int dd = quad_sum((int)__builtin_amdgcn_sad_u8(sv4, rec4, 0u));
+            const CoopStat st = quad_cavlc(S.ct, Q, q, 0, S.lvq[c.tid >> 2]);
+            const int bits = st.tc ? st.rest + coop_token_len(S.ct, nC, st.tc, st.t1) : 0;
+            const double cost = exact ? 0.0 : dadd((double)dd, dmul(F.lambda, (double)bits));
+            // resolution in mode order (rdo.c:1931-2014), lane 4 m standing for
+            // mode m: the scan stops at the first exact mode; before it, the
+            // last coded mode writes the counter and the first strict minimum wins
+            const bool v0 = ok && rr == 0;
+            const unsigned long long bex = __ballot(v0 && exact), bnz = __ballot(v0 && st.tc > 0);
+            const int limitl = bex ? __ffsll((long long)bex) - 1 : 36;
+            const unsigned long long W = bnz & ((1ull << limitl) - 1ull);
+            const int lastwl = W ? 63 - __clzll((long long)W) : -1;
+            double dmin;
+            int bestl;
+            bool best_zero;
+            if (bex) {
+                dmin = 0.0;
+                bestl = limitl;
+                best_zero = true;
+            }
+            else {
+                const double rm = row_min_f64(v0 ? cost : 1.7976931348623157e308);  // rows 0-2 hold the nine modes
+                double mn = 1.7976931348623157e308;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const unsigned long long b64 = __builtin_bit_cast(unsigned long long, rm);
+                    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b64 >> 32), 16 * k);
+                    const unsigned lw = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b64, 16 * k);
+                    mn = fmin(mn, __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lw));
+                }
+                dmin = mn;
+                bestl = __ffsll((long long)__ballot(v0 && cost == mn)) - 1;
+                best_zero = !((W >> bestl) & 1);
+            }
+            // (every value from registers: the stores carry no dependent load)
+            const int bdist = __builtin_amdgcn_readlane(dd, bestl);  // d_min_dist4x4 (rdo.c:2011, 2023); 0 for an exact mode
+            const int lwsct = lastwl >= 0 ? __builtin_amdgcn_readlane(st.sctr, lastwl) : -1;
+            const int lwtc = lastwl >= 0 ? __builtin_amdgcn_readlane(st.tc, lastwl) : -1;
+            if (lane == 0) {
+                S.i4r_dmin[blk] = dmin;
+                S.i4r_dist[blk] = bdist;
+                S.i4r_sct[blk] = lwsct;
+                S.i4r_zero[blk] = best_zero;
+                S.i4mode[blk] = (int8_t)(bestl >> 2);
+                if (lastwl >= 0) S.tc[blk] = (int8_t)lwtc;
+                // the verification record (i4_verify): the costs used an nC
+                // only without an exact mode and with a coded one
+                S.ih.i4_ncls[blk] = (int8_t)(!bex && W ? nc_class(nC) : -1);
+                S.ih.i4_lwtc[blk] = (int8_t)lwtc;
+            }
+            if ((lane >> 2) == (bestl >> 2)) {  // the chosen mode's quad: its reconstruction rows and levels
+                *reinterpret_cast<uint32_t*>(&S.rec[(yO + rr) * 16 + xO]) = rec4;
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) S.luma_level[blk][(Q.zz >> (4 * cc)) & 15] = q[cc];
+            }
         }
 #if defined(HL_I4_PROF)
-        HL_PROF_ADD(c, 13, ti1);  // the modes' evaluation (own wave)
+        HL_PROF_ADD(c, 13, ti1);  // the slot's modes and resolution (own wave)
         HL_PROF_T(ti2);
 #endif
         HL_SYNC();
 #if defined(HL_I4_PROF)
-        HL_PROF_ADD(c, 14, ti2);  // its barrier
-        HL_PROF_T(ti3);
-#endif
-        // resolution in mode order (rdo.c:1931-2014), vectorised, one 16-lane
-        // row per slot: the scan stops at the first exact mode; before it, the
-        // last coded mode writes the counter and the first strict minimum wins
-        {
-            const int sl = (c.tid >> 4) & 1, l = c.tid & 15;
-            const bool ok = sl < nslot && l < 9 && S.i4_cost_ok[sl][l];
-            const bool ex = ok && S.i4_exact[sl][l], nz = ok && S.i4_nz[sl][l];
-            const unsigned long long bex = __ballot(ex), bnz = __ballot(nz);
-            const int sct = ok ? S.i4_sctr[sl][l] : 0;
-            const int dl = ok ? S.i4_dist[sl][l] : 0, tl = ok ? S.i4_tc[sl][l] : 0;
-            const double v = ok ? S.i4_cost[sl][l] : 1.7976931348623157e308;
-            const double mn = row_min_f64(v);
-            const unsigned long long bmin = __ballot(ok && v == mn);
-            int bests[2], lastws[2];
-            for (int k = 0; k < nslot; ++k) {
-                const int blk = k ? b1 : b0;
-                const unsigned E = (unsigned)(bex >> (16 * k)) & 0xFFFFu;
-                const int limit = E ? __ffs(E) - 1 : 9;
-                const unsigned W = ((unsigned)(bnz >> (16 * k)) & 0xFFFFu) & ((1u << limit) - 1u);
-                const int lastw = W ? 31 - __clz(W) : -1;
-                double dmin;
-                int best;
-                bool best_zero;
-                if (E) {
-                    dmin = 0.0;
-                    best = limit;
-                    best_zero = true;
-                }
-                else {
-                    const unsigned long long b64 = __builtin_bit_cast(unsigned long long, mn);
-                    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b64 >> 32), 16 * k);
-                    const unsigned lw = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b64, 16 * k);
-                    dmin = __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lw);
-                    best = __ffs((unsigned)(bmin >> (16 * k)) & 0xFFFFu) - 1;
-                    best_zero = !((W >> best) & 1);
-                }
-                bests[k] = best;
-                lastws[k] = lastw;
-                // (every value from registers: the stores carry no dependent load)
-                const int bdist = __builtin_amdgcn_readlane(dl, 16 * k + best);  // d_min_dist4x4 (rdo.c:2011, 2023); 0 for an exact mode
-                const int lwsct = lastw >= 0 ? __builtin_amdgcn_readlane(sct, 16 * k + lastw) : -1;
-                const int lwtc = lastw >= 0 ? __builtin_amdgcn_readlane(tl, 16 * k + lastw) : -1;
-                if (c.tid == 0) {
-                    S.i4r_dmin[blk] = dmin;
-                    S.i4r_dist[blk] = bdist;
-                    S.i4r_sct[blk] = lwsct;
-                    S.i4r_zero[blk] = best_zero;
-                    S.i4mode[blk] = (int8_t)best;
-                    if (lastw >= 0) S.tc[blk] = (int8_t)lwtc;
-                    // the verification record (i4_verify): the costs used an nC
-                    // only without an exact mode and with a coded one
-                    S.ih.i4_ncls[blk] = (int8_t)(!E && W ? nc_class(k ? nC1 : nC0) : -1);
-                    S.ih.i4_lwtc[blk] = (int8_t)lwtc;
-                }
-            }
-            if (c.tid < 16 * nslot) {
-                const int k = c.tid >> 4, t = c.tid & 15, blk = k ? b1 : b0;
-                const int best = k ? bests[1] : bests[0];
-                S.rec[(blk_y(blk) + (t >> 2)) * 16 + blk_x(blk) + (t & 3)] = S.i4_rec[k][best][t];
-                S.luma_level[blk][t] = S.i4_lv[k][best][t];
-            }
-        }
-        if (d + 1 < kSteps) i4_nbrs(d + 1);
-        HL_SYNC();
-#if defined(HL_I4_PROF)
-        HL_PROF_ADD(c, 15, ti3);  // resolution + barrier
+        HL_PROF_ADD(c, 14, ti2);  // the step's barrier
 #endif
     }
     int last_sct = -1;

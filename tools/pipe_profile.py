@@ -30,7 +30,7 @@ if os.environ.get("HL_BAR_NAMES"):  # a build with -DHL_BAR_PROF: barrier cycles
     PHASES[15] = "barriers:max wave"
     PHASES[18] = "barriers:min wave"
 if os.environ.get("HL_I4_NAMES"):  # a build with -DHL_I4_PROF: slots 12..15 time guess_i4's wavefront steps
-    PHASES[12:16] = ["i4:neighbours", "i4:modes", "i4:modes barrier", "i4:resolution+barrier"]
+    PHASES[13:15] = ["i4:slot (modes + resolution)", "i4:step barrier"]
 if os.environ.get("HL_STEP_NAMES"):  # a build with -DHL_STEP_PROF: slots 12..15, 18, 19 time the steps' sub-phases
     PHASES[12:16] = ["step:loads", "step:quad work", "step:eval barrier", "step:results+minima"]
     PHASES[18] = "step:chain resolved"
