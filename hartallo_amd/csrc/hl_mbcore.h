@@ -81,6 +81,9 @@ __device__ __forceinline__ void hl_sync_prof(int line)
         (c).pacc[slot] += __builtin_readcyclecounter() - (t0);   \
         (c).pcnt[slot] += 1;                                     \
     } while (0)
+#if !defined(HL_STEP_PROF) && !defined(HL_I4_PROF) && !defined(HL_NBLK_PROF) && !defined(HL_BAR_PROF)
+#define HL_PROF_MISC 1  // slots 14, 15, 18: chroma reconstruction, the intra decision's tail, inter prediction
+#endif
 constexpr int kProfSlots = 20;  // prof[2 * slot], prof[2 * slot + 1] (< 40: the pipelined kernel uses 40-44)
 #else
 #define HL_PROF_T(v) const unsigned long long v = 0
@@ -2405,6 +2408,57 @@ HD void reconstruct_chroma(Ctx& c, bool intra_flag)
     HL_FRESH_TID_K(c, 1);
     const FrameArgs& F = c.F;
     Shared& S = c.S;
+#if defined(HL_PROF_MISC)
+    HL_PROF_T(trc);
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+    // one 4-lane quad per chroma 4x4 block (lanes 0-31: Cb blocks 0-3, Cr
+    // blocks 0-3), lane r = block row r (hl_quad.h) at the chroma QP
+    const LaneQ Qc = make_laneq(c.tid, F.qpc);
+    const int qbc = 15 + F.qpc / 6, fqc = (1 << qbc) / 3;  // intra rounding for every MB (rdo.c:2588,2618)
+    if (c.tid < 32) {
+        const int t = c.tid >> 2, r = c.tid & 3, comp = t >> 2, b = t & 3, xO = (b & 1) * 4, yO = (b >> 1) * 4;
+        const uint32_t sv = *reinterpret_cast<const uint32_t*>(&S.srcc[comp][(yO + r) * 8 + xO]);
+        const int* pc = &S.predc[comp][(yO + r) * 8 + xO];
+        int x[4];
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) x[cc] = (int)((sv >> (8 * cc)) & 255) - pc[cc];
+        int dc = 0, cacb = 0, cdcb = 0, tc = 0, sctr = -1;
+        if (quad_or(x[0] | x[1] | x[2] | x[3]) != 0) {  // (quad-uniform)
+            int y[4], q[4];
+            quad_fwd(Qc, x, y);
+            int mb = 0;
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+                q[cc] = quad_q1(y[cc], (cc & 1) ? Qc.mfO : Qc.mfE, qbc, fqc);
+                const int zz = (int)((Qc.zz >> (4 * cc)) & 15);
+                if (zz) {  // ChromaACLevel: scan positions 1-15 at list index 0-14
+                    S.cac[comp][b][zz - 1] = (int16_t)q[cc];
+                    mb |= q[cc] ? (1 << (zz - 1)) | ((q[cc] == 1 || q[cc] == -1) << (zz + 15)) : 0;
+                }
+            }
+            // list index 15 is read stale, as the CAVLC statistics see it
+            const int st = S.cac[comp][b][15];
+            const uint32_t masks = (uint32_t)quad_or(mb) | (st ? (1u << 15) | ((uint32_t)(st == 1 || st == -1) << 31) : 0u);
+            const uint32_t nz = masks & 0xFFFFu, ones = masks >> 16;
+            dc = dpp_x<0x00>(y[0]);  // coefficient (0, 0): lane 0 of the quad (quad_perm 0,0,0,0)
+            cacb = nz != 0;
+            cdcb = dc != 0;
+            if (cacb) {  // cavlc_stat's TotalCoeff and single-coefficient counter
+                const int hi = 31 - __clz(nz);
+                tc = __popc(nz);
+                sctr = (tc == 1 && ones == nz) ? (hi == 0 ? 3 : (hi < 3 ? 2 : (hi < 6 ? 1 : 0))) : 9;
+            }
+        }
+        if (r == 0) {
+            S.cres_dc[comp][b] = dc;
+            S.cres_cac[comp][b] = cacb;
+            S.cres_cdc[comp][b] = cdcb;
+            S.cres_tc[comp][b] = tc;
+            S.cres_sctr[comp][b] = sctr;
+        }
+    }
+#else
     for (int t = c.tid; t < 8; t += c.nthr) {
         const int comp = t >> 2, b = t & 3, xO = (b & 1) * 4, yO = (b >> 1) * 4;
         int res[16];
@@ -2440,6 +2494,7 @@ HD void reconstruct_chroma(Ctx& c, bool intra_flag)
         S.cres_tc[comp][b] = st.tc;
         S.cres_sctr[comp][b] = st.sctr;
     }
+#endif
     HL_SYNC();
     // sequential single-coefficient gating (uniform)
     int single[2] = {0, 0}, tcs[2] = {0, 0}, cac[2] = {0, 0}, cdc[2] = {0, 0};
@@ -2483,7 +2538,38 @@ HD void reconstruct_chroma(Ctx& c, bool intra_flag)
             for (int i = 0; i < 4; ++i) S.cdc_level[comp][i] = dcl[comp][i];
         }
     }
-    // decode (transf.c:161-294): thread per 4x4 chroma block
+    // decode (transf.c:161-294)
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (c.tid < 32) {  // the quads of the first pass: lane r writes row r of its block
+        const int t = c.tid >> 2, r = c.tid & 3, comp = t >> 2, b = t & 3, xO = (b & 1) * 4, yO = (b >> 1) * 4;
+        const int* pc = &S.predc[comp][(yO + r) * 8 + xO];
+        int rr[4] = {0, 0, 0, 0};
+        if (cdc[comp] || cac[comp]) {
+            int dcc = 0;
+            if (cdc[comp]) {
+                const int qP = F.qpc, scale = level_scale(qP % 6, 0, 0);
+                const int* L = dcl[comp];
+                const int f00 = (L[0] + L[2]) + (L[1] + L[3]), f01 = (L[0] + L[2]) - (L[1] + L[3]);
+                const int f10 = (L[0] - L[2]) + (L[1] - L[3]), f11 = (L[0] - L[2]) - (L[1] - L[3]);
+                const int f = b == 0 ? f00 : (b == 1 ? f01 : (b == 2 ? f10 : f11));
+                dcc = ((f * scale) << (qP / 6)) >> 5;
+            }
+            if (dcc || (cac[comp] & (1 << b))) {  // (quad-uniform)
+                int q[4];
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) {
+                    const int zz = (int)((Qc.zz >> (4 * cc)) & 15);
+                    q[cc] = zz ? S.cac[comp][b][zz - 1] : 0;
+                }
+                quad_idct(Qc, q, F.qpc, rr, true, dcc);
+            }
+        }
+        uint32_t rec = 0;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) rec |= (uint32_t)clip255(pc[cc] + rr[cc]) << (8 * cc);
+        *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(gmem(F.cur[1 + comp]) + ((c.yL >> 1) + yO + r) * F.Wc + (c.xL >> 1) + xO) = rec;
+    }
+#else
     for (int t = c.tid; t < 8; t += c.nthr) {
         const int comp = t >> 2, b = t & 3, xO = (b & 1) * 4, yO = (b >> 1) * 4;
         int r[16];
@@ -2513,7 +2599,11 @@ HD void reconstruct_chroma(Ctx& c, bool intra_flag)
             gmem(F.cur[1 + comp])[((c.yL >> 1) + yO + (i >> 2)) * F.Wc + (c.xL >> 1) + xO + (i & 3)] = (uint8_t)v;
         }
     }
+#endif
     HL_SYNC();
+#if defined(HL_PROF_MISC)
+    HL_PROF_ADD(c, 14, trc);
+#endif
 }
 
 HD void guess_cbp(Shared& S)  // rdo.c:2703-2782 (lane 0)
@@ -3079,6 +3169,10 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             // nC is the same for all nine modes of a block: they only rewrite it
             const int nC = uni(nc_luma_of(S, blk, [&](int ni) -> int { return S.tc[ni]; }));
+#if defined(HL_I4_PROF)
+            HL_PROF_ADD(c, 12, ti1);  // neighbours, nC
+            HL_PROF_T(ti3);
+#endif
             const int16_t* nb = S.i4nb[sl];
             const bool ok = (lane >> 2) < 9 && i4_avail(m, nb);
             const uint32_t sv4 = *reinterpret_cast<const uint32_t*>(&S.src[(yO + rr) * 16 + xO]);
@@ -3104,6 +3198,10 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
             const CoopStat st = quad_cavlc(S.ct, Q, q, 0, S.lvq[c.tid >> 2]);
             const int bits = st.tc ? st.rest + coop_token_len(S.ct, nC, st.tc, st.t1) : 0;
             const double cost = exact ? 0.0 : dadd((double)dd, dmul(F.lambda, (double)bits));
+#if defined(HL_I4_PROF)
+            HL_PROF_ADD(c, 13, ti3);  // the nine modes
+            HL_PROF_T(ti4);
+#endif
             // resolution in mode order (rdo.c:1931-2014), lane 4 m standing for
             // mode m: the scan stops at the first exact mode; before it, the
             // last coded mode writes the counter and the first strict minimum wins
@@ -3155,9 +3253,11 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
 #pragma unroll
                 for (int cc = 0; cc < 4; ++cc) S.luma_level[blk][(Q.zz >> (4 * cc)) & 15] = q[cc];
             }
+#if defined(HL_I4_PROF)
+            HL_PROF_ADD(c, 15, ti4);  // the resolution
+#endif
         }
 #if defined(HL_I4_PROF)
-        HL_PROF_ADD(c, 13, ti1);  // the slot's modes and resolution (own wave)
         HL_PROF_T(ti2);
 #endif
         HL_SYNC();
@@ -3445,6 +3545,9 @@ HD double guess_intra(Ctx& c, const IntraSpec* hin = nullptr)
         guess_i4(c, c4, cbp4, d4);
     }
     HL_PROF_ADD(c, 11, t4);
+#if defined(HL_PROF_MISC)
+    HL_PROF_T(ttl);
+#endif
     HL_SYNC();
     const int i16mode = S.i16mode;
     const int cmode = i16mode == 0 ? 2 : (i16mode == 3 ? 3 : (i16mode == 1 ? 1 : 0));
@@ -3490,6 +3593,9 @@ HD double guess_intra(Ctx& c, const IntraSpec* hin = nullptr)
         if (!F.is_intra) S.mb_type += 5;
     }
     HL_SYNC();
+#if defined(HL_PROF_MISC)
+    HL_PROF_ADD(c, 15, ttl);
+#endif
     return c16 < c4 ? c16 : c4;
 }
 
@@ -3510,6 +3616,9 @@ HD void inter_pred_mb(Ctx& c, bool chroma_only_16x16, bool luma)
     HL_FRESH_TID_K(c, 9);
     const FrameArgs& F = c.F;
     Shared& S = c.S;
+#if defined(HL_PROF_MISC)
+    HL_PROF_T(tip);
+#endif
     if (luma) {
 #if defined(__HIP_DEVICE_COMPILE__)
         // one 4-lane quad per 4x4 block, lane r = row r: the quarter-pel
@@ -3573,6 +3682,9 @@ HD void inter_pred_mb(Ctx& c, bool chroma_only_16x16, bool luma)
         }
     }
     HL_SYNC();
+#if defined(HL_PROF_MISC)
+    HL_PROF_ADD(c, 18, tip);
+#endif
 }
 
 // rdo.c:2274-2500 luma part (chroma via reconstruct_chroma)

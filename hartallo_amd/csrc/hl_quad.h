@@ -134,7 +134,9 @@ __device__ __forceinline__ int quad_q1(int w, int mf, int qbits, int f)
 //   stage 2, partner r ^ 3: h0 = g0 + g3 | h1 = g1 + g2 | h2 = g1 - g2 | h3 = g0 - g3
 // Dequantised values stay below 2^18 and every sum below 2^22 for levels of
 // 8-bit residuals at any QP, so the 24-bit multiplies are exact.
-__device__ __forceinline__ void quad_idct(const LaneQ& Q, const int q[4], int qP, int out[4])
+// keep_dc: coefficient (0, 0) is dcv, already scaled (Intra16x16 luma and
+// chroma: dequant_idct's keep_dc), in the lane holding coefficient row 0
+__device__ __forceinline__ void quad_idct(const LaneQ& Q, const int q[4], int qP, int out[4], bool keep_dc = false, int dcv = 0)
 {
     // 8.5.12.1 as ((p << a) + r) >> b with a, r, b uniform: qP >= 24 shifts
     // left by q6 - 4, below it rounds and shifts right by 4 - q6
@@ -146,6 +148,7 @@ __device__ __forceinline__ void quad_idct(const LaneQ& Q, const int q[4], int qP
         const int p = __mul24(q[c], (c & 1) ? Q.lsO : Q.lsE);
         d[c] = ((p << sa) + sr) >> sb;
     }
+    if (keep_dc && Q.r == 0) d[0] = dcv;
     const int e0 = d[0] + d[2], e1 = d[0] - d[2], e2 = (d[1] >> 1) - d[3], e3 = d[1] + (d[3] >> 1);
     const int f[4] = {e0 + e3, e1 + e2, e1 - e2, e0 - e3};
     const int kx = opaque_w(Q.r == 1 ? -1 : 1), sh = Q.r >> 1, kp = opaque_w(Q.r == 2 ? -1 : 1), s1 = opaque_w(Q.r < 2 ? 1 : -1);

@@ -25,12 +25,13 @@ from hartallo_amd import Encoder, synth  # noqa: E402
 
 PHASES = ["eval:block", "eval:nC", "eval:reduce", "search_partition", "mvp", "guess_intra(P)", "mb_begin", "mb_end", "whole MB",
           "reach_wait", "intra:i16", "intra:i4", "early-term modes", "inter finalize", "", "", "step:candidates", "step:selection", "", "helper join"]
+PHASES[14], PHASES[15], PHASES[18] = "reconstruct_chroma", "intra tail (chroma, CBP)", "inter_pred_mb"  # default profiling build
 if os.environ.get("HL_BAR_NAMES"):  # a build with -DHL_BAR_PROF: barrier cycles per MB (all waves / most / least waiting wave)
     PHASES[14] = "barriers:all waves"
     PHASES[15] = "barriers:max wave"
     PHASES[18] = "barriers:min wave"
 if os.environ.get("HL_I4_NAMES"):  # a build with -DHL_I4_PROF: slots 12..15 time guess_i4's wavefront steps
-    PHASES[13:15] = ["i4:slot (modes + resolution)", "i4:step barrier"]
+    PHASES[12:16] = ["i4:neighbours+nC", "i4:modes", "i4:step barrier", "i4:resolution"]
 if os.environ.get("HL_STEP_NAMES"):  # a build with -DHL_STEP_PROF: slots 12..15, 18, 19 time the steps' sub-phases
     PHASES[12:16] = ["step:loads", "step:quad work", "step:eval barrier", "step:results+minima"]
     PHASES[18] = "step:chain resolved"
