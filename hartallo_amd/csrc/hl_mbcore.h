@@ -315,7 +315,7 @@ struct Shared {
     int16_t best_mv[4][4][2], best_mvp[4][4][2];
     // --- intra scratch
     alignas(16) int32_t pred[256];
-    int32_t i16_ac[16][16], i16_dcc[32];  // (i16_ac: scratch of the pipelined task's plane blocks)
+    int32_t i16_ac[16][16], i16_dcc[64];  // (i16_ac: scratch of the pipelined task's plane blocks)
     int32_t i16_called[16], i16_bits[16], i16_dist[32], i16_distz[32];  // (i16_dcc / _dist / _distz: two modes' rows)
     alignas(16) int16_t i16_best_ac[16][16];
     alignas(16) int16_t i16_best_dc[16];
@@ -337,7 +337,7 @@ struct Shared {
     int32_t i4r_dist[16], i4r_sct[16], i4r_zero[16];
     int32_t luma_level[16][16];
     int16_t i4nb[2][16];         // neighbours of the current 4x4 blocks (p[13] layout)
-    int32_t dcY[32];             // I16x16: scaled DC per DC-matrix position (two modes)
+    int32_t dcY[64];             // I16x16: scaled DC per DC-matrix position (per mode)
     int32_t chain_x;             // resolve_chain result
     int32_t hs_x;                // intra helper state seen by the MB (HS_*)
     int32_t hs3_x;               // 8x8-family helper state seen by the MB
@@ -2753,70 +2753,83 @@ HD void i16_heavy(Ctx& c)
     const FrameArgs& F = c.F;
     Shared& S = c.S;
 #if defined(__HIP_DEVICE_COMPILE__)
-    // one 16-lane row per 4x4 block; two modes per round (rows 0-15 mode m0,
-    // rows 16-31 mode m0 + 1: waves 0-3 and 4-7) at 512 lanes
-    constexpr int kSlots = kMbThreads >= 512 ? 2 : 1;
-    const int row = c.tid >> 4, blk = row & 15, slot = row >> 4;
-    const int qbits = 15 + F.qp / 6, fq = (1 << qbits) / 3;
-    const int x = blk_x(blk) + (c.K.p & 3), y = blk_y(blk) + (c.K.p >> 2);
-    for (int m0 = 0; m0 < 4; m0 += kSlots) {
-        const int mode = m0 + slot;  // (wave-uniform)
-        const bool act = slot < kSlots && i16_mode_avail(S, mode);
-        int pred = 0, sv = 0, q = 0;
-        if (act) {  // blocks: transform, quant, AC statistics
-            int dcv, pa, pb, pc;
-            i16_params(S, mode, dcv, pa, pb, pc);
-            dcv = uni(dcv);
-            pa = uni(pa);
-            pb = uni(pb);
-            pc = uni(pc);
-            pred = i16_pred(S, mode, x, y, dcv, pa, pb, pc);
-            sv = S.src[y * 16 + x];
-            const int w = coop_fwd(c.K, sv - pred);
-            q = coop_quant(w, c.K.mf, qbits, fq);
-            const bool qz = row_or(q != 0) == 0;
-            const CoopStat st = coop_cavlc(S.ct, q, c.K.s - 1, S.lvs[row]);
-            S.ih_ac[mode][blk][c.K.s == 0 ? 15 : c.K.s - 1] = (int16_t)(c.K.s == 0 ? 0 : q);
-            S.ih_pred[mode][y * 16 + x] = (uint8_t)pred;
-            if (c.K.p == 0) {
-                S.i16_dcc[row] = w;
-                S.ih.blk[mode][blk] = (qz ? 0 : 1) | (st.tc << 1) | (st.t1 << 6) | ((st.sctr + 1) << 8) | (st.rest << 16);
-            }
+    // Wave m evaluates mode m on its own (waves 0-3): one 4-lane quad per 4x4
+    // block, lane r = block row r (hl_quad.h); the DC block on lanes 0-15 of
+    // the wave (16-lane Hadamard, hl_coop.h); the mode's distortions summed
+    // over its quads.  Only the waves' LDS writes need ordering inside the
+    // wave, so the four modes run without a workgroup barrier.
+    static_assert(kMbThreads >= 256, "one wave per Intra16x16 mode");
+    const int mode = c.tid >> 6, lane = c.tid & 63, blk = lane >> 2, r = lane & 3;
+    if (mode < 4 && i16_mode_avail(S, mode)) {  // (wave-uniform)
+        const int qp = uni(F.qp), qbits = 15 + qp / 6, fq = (1 << qbits) / 3;
+        const LaneQ& Q = c.Q;
+        int dcv, pa, pb, pc;
+        i16_params(S, mode, dcv, pa, pb, pc);
+        dcv = uni(dcv);
+        pa = uni(pa);
+        pb = uni(pb);
+        pc = uni(pc);
+        const int xO = blk_x(blk), y = blk_y(blk) + r;
+        const uint32_t sv = *reinterpret_cast<const uint32_t*>(&S.src[y * 16 + xO]);
+        int x[4], w[4], q[4];
+        uint32_t pr = 0;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            const int p = i16_pred(S, mode, xO + cc, y, dcv, pa, pb, pc);
+            pr |= (uint32_t)p << (8 * cc);
+            x[cc] = (int)((sv >> (8 * cc)) & 255) - p;
         }
-        HL_SYNC();
-        if (c.tid < 16 * kSlots && i16_mode_avail(S, m0 + (c.tid >> 4))) {  // the DC blocks: Hadamard, quant, CAVLC, scaling
-            const int ds = c.tid >> 4, dm = m0 + ds;
-            const int hh = coop_lin(c.K.had, S.i16_dcc[ds * 16 + kDcPos[c.K.p]]) >> 1;
-            const int qd = quant_dc(F.qp, true, hh);
-            const CoopStat st = coop_cavlc(S.ct, qd, c.K.s, S.lvs[ds]);
-            S.ih_dcl[dm][c.K.s] = (int16_t)qd;
+        *reinterpret_cast<uint32_t*>(&S.ih_pred[mode][y * 16 + xO]) = pr;
+        // blocks: transform, quant, AC statistics
+        quad_fwd(Q, x, w);
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            q[cc] = quad_q1(w[cc], (cc & 1) ? Q.mfO : Q.mfE, qbits, fq);
+            const int zz = (int)((Q.zz >> (4 * cc)) & 15);
+            S.ih_ac[mode][blk][zz == 0 ? 15 : zz - 1] = (int16_t)(zz == 0 ? 0 : q[cc]);
+        }
+        const bool qz = quad_or(q[0] | q[1] | q[2] | q[3]) == 0;
+        const CoopStat st = quad_cavlc(S.ct, Q, q, 1, S.lvq[c.tid >> 2]);
+        if (r == 0) {
+            S.i16_dcc[mode * 16 + blk] = w[0];  // the block's DC coefficient (lane 0 holds coefficient row 0)
+            S.ih.blk[mode][blk] = (qz ? 0 : 1) | (st.tc << 1) | (st.t1 << 6) | ((st.sctr + 1) << 8) | (st.rest << 16);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane < 16) {  // the DC block: Hadamard, quant, CAVLC, scaling
+            const int hh = coop_lin(c.K.had, S.i16_dcc[mode * 16 + kDcPos[c.K.p]]) >> 1;
+            const int qd = quant_dc(qp, true, hh);
+            const CoopStat sd = coop_cavlc(S.ct, qd, c.K.s, S.lvs[c.tid >> 4]);
+            S.ih_dcl[mode][c.K.s] = (int16_t)qd;
             const int f = coop_lin(c.K.had, qd);
-            const int scale = level_scale(F.qp % 6, 0, 0), q6 = F.qp / 6;
-            S.dcY[ds * 16 + c.K.p] = F.qp >= 36 ? (f * scale) << (q6 - 6) : (f * scale + (1 << (5 - q6))) >> (6 - q6);
-            if ((c.tid & 15) == 0) {  // block 0's nC neighbours lie outside the MB: the DC rate is fixed
+            const int scale = level_scale(qp % 6, 0, 0), q6 = qp / 6;
+            S.dcY[mode * 16 + c.K.p] = qp >= 36 ? (f * scale) << (q6 - 6) : (f * scale + (1 << (5 - q6))) >> (6 - q6);
+            if (lane == 0) {  // block 0's nC neighbours lie outside the MB: the DC rate is fixed
                 const int nC = nc_luma_of(S, 0, [&](int ni) -> int { return S.tc[ni]; });
-                S.ih.dcs[dm][0] = st.rest + coop_token_len(S.ct, nC, st.tc, st.t1);
-                S.ih.dcs[dm][1] = st.tc;
-                S.ih.dcs[dm][2] = st.sctr;
-                S.ih.dcs[dm][3] = 0;
+                S.ih.dcs[mode][0] = sd.rest + coop_token_len(S.ct, nC, sd.tc, sd.t1);
+                S.ih.dcs[mode][1] = sd.tc;
+                S.ih.dcs[mode][2] = sd.sctr;
+                S.ih.dcs[mode][3] = 0;
             }
         }
-        HL_SYNC();
-        if (act) {  // reconstruction with the residual; both distortions
-            const int r = coop_idct(c.K, c.K.p == 0 ? S.dcY[slot * 16 + kDcPos[blk]] : coop_dequant(q, c.K.ls, F.qp));
-            const int rec = clip255(pred + r);
-            S.ih_rec[mode][y * 16 + x] = (uint8_t)rec;
-            const int df = row_sum(iabs(sv - rec)), dz = row_sum(iabs(sv - pred));
-            if (c.K.p == 0) {
-                S.i16_dist[row] = df;
-                S.i16_distz[row] = dz;
-            }
-        }
-        HL_SYNC();
-        if (c.tid < 32 * kSlots && i16_mode_avail(S, m0 + (c.tid >> 5))) {  // lanes 32 s + 16 z + b: slot s, z = without residual
-            const int ds = c.tid >> 5, z = (c.tid >> 4) & 1, b = c.tid & 15;
-            const int v = row_sum(z ? S.i16_distz[ds * 16 + b] : S.i16_dist[ds * 16 + b]);
-            if (b == 0) S.ih.dist[m0 + ds][z] = v;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // reconstruction with the residual (the scaled DC kept); both distortions
+        int rr[4];
+        quad_idct(Q, q, qp, rr, true, S.dcY[mode * 16 + kDcPos[blk]]);
+        uint32_t rec = 0;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) rec |= (uint32_t)clip255((int)((pr >> (8 * cc)) & 255) + rr[cc]) << (8 * cc);
+        *reinterpret_cast<uint32_t*>(&S.ih_rec[mode][y * 16 + xO]) = rec;
+        // per-row sums of |residual| over the wave, then its four 16-lane rows
+        const int df = row_sum((int)__builtin_amdgcn_sad_u8(sv, rec, 0u)), dz = row_sum((int)__builtin_amdgcn_sad_u8(sv, pr, 0u));
+        const int tf = __builtin_amdgcn_readlane(df, 0) + __builtin_amdgcn_readlane(df, 16) + __builtin_amdgcn_readlane(df, 32) + __builtin_amdgcn_readlane(df, 48);
+        const int tz = __builtin_amdgcn_readlane(dz, 0) + __builtin_amdgcn_readlane(dz, 16) + __builtin_amdgcn_readlane(dz, 32) + __builtin_amdgcn_readlane(dz, 48);
+        if (lane == 0) {
+            S.ih.dist[mode][0] = tf;
+            S.ih.dist[mode][1] = tz;
         }
     }
     HL_SYNC();
@@ -3553,7 +3566,38 @@ HD double guess_intra(Ctx& c, const IntraSpec* hin = nullptr)
     const int cmode = i16mode == 0 ? 2 : (i16mode == 3 ? 3 : (i16mode == 1 ? 1 : 0));
     bool is_i16 = false;
     if (c4 < c16) {
-        HL_SYNC();
+#if defined(__HIP_DEVICE_COMPILE__)
+        // the predicted modes of the 16 blocks at once, in lanes 0-15 of
+        // every wave (pred_modes_4x4 on lane l = block l; wave 0 stores them):
+        // the count of mode remainders is then known to every wave without a
+        // barrier.  (The barrier above ordered every read of the fields lane 0
+        // rewrites here; the next reads are behind intra_chroma_pred's.)
+        const int l = c.tid & 63;
+        bool pf = true;
+        if (l < 16) {
+            const int blk = l, bx = blk_x(blk), by = blk_y(blk), m = S.i4mode[blk];
+            const bool aA = bx ? true : S.nb[1].avail != 0, aB = by ? true : S.nb[2].avail != 0;
+            const int pmA = bx ? PM_I4 : S.nb_pm0[1], pmB = by ? PM_I4 : S.nb_pm0[2];
+            const int iA = bx ? S.i4mode[blk_idx(bx - 4, by)] : (aA ? S.nb_i4[1][blk_idx(12, by)] : 2);
+            const int iB = by ? S.i4mode[blk_idx(bx, by - 4)] : (aB ? S.nb_i4[2][blk_idx(bx, 12)] : 2);
+            const bool dcf = !aA || !aB;
+            const int mA = (dcf || pmA != PM_I4) ? 2 : iA, mB = (dcf || pmB != PM_I4) ? 2 : iB;
+            const int pred = mA < mB ? mA : mB;
+            pf = pred == m;
+            if (c.tid < 16) {
+                S.prev_flag[blk] = pf ? 1 : 0;
+                if (!pf) S.rem_mode[blk] = (int8_t)(m < pred ? m : m - 1);
+            }
+        }
+        const int nz = __popcll(__ballot(!pf));
+        if (c.tid == 0) {
+            S.mb_type = 0;
+            S.e_type = ET_I_NXN;
+            S.flags = FL_INTRA;
+            S.pm0 = PM_I4;
+            S.cbp_l4x4 = cbp4;
+        }
+#else
         if (c.tid == 0) {
             S.mb_type = 0;
             S.e_type = ET_I_NXN;
@@ -3562,13 +3606,12 @@ HD double guess_intra(Ctx& c, const IntraSpec* hin = nullptr)
             S.cbp_l4x4 = cbp4;
             pred_modes_4x4(S);
         }
-        HL_SYNC();
         int nz = 0;
         for (int b = 0; b < 16; ++b) nz += !S.prev_flag[b];
+#endif
         c4 = dadd(c4, dmul(F.lambda, (double)(16 + nz * 3)));
     }
     if (c16 <= c4) is_i16 = true;
-    HL_SYNC();
     if (c.tid == 0) {
         S.chroma_mode = cmode;
         S.mad = is_i16 ? d16 : d4;
@@ -3580,7 +3623,6 @@ HD double guess_intra(Ctx& c, const IntraSpec* hin = nullptr)
             S.cbp_l4x4 = cbp16;
         }
     }
-    HL_SYNC();
     intra_chroma_pred(c, cmode);
     reconstruct_chroma(c, true);
     if (is_i16) {

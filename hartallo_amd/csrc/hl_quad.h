@@ -22,6 +22,9 @@
 namespace hl {
 
 constexpr int kQX1 = 0xB1, kQX2 = 0x4E, kQX3 = 0x1B;  // quad_perm lane ^ 1, lane ^ 2, lane ^ 3
+#ifndef HL_CAVLC_REGLOOP  // 1: quad_cavlc's level chain over registers (see there)
+#define HL_CAVLC_REGLOOP 1
+#endif
 
 // A DPP read kept as its own v_mov_b32_dpp: the empty asm stops LLVM's DPP
 // combiner from folding it into the subtraction that consumes it.  On the
@@ -238,11 +241,28 @@ __device__ __forceinline__ CoopStat quad_cavlc(const CoopTables& T, const LaneQ&
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         int sl = sl0;
+#if HL_CAVLC_REGLOOP
+        // the 16 words in registers at once (four ds_read_b128 in flight), then
+        // the chain over them unrolled: no LDS round trip per level
+        const int4 w0 = reinterpret_cast<const int4*>(lvs)[0], w1 = reinterpret_cast<const int4*>(lvs)[1];
+        const int4 w2 = reinterpret_cast<const int4*>(lvs)[2], w3 = reinterpret_cast<const int4*>(lvs)[3];
+        const int v[16] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z, w3.w};
+        const int n = tc - t1;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (__ballot(k < n) == 0) break;  // (wave-uniform exit)
+            if (k < n) {
+                bits += level_len(sl, v[k] >> 16);
+                sl = next_sl(sl, v[k] & 0xFFFF);
+            }
+        }
+#else
         for (int k = 0; k < tc - t1; ++k) {
             const int v = lvs[k];
             bits += level_len(sl, v >> 16);
             sl = next_sl(sl, v & 0xFFFF);
         }
+#endif
     }
     st.tc = tc;
     st.t1 = tc ? t1 : 0;
