@@ -267,7 +267,12 @@ __device__ __forceinline__ CoopStat quad_cavlc(const CoopTables& T, const LaneQ&
     st.tc = tc;
     st.t1 = tc ? t1 : 0;
     st.rest = tc ? bits : 0;
-    st.sctr = tc == 0 ? -1 : ((tc == 1 && ones == nz) ? (hi == 0 ? 3 : (hi < 3 ? 2 : (hi < 6 ? 1 : 0))) : 9);
+    // single-coefficient counter: 3 / 2 / 1 / 0 for a lone +-1 at list index
+    // 0 / 1-2 / 3-5 / 6+, 2 bits per index in 0x56B; 9 otherwise; -1 if none
+    // (selects only: the nested conditional became branches)
+    const int lone = (int)((0x56Bu >> (2 * hi)) & 3u);
+    const int sc = (int)(tc == 1) & (int)(ones == nz) ? lone : 9;
+    st.sctr = tc ? sc : -1;
     return st;
 }
 
