@@ -28,17 +28,23 @@ HD uint8_t qpel_plane_sample(const uint8_t* ref, int W, int H, int plane, int x,
 #if defined(__HIPCC__)
 // Quarter-pel planes (full, b, h, j) of a reference picture, padded by kPad
 // (qpel_plane_sample, hl_filters.h: every tap coordinate clamped to the
-// picture independently, interpol.c:74-225).  One workgroup per 256x16 tile
-// of the padded planes: the clamped source tile with its 6-tap apron is
-// staged in LDS as 4-byte words (one aligned global load per word inside the
-// picture), then every lane computes 16 consecutive samples of one row of
-// each plane from 6 LDS rows and writes them as one 16-byte store per plane.
-// HBM-bound: 1 B/px read, 4 B per padded pixel written.
-constexpr int kPlTileW = 256, kPlTileH = 16;
+// picture independently, interpol.c:74-225).  One workgroup per
+// (16 kPlSpt) x 16 tile of the padded planes: the clamped source tile with
+// its 6-tap apron is staged in LDS as 4-byte words (one aligned global load
+// per word inside the picture), then every lane computes kPlSpt consecutive
+// samples of one row of each plane from 6 LDS rows and writes them with one
+// store per plane.  HBM-bound: 1 B/px read, 4 B per padded pixel written.
+#ifndef HL_PL_SPT
+#define HL_PL_SPT 8  // samples per lane and plane: 4, 8 or 16 (8: 6.5 us per 1088p picture, 16: 8.0, 4: 8.1, profiles/r05_ab_planes_samples_per_lane.log)
+#endif
+constexpr int kPlSpt = HL_PL_SPT;
+static_assert(kPlSpt == 4 || kPlSpt == 8 || kPlSpt == 16, "a lane's samples are one 4-, 8- or 16-byte store per plane");
+constexpr int kPlTileW = 16 * kPlSpt, kPlTileH = 16;
 __global__ __launch_bounds__(256) void k_planes(const uint8_t* __restrict__ ref, int W, int H, uint8_t* __restrict__ pl0, int pstride,
                                                 int plsz)
 {
     constexpr int TWW = (kPlTileW + 8) / 4, TR = kPlTileH + 5;  // words per tile row (apron 2 + 3, alignment 3), rows
+    constexpr int NW = kPlSpt / 4;                               // output words per lane and plane
     __shared__ uint32_t T[TR][TWW + 1];
     const int PW = W + 2 * kPad, PH = H + 2 * kPad;
     const int tx = blockIdx.x * kPlTileW, ty = blockIdx.y * kPlTileH;  // tile origin, padded coordinates
@@ -64,19 +70,21 @@ __global__ __launch_bounds__(256) void k_planes(const uint8_t* __restrict__ ref,
     }
     __syncthreads();
     const int tr = threadIdx.x >> 4, tc = threadIdx.x & 15;
-    const int py = ty + tr, px = tx + tc * 16;
-    if (py >= PH || px >= PW) return;  // PW is a multiple of 16: a 16-sample group never straddles it
-    // columns tc*16 + o + j (j = 0..20) of rows tr..tr+5: bytes of words tc*4 .. tc*4+5
+    const int py = ty + tr, px = tx + tc * kPlSpt;
+    if (py >= PH || px >= PW) return;  // PW is a multiple of 16: a lane's group never straddles it
+    // columns tc*kPlSpt + o + j (j = 0..kPlSpt+4) of rows tr..tr+5
     auto byte_at = [&](int r, int j) -> int {
-        const int c = tc * 16 + o + j;
+        const int c = tc * kPlSpt + o + j;
         return (int)((T[tr + r][c >> 2] >> (8 * (c & 3))) & 0xffu);
     };
-    int vs[21];
+    int vs[kPlSpt + 5];
 #pragma unroll
-    for (int j = 0; j < 21; ++j) vs[j] = tap6(byte_at(0, j), byte_at(1, j), byte_at(2, j), byte_at(3, j), byte_at(4, j), byte_at(5, j));
-    uint32_t f[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, h[4] = {0, 0, 0, 0}, jj[4] = {0, 0, 0, 0};
+    for (int j = 0; j < kPlSpt + 5; ++j) vs[j] = tap6(byte_at(0, j), byte_at(1, j), byte_at(2, j), byte_at(3, j), byte_at(4, j), byte_at(5, j));
+    uint32_t f[NW], b[NW], h[NW], jj[NW];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int q = 0; q < NW; ++q) f[q] = b[q] = h[q] = jj[q] = 0;
+#pragma unroll
+    for (int k = 0; k < kPlSpt; ++k) {
         const int sf = byte_at(2, k + 2);
         int vb = (tap6(byte_at(2, k), byte_at(2, k + 1), sf, byte_at(2, k + 3), byte_at(2, k + 4), byte_at(2, k + 5)) + 16) >> 5;
         int vh = (vs[k + 2] + 16) >> 5;
@@ -93,10 +101,15 @@ __global__ __launch_bounds__(256) void k_planes(const uint8_t* __restrict__ ref,
         jj[q] |= (uint32_t)clip255(vj) << sh;
     }
     const size_t at = (size_t)py * pstride + px;
-    *reinterpret_cast<uint4*>(pl0 + at) = make_uint4(f[0], f[1], f[2], f[3]);
-    *reinterpret_cast<uint4*>(pl0 + plsz + at) = make_uint4(b[0], b[1], b[2], b[3]);
-    *reinterpret_cast<uint4*>(pl0 + 2 * (size_t)plsz + at) = make_uint4(h[0], h[1], h[2], h[3]);
-    *reinterpret_cast<uint4*>(pl0 + 3 * (size_t)plsz + at) = make_uint4(jj[0], jj[1], jj[2], jj[3]);
+    auto put = [&](uint8_t* p, const uint32_t* w) {
+        if constexpr (NW == 4) *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+        else if constexpr (NW == 2) *reinterpret_cast<uint2*>(p) = make_uint2(w[0], w[1]);
+        else *reinterpret_cast<uint32_t*>(p) = w[0];
+    };
+    put(pl0 + at, f);
+    put(pl0 + plsz + at, b);
+    put(pl0 + 2 * (size_t)plsz + at, h);
+    put(pl0 + 3 * (size_t)plsz + at, jj);
 }
 #endif
 
