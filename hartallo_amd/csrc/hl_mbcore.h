@@ -130,6 +130,9 @@ constexpr int kSpecMaxBlocks = HL_QUAD_EVAL ? HL_SPEC_MAX_BLOCKS : 8;
 #ifndef HL_LDS_WINDOW
 #define HL_LDS_WINDOW 0
 #endif
+#ifndef HL_DEFER_COMMIT  // 1: a search pass's commit after the next pass's candidate generation
+#define HL_DEFER_COMMIT 0
+#endif
 #ifndef HL_LDS_WINDOW_DMA  // 1: the window filled by LDS-DMA (with HL_LDS_WINDOW=1)
 #define HL_LDS_WINDOW_DMA 0
 #endif
@@ -1968,6 +1971,14 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     // point enabled; the half stage starts at the integer MV value read as
     // half-pel (me_ds.c:360)
     auto centre_of = [](int st, int m) { return st == 0 ? m : m >> 2; };
+#if defined(__HIP_DEVICE_COMPILE__) && HL_DEFER_COMMIT
+    // a pass's commit of the live state (commit_candidates) runs after the
+    // next pass's candidates are generated: the generation reads only the
+    // resolved search state, the commit only the pass's results, so the two
+    // dependent chains interleave; the next evaluation reads what the commit
+    // wrote (S.tc, the chain) after both
+    int pend_used = 0, pend_last = -1;
+#endif
     while (stage >= 0) {
         HL_PROF_T(tgap);
         // the chain: step 0 = the current step, then fresh stages from the
@@ -2017,6 +2028,10 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         }
 #if defined(HL_STEP_PROF)
         HL_PROF_ADD(c, 19, tgen);  // the pass's candidates generated and stored
+#endif
+#if HL_DEFER_COMMIT
+        if (pend_used) commit_candidates<REC>(c, g, pend_used, pend_last);  // the previous pass's (see above)
+        pend_used = 0;
 #endif
 #else
         {
@@ -2180,12 +2195,20 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
 #if defined(HL_STEP_PROF)
         HL_PROF_ADD(c, 18, tres);  // the chain resolved
 #endif
+#if HL_DEFER_COMMIT
+        pend_used = used;
+        pend_last = pv_last;
+#else
         if (used) commit_candidates<REC>(c, g, used, pv_last);
+#endif
 #else
         if (used) commit_candidates<REC>(c, g, used);
 #endif
         HL_PROF_ADD(c, 17, tsel);
     }
+#if defined(__HIP_DEVICE_COMPILE__) && HL_DEFER_COMMIT
+    if (pend_used) commit_candidates<REC>(c, g, pend_used, pend_last);
+#endif
     // (no barrier before these stores: after the last pass, waves still read
     // only the pass's candidate results, S.cd / S.wc / S.be_tcb, which lane 0
     // does not write here; the barrier below orders them for the next search)

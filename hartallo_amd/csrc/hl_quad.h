@@ -207,34 +207,50 @@ __device__ __forceinline__ CoopStat quad_cavlc(const CoopTables& T, const LaneQ&
     const int tzv = (&T.tz[0][0])[tzi < 15 * 16 ? tzi : 0];
     const int tzb = ((int)(tc > 0) & (int)(tc < 16)) ? tzv : 0;  // total_zeros length
     const int sl0 = ((int)(tc > 10) & (int)(t1 < 3)) ? 1 : 0;
-    int sum = 0, slow = 0, rbs = 0, m[4], lc[4], lvl[4];
+    // the first level coded with level_prefix/suffix: list index pf, the
+    // highest nonzero below the t1 trailing ones (-1: none)
+    uint32_t rest = nz;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) rest = k < t1 ? rest & ~(1u << ((31 - __clz(rest)) & 31)) : rest;
+    const int pf = rest ? 31 - __clz(rest) : -1;
+    int rbs = 0, absum = 0, slow = 0, lf = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int lis = li[c] < 0 ? 0 : li[c];
-        const int j = __popc(nz >> (lis + 1));  // order from the top
         const uint32_t lower = nz & ((1u << lis) - 1u);
         const int zl = lis - __popc(lower);
         const int run = lis - 1 - (31 - __clz(lower));  // lis when lower == 0 (__clz(0) = 32)
-        const int rb = (nzl[c] & (int)(lower != 0) & (int)(zl > 0)) ? quad_rb_len(zl, run) : 0;
-        m[c] = j - t1;
-        int l = L[c] > 0 ? (L[c] << 1) - 2 : -(L[c] << 1) - 1;
-        l -= ((int)(m[c] == 0) & (int)(t1 < 3) & (int)(l >= 2)) ? 2 : 0;
-        lc[c] = l;
-        lvl[c] = nzl[c] & (int)(m[c] >= 0);  // a level coded with level_prefix/suffix
-        slow |= lvl[c] & (int)(aL[c] > 3);
-        // fast path (no level above 3 in the block): suffixLength is sl0 for the
-        // first level and 1 after it; 0: lc + 1 (lc < 14), 1: (lc >> 1) + 2 (lc < 28)
-        const int len = ((int)(m[c] == 0) & (int)(sl0 == 0)) ? l + 1 : (l >> 1) + 2;
-        rbs += rb;
-        sum += rb + (lvl[c] ? len : 0);
+        rbs += (nzl[c] & (int)(lower != 0) & (int)(zl > 0)) ? quad_rb_len(zl, run) : 0;
+        absum += nzl[c] ? aL[c] : 0;
+        slow |= nzl[c] & (int)(aL[c] > 3);  // (a trailing one has magnitude 1)
+        lf = (nzl[c] & (int)(li[c] == pf)) ? L[c] : lf;
     }
     const bool qslow = quad_or(slow) != 0;  // uniform per quad
     int bits;
-    if (!qslow) bits = t1 + tzb + quad_sum(sum);
+    if (!qslow) {
+        // fast path (no level above 3 in the block): suffixLength is sl0 for
+        // the first level and 1 after it, where a level of magnitude a takes
+        // a + 1 bits; so the levels take (sum of magnitudes + tc) - 2 t1 (the
+        // trailing ones' share) with the first level's own length in place of
+        // its a + 1.  The first level (one lane of the quad) rides in the
+        // upper half of the sum.
+        const int q = quad_sum(rbs + absum + (lf << 16));
+        const int lo16 = q & 0xFFFF, lfq = (q - lo16) >> 16;
+        const int af = lfq < 0 ? -lfq : lfq;
+        int l = lfq > 0 ? (lfq << 1) - 2 : -(lfq << 1) - 1;
+        l -= ((int)(t1 < 3) & (int)(l >= 2)) ? 2 : 0;
+        const int lenf = sl0 == 0 ? l + 1 : (l >> 1) + 2;  // 0: lc + 1 (lc < 14), 1: (lc >> 1) + 2 (lc < 28)
+        bits = t1 + tzb + lo16 + tc - 2 * t1 + (tc > t1 ? lenf - (af + 1) : 0);
+    }
     else {
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-            if (lvl[c]) lvs[m[c]] = (lc[c] << 16) | aL[c];
+        for (int c = 0; c < 4; ++c) {
+            const int lis = li[c] < 0 ? 0 : li[c];
+            const int m = __popc(nz >> (lis + 1)) - t1;  // order from the top, past the trailing ones
+            int l = L[c] > 0 ? (L[c] << 1) - 2 : -(L[c] << 1) - 1;
+            l -= ((int)(m == 0) & (int)(t1 < 3) & (int)(l >= 2)) ? 2 : 0;
+            if (nzl[c] & (int)(m >= 0)) lvs[m] = (l << 16) | aL[c];  // a level coded with level_prefix/suffix
+        }
         bits = t1 + tzb + quad_sum(rbs);
         // the suffixLength chain over the block's levels, in order (residual.c:813-858)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
