@@ -183,12 +183,27 @@ struct CoopTables {
     uint8_t tz[15][16];      // total_zeros lengths
     uint8_t tok[3][4][17];   // coeff_token lengths, nC < 8
     uint8_t pad[4];
+    uint8_t rb[16][16];      // run_before lengths [zerosLeft][run] (0 for zerosLeft 0 and run > zerosLeft)
 };
+
+// CoopTables::rb as a constant (Table 9-10 by zerosLeft and run)
+struct RbTab {
+    uint8_t v[16][16];
+};
+constexpr RbTab make_rb_tab()
+{
+    RbTab t{};
+    for (int zl = 1; zl < 16; ++zl)
+        for (int run = 0; run <= zl && run < 15; ++run) t.v[zl][run] = kRbLen[zl <= 6 ? zl - 1 : 6][run];
+    return t;
+}
+constexpr RbTab kRbTab = make_rb_tab();
 
 __device__ __forceinline__ void coop_tables_init(CoopTables& T, int tid, int nthr)
 {
     for (int i = tid; i < 15 * 16; i += nthr) T.tz[i >> 4][i & 15] = kTzLen[i >> 4][i & 15];
     for (int i = tid; i < 3 * 4 * 17; i += nthr) T.tok[i / 68][(i / 17) % 4][i % 17] = kTokLen[i / 68][(i / 17) % 4][i % 17];
+    for (int i = tid; i < 16 * 16; i += nthr) T.rb[i >> 4][i & 15] = kRbTab.v[i >> 4][i & 15];
 }
 
 __device__ __forceinline__ int coop_token_len(const CoopTables& T, int nC, int tc, int t1)

@@ -816,7 +816,7 @@ __device__ __forceinline__ void mb_begin(Ctx& c)
     static_assert(5 * kW + 32 <= 448 && kMbThreads >= 464, "mb_begin lane map");
     // ---- round 1: loads (addresses clamped to valid memory, values unused there)
     uint4 q = make_uint4(0, 0, 0, 0);
-    int b1 = kNA, b2 = 0, b3 = 0;
+    int b1 = kNA, b2 = 0, b3 = 0, b4 = 0;
     if (tid < 5 * kW) {
         const int w = tid / kW, i = tid - w * kW;
         const int off = w == 0 ? 0 : (w == 1 ? -1 : (w == 2 ? -F.mbw : (w == 3 ? -F.mbw + 1 : -F.mbw - 1)));
@@ -850,6 +850,7 @@ __device__ __forceinline__ void mb_begin(Ctx& c)
     }
     if (tid < 15 * 16) b2 = kTzLen[tid >> 4][tid & 15];
     if (tid < 3 * 4 * 17) b3 = kTokLen[tid / 68][(tid / 17) % 4][tid % 17];
+    if (HL_RB_TABLE && tid >= 256) b4 = kRbTab.v[(tid - 256) >> 4][tid & 15];
     // ---- stores
     if (tid < 5 * kW) reinterpret_cast<uint4*>(S.nbst)[tid] = q;
     else if (tid < 5 * kW + 16) reinterpret_cast<uint4*>(S.src)[tid - 5 * kW] = q;
@@ -863,6 +864,7 @@ __device__ __forceinline__ void mb_begin(Ctx& c)
     else if (tid >= 96 && tid < 112) S.cleft[(tid - 96) >> 3][(tid - 96) & 7] = (int16_t)b1;
     if (tid < 15 * 16) S.ct.tz[tid >> 4][tid & 15] = (uint8_t)b2;
     if (tid < 3 * 4 * 17) S.ct.tok[tid / 68][(tid / 17) % 4][tid % 17] = (uint8_t)b3;
+    if (HL_RB_TABLE && tid >= 256) S.ct.rb[(tid - 256) >> 4][tid & 15] = (uint8_t)b4;
     if (tid >= 448 && tid < 464) {
         const int8_t* e = kQpelTab[tid - 448];
         S.qtab[tid - 448] = (uint32_t)(e[0] | (e[1] << 2) | (e[2] << 3) | ((e[3] >= 0) << 4) | ((e[3] >= 0 ? e[3] : 0) << 5) | (e[4] << 7) | (e[5] << 8));

@@ -22,6 +22,9 @@
 namespace hl {
 
 constexpr int kQX1 = 0xB1, kQX2 = 0x4E, kQX3 = 0x1B;  // quad_perm lane ^ 1, lane ^ 2, lane ^ 3
+#ifndef HL_RB_TABLE  // 1: run_before lengths from an LDS table instead of the packed closed form
+#define HL_RB_TABLE 1
+#endif
 #ifndef HL_CAVLC_REGLOOP  // 1: quad_cavlc's level chain over registers (see there)
 #define HL_CAVLC_REGLOOP 1
 #endif
@@ -213,19 +216,26 @@ __device__ __forceinline__ CoopStat quad_cavlc(const CoopTables& T, const LaneQ&
 #pragma unroll
     for (int k = 0; k < 3; ++k) rest = k < t1 ? rest & ~(1u << ((31 - __clz(rest)) & 31)) : rest;
     const int pf = rest ? 31 - __clz(rest) : -1;
-    int rbs = 0, absum = 0, slow = 0, lf = 0;
+    int rbs = 0, absum = 0, amax = 0, lf = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int lis = li[c] < 0 ? 0 : li[c];
         const uint32_t lower = nz & ((1u << lis) - 1u);
         const int zl = lis - __popc(lower);
         const int run = lis - 1 - (31 - __clz(lower));  // lis when lower == 0 (__clz(0) = 32)
+#if HL_RB_TABLE
+        // run_before length from the LDS table (zerosLeft 0 reads 0)
+        const int rbv = T.rb[zl & 15][run & 15];
+        rbs += (nzl[c] & (int)(lower != 0)) ? rbv : 0;
+#else
         rbs += (nzl[c] & (int)(lower != 0) & (int)(zl > 0)) ? quad_rb_len(zl, run) : 0;
-        absum += nzl[c] ? aL[c] : 0;
-        slow |= nzl[c] & (int)(aL[c] > 3);  // (a trailing one has magnitude 1)
+#endif
+        const int am = nzl[c] ? aL[c] : 0;
+        absum += am;
+        amax = max(amax, am);
         lf = (nzl[c] & (int)(li[c] == pf)) ? L[c] : lf;
     }
-    const bool qslow = quad_or(slow) != 0;  // uniform per quad
+    const bool qslow = quad_or((int)(amax > 3)) != 0;  // uniform per quad (a trailing one has magnitude 1)
     int bits;
     if (!qslow) {
         // fast path (no level above 3 in the block): suffixLength is sl0 for
