@@ -194,7 +194,7 @@ __device__ __forceinline__ CoopStat quad_cavlc(const CoopTables& T, const LaneQ&
         aL[c] = L[c] < 0 ? -L[c] : L[c];
         nzl[c] = (int)(li[c] >= 0) & (int)(L[c] != 0);
         const uint32_t sh = (uint32_t)li[c] & 15u;
-        const uint32_t bits = (1u << sh) | ((uint32_t)(aL[c] == 1) << (sh + 16));
+        const uint32_t bits = (aL[c] == 1 ? 0x10001u : 1u) << sh;  // nonzero, and magnitude 1 (bit + 16)
         mb |= nzl[c] ? (int)bits : 0;
     }
     const uint32_t masks = (uint32_t)quad_or(mb);
@@ -212,10 +212,12 @@ __device__ __forceinline__ CoopStat quad_cavlc(const CoopTables& T, const LaneQ&
     const int sl0 = ((int)(tc > 10) & (int)(t1 < 3)) ? 1 : 0;
     // the first level coded with level_prefix/suffix: list index pf, the
     // highest nonzero below the t1 trailing ones (-1: none)
+    // (with at most three trailing ones that is the highest coefficient above
+    // magnitude 1, hb; with more, the fourth nonzero from the top)
     uint32_t rest = nz;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) rest = k < t1 ? rest & ~(1u << ((31 - __clz(rest)) & 31)) : rest;
-    const int pf = rest ? 31 - __clz(rest) : -1;
+    for (int k = 0; k < 3; ++k) rest &= ~(1u << ((31 - __clz(rest)) & 31));
+    const int pf = t1a <= 3 ? hb : 31 - __clz(rest);
     int rbs = 0, absum = 0, amax = 0, lf = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
