@@ -130,6 +130,9 @@ constexpr int kSpecMaxBlocks = HL_QUAD_EVAL ? HL_SPEC_MAX_BLOCKS : 8;
 #ifndef HL_LDS_WINDOW
 #define HL_LDS_WINDOW 0
 #endif
+#ifndef HL_TC_MASKS  // 1: per-block masks of the candidates with a nonzero TotalCoeff (LDS OR in the
+#define HL_TC_MASKS 1  // evaluation) instead of scanning the TotalCoeff rows for the last writer
+#endif
 #ifndef HL_DEFER_COMMIT  // 1: a search pass's commit after the next pass's candidate generation
 #define HL_DEFER_COMMIT 0
 #endif
@@ -302,6 +305,7 @@ struct Shared {
     // already write the next step's -- a step only reuses the buffer of the
     // step before the previous one, whose readers all passed a barrier since.
     alignas(16) uint8_t be_tcb[2][16][kMaxCand];         // TotalCoeff [parity][block][candidate]
+    uint32_t be_tcm[3][16];  // HL_TC_MASKS: candidates with a nonzero TotalCoeff [pass mod 3][block]
     alignas(16) int32_t lvs[kMaxWaves * 4][16];          // per-row level scratch of coop_cavlc
     alignas(16) int32_t lvq[kMaxWaves * 16][16];         // per-quad level scratch of quad_cavlc
     CoopTables ct;
@@ -417,6 +421,7 @@ struct Ctx {
     int wux = 0, wuy = 0;   // usable columns / rows of the LDS search window (0: none)
     int spec = 0;           // 1 = chain is still a row-start speculation (uniform)
     int par = 0;            // buffer parity of the last candidate step (Shared::cd, be_tcb)
+    int p3 = 0;             // the last candidate step's slot of Shared::be_tcm (pass mod 3)
     int f3rec = 0;          // 1 = fam3_helper: record entry-value intervals and written blocks (Shared::f3*)
 #if defined(HL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
     unsigned long long pacc[kProfSlots] = {};
@@ -865,6 +870,7 @@ __device__ __forceinline__ void mb_begin(Ctx& c)
     if (tid < 15 * 16) S.ct.tz[tid >> 4][tid & 15] = (uint8_t)b2;
     if (tid < 3 * 4 * 17) S.ct.tok[tid / 68][(tid / 17) % 4][tid % 17] = (uint8_t)b3;
     if (HL_RB_TABLE && tid >= 256) S.ct.rb[(tid - 256) >> 4][tid & 15] = (uint8_t)b4;
+    if (tid >= kMbThreads - 48) (&S.be_tcm[0][0])[tid - (kMbThreads - 48)] = 0u;  // every slot empty at the MB start
     if (tid >= 448 && tid < 464) {
         const int8_t* e = kQpelTab[tid - 448];
         S.qtab[tid - 448] = (uint32_t)(e[0] | (e[1] << 2) | (e[2] << 3) | ((e[3] >= 0) << 4) | ((e[3] >= 0 ? e[3] : 0) << 5) | (e[4] << 7) | (e[5] << 8));
@@ -1002,6 +1008,7 @@ HD void mb_begin(Ctx& c)
     const int av[5] = {1, hasA, hasB, hasC, hasD};
 #if defined(__HIP_DEVICE_COMPILE__)
     coop_tables_init(S.ct, tid, nthr);
+    for (int t = tid; t < 48; t += nthr) (&S.be_tcm[0][0])[t] = 0u;  // every slot empty at the MB start
     for (int t = tid; t < 16; t += nthr) {
         const int8_t* e = kQpelTab[t];
         S.qtab[t] = (uint32_t)(e[0] | (e[1] << 2) | (e[2] << 3) | ((e[3] >= 0) << 4) | ((e[3] >= 0 ? e[3] : 0) << 5) | (e[4] << 7) | (e[5] << 8));
@@ -1251,6 +1258,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
     const FrameArgs& F = c.F;
     Shared& S = c.S;
     c.par ^= 1;
+    c.p3 = c.p3 == 2 ? 0 : c.p3 + 1;
     Shared::CandRes& R = S.cd[c.par];
     uint8_t(&tcb)[16][kMaxCand] = S.be_tcb[c.par];
     HL_PROF_T(tp0);
@@ -1355,6 +1363,9 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                     S.be_w1[ci][k] = st.rest | (dist << 16);
                     S.be_w2[ci][k] = tok;
                     tcb[k][ci] = (uint8_t)st.tc;
+#if HL_TC_MASKS
+                    if (st.tc) atomicOr(&S.be_tcm[c.p3][k], 1u << ci);
+#endif
                     if (g.nblk == 1) {
                         // a single-block partition: both nC neighbours lie outside it, so the
                         // nC (and the candidate's cost) needs no other block (phase 2 skipped)
@@ -1482,6 +1493,12 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
 #else
     HL_SYNC();
 #endif
+#if defined(__HIP_DEVICE_COMPILE__) && HL_QUAD_EVAL && HL_TC_MASKS
+    // the slot the pass after next ORs into: its last readers (the phase 2
+    // and commit of the pass before this one) are done, and its first
+    // writer runs after the next pass's barrier above
+    if (c.tid < 16) S.be_tcm[c.p3 == 0 ? 2 : c.p3 - 1][c.tid] = 0;
+#endif
 #if defined(HL_NBLK_PROF)  // phase 1 by partition size: slots 12..15 = 1, 2, 4, 8+ blocks
     HL_PROF_ADD(c, 12 + (g.nblk >= 8 ? 3 : g.lnb), tp0);
 #endif
@@ -1523,7 +1540,12 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                     nA = aA ? eA : 0;
                 }
                 else if (cbp & (1 << (niA >> 2))) {
+#if HL_TC_MASKS
+                    const uint32_t mA = inA ? S.be_tcm[c.p3][kkA] & allow : 0u;
+                    const int v = mA ? (int)rA[31 - __clz(mA)] : -1;
+#else
                     const int v = inA ? tcb_last(rA, allow) : -1;
+#endif
                     nA = v >= 0 ? v : tA;
                     enA = HL_F3REC(c) && v < 0 && !((f3w >> niA) & 1);
                 }
@@ -1532,7 +1554,12 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                     nB = aB ? eB : 0;
                 }
                 else if (cbp & (1 << (niB >> 2))) {
+#if HL_TC_MASKS
+                    const uint32_t mB = inB ? S.be_tcm[c.p3][kkB] & allow : 0u;
+                    const int v = mB ? (int)rB[31 - __clz(mB)] : -1;
+#else
                     const int v = inB ? tcb_last(rB, allow) : -1;
+#endif
                     nB = v >= 0 ? v : tB;
                     enB = HL_F3REC(c) && v < 0 && !((f3w >> niB) & 1);
                 }
@@ -1689,7 +1716,12 @@ HD void commit_candidates(Ctx& c, const PartGeo& g, int n, int last_l = -2)
     const uint8_t(&tcb)[16][kMaxCand] = S.be_tcb[c.par];
     if (c.tid < g.nblk) {
         const int k = c.tid;
+#if HL_TC_MASKS
+        const uint32_t mk = S.be_tcm[c.p3][k] & (n >= 32 ? ~0u : (1u << n) - 1u);
+        const int v = mk ? (int)tcb[k][31 - __clz(mk)] : -1;
+#else
         const int v = tcb_last(tcb[k], n >= 32 ? ~0u : (1u << n) - 1u);
+#endif
         const int bi = blk_idx(g.px + ((k & (g.nbw - 1)) << 2), g.py + ((k >> g.lbw) << 2));
         if (v >= 0) {
             S.tc[bi] = (int8_t)v;
