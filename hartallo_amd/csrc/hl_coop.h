@@ -184,6 +184,7 @@ struct CoopTables {
     uint8_t tok[3][4][17];   // coeff_token lengths, nC < 8
     uint8_t pad[4];
     uint8_t rb[16][16];      // run_before lengths [zerosLeft][run] (0 for zerosLeft 0 and run > zerosLeft)
+    uint32_t tok3[4][17];    // [t1][tc]: the coeff_token lengths of nC classes 0-2 in 5-bit fields, 6 (class 3) at bit 15
 };
 
 // CoopTables::rb as a constant (Table 9-10 by zerosLeft and run)
@@ -198,12 +199,25 @@ constexpr RbTab make_rb_tab()
     return t;
 }
 constexpr RbTab kRbTab = make_rb_tab();
+struct Tok3Tab {
+    uint32_t v[4][17];
+};
+constexpr Tok3Tab make_tok3_tab()
+{
+    Tok3Tab t{};
+    for (int t1 = 0; t1 < 4; ++t1)
+        for (int tc = 0; tc < 17; ++tc)
+            t.v[t1][tc] = (uint32_t)kTokLen[0][t1][tc] | (uint32_t)kTokLen[1][t1][tc] << 5 | (uint32_t)kTokLen[2][t1][tc] << 10 | 6u << 15;
+    return t;
+}
+constexpr Tok3Tab kTok3Tab = make_tok3_tab();
 
 __device__ __forceinline__ void coop_tables_init(CoopTables& T, int tid, int nthr)
 {
     for (int i = tid; i < 15 * 16; i += nthr) T.tz[i >> 4][i & 15] = kTzLen[i >> 4][i & 15];
     for (int i = tid; i < 3 * 4 * 17; i += nthr) T.tok[i / 68][(i / 17) % 4][i % 17] = kTokLen[i / 68][(i / 17) % 4][i % 17];
     for (int i = tid; i < 16 * 16; i += nthr) T.rb[i >> 4][i & 15] = kRbTab.v[i >> 4][i & 15];
+    for (int i = tid; i < 4 * 17; i += nthr) T.tok3[i / 17][i % 17] = kTok3Tab.v[i / 17][i % 17];
 }
 
 __device__ __forceinline__ int coop_token_len(const CoopTables& T, int nC, int tc, int t1)

@@ -130,6 +130,9 @@ constexpr int kSpecMaxBlocks = HL_QUAD_EVAL ? HL_SPEC_MAX_BLOCKS : 8;
 #ifndef HL_LDS_WINDOW
 #define HL_LDS_WINDOW 0
 #endif
+#ifndef HL_QOFF_TABLE  // 1: put_cand's sample offsets from a per-phase table built at the MB start
+#define HL_QOFF_TABLE 1
+#endif
 #ifndef HL_TC_MASKS  // 1: per-block masks of the candidates with a nonzero TotalCoeff (LDS OR in the
 #define HL_TC_MASKS 1  // evaluation) instead of scanning the TotalCoeff rows for the last writer
 #endif
@@ -298,7 +301,7 @@ struct Shared {
     CandSlot wc[kMaxWaves][kMaxCand];  // candidates of the step, one copy per wave (each wave writes its own)
     int32_t be_nz[kMaxCand][16], be_tc[kMaxCand][16], be_t1[kMaxCand][16], be_sctr[kMaxCand][16], be_bits[kMaxCand][16],
         be_dist[kMaxCand][16];
-    int32_t be_w0[kMaxCand][16], be_w1[kMaxCand][16], be_w2[kMaxCand][16];  // packed block statistics (device path)
+    alignas(16) int4 be_w[kMaxCand][16];  // packed block statistics (device path): w0, w1, w2 of eval_candidates, -
     // Per-step results are double-buffered by step parity (Ctx::par): after a
     // step's last barrier, waves still read its results (the candidate scan,
     // the live TotalCoeffs update, the Single_ctr chain) while faster waves
@@ -310,6 +313,7 @@ struct Shared {
     alignas(16) int32_t lvq[kMaxWaves * 16][16];         // per-quad level scratch of quad_cavlc
     CoopTables ct;
     uint32_t qtab[16];                                   // packed quarter-pel phase table
+    alignas(8) int2 qoff[16];  // per phase: plane offsets of the two prediction samples relative to (X, Y) (put_cand)
     struct CandRes {
         double cost[kMaxCand];
         int32_t bits[kMaxCand], dist[kMaxCand], single[kMaxCand], cbp[kMaxCand], last[kMaxCand];
@@ -856,6 +860,8 @@ __device__ __forceinline__ void mb_begin(Ctx& c)
     if (tid < 15 * 16) b2 = kTzLen[tid >> 4][tid & 15];
     if (tid < 3 * 4 * 17) b3 = kTokLen[tid / 68][(tid / 17) % 4][tid % 17];
     if (HL_RB_TABLE && tid >= 256) b4 = kRbTab.v[(tid - 256) >> 4][tid & 15];
+    uint32_t b5 = 0;
+    if (tid >= 240 && tid < 240 + 4 * 17) b5 = kTok3Tab.v[(tid - 240) / 17][(tid - 240) % 17];
     // ---- stores
     if (tid < 5 * kW) reinterpret_cast<uint4*>(S.nbst)[tid] = q;
     else if (tid < 5 * kW + 16) reinterpret_cast<uint4*>(S.src)[tid - 5 * kW] = q;
@@ -870,10 +876,14 @@ __device__ __forceinline__ void mb_begin(Ctx& c)
     if (tid < 15 * 16) S.ct.tz[tid >> 4][tid & 15] = (uint8_t)b2;
     if (tid < 3 * 4 * 17) S.ct.tok[tid / 68][(tid / 17) % 4][tid % 17] = (uint8_t)b3;
     if (HL_RB_TABLE && tid >= 256) S.ct.rb[(tid - 256) >> 4][tid & 15] = (uint8_t)b4;
+    if (tid >= 240 && tid < 240 + 4 * 17) S.ct.tok3[(tid - 240) / 17][(tid - 240) % 17] = b5;
     if (tid >= kMbThreads - 48) (&S.be_tcm[0][0])[tid - (kMbThreads - 48)] = 0u;  // every slot empty at the MB start
     if (tid >= 448 && tid < 464) {
         const int8_t* e = kQpelTab[tid - 448];
-        S.qtab[tid - 448] = (uint32_t)(e[0] | (e[1] << 2) | (e[2] << 3) | ((e[3] >= 0) << 4) | ((e[3] >= 0 ? e[3] : 0) << 5) | (e[4] << 7) | (e[5] << 8));
+        const uint32_t q = (uint32_t)(e[0] | (e[1] << 2) | (e[2] << 3) | ((e[3] >= 0) << 4) | ((e[3] >= 0 ? e[3] : 0) << 5) | (e[4] << 7) | (e[5] << 8));
+        S.qtab[tid - 448] = q;
+        const int o1 = (int)(q & 3) * F.plsz + (int)((q >> 3) & 1) * F.pstride + (int)((q >> 2) & 1);
+        S.qoff[tid - 448] = make_int2(o1, (q & 16) ? (int)((q >> 5) & 3) * F.plsz + (int)((q >> 8) & 1) * F.pstride + (int)((q >> 7) & 1) : o1);
     }
     HL_SYNC();
     // ---- round 2: derivations from LDS, spread over the waves
@@ -1011,7 +1021,10 @@ HD void mb_begin(Ctx& c)
     for (int t = tid; t < 48; t += nthr) (&S.be_tcm[0][0])[t] = 0u;  // every slot empty at the MB start
     for (int t = tid; t < 16; t += nthr) {
         const int8_t* e = kQpelTab[t];
-        S.qtab[t] = (uint32_t)(e[0] | (e[1] << 2) | (e[2] << 3) | ((e[3] >= 0) << 4) | ((e[3] >= 0 ? e[3] : 0) << 5) | (e[4] << 7) | (e[5] << 8));
+        const uint32_t q = (uint32_t)(e[0] | (e[1] << 2) | (e[2] << 3) | ((e[3] >= 0) << 4) | ((e[3] >= 0 ? e[3] : 0) << 5) | (e[4] << 7) | (e[5] << 8));
+        S.qtab[t] = q;
+        const int o1 = (int)(q & 3) * F.plsz + (int)((q >> 3) & 1) * F.pstride + (int)((q >> 2) & 1);
+        S.qoff[t] = make_int2(o1, (q & 16) ? (int)((q >> 5) & 3) * F.plsz + (int)((q >> 8) & 1) * F.pstride + (int)((q >> 7) & 1) : o1);
     }
 #endif
     // source samples
@@ -1189,8 +1202,17 @@ HD void put_cand(Ctx& c, int xo, int yo, int pw, int pht, int i, int mx, int my,
     const uint32_t e = (uint32_t)(w >> (9 * (ph < 7 ? ph : (ph < 14 ? ph - 7 : ph - 14)))) & 0x1FF;
     const int X = clip3(-17, F.W + 17, c.xL + xo + (mx >> 2)) + kPad, Y = clip3(-17, F.H + 17, c.yL + yo + (my >> 2)) + kPad;
     CandSlot cs;
+#if defined(__HIP_DEVICE_COMPILE__) && HL_QOFF_TABLE
+    // the phase's two sample offsets from the MB start's table (S.qoff)
+    const int2 qo = c.S.qoff[ph];
+    const int base = Y * F.pstride + X;
+    cs.off1 = qo.x + base;
+    cs.off2 = qo.y + base;
+    (void)e;
+#else
     cs.off1 = (int)(e & 3) * F.plsz + (Y + (int)((e >> 3) & 1)) * F.pstride + X + (int)((e >> 2) & 1);
     cs.off2 = (e & 16) ? (int)((e >> 5) & 3) * F.plsz + (Y + (int)((e >> 8) & 1)) * F.pstride + X + (int)((e >> 7) & 1) : cs.off1;
+#endif
     cs.mvx = (int16_t)mx;
     cs.mvy = (int16_t)my;
     cs.pad = pt;  // diamond point index
@@ -1355,13 +1377,10 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                     for (int cc = 0; cc < 4; ++cc) rec |= (uint32_t)clip255((int)((pr[j] >> (8 * cc)) & 255) + r[cc]) << (8 * cc);
                     dist = quad_sum((int)__builtin_amdgcn_sad_u8(sv[j], rec, 0u));
                     st = quad_cavlc(S.ct, Q, q, 0, S.lvq[qg]);
-                    if (Q.r == 0 && st.tc)  // coeff_token lengths for the four nC classes
-                        tok = S.ct.tok[0][st.t1][st.tc] | (S.ct.tok[1][st.t1][st.tc] << 5) | (S.ct.tok[2][st.t1][st.tc] << 10) | (6 << 15);
+                    if (Q.r == 0 && st.tc) tok = (int)S.ct.tok3[st.t1][st.tc];  // coeff_token lengths for the four nC classes
                 }
                 if (Q.r == 0) {
-                    S.be_w0[ci][k] = st.tc | (st.t1 << 5) | ((st.sctr + 1) << 8);
-                    S.be_w1[ci][k] = st.rest | (dist << 16);
-                    S.be_w2[ci][k] = tok;
+                    S.be_w[ci][k] = make_int4(st.tc | (st.t1 << 5) | ((st.sctr + 1) << 8), st.rest | (dist << 16), tok, 0);
                     tcb[k][ci] = (uint8_t)st.tc;
 #if HL_TC_MASKS
                     if (st.tc) atomicOr(&S.be_tcm[c.p3][k], 1u << ci);
@@ -1464,9 +1483,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                 HL_PROF_ADD(c, 15, ta3);
 #endif
                 if (c.K.p == 0) {
-                    S.be_w0[ci][k] = st.tc | (st.t1 << 5) | ((st.sctr + 1) << 8);
-                    S.be_w1[ci][k] = st.rest | (dist << 16);
-                    S.be_w2[ci][k] = tok;
+                    S.be_w[ci][k] = make_int4(st.tc | (st.t1 << 5) | ((st.sctr + 1) << 8), st.rest | (dist << 16), tok, 0);
                     tcb[k][ci] = (uint8_t)st.tc;
                     if (g.nblk == 1) {
                         // a single-block partition: both nC neighbours lie outside it, so the
@@ -1522,7 +1539,8 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         const int niA = bx ? blk_idx(bx - 4, by) : 0, niB = by ? blk_idx(bx, by - 4) : 0;
         const bool inA = bx - 4 >= g.px, inB = by - 4 >= g.py;  // neighbour inside the partition
         const int kkA = inA ? ((hy << g.lbw) + hx - 1) : 0, kkB = inB ? (((hy - 1) << g.lbw) + hx) : 0;
-        const int w0 = S.be_w0[ci][k], w1 = S.be_w1[ci][k], w2 = S.be_w2[ci][k];
+        const int4 wq = S.be_w[ci][k];
+        const int w0 = wq.x, w1 = wq.y, w2 = wq.z;
         const int eA = S.extA[bi], eB = S.extB[bi], cbp = S.cbp_l, tA = S.tc[niA], tB = S.tc[niB];
         const int f3w = HL_F3REC(c) ? S.f3w : 0;
         const uint8_t *rA = tcb[kkA], *rB = tcb[kkB];
@@ -1594,8 +1612,10 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                 last = ((k + 1) << 4) | sctr;
             }
         }
-        bits = row_sum(bits);
-        dist = row_sum(dist);
+        // bits (< 2^15 over 16 blocks) and distortion (< 2^17) in one row sum
+        const uint32_t pk = (uint32_t)row_sum((int)((uint32_t)bits | ((uint32_t)dist << 15)));
+        bits = (int)(pk & 0x7FFFu);
+        dist = (int)(pk >> 15);
         cs_sum = row_sum(cs_sum);
         last = row_max(last);
         if (k0 == 0) {
