@@ -130,6 +130,12 @@ constexpr int kSpecMaxBlocks = HL_QUAD_EVAL ? HL_SPEC_MAX_BLOCKS : 8;
 #ifndef HL_LDS_WINDOW
 #define HL_LDS_WINDOW 0
 #endif
+#ifndef HL_NC_SELECTS  // 1: the cost phase's neighbour TotalCoeffs and sums as selects (no branches)
+#define HL_NC_SELECTS 1
+#endif
+#ifndef HL_GRID_LANES  // 1: a searched partition's motion-grid cells written lane-parallel (shift indexing)
+#define HL_GRID_LANES 1
+#endif
 #ifndef HL_QOFF_TABLE  // 1: put_cand's sample offsets from a per-phase table built at the MB start
 #define HL_QOFF_TABLE 1
 #endif
@@ -1547,6 +1553,32 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         const CandSlot cs = S.wc[wave][ci];
         int bits = 0, dist = 0, cs_sum = 0, last = 0;
         const int tc = w0 & 31;
+#if HL_NC_SELECTS
+        if (!HL_FAM3 || !REC) {
+            // selects throughout (no exec-mask branches): the neighbours'
+            // TotalCoeffs as the nC reads them (live value of the last
+            // candidate up to ci that coded the block inside the partition,
+            // else the live state; 0 without coded luma in the 8x8; the
+            // neighbouring MB's value at the MB edge, -1 = not available)
+            const uint32_t allow = ci == 31 ? ~0u : (2u << ci) - 1u;  // candidates 0..ci
+            const bool cA = (cbp >> (niA >> 2)) & 1, cB = (cbp >> (niB >> 2)) & 1;
+            const uint32_t mA = inA ? S.be_tcm[c.p3][kkA] & allow : 0u, mB = inB ? S.be_tcm[c.p3][kkB] & allow : 0u;
+            const int vA = rA[mA ? 31 - __clz(mA) : 0], vB = rB[mB ? 31 - __clz(mB) : 0];
+            const bool aA = bx ? true : eA >= 0, aB = by ? true : eB >= 0;
+            const int nA = bx ? (cA ? (mA ? vA : tA) : 0) : (aA ? eA : 0);
+            const int nB = by ? (cB ? (mB ? vB : tB) : 0) : (aB ? eB : 0);
+            const int nC = (aA && aB) ? (nA + nB + 1) >> 1 : (aA ? nA : (aB ? nB : 0));
+            const int cls = nC < 2 ? 0 : (nC < 4 ? 1 : (nC < 8 ? 2 : 3));
+            const int sctr = ((w0 >> 8) & 15) - 1;
+            const bool coded = valid && tc;
+            dist = valid ? w1 >> 16 : 0;
+            bits = coded ? (w1 & 0xFFFF) + ((w2 >> (5 * cls)) & 31) : 0;
+            cs_sum = coded ? (1 << bi) | (sctr << 16) : 0;
+            last = coded ? ((k + 1) << 4) | sctr : 0;
+            (void)f3w;
+        }
+        else
+#endif
         if (valid) {
             dist = w1 >> 16;
             if (tc) {
@@ -2277,8 +2309,19 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         S.bmvp[pi][spi][1] = (int16_t)pmv[1];
         S.nb[0].mv[pi][spi][0] = (int16_t)b.mv[0];  // MvL0 feeds the MVP of later partitions
         S.nb[0].mv[pi][spi][1] = (int16_t)b.mv[1];
+#if !(defined(__HIP_DEVICE_COMPILE__) && HL_GRID_LANES)
         grid_set(S, g.px, g.py, g.pw, g.ph, b.mv[0], b.mv[1]);
+#endif
     }
+#if defined(__HIP_DEVICE_COMPILE__) && HL_GRID_LANES
+    // the partition's 4x4 blocks in the motion grid, lane k of wave 0 block k
+    // (shifts by the partition's log2 width, no division)
+    if (c.tid < g.nblk) {
+        const int bx = (g.px >> 2) + (c.tid & (g.nbw - 1)), by = (g.py >> 2) + (c.tid >> g.lbw);
+        S.mvs[by + 1][bx + 1] = 2;
+        S.mvg[by + 1][bx + 1] = (b.mv[0] & 0xFFFF) | (b.mv[1] << 16);
+    }
+#endif
     HL_SYNC();
     HL_PROF_ADD(c, 3, tsp);
     return probably;
