@@ -130,6 +130,9 @@ constexpr int kSpecMaxBlocks = HL_QUAD_EVAL ? HL_SPEC_MAX_BLOCKS : 8;
 #ifndef HL_LDS_WINDOW
 #define HL_LDS_WINDOW 0
 #endif
+#ifndef HL_MVP_SELECTS  // 1: the motion vector predictor as selects
+#define HL_MVP_SELECTS 1
+#endif
 #ifndef HL_NC_SELECTS  // 1: the cost phase's neighbour TotalCoeffs and sums as selects (no branches)
 #define HL_NC_SELECTS 1
 #endif
@@ -582,6 +585,27 @@ HD void mvp(const Shared& S, const PartShape& ps, int pi, int spi, int out[2])
     }
     MvN nb[3];
     nb_motion(S, x + xS, y + yS, ppw, nb);
+#if defined(__HIP_DEVICE_COMPILE__) && HL_MVP_SELECTS
+    {
+        // 8.4.1.3 as selects (the values are uniform but live in VGPRs: every
+        // branch on them would be an exec-mask branch)
+        const MvN A = nb[0], B = nb[1], C = nb[2];
+        const bool a2 = A.st == 2, b2 = B.st == 2, c2 = C.st == 2;
+        const bool p168 = ps.part_w == 16 && ps.part_h == 8, p816 = ps.part_w == 8 && ps.part_h == 16;
+        int sel = (p168 && pi == 0 && b2) ? 1 : ((p168 && pi == 1 && a2) ? 0 : ((p816 && pi == 0 && a2) ? 0 : ((p816 && pi == 1 && c2) ? 2 : -1)));
+        const bool rep = B.st == 0 && C.st == 0 && A.st != 0;  // B and C replaced by A
+        const bool eb2 = rep ? a2 : b2, ec2 = rep ? a2 : c2;
+        const int bx = rep ? A.mv[0] : B.mv[0], by = rep ? A.mv[1] : B.mv[1];
+        const int cx = rep ? A.mv[0] : C.mv[0], cy = rep ? A.mv[1] : C.mv[1];
+        const int one = (a2 && !eb2 && !ec2) ? 0 : ((eb2 && !ec2 && !a2) ? 1 : ((ec2 && !eb2 && !a2) ? 2 : -1));
+        sel = sel >= 0 ? sel : one;
+        // (a directional pick of B or C needs it inter-coded, so no
+        // replacement happened: bx / cx are B's / C's own motion then)
+        out[0] = sel == 0 ? A.mv[0] : (sel == 1 ? bx : (sel == 2 ? cx : median3(A.mv[0], bx, cx)));
+        out[1] = sel == 0 ? A.mv[1] : (sel == 1 ? by : (sel == 2 ? cy : median3(A.mv[1], by, cy)));
+        return;
+    }
+#endif
     // named values + selects (no dynamically indexed arrays: they go to scratch)
     MvN A = nb[0], B = nb[1], C = nb[2];
     int rA = A.st == 2 ? 0 : -1, rB = B.st == 2 ? 0 : -1, rC = C.st == 2 ? 0 : -1;
