@@ -517,12 +517,29 @@ HD int nb_loc(const Shared& S, int xN, int yN, int maxW, int maxH, int& xW, int&
 
 HD bool is8x8(int et) { return et == ET_P8x8 || et == ET_P8x8REF0; }
 
+// log2 of a power of two (partition sizes 4, 8, 16): divisions by a
+// runtime partition size compile to long VALU sequences; shifts do not
+HD int lg2(int v)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return 31 - __clz(v);
+#else
+    return 31 - __builtin_clz((unsigned)v);
+#endif
+}
+// origin of partition pi of a 16x16 MB split into pw x ph partitions
+HD int part_x(int pi, int pw) { return (pi & ((16 >> lg2(pw)) - 1)) << lg2(pw); }
+HD int part_y(int pi, int pw, int ph) { return (pi >> (4 - lg2(pw))) << lg2(ph); }
+// origin of sub-partition spi of an 8x8 partition split into sw x sh
+HD int sub_x(int spi, int sw) { return (spi & ((8 >> lg2(sw)) - 1)) << lg2(sw); }
+HD int sub_y(int spi, int sw, int sh) { return (spi >> (3 - lg2(sw))) << lg2(sh); }
+
 HD void sub_part_idx(const NbInfo& n, int xW, int yW, int& pi, int& spi)  // mb.h:313-339
 {
     if (n.intra) pi = 0;
-    else pi = (16 / n.part_w) * (yW / n.part_h) + (xW / n.part_w);
+    else pi = ((yW >> lg2(n.part_h)) << (4 - lg2(n.part_w))) + (xW >> lg2(n.part_w));
     if (!is8x8(n.e_type)) spi = 0;
-    else spi = (8 / n.sub_w[pi]) * ((yW % 8) / n.sub_h[pi]) + ((xW % 8) / n.sub_w[pi]);
+    else spi = (((yW & 7) >> lg2(n.sub_h[pi])) << (3 - lg2(n.sub_w[pi]))) + ((xW & 7) >> lg2(n.sub_w[pi]));
 }
 
 // Motion of the 4x4 blocks around and inside the current MB, in LDS:
@@ -575,12 +592,12 @@ struct PartShape {
 // 8.4.1.3 (utils.c:751-831) for partition (pi, spi) of partitioning ps
 HD void mvp(const Shared& S, const PartShape& ps, int pi, int spi, int out[2])
 {
-    const int x = (pi % (16 / ps.part_w)) * ps.part_w;
-    const int y = (pi / (16 / ps.part_w)) * ps.part_h;
+    const int x = part_x(pi, ps.part_w);
+    const int y = part_y(pi, ps.part_w, ps.part_h);
     int xS = 0, yS = 0, ppw = ps.part_w;
     if (ps.is8) {
-        xS = (spi % (8 / ps.sub_w)) * ps.sub_w;
-        yS = (spi / (8 / ps.sub_w)) * ps.sub_h;
+        xS = sub_x(spi, ps.sub_w);
+        yS = sub_y(spi, ps.sub_w, ps.sub_h);
         ppw = ps.sub_w;
     }
     MvN nb[3];
@@ -1925,11 +1942,11 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     // (no HL_FRESH_TID here: ROCm 7.2's greedy register allocator crashes on it)
     Shared& S = c.S;
     HL_PROF_T(tsp);
-    const int xP = (pi % (16 / pd.part_w)) * pd.part_w, yP = (pi / (16 / pd.part_w)) * pd.part_h;
+    const int xP = part_x(pi, pd.part_w), yP = part_y(pi, pd.part_w, pd.part_h);
     int xS = 0, yS = 0;
     if (pd.num_part == 4) {
-        xS = (spi % (8 / pd.sub_w)) * pd.sub_w;
-        yS = (spi / (8 / pd.sub_w)) * pd.sub_h;
+        xS = sub_x(spi, pd.sub_w);
+        yS = sub_y(spi, pd.sub_w, pd.sub_h);
     }
     PartGeo g;
     g.px = xP + xS;
@@ -3791,9 +3808,9 @@ HD double guess_intra(Ctx& c, const IntraSpec* hin = nullptr)
 HD void part_of(const Shared& S, int lx, int ly, int& pi, int& spi)
 {
     const NbInfo& n = S.nb[0];
-    pi = (16 / n.part_w) * (ly / n.part_h) + (lx / n.part_w);
+    pi = ((ly >> lg2(n.part_h)) << (4 - lg2(n.part_w))) + (lx >> lg2(n.part_w));
     if (!is8x8(n.e_type)) spi = 0;
-    else spi = (8 / n.sub_w[pi]) * ((ly % 8) / n.sub_h[pi]) + ((lx % 8) / n.sub_w[pi]);
+    else spi = (((ly & 7) >> lg2(n.sub_h[pi])) << (3 - lg2(n.sub_w[pi]))) + ((lx & 7) >> lg2(n.sub_w[pi]));
 }
 
 // luma prediction of the MB into S.pred, chroma into S.predc; mv from S.nb[0].mv
@@ -3814,11 +3831,11 @@ HD void inter_pred_mb(Ctx& c, bool chroma_only_16x16, bool luma)
             int pi, spi;
             part_of(S, bx, by, pi, spi);
             const NbInfo& n = S.nb[0];
-            const int xP = (pi % (16 / n.part_w)) * n.part_w, yP = (pi / (16 / n.part_w)) * n.part_h;
+            const int xP = part_x(pi, n.part_w), yP = part_y(pi, n.part_w, n.part_h);
             int xS = 0, yS = 0;
             if (is8x8(n.e_type)) {
-                xS = (spi % (8 / n.sub_w[pi])) * n.sub_w[pi];
-                yS = (spi / (8 / n.sub_w[pi])) * n.sub_h[pi];
+                xS = sub_x(spi, n.sub_w[pi]);
+                yS = sub_y(spi, n.sub_w[pi], n.sub_h[pi]);
             }
             const int mvx = n.mv[pi][spi][0], mvy = n.mv[pi][spi][1];
             const int X = clip3(-17, F.W + 17, c.xL + xP + xS + (mvx >> 2)) + kPad + bx - xP - xS;
@@ -3837,11 +3854,11 @@ HD void inter_pred_mb(Ctx& c, bool chroma_only_16x16, bool luma)
             int pi, spi;
             part_of(S, bx, by, pi, spi);
             const NbInfo& n = S.nb[0];
-            const int xP = (pi % (16 / n.part_w)) * n.part_w, yP = (pi / (16 / n.part_w)) * n.part_h;
+            const int xP = part_x(pi, n.part_w), yP = part_y(pi, n.part_w, n.part_h);
             int xS = 0, yS = 0;
             if (is8x8(n.e_type)) {
-                xS = (spi % (8 / n.sub_w[pi])) * n.sub_w[pi];
-                yS = (spi / (8 / n.sub_w[pi])) * n.sub_h[pi];
+                xS = sub_x(spi, n.sub_w[pi]);
+                yS = sub_y(spi, n.sub_w[pi], n.sub_h[pi]);
             }
             const int mvx = n.mv[pi][spi][0], mvy = n.mv[pi][spi][1];
             const int X = clip3(-17, F.W + 17, c.xL + xP + xS + (mvx >> 2)) + bx - xP - xS;
