@@ -947,8 +947,8 @@ __device__ __forceinline__ void mb_begin(Ctx& c)
             if (M.flags & FL_INTRA) st = 1;
             else {
                 const int x = xW * 4, y = yW * 4;
-                const int pi = (16 / M.part_w) * (y / M.part_h) + (x / M.part_w);
-                const int spi = is8x8(M.e_type) ? (8 / M.sub_w[pi]) * ((y % 8) / M.sub_h[pi]) + ((x % 8) / M.sub_w[pi]) : 0;
+                const int pi = ((y >> lg2(M.part_h)) << (4 - lg2(M.part_w))) + (x >> lg2(M.part_w));
+                const int spi = is8x8(M.e_type) ? (((y & 7) >> lg2(M.sub_h[pi])) << (3 - lg2(M.sub_w[pi]))) + ((x & 7) >> lg2(M.sub_w[pi])) : 0;
                 st = 2;
                 v = (M.mv[pi][spi][0] & 0xFFFF) | (M.mv[pi][spi][1] << 16);
             }
@@ -1129,8 +1129,8 @@ HD void mb_begin(Ctx& c)
             if (M.flags & FL_INTRA) st = 1;
             else {
                 const int x = xW * 4, y = yW * 4;
-                const int pi = (16 / M.part_w) * (y / M.part_h) + (x / M.part_w);
-                const int spi = is8x8(M.e_type) ? (8 / M.sub_w[pi]) * ((y % 8) / M.sub_h[pi]) + ((x % 8) / M.sub_w[pi]) : 0;
+                const int pi = ((y >> lg2(M.part_h)) << (4 - lg2(M.part_w))) + (x >> lg2(M.part_w));
+                const int spi = is8x8(M.e_type) ? (((y & 7) >> lg2(M.sub_h[pi])) << (3 - lg2(M.sub_w[pi]))) + ((x & 7) >> lg2(M.sub_w[pi])) : 0;
                 st = 2;
                 v = (M.mv[pi][spi][0] & 0xFFFF) | (M.mv[pi][spi][1] << 16);
             }
@@ -2111,11 +2111,15 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         // the chain: step 0 = the current step, then fresh stages from the
         // predicted best MV (pmv after the MVP/(0,0) step, else unchanged)
         const int pmx = stage == 3 ? pmv[0] : b.mv[0], pmy = stage == 3 ? pmv[1] : b.mv[1];
-        int nseg = 1, room = budget - (stage == 3 ? 2 : 9);
-        while (nseg < kMaxSeg && stage - nseg >= 0 && room >= (stage - nseg == 1 ? 5 : 9)) {
-            room -= stage - nseg == 1 ? 5 : 9;
-            ++nseg;
-        }
+        // steps that fit the pass after the current one (each its stage's full
+        // point count: 5 half-pel, 9 otherwise), in closed form: the uniform
+        // loop this replaces ran as an exec-mask loop
+        static_assert(kMaxSeg == 4, "three continuation steps");
+        const int room0 = budget - (stage == 3 ? 2 : 9);
+        const int c1 = stage - 1 == 1 ? 5 : 9, c2 = stage - 2 == 1 ? 5 : 9, c3 = stage - 3 == 1 ? 5 : 9;
+        const bool ok1 = stage >= 1 && room0 >= c1, ok2 = ok1 && stage >= 2 && room0 - c1 >= c2;
+        const bool ok3 = ok2 && stage >= 3 && room0 - c1 - c2 >= c3;
+        const int nseg = 1 + (int)ok1 + (int)ok2 + (int)ok3;
         int lo[kMaxSeg] = {0, 0, 0, 0}, n[kMaxSeg] = {0, 0, 0, 0};
 #if defined(__HIP_DEVICE_COMPILE__)
 #if defined(HL_STEP_PROF)
