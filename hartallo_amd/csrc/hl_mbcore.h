@@ -130,6 +130,9 @@ constexpr int kSpecMaxBlocks = HL_QUAD_EVAL ? HL_SPEC_MAX_BLOCKS : 8;
 #ifndef HL_LDS_WINDOW
 #define HL_LDS_WINDOW 0
 #endif
+#ifndef HL_RESOLVE_SELECTS  // 1: a pass's chain resolution as selects
+#define HL_RESOLVE_SELECTS 0
+#endif
 #ifndef HL_MVP_SELECTS  // 1: the motion vector predictor as selects
 #define HL_MVP_SELECTS 1
 #endif
@@ -2260,6 +2263,68 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         // that cost, and every step before it ends its stage.  The stage's
         // window is the one re-centred when it began (kept by a move).
         int used;
+#if defined(__HIP_DEVICE_COMPILE__) && HL_RESOLVE_SELECTS
+        {
+            // the same resolution as selects: the state is uniform but held in
+            // VGPRs, so each branch on it would be an exec-mask branch
+            auto rl = [](int v, int l) { return __builtin_amdgcn_readlane(v, l); };
+            // the MVP/(0,0) step (stage 3 passes only)
+            const bool s3 = stage == 3;
+            const int bi0 = sb[0] < 0 ? 0 : sb[0];
+            const bool t0 = s3 && sm[0] < b.cost;
+            b.cost = t0 ? sm[0] : b.cost;
+            b.single = t0 ? rl(pv_single, bi0) : b.single;
+            b.dist = t0 ? rl(pv_dist, bi0) : b.dist;
+            b.cbp = t0 ? rl(pv_cbp, bi0) : b.cbp;
+            b.mv[0] = t0 ? rl(pv_mvx, bi0) : b.mv[0];
+            b.mv[1] = t0 ? rl(pv_mvy, bi0) : b.mv[1];
+            const int j0 = s3 ? 1 : 0;
+            const bool cut = s3 && (b.mv[0] != pmv[0] || b.mv[1] != pmv[1]);  // the (0,0) candidate won: the continuations assumed the MVP
+            const int st0 = s3 ? 2 : stage;
+            const int cx3 = centre_of(2, b.mv[0]), cy3 = centre_of(2, b.mv[1]);
+            cx = s3 ? cx3 : cx;
+            cy = s3 ? cy3 : cy;
+            flags = s3 ? 0x1FF : flags;
+            left = s3 ? cx3 - range : left;
+            right = s3 ? cx3 + range : right;
+            top = s3 ? cy3 - range : top;
+            bottom = s3 ? cy3 + range : bottom;
+            unsigned mv_mask = 0;  // steps with a candidate below the best cost
+#pragma unroll
+            for (int j = 0; j < kMaxSeg; ++j) mv_mask |= (j >= j0 && j < nseg && n[j] && sm[j] < b.cost) ? 1u << j : 0u;
+            const bool moved = !cut && mv_mask != 0, none = !cut && mv_mask == 0;
+            // a move at step jm: the steps before it ended their stages (the
+            // stage began at step jm, its window re-centred then, on the best
+            // MV before the move); the stage goes on from the new centre
+            const int jm = mv_mask ? __builtin_ctz(mv_mask) : 0;
+            const int stm = st0 - (jm > j0 ? jm - j0 : 0);
+            const int wx = centre_of(stm, b.mv[0]), wy = centre_of(stm, b.mv[1]);
+            const bool rewin = moved && jm > j0;
+            const int bim = jm == 0 ? sb[0] : (jm == 1 ? sb[1] : (jm == 2 ? sb[2] : sb[3]));
+            const double smm = jm == 0 ? sm[0] : (jm == 1 ? sm[1] : (jm == 2 ? sm[2] : sm[3]));
+            const int bimc = bim < 0 ? 0 : bim;
+            const int mvx = rl(pv_mvx, bimc), mvy = rl(pv_mvy, bimc), pad = rl(pv_pad, bimc);
+            // no step moved: each ended its stage
+            const int stn = st0 - (nseg - j0);
+            const int nx = centre_of(stn < 0 ? 0 : stn, b.mv[0]), ny = centre_of(stn < 0 ? 0 : stn, b.mv[1]);
+            const bool renew = none && stn >= 0;
+            left = rewin ? wx - range : (renew ? nx - range : left);
+            right = rewin ? wx + range : (renew ? nx + range : right);
+            top = rewin ? wy - range : (renew ? ny - range : top);
+            bottom = rewin ? wy + range : (renew ? ny + range : bottom);
+            b.cost = moved ? smm : b.cost;
+            b.single = moved ? rl(pv_single, bimc) : b.single;
+            b.dist = moved ? rl(pv_dist, bimc) : b.dist;
+            b.cbp = moved ? rl(pv_cbp, bimc) : b.cbp;
+            b.mv[0] = moved ? mvx : b.mv[0];
+            b.mv[1] = moved ? mvy : b.mv[1];
+            cx = moved ? mvx >> stm : (renew ? nx : cx);
+            cy = moved ? mvy >> stm : (renew ? ny : cy);
+            flags = moved ? mask_of(stm, pad) : (renew ? 0x1FF : flags);
+            stage = cut ? st0 : (moved ? stm : stn);
+            used = cut ? lo[0] + n[0] : (moved ? lo[jm] + n[jm] : lo[nseg - 1] + n[nseg - 1]);
+        }
+#else
         {
             int j0 = 0;
             bool cut = false;  // the (0,0) candidate won: the continuations assumed the MVP
@@ -2322,6 +2387,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
                 used = lo[nseg - 1] + n[nseg - 1];
             }
         }
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
 #if defined(HL_STEP_PROF)
         HL_PROF_ADD(c, 18, tres);  // the chain resolved
