@@ -2729,6 +2729,23 @@ HD void reconstruct_chroma(Ctx& c, bool intra_flag)
     HL_SYNC();
     // sequential single-coefficient gating (uniform)
     int single[2] = {0, 0}, tcs[2] = {0, 0}, cac[2] = {0, 0}, cdc[2] = {0, 0};
+#if defined(__HIP_DEVICE_COMPILE__)
+    // as selects (uniform values in VGPRs: each if would be an exec-mask branch)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int comp = 0; comp < 2; ++comp) {
+            const int ca = S.cres_cac[comp][b], sc = S.cres_sctr[comp][b];
+            cac[comp] |= ca << b;
+            cdc[comp] |= S.cres_cdc[comp][b] << b;
+            const bool w = single[comp] < 7 && ca;
+            single[comp] += w ? sc : 0;
+            tcs[comp] += w ? S.cres_tc[comp][b] : 0;
+            c.chain = w ? sc : c.chain;  // chain_write
+            c.fresh = w ? 1 : c.fresh;
+            c.spec = w ? 0 : c.spec;
+        }
+#else
     for (int b = 0; b < 4; ++b)
         for (int comp = 0; comp < 2; ++comp) {
             cac[comp] |= S.cres_cac[comp][b] << b;
@@ -2739,6 +2756,7 @@ HD void reconstruct_chroma(Ctx& c, bool intra_flag)
                 chain_write(c, S.cres_sctr[comp][b]);
             }
         }
+#endif
     // TotalCoeffs are written only for blocks passed to write_block (lane 0)
     if (c.tid == 0) {
         int sg[2] = {0, 0};
@@ -2749,9 +2767,10 @@ HD void reconstruct_chroma(Ctx& c, bool intra_flag)
                     S.tcc[comp][b] = (int8_t)S.cres_tc[comp][b];
                 }
     }
-    for (int comp = 0; comp < 2; ++comp)
-        if (single[comp] < 7 && tcs[comp] == 1) cac[comp] = 0;
+#pragma unroll
+    for (int comp = 0; comp < 2; ++comp) cac[comp] = (single[comp] < 7 && tcs[comp] == 1) ? 0 : cac[comp];
     int dcl[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
     for (int comp = 0; comp < 2; ++comp)
         if (cdc[comp]) {
             const int* D = S.cres_dc[comp];
