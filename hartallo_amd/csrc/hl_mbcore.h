@@ -2131,28 +2131,21 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         {  // lane 16 j + i of every wave checks point i of step j; enabled points are compacted in order
             const int i = c.tid & 63, j = i >> 4, pt = min(i & 15, 8);
             const int st = stage - j;  // step j's stage (3 = MVP/(0,0))
-            bool en = false;
-            int mx = 0, my = 0, sh = 0;
-            if (j < nseg) {
-                if (st == 3) {
-                    en = (i & 15) < nc0;
-                    mx = (i & 15) ? 0 : pmv[0];
-                    my = (i & 15) ? 0 : pmv[1];
-                }
-                else {
-                    const uint32_t pkx = st == 2 ? pIntX : (st == 1 ? pHalfX : pQuarX);
-                    const uint32_t pky = st == 2 ? pIntY : (st == 1 ? pHalfY : pQuarY);
-                    const bool fresh = j > 0 || stage == 3;
-                    const int ccx = fresh ? centre_of(st, pmx) : cx, ccy = fresh ? centre_of(st, pmy) : cy;
-                    const int l0 = fresh ? ccx - range : left, r0 = fresh ? ccx + range : right;
-                    const int t0 = fresh ? ccy - range : top, b0 = fresh ? ccy + range : bottom;
-                    const int fl = fresh ? 0x1FF : flags;
-                    mx = ccx + (int)((pkx >> (3 * pt)) & 7) - 2;
-                    my = ccy + (int)((pky >> (3 * pt)) & 7) - 2;
-                    sh = st == 2 ? 2 : (st == 1 ? 1 : 0);
-                    en = (i & 15) < (st == 1 ? 5 : 9) && ((fl >> (i & 15)) & 1) && mx >= l0 && mx <= r0 && my >= t0 && my <= b0;
-                }
-            }
+            // (both kinds of step computed and selected: the lanes' steps differ,
+            // so branches on them would run both sides under exec masks anyway)
+            const uint32_t pkx = st == 2 ? pIntX : (st == 1 ? pHalfX : pQuarX);
+            const uint32_t pky = st == 2 ? pIntY : (st == 1 ? pHalfY : pQuarY);
+            const bool fresh = j > 0 || stage == 3;
+            const int ccx = fresh ? centre_of(st, pmx) : cx, ccy = fresh ? centre_of(st, pmy) : cy;
+            const int l0 = fresh ? ccx - range : left, r0 = fresh ? ccx + range : right;
+            const int t0 = fresh ? ccy - range : top, b0 = fresh ? ccy + range : bottom;
+            const int fl = fresh ? 0x1FF : flags;
+            const int dmx = ccx + (int)((pkx >> (3 * pt)) & 7) - 2, dmy = ccy + (int)((pky >> (3 * pt)) & 7) - 2;
+            const bool den = (i & 15) < (st == 1 ? 5 : 9) && ((fl >> (i & 15)) & 1) && dmx >= l0 && dmx <= r0 && dmy >= t0 && dmy <= b0;
+            const bool s3 = st == 3;
+            const bool en = j < nseg && (s3 ? (i & 15) < nc0 : den);
+            const int mx = s3 ? ((i & 15) ? 0 : pmv[0]) : dmx, my = s3 ? ((i & 15) ? 0 : pmv[1]) : dmy;
+            const int sh = st == 2 ? 2 : (st == 1 ? 1 : 0);
             const unsigned long long bal = __ballot(en);
             for (int k = 0; k < kMaxSeg; ++k) {
                 lo[k] = __popcll(bal & ((1ull << (16 * k)) - 1ull));
