@@ -130,6 +130,9 @@ constexpr int kSpecMaxBlocks = HL_QUAD_EVAL ? HL_SPEC_MAX_BLOCKS : 8;
 #ifndef HL_LDS_WINDOW
 #define HL_LDS_WINDOW 0
 #endif
+#ifndef HL_ROWS_PERMLANE  // 1: a pass's step minima combined across the two 16-lane rows by v_permlane16_swap
+#define HL_ROWS_PERMLANE 0
+#endif
 #ifndef HL_RESOLVE_SELECTS  // 1: a pass's chain resolution as selects
 #define HL_RESOLVE_SELECTS 0
 #endif
@@ -2230,10 +2233,19 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
 #pragma unroll
             for (int j = 0; j < kMaxSeg; ++j) {
                 const unsigned long long b0 = __builtin_bit_cast(unsigned long long, rm[j]);
+#if HL_ROWS_PERMLANE
+                // the two rows' minima exchanged by v_permlane16_swap (lanes
+                // 16-31 <-> 0-15, in registers): every lane holds both, no readlane
+                const auto lo2 = __builtin_amdgcn_permlane16_swap((unsigned)b0, (unsigned)b0, false, false);
+                const auto hi2 = __builtin_amdgcn_permlane16_swap((unsigned)(b0 >> 32), (unsigned)(b0 >> 32), false, false);
+                const double m0 = __builtin_bit_cast(double, (unsigned long long)hi2[0] << 32 | lo2[0]);
+                const double m1 = __builtin_bit_cast(double, (unsigned long long)hi2[1] << 32 | lo2[1]);
+#else
                 const double m0 = __builtin_bit_cast(double, (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(b0 >> 32), 0) << 32 |
                                                                  (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b0, 0));
                 const double m1 = __builtin_bit_cast(double, (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(b0 >> 32), 16) << 32 |
                                                                  (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b0, 16));
+#endif
                 sm[j] = fmin(m0, m1);
                 sb[j] = __ffsll((long long)(__ballot(in[j] && v[j] == sm[j]) & 0xFFFFFFFFull)) - 1;
             }
