@@ -261,6 +261,21 @@ __device__ void task_filters(const PipeFrame& PF, Shared& S, int x, int y, int m
     }
 }
 
+// a / d for 0 <= a < 2^24 and 0 < d < 2^12 from a float reciprocal of d and
+// one correction each way (exact): integer division by a runtime value is a
+// long VALU sequence, and the scheduler divides by the picture width, the MB
+// count and the stream and picture counts on every pop and task
+__device__ __forceinline__ int udiv_small(int a, int d, float inv)
+{
+    int q = (int)((float)a * inv);
+    q -= q * d > a ? 1 : 0;
+    q += (q + 1) * d <= a ? 1 : 0;
+    return q;
+}
+struct SchedRecip {
+    float mbw, nmb, S, spp;  // 1 / (MBs per row, MBs per picture, streams, pictures per stream)
+};
+
 // Every picture's ready queue is split into kSubQ sub-queues (MB address %
 // kSubQ) with their own heads: a workgroup prefers its own sub-queue
 // (blockIdx % kSubQ) among tasks of similar priority, so that hundreds of
@@ -335,7 +350,7 @@ __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
 // call read it (-1: none yet); the scan uses it while this call's read is in
 // flight (a stale value only shifts the window late: its first pictures are
 // finished ones, with empty queues)
-__device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc
+__device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc, const SchedRecip& rc
 #if defined(HL_PROFILE)
                         , unsigned long long* pst  // profiling: [0] attempts on a macroblock, [1] lost, [2] empty rounds
 #endif
@@ -356,7 +371,7 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc
         bool ins[kScan];
 #pragma unroll
         for (int i = 0; i < kScan; ++i) {
-            const int e = lane + 64 * i, sq = e % kSubQ, rr = e / kSubQ, sj = rr % S, j = rr / S;
+            const int e = lane + 64 * i, sq = e % kSubQ, rr = e / kSubQ, j = udiv_small(rr, S, rc.S), sj = rr - j * S;
             const int k = __shfl(ol, sj, 64) + j;
             ins[i] = j < max(1, P.window / S) && k < P.spp;
             fl[i] = sj * P.spp + k;  // picture slot, its sub-queue
@@ -401,7 +416,7 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc
 #pragma unroll
             for (int i = 0; i < kScan; ++i) {
                 if (qv[i] > 0) {
-                    const int a = qv[i] - 1, y = a / mbw, x = a - y * mbw;
+                    const int a = qv[i] - 1, y = udiv_small(a, mbw, rc.mbw), x = a - y * mbw;
                     const int own = sqs[i] == (int)(blockIdx.x % kSubQ) ? 12 : 0;  // preference for the workgroup's sub-queue
                     const int kk = (((mbw - 1 - x) + 2 * (mbh - 1 - y) - P.hop * js[i] + own + 4096) << 6) | (63 - lane);
                     if (kk > key) {
@@ -552,6 +567,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
     const bool in_order = blockIdx.x == 0;  // claims tasks in run order (claim_next)
     int cursor = 0;
     int olc = -1;  // wave 0: pop_task's oldest pictures of the previous call
+    const SchedRecip rc{1.0f / (float)mbw, 1.0f / (float)nmb, 1.0f / (float)P.nstreams, 1.0f / (float)P.spp};
 #if defined(HL_PRIO_YOUNG)
     // the second-dispatched half of the workgroup (waves 4-7) loses every VALU
     // arbitration to its SIMD partner at equal priority (MI355X_MICROARCH.md,
@@ -572,7 +588,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         const unsigned long long pt0 = __builtin_readcyclecounter();
 #endif
         if (threadIdx.x < 64) {
-            const int t = in_order ? claim_next(P, nmb, cursor) : pop_task(P, nmb, mbw, mbh, olc
+            const int t = in_order ? claim_next(P, nmb, cursor) : pop_task(P, nmb, mbw, mbh, olc, rc
 #if defined(HL_PROFILE)
                                                                                            , pst
 #endif
@@ -599,11 +615,12 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         // across the whole body (160 spilled VGPRs without this)
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
-        const int f = t / nmb, addr = t - f * nmb;
+        const int f = udiv_small(t, nmb, rc.nmb), addr = t - f * nmb;
         const PipeFrame& PF = P.fr[f];
-        const int x = addr % mbw, y = addr / mbw;
+        const int y = udiv_small(addr, mbw, rc.mbw), x = addr - y * mbw;
+        const int fq = udiv_small(f, P.spp, rc.spp), fk = f - fq * P.spp, fb = f - fk;  // picture fk of the stream whose first slot is fb
         int gx = 1 << 20, gy = 1 << 20;
-        if (f % P.spp > 0) {  // the reference is a picture of this run (of the same stream)
+        if (fk > 0) {  // the reference is a picture of this run (of the same stream)
             gx = min(x + P.reach, mbw - 1);
             gy = min(y + P.reach, mbh - 1);
         }
@@ -656,7 +673,6 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #if defined(HL_PROFILE)
         const unsigned long long pt2 = __builtin_readcyclecounter();
 #endif
-        const int fk = f % P.spp, fb = f - fk;  // picture fk of the stream whose first slot is fb
         // Releases successors (Guideline 16: every wave drained, barrier, ONE
         // release whose own wait is explicit, then relaxed atomics: the L2
         // write-back of the release fence covers the payload, and every
@@ -784,7 +800,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
             // a stream's pictures finish in order: the last MB depends on every
             // other one and on the previous picture's last MB
             if (tid == 0 && addr == nmb - 1) {
-                __hip_atomic_store(P.oldest + f / P.spp, fk + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(P.oldest + fq, fk + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                 // every record of the picture is in host memory (each task released at system scope)
                 if (PF.progress) __hip_atomic_store(PF.progress, fk + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (P.pub_clock) P.pub_clock[f] = wall_clock64();
