@@ -3500,21 +3500,25 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
                 bestl = __ffsll((long long)__ballot(v0 && cost == mn)) - 1;
                 best_zero = !((W >> bestl) & 1);
             }
-            // (every value from registers: the stores carry no dependent load)
-            const int bdist = __builtin_amdgcn_readlane(dd, bestl);  // d_min_dist4x4 (rdo.c:2011, 2023); 0 for an exact mode
-            const int lwsct = lastwl >= 0 ? __builtin_amdgcn_readlane(st.sctr, lastwl) : -1;
-            const int lwtc = lastwl >= 0 ? __builtin_amdgcn_readlane(st.tc, lastwl) : -1;
+            // (every value from registers, each stored by the lane that holds it:
+            // no readlane; the stores carry no dependent load)
             if (lane == 0) {
                 S.i4r_dmin[blk] = dmin;
-                S.i4r_dist[blk] = bdist;
-                S.i4r_sct[blk] = lwsct;
                 S.i4r_zero[blk] = best_zero;
                 S.i4mode[blk] = (int8_t)(bestl >> 2);
-                if (lastwl >= 0) S.tc[blk] = (int8_t)lwtc;
                 // the verification record (i4_verify): the costs used an nC
                 // only without an exact mode and with a coded one
                 S.ih.i4_ncls[blk] = (int8_t)(!bex && W ? nc_class(nC) : -1);
-                S.ih.i4_lwtc[blk] = (int8_t)lwtc;
+                if (lastwl < 0) {
+                    S.i4r_sct[blk] = -1;
+                    S.ih.i4_lwtc[blk] = -1;
+                }
+            }
+            if (lane == bestl) S.i4r_dist[blk] = dd;  // d_min_dist4x4 (rdo.c:2011, 2023); 0 for an exact mode
+            if (lane == lastwl) {  // the last coded mode before the scan stopped writes the counter and TotalCoeff
+                S.i4r_sct[blk] = st.sctr;
+                S.tc[blk] = (int8_t)st.tc;
+                S.ih.i4_lwtc[blk] = (int8_t)st.tc;
             }
             if ((lane >> 2) == (bestl >> 2)) {  // the chosen mode's quad: its reconstruction rows and levels
                 *reinterpret_cast<uint32_t*>(&S.rec[(yO + rr) * 16 + xO]) = rec4;
