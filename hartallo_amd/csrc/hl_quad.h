@@ -90,8 +90,11 @@ __device__ __forceinline__ LaneQ make_laneq(int tid, int qp)
         }
     Q.mfE = mfE;
     Q.mfO = mfO;
-    Q.lsE = lsE;
-    Q.lsO = lsO;
+    // the level scales pre-shifted by 8.5.12.1's left shift at qp >= 24
+    // (quad_idct then only adds its rounding and shifts right below 24)
+    const int sa = qp >= 24 ? qp / 6 - 4 : 0;
+    Q.lsE = lsE << sa;
+    Q.lsO = lsO << sa;
     return Q;
 }
 
@@ -146,14 +149,12 @@ __device__ __forceinline__ void quad_idct(const LaneQ& Q, const int q[4], int qP
 {
     // 8.5.12.1 as ((p << a) + r) >> b with a, r, b uniform: qP >= 24 shifts
     // left by q6 - 4, below it rounds and shifts right by 4 - q6
+    // (the left shift at qP >= 24 is folded into Q's level scales, make_laneq)
     const int q6 = qP / 6;
-    const int sa = qP >= 24 ? q6 - 4 : 0, sr = qP >= 24 ? 0 : 1 << (3 - q6), sb = qP >= 24 ? 0 : 4 - q6;
+    const int sr = qP >= 24 ? 0 : 1 << (3 - q6), sb = qP >= 24 ? 0 : 4 - q6;
     int d[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const int p = __mul24(q[c], (c & 1) ? Q.lsO : Q.lsE);
-        d[c] = ((p << sa) + sr) >> sb;
-    }
+    for (int c = 0; c < 4; ++c) d[c] = (__mul24(q[c], (c & 1) ? Q.lsO : Q.lsE) + sr) >> sb;
     if (keep_dc && Q.r == 0) d[0] = dcv;
     const int e0 = d[0] + d[2], e1 = d[0] - d[2], e2 = (d[1] >> 1) - d[3], e3 = d[1] + (d[3] >> 1);
     const int f[4] = {e0 + e3, e1 + e2, e1 - e2, e0 - e3};
