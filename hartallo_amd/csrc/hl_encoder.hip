@@ -272,6 +272,17 @@ __device__ __forceinline__ int udiv_small(int a, int d, float inv)
     q += (q + 1) * d <= a ? 1 : 0;
     return q;
 }
+// 1: scheduler reciprocals in LDS, task coordinates and the wave's first
+// lane index in SGPRs (k_pipeline): VGPR spills 15 -> 13, but 0.4 % slower
+// (profiles/r05_ab_sched_lds_sgpr_coords_not_kept.log)
+#ifndef HL_SCHED_LDS
+#define HL_SCHED_LDS 0
+#endif
+#if HL_SCHED_LDS
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+#else
+__device__ __forceinline__ int uni(int v) { return v; }
+#endif
 struct SchedRecip {
     float mbw, nmb, S, spp;  // 1 / (MBs per row, MBs per picture, streams, pictures per stream)
 };
@@ -356,7 +367,7 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc, 
 #endif
 )
 {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     int empty = 0;
     for (;;) {
@@ -523,7 +534,7 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc, 
 // workgroups (one included) -- no geometry can deadlock.
 __device__ int claim_next(const PipeArgs& P, int nmb, int& cursor)
 {
-    const int lane = threadIdx.x & 63, total = P.nframes * nmb;
+    const int lane = __lane_id(), total = P.nframes * nmb;
     for (;; ++cursor) {
         if (cursor >= total) return -1;
         int c = 0;
@@ -567,7 +578,22 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
     const bool in_order = blockIdx.x == 0;  // claims tasks in run order (claim_next)
     int cursor = 0;
     int olc = -1;  // wave 0: pop_task's oldest pictures of the previous call
+#if HL_SCHED_LDS
+    // the scheduler's reciprocals in LDS and the wave's first lane index in an
+    // SGPR: loop-invariant VGPRs (the work-item index, the four reciprocals)
+    // were spilled at the loop head and restored inside the macroblock body
+    __shared__ SchedRecip s_rc;
+    if (threadIdx.x == 0) s_rc = SchedRecip{1.0f / (float)mbw, 1.0f / (float)nmb, 1.0f / (float)P.nstreams, 1.0f / (float)P.spp};
+    const int wbase = __builtin_amdgcn_readfirstlane(threadIdx.x) & ~63;
+#define HL_RC s_rc
+#define HL_WAVE0 (wbase == 0)
+#define HL_TID (wbase + (int)__lane_id())
+#else
     const SchedRecip rc{1.0f / (float)mbw, 1.0f / (float)nmb, 1.0f / (float)P.nstreams, 1.0f / (float)P.spp};
+#define HL_RC rc
+#define HL_WAVE0 (threadIdx.x < 64)
+#define HL_TID ((int)threadIdx.x)
+#endif
 #if defined(HL_PRIO_YOUNG)
     // the second-dispatched half of the workgroup (waves 4-7) loses every VALU
     // arbitration to its SIMD partner at equal priority (MI355X_MICROARCH.md,
@@ -587,15 +613,15 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #if defined(HL_PROFILE)
         const unsigned long long pt0 = __builtin_readcyclecounter();
 #endif
-        if (threadIdx.x < 64) {
-            const int t = in_order ? claim_next(P, nmb, cursor) : pop_task(P, nmb, mbw, mbh, olc, rc
+        if (HL_WAVE0) {
+            const int t = in_order ? claim_next(P, nmb, cursor) : pop_task(P, nmb, mbw, mbh, olc, HL_RC
 #if defined(HL_PROFILE)
                                                                                            , pst
 #endif
             );
             if (!HL_EARLY_ACQ || in_order) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);  // (pop_task acquires itself)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
-            if (threadIdx.x == 0) s_task = t;
+            if (__lane_id() == 0) s_task = t;
         }
         __syncthreads();
         int t = __builtin_amdgcn_readfirstlane(s_task);
@@ -613,12 +639,17 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         // opaque per task: keeps the compiler from hoisting encode_mb's
         // lane-index arithmetic out of the task loop and holding it live
         // across the whole body (160 spilled VGPRs without this)
-        int tid = threadIdx.x;
+        int tid = HL_TID;
         asm volatile("" : "+v"(tid));
-        const int f = udiv_small(t, nmb, rc.nmb), addr = t - f * nmb;
+#if HL_SCHED_LDS
+        const SchedRecip rc = s_rc;
+#endif
+        // (the task's coordinates are uniform: computed on the VALU (float
+        // reciprocals), held in SGPRs across the macroblock body)
+        const int f = uni(udiv_small(t, nmb, rc.nmb)), addr = t - f * nmb;
         const PipeFrame& PF = P.fr[f];
-        const int y = udiv_small(addr, mbw, rc.mbw), x = addr - y * mbw;
-        const int fq = udiv_small(f, P.spp, rc.spp), fk = f - fq * P.spp, fb = f - fk;  // picture fk of the stream whose first slot is fb
+        const int y = uni(udiv_small(addr, mbw, rc.mbw)), x = addr - y * mbw;
+        const int fq = uni(udiv_small(f, P.spp, rc.spp)), fk = f - fq * P.spp, fb = f - fk;  // picture fk of the stream whose first slot is fb
         int gx = 1 << 20, gy = 1 << 20;
         if (fk > 0) {  // the reference is a picture of this run (of the same stream)
             gx = min(x + P.reach, mbw - 1);
@@ -629,8 +660,8 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #endif
         // the left neighbour's chain record was written by another workgroup:
         // vector loads behind the pop's acquire (never the scalar cache)
-        const int s_in = x == 0 ? PF.F.spec[y] : ld_relaxed(&PF.F.chain[addr - 1].s_out);
-        const int spec_in = x == 0 ? 1 : ld_relaxed(&PF.F.chain[addr - 1].spec);
+        const int s_in = uni(x == 0 ? PF.F.spec[y] : ld_relaxed(&PF.F.chain[addr - 1].s_out));
+        const int spec_in = uni(x == 0 ? 1 : ld_relaxed(&PF.F.chain[addr - 1].spec));
         HL_POISON(S, (uint32_t)t * 7919u + blockIdx.x);
 #if defined(HL_DIAG) && HL_DIAG == 2
         __syncthreads();
@@ -830,6 +861,9 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
     }
 #endif
 }
+#undef HL_RC
+#undef HL_WAVE0
+#undef HL_TID
 
 #if !defined(HL_KERNELS_ONLY)  // (hl_encoder_fam3.hip compiles the kernels above again, with HL_FAM3=1)
 extern "C" hipError_t hl_fam3_launch_pipeline(const void* args, size_t psz, int mbw, int mbh, int workgroups, hipStream_t stream);
