@@ -422,6 +422,12 @@ struct Shared {
 #ifndef HL_FRESH_MASK
 #define HL_FRESH_MASK 0xFFE
 #endif
+// the quad pipeline's scan-order word (LaneQ::zz) recomputed at the start
+// of the evaluation pass (bit 0) / of the later phases (bit 1) instead of held
+// from the MB's start
+#ifndef HL_FRESH_ZZ
+#define HL_FRESH_ZZ 2
+#endif
 #define HL_FRESH_TID_K(c, k) \
     do { \
         if ((HL_FRESH_MASK >> (k)) & 1) HL_FRESH_TID(c); \
@@ -432,7 +438,10 @@ struct Ctx {
     int tid, nthr;
     int addr, mbx, mby, xL, yL;
     int chain, fresh, dep;  // rdo.Single_ctr emulation (uniform)
-    const LaneK& K;         // per-lane constants of the 16-lane block pipeline (device; Shared::lk)
+    // per-lane constants of the 16-lane block pipeline (Shared::lk), addressed
+    // from the phase's lane index at each use (an address held from the MB's
+    // start was spilled across the partition searches)
+    __host__ __device__ const LaneK& k() const { return S.lk[tid & 15]; }
 #if defined(__HIP_DEVICE_COMPILE__)
     LaneQ Q{};              // per-lane constants of the quad block pipeline (registers: the search loop reads them every pass)
 #endif
@@ -1347,7 +1356,8 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         const int n = ncand << g.lnb;
         const int qp = uni(F.qp);  // scalar: the quantiser's shifts and the dequantiser's form are uniform
         const int qbits = 15 + qp / 6, f = (1 << qbits) / 6;
-        const LaneQ& Q = c.Q;
+        LaneQ Q = c.Q;
+        if (HL_FRESH_ZZ & 1) Q.zz = laneq_zz_fresh(Q.r);
         const auto base = gmem(F.pl[0]);
         // single-block partitions: both nC neighbours lie outside the partition,
         // so nC is fixed for its whole search (read here, beside the loads)
@@ -1465,7 +1475,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         const int wave = c.tid >> 6, grp = c.tid >> 4, ngrp = c.nthr >> 4;
         const int n = ncand << g.lnb;
         const int qbits = 15 + F.qp / 6, f = (1 << qbits) / 6;
-        const int pr = c.K.p >> 2, pc = c.K.p & 3;
+        const int pr = c.k().p >> 2, pc = c.k().p & 3;
         const auto base = gmem(F.pl[0]);
         int pa[kMaxPass], pb[kMaxPass], sv[kMaxPass];
         // single-block partitions: both nC neighbours lie outside the partition,
@@ -1509,7 +1519,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                 const int ci = item >> g.lnb, k = item & (g.nblk - 1);
                 const int pred = (pa[j] + pb[j] + 1) >> 1;
                 const int res = sv[j] - pred;
-                const int q = coop_quant(coop_fwd(c.K, res), c.K.mf, qbits, f);
+                const int q = coop_quant(coop_fwd(c.k(), res), c.k().mf, qbits, f);
 #if defined(HL_STEP_PROF)
                 HL_PROF_ADD(c, 13, ta1);
                 HL_PROF_T(ta2);
@@ -1522,10 +1532,10 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                 else {
                     // reconstruction distortion first: independent of the CAVLC
                     // chain, so the two DPP chains interleave in one basic block
-                    const int r = coop_idct(c.K, coop_dequant(q, c.K.ls, F.qp));
+                    const int r = coop_idct(c.k(), coop_dequant(q, c.k().ls, F.qp));
                     dist = row_sum(iabs(sv[j] - clip255(pred + r)));
-                    st = coop_cavlc(S.ct, q, c.K.s, S.lvs[grp]);
-                    if (c.K.p == 0 && st.tc)  // coeff_token lengths for the four nC classes
+                    st = coop_cavlc(S.ct, q, c.k().s, S.lvs[grp]);
+                    if (c.k().p == 0 && st.tc)  // coeff_token lengths for the four nC classes
                         tok = S.ct.tok[0][st.t1][st.tc] | (S.ct.tok[1][st.t1][st.tc] << 5) | (S.ct.tok[2][st.t1][st.tc] << 10) | (6 << 15);
                 }
 #if defined(HL_STEP_PROF)
@@ -1535,7 +1545,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
 #if defined(HL_STEP_PROF)
                 HL_PROF_ADD(c, 15, ta3);
 #endif
-                if (c.K.p == 0) {
+                if (c.k().p == 0) {
                     S.be_w[ci][k] = make_int4(st.tc | (st.t1 << 5) | ((st.sctr + 1) << 8), st.rest | (dist << 16), tok, 0);
                     tcb[k][ci] = (uint8_t)st.tc;
                     if (g.nblk == 1) {
@@ -3017,7 +3027,8 @@ HD void i16_heavy(Ctx& c)
     const int mode = c.tid >> 6, lane = c.tid & 63, blk = lane >> 2, r = lane & 3;
     if (mode < 4 && i16_mode_avail(S, mode)) {  // (wave-uniform)
         const int qp = uni(F.qp), qbits = 15 + qp / 6, fq = (1 << qbits) / 3;
-        const LaneQ& Q = c.Q;
+        LaneQ Q = c.Q;
+        if (HL_FRESH_ZZ & 2) Q.zz = laneq_zz_fresh(Q.r);
         int dcv, pa, pb, pc;
         i16_params(S, mode, dcv, pa, pb, pc);
         dcv = uni(dcv);
@@ -3053,13 +3064,13 @@ HD void i16_heavy(Ctx& c)
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (lane < 16) {  // the DC block: Hadamard, quant, CAVLC, scaling
-            const int hh = coop_lin(c.K.had, S.i16_dcc[mode * 16 + kDcPos[c.K.p]]) >> 1;
+            const int hh = coop_lin(c.k().had, S.i16_dcc[mode * 16 + kDcPos[c.k().p]]) >> 1;
             const int qd = quant_dc(qp, true, hh);
-            const CoopStat sd = coop_cavlc(S.ct, qd, c.K.s, S.lvs[c.tid >> 4]);
-            S.ih_dcl[mode][c.K.s] = (int16_t)qd;
-            const int f = coop_lin(c.K.had, qd);
+            const CoopStat sd = coop_cavlc(S.ct, qd, c.k().s, S.lvs[c.tid >> 4]);
+            S.ih_dcl[mode][c.k().s] = (int16_t)qd;
+            const int f = coop_lin(c.k().had, qd);
             const int scale = level_scale(qp % 6, 0, 0), q6 = qp / 6;
-            S.dcY[mode * 16 + c.K.p] = qp >= 36 ? (f * scale) << (q6 - 6) : (f * scale + (1 << (5 - q6))) >> (6 - q6);
+            S.dcY[mode * 16 + c.k().p] = qp >= 36 ? (f * scale) << (q6 - 6) : (f * scale + (1 << (5 - q6))) >> (6 - q6);
             if (lane == 0) {  // block 0's nC neighbours lie outside the MB: the DC rate is fixed
                 const int nC = nc_luma_of(S, 0, [&](int ni) -> int { return S.tc[ni]; });
                 S.ih.dcs[mode][0] = sd.rest + coop_token_len(S.ct, nC, sd.tc, sd.t1);
@@ -3403,7 +3414,8 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
     const int lane = c.tid & 63, sl = c.tid >> 6;
     const int qp = uni(F.qp), qbits = 15 + qp / 6, fq = (1 << qbits) / 3;
     const int m = min(lane >> 2, 8), rr = lane & 3;  // this quad's mode, this lane's block row
-    const LaneQ& Q = c.Q;
+    LaneQ Q = c.Q;
+    if (HL_FRESH_ZZ & 2) Q.zz = laneq_zz_fresh(Q.r);
     uint32_t te[4];  // the prediction taps of the lane's four samples (kI4Tab)
 #pragma unroll
     for (int cc = 0; cc < 4; ++cc) te[cc] = kI4Tab.e[m][rr * 4 + cc];
@@ -3998,7 +4010,8 @@ HD void reconstruct_inter_luma(Ctx& c, int single_luma)
     // one 4-lane quad per 4x4 block (hl_quad.h, as the search evaluated it)
     if (c.tid < 64) {
         const int t = c.tid >> 2, r = c.tid & 3, bx = blk_x(t), by = blk_y(t);
-        const LaneQ& Q = c.Q;
+        LaneQ Q = c.Q;
+        if (HL_FRESH_ZZ & 2) Q.zz = laneq_zz_fresh(Q.r);
         const int4 pv = *reinterpret_cast<const int4*>(&S.pred[(by + r) * 16 + bx]);
         const int pr[4] = {pv.x, pv.y, pv.z, pv.w};
         const uint32_t sv = *reinterpret_cast<const uint32_t*>(&S.src[(by + r) * 16 + bx]);
@@ -4963,7 +4976,7 @@ HD void intra_helper(
 #endif
     const FrameArgs& F, Shared& S, int addr, int tid, int nthr, int s_in, IntraSpec* out)
 {
-    Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0, S.lk[tid & 15]};
+    Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0};
 #if defined(__HIP_DEVICE_COMPILE__)
     if (tid < 16) S.lk[tid] = make_lanek(tid, F.qp, F.qpc);
     c.Q = make_laneq(tid, F.qp);
@@ -5020,7 +5033,7 @@ HD void intra_helper(
 HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, int s_in, int gx = 1 << 20, int gy = 1 << 20,
                int spec_in = 1, Fam3Out* f3out = nullptr)
 {
-    Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0, S.lk[tid & 15]};
+    Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0};
     c.gx = gx;
     c.gy = gy;
     c.spec = spec_in;

@@ -69,10 +69,19 @@ struct LaneQ {
 // the two-stage butterflies below leave rows 1 and 2 swapped (0, 2, 1, 3).
 __device__ __forceinline__ int quad_coef_row(int r) { return ((r & 1) << 1) | (r >> 1); }
 
+// kZzInv[r * 4 + c]: scan index of raster position (r, c)
+constexpr uint64_t kZzRows = 0xFEA9DB83C7426510ull;  // rows of {0,1,5,6},{2,4,7,12},{3,8,11,13},{9,10,14,15}, 4 bits each
+
+// LaneQ::zz recomputed from an opaque copy of the lane's row where a phase
+// starts: a zz held from the MB's start was spilled across the searches
+__device__ __forceinline__ uint32_t laneq_zz_fresh(int r)
+{
+    asm volatile("" : "+v"(r));
+    return (uint32_t)(kZzRows >> (16 * quad_coef_row(r))) & 0xFFFFu;
+}
+
 __device__ __forceinline__ LaneQ make_laneq(int tid, int qp)
 {
-    // kZzInv[r * 4 + c]: scan index of raster position (r, c)
-    constexpr uint64_t kZzRows = 0xFEA9DB83C7426510ull;  // rows of {0,1,5,6},{2,4,7,12},{3,8,11,13},{9,10,14,15}, 4 bits each
     LaneQ Q;
     Q.r = tid & 3;
     const int r = quad_coef_row(Q.r);  // the quantiser's, scan's and dequantiser's row
