@@ -261,8 +261,10 @@ __device__ void task_filters(const PipeFrame& PF, Shared& S, int x, int y, int m
     }
 }
 
-// a / d for 0 <= a < 2^24 and 0 < d < 2^12 from a float reciprocal of d and
-// one correction each way (exact): integer division by a runtime value is a
+// a / d for 0 <= a < 2^24 and quotients below 2^20 from a float reciprocal
+// of d (correctly rounded or the 1-ulp v_rcp_f32: the product is within one
+// of the quotient) and one correction each way (exact; the scheduler's
+// quotients are pictures, rows and streams): integer division by a runtime value is a
 // long VALU sequence, and the scheduler divides by the picture width, the MB
 // count and the stream and picture counts on every pop and task
 __device__ __forceinline__ int udiv_small(int a, int d, float inv)
@@ -272,6 +274,9 @@ __device__ __forceinline__ int udiv_small(int a, int d, float inv)
     q += (q + 1) * d <= a ? 1 : 0;
     return q;
 }
+#ifndef HL_ARGS_OPAQUE
+#define HL_ARGS_OPAQUE 1
+#endif
 // 1: scheduler reciprocals in LDS, task coordinates and the wave's first
 // lane index in SGPRs (k_pipeline): VGPR spills 15 -> 13, but 0.4 % slower
 // (profiles/r05_ab_sched_lds_sgpr_coords_not_kept.log)
@@ -569,8 +574,9 @@ __device__ int claim_next(const PipeArgs& P, int nmb, int& cursor)
 #ifndef HL_CNT_SPLIT
 #define HL_CNT_SPLIT 1
 #endif
-__global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(PipeArgs P, int mbw, int mbh)
+__global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(PipeArgs Pk, int mbw, int mbh)
 {
+    const PipeArgs& P0 = Pk;  // (the prologue's reads; the loop reads P, below)
     __shared__ Shared S;
     __shared__ FrameArgs sF;  // the task's frame arguments (frame_args_to_lds)
     __shared__ int32_t s_task;
@@ -583,13 +589,15 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
     // SGPR: loop-invariant VGPRs (the work-item index, the four reciprocals)
     // were spilled at the loop head and restored inside the macroblock body
     __shared__ SchedRecip s_rc;
-    if (threadIdx.x == 0) s_rc = SchedRecip{1.0f / (float)mbw, 1.0f / (float)nmb, 1.0f / (float)P.nstreams, 1.0f / (float)P.spp};
+    if (threadIdx.x == 0) s_rc = SchedRecip{1.0f / (float)mbw, 1.0f / (float)nmb, 1.0f / (float)P0.nstreams, 1.0f / (float)P0.spp};
     const int wbase = __builtin_amdgcn_readfirstlane(threadIdx.x) & ~63;
 #define HL_RC s_rc
 #define HL_WAVE0 (wbase == 0)
 #define HL_TID (wbase + (int)__lane_id())
 #else
-    const SchedRecip rc{1.0f / (float)mbw, 1.0f / (float)nmb, 1.0f / (float)P.nstreams, 1.0f / (float)P.spp};
+#if !HL_ARGS_OPAQUE
+    const SchedRecip rc{1.0f / (float)mbw, 1.0f / (float)nmb, 1.0f / (float)P0.nstreams, 1.0f / (float)P0.spp};
+#endif
 #define HL_RC rc
 #define HL_WAVE0 (threadIdx.x < 64)
 #define HL_TID ((int)threadIdx.x)
@@ -607,9 +615,29 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
     unsigned long long pst[3] = {0, 0, 0};  // pop_task rounds (wave 0)
     unsigned long long ptail[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // after the filters: barrier, release fence, successors' release; early release; its fence, release, spin, acquire
     const unsigned long long pw_t0 = __builtin_readcyclecounter();
-    unsigned long long* prof = P.fr[0].F.prof;
+    unsigned long long* prof = P0.fr[0].F.prof;
 #endif
     for (;;) {
+#if HL_ARGS_OPAQUE
+        // the run's arguments read from the kernel-argument segment in every
+        // task (scalar loads through a pointer the compiler cannot follow),
+        // not held in registers across the task body (spilled in the prologue)
+        using KArgs = __attribute__((address_space(4))) const PipeArgs;
+        KArgs* pk = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(pk));
+        const PipeArgs& P = *(const PipeArgs*)pk;
+#if !HL_SCHED_LDS
+        // the scheduler's reciprocals per task, from opaque copies (hoisted,
+        // they were held across the body too); udiv_small corrects the
+        // approximate reciprocal's quotient
+        float rw = (float)mbw, rn = (float)nmb;
+        asm volatile("" : "+v"(rw), "+v"(rn));
+        const SchedRecip rc{__builtin_amdgcn_rcpf(rw), __builtin_amdgcn_rcpf(rn), __builtin_amdgcn_rcpf((float)P.nstreams),
+                            __builtin_amdgcn_rcpf((float)P.spp)};
+#endif
+#else
+        const PipeArgs& P = P0;
+#endif
 #if defined(HL_PROFILE)
         const unsigned long long pt0 = __builtin_readcyclecounter();
 #endif
