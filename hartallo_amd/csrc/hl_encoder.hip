@@ -277,6 +277,9 @@ __device__ __forceinline__ int udiv_small(int a, int d, float inv)
 #ifndef HL_ARGS_OPAQUE
 #define HL_ARGS_OPAQUE 1
 #endif
+#ifndef HL_LOOP_STATE_LDS
+#define HL_LOOP_STATE_LDS 1
+#endif
 // 1: scheduler reciprocals in LDS, task coordinates and the wave's first
 // lane index in SGPRs (k_pipeline): VGPR spills 15 -> 13, but 0.4 % slower
 // (profiles/r05_ab_sched_lds_sgpr_coords_not_kept.log)
@@ -582,8 +585,19 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
     __shared__ int32_t s_task;
     const int nmb = mbw * mbh;
     const bool in_order = blockIdx.x == 0;  // claims tasks in run order (claim_next)
+#if HL_LOOP_STATE_LDS
+    // wave 0's loop state per lane in LDS (claim_next's cursor, pop_task's
+    // oldest pictures of the previous call): held in VGPRs, the two were
+    // spilled in the prologue
+    __shared__ int s_sched[2][64];
+    if (threadIdx.x < 64) {
+        s_sched[0][threadIdx.x] = 0;
+        s_sched[1][threadIdx.x] = -1;
+    }
+#else
     int cursor = 0;
     int olc = -1;  // wave 0: pop_task's oldest pictures of the previous call
+#endif
 #if HL_SCHED_LDS
     // the scheduler's reciprocals in LDS and the wave's first lane index in an
     // SGPR: loop-invariant VGPRs (the work-item index, the four reciprocals)
@@ -599,8 +613,16 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
     const SchedRecip rc{1.0f / (float)mbw, 1.0f / (float)nmb, 1.0f / (float)P0.nstreams, 1.0f / (float)P0.spp};
 #endif
 #define HL_RC rc
+#if HL_LOOP_STATE_LDS
+    // the wave's first lane index in an SGPR (the work-item index VGPR was
+    // spilled in the prologue and reloaded per task)
+    const int wbase = __builtin_amdgcn_readfirstlane(threadIdx.x) & ~63;
+#define HL_WAVE0 (wbase == 0)
+#define HL_TID (wbase + (int)__lane_id())
+#else
 #define HL_WAVE0 (threadIdx.x < 64)
 #define HL_TID ((int)threadIdx.x)
+#endif
 #endif
 #if defined(HL_PRIO_YOUNG)
     // the second-dispatched half of the workgroup (waves 4-7) loses every VALU
@@ -630,9 +652,9 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         // the scheduler's reciprocals per task, from opaque copies (hoisted,
         // they were held across the body too); udiv_small corrects the
         // approximate reciprocal's quotient
-        float rw = (float)mbw, rn = (float)nmb;
-        asm volatile("" : "+v"(rw), "+v"(rn));
-        const SchedRecip rc{__builtin_amdgcn_rcpf(rw), __builtin_amdgcn_rcpf(rn), __builtin_amdgcn_rcpf((float)P.nstreams),
+        int iw = mbw, in = nmb;
+        asm volatile("" : "+s"(iw), "+s"(in));
+        const SchedRecip rc{__builtin_amdgcn_rcpf((float)iw), __builtin_amdgcn_rcpf((float)in), __builtin_amdgcn_rcpf((float)P.nstreams),
                             __builtin_amdgcn_rcpf((float)P.spp)};
 #endif
 #else
@@ -642,11 +664,20 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         const unsigned long long pt0 = __builtin_readcyclecounter();
 #endif
         if (HL_WAVE0) {
+#if HL_LOOP_STATE_LDS
+            int ln = __lane_id();
+            asm volatile("" : "+v"(ln));  // (its LDS address computed here, not held)
+            int cursor = s_sched[0][ln], olc = s_sched[1][ln];
+#endif
             const int t = in_order ? claim_next(P, nmb, cursor) : pop_task(P, nmb, mbw, mbh, olc, HL_RC
 #if defined(HL_PROFILE)
                                                                                            , pst
 #endif
             );
+#if HL_LOOP_STATE_LDS
+            s_sched[0][ln] = cursor;
+            s_sched[1][ln] = olc;
+#endif
             if (!HL_EARLY_ACQ || in_order) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);  // (pop_task acquires itself)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
             if (__lane_id() == 0) s_task = t;
