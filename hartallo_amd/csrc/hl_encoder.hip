@@ -174,6 +174,10 @@ __global__ __launch_bounds__(64) void k_deblock_rows(DeblockArgs D, int32_t* row
 }
 #endif
 
+// 1: the task's plane and deblocked-sample stores non-temporal
+#ifndef HL_NT_STORES
+#define HL_NT_STORES 0
+#endif
 // Deblocking and plane blocks of task (x, y) (hl_pipeline.h).
 // The deblocking of one MB in the LDS tile (DbMbTile, hl_filters.h) that
 // aliases the decision's prediction scratch (free once the MB is decided):
@@ -233,10 +237,17 @@ __device__ void plane_block_lds(const uint8_t* ref, int W, uint8_t* pl0, int pst
             j |= (uint32_t)clip255(vj) << (8 * k);
         }
         const size_t o = (size_t)(Y * 16 + r + kPad) * pstride + X * 16 + c0 + kPad;
+#if HL_NT_STORES
+        __builtin_nontemporal_store(f, gmem(reinterpret_cast<uint32_t*>(pl0 + o)));
+        __builtin_nontemporal_store(b, gmem(reinterpret_cast<uint32_t*>(pl0 + plsz + o)));
+        __builtin_nontemporal_store(h, gmem(reinterpret_cast<uint32_t*>(pl0 + 2 * (size_t)plsz + o)));
+        __builtin_nontemporal_store(j, gmem(reinterpret_cast<uint32_t*>(pl0 + 3 * (size_t)plsz + o)));
+#else
         *gmem(reinterpret_cast<uint32_t*>(pl0 + o)) = f;
         *gmem(reinterpret_cast<uint32_t*>(pl0 + plsz + o)) = b;
         *gmem(reinterpret_cast<uint32_t*>(pl0 + 2 * (size_t)plsz + o)) = h;
         *gmem(reinterpret_cast<uint32_t*>(pl0 + 3 * (size_t)plsz + o)) = j;
+#endif
     }
     __syncthreads();  // the scratch is reused by the next block
 }
