@@ -121,7 +121,10 @@ constexpr int kMaxPass = (9 * 16 + kMbRows - 1) / kMbRows;  // rows per lane for
 #endif
 // quad rounds per pass: 2 x 128 blocks at 512 lanes; smaller workgroups take
 // enough rounds for the largest non-speculative step (9 16x16 candidates)
-constexpr int kQPass = kMbThreads >= 512 ? 2 : (9 * 16 + (kMbThreads >> 2) - 1) / (kMbThreads >> 2);
+#ifndef HL_QPASS
+#define HL_QPASS 2  // quad rounds a 512-lane pass holds (3: a 16x16 pass holds two steps)
+#endif
+constexpr int kQPass = kMbThreads >= 512 ? HL_QPASS : (9 * 16 + (kMbThreads >> 2) - 1) / (kMbThreads >> 2);
 constexpr int kPassItems = HL_QUAD_EVAL ? kQPass * (kMbThreads >> 2) : kMaxPass * kMbRows;
 constexpr int kSpecMaxBlocks = HL_QUAD_EVAL ? HL_SPEC_MAX_BLOCKS : 8;
 
