@@ -17,8 +17,8 @@ CXXFLAGS := -std=c++17 -O3 -fPIC -ffp-contract=off -Wall -Wno-unused-function -W
 # profiles/r02_sched_strategy_ab.log)
 DEVFLAGS := -mllvm -amdgpu-sched-strategy=iterative-ilp
 
-.PHONY: all product emu unit oracle profile poison variant clean
-all: product emu unit oracle
+.PHONY: all product emu unit oracle profile poison variant sanitize ubsan clean
+all: product emu unit oracle sanitize
 
 product: hartallo_amd/libhartallo_amd.so
 emu: tests/emu/libhl_emu.so
@@ -32,6 +32,35 @@ tests/emu/libhl_emu.so: tests/emu/hl_emu.hip $(HOSTSRC) $(HDRS)
 
 tests/gpu_unit/libhl_unit.so: tests/gpu_unit/hl_unit.hip $(HDRS)
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -shared -o $@ tests/gpu_unit/hl_unit.hip
+
+# sanitizer builds of the host code (tests/test_sanitizers.py, CPU):
+#   tests/sanitize/libhl_emu_asan.so  the emulator (the kernel logic on the
+#       host) under AddressSanitizer, the product's host writer (hl_writer.cpp)
+#       and rate controller (hl_rc.cpp) under AddressSanitizer +
+#       UndefinedBehaviorSanitizer; run with the clang ASan runtime preloaded
+#   tests/sanitize/rowgate_tsan  the pipelined run's row-gated slice writers
+#       (hl_writer.h RowGate) under ThreadSanitizer
+# (hipcc: every -fsanitize= directly after -Xarch_host, host code only)
+SANFLAGS := -std=c++17 -O1 -g -fno-omit-frame-pointer -fPIC -ffp-contract=off -Wno-unused-function -Wno-unused-variable
+ASAN := -Xarch_host -fsanitize=address
+UBSAN := -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined
+sanitize: tests/sanitize/libhl_emu_asan.so tests/sanitize/rowgate_tsan
+tests/sanitize/hl_writer_asan.o: $(CSRC)/hl_writer.cpp $(HDRS)
+	$(HIPCC) --offload-arch=$(ARCH) $(SANFLAGS) $(ASAN) $(UBSAN) -c -o $@ $<
+tests/sanitize/hl_rc_asan.o: $(CSRC)/hl_rc.cpp $(HDRS)
+	$(HIPCC) --offload-arch=$(ARCH) $(SANFLAGS) $(ASAN) $(UBSAN) -c -o $@ $<
+tests/sanitize/hl_emu_asan.o: tests/emu/hl_emu.hip $(HDRS)
+	$(HIPCC) --offload-arch=$(ARCH) $(SANFLAGS) -DHL_FAM3=1 $(ASAN) -c -o $@ $<
+tests/sanitize/libhl_emu_asan.so: tests/sanitize/hl_emu_asan.o tests/sanitize/hl_writer_asan.o tests/sanitize/hl_rc_asan.o
+	$(HIPCC) --offload-arch=$(ARCH) $(ASAN) $(UBSAN) -shared-libsan -shared -o $@ $^
+tests/sanitize/rowgate_tsan: tests/sanitize/rowgate_tsan.cpp $(CSRC)/hl_writer.cpp $(HDRS)
+	$(HIPCC) $(SANFLAGS) -Xarch_host -fsanitize=thread -o $@ tests/sanitize/rowgate_tsan.cpp $(CSRC)/hl_writer.cpp -lpthread
+# the emulator under UndefinedBehaviorSanitizer too: a 16-minute compile of
+# the kernel logic, run once per change of the shift / overflow idioms
+# (DESIGN.md §2); tests/test_sanitizers.py uses it when it is present
+ubsan: tests/sanitize/libhl_emu_ubsan.so
+tests/sanitize/libhl_emu_ubsan.so: tests/emu/hl_emu.hip $(HOSTSRC) $(HDRS)
+	$(HIPCC) --offload-arch=$(ARCH) $(SANFLAGS) -DHL_FAM3=1 $(ASAN) $(UBSAN) -shared-libsan -shared -o $@ tests/emu/hl_emu.hip $(HOSTSRC)
 
 # profiling build: same library (same device scheduling flags) with per-phase
 # clock64 counters (tools/phase_profile.py)
@@ -66,5 +95,5 @@ oracle: product  # oracle/_ref/drop_in_enc links the product library
 	$(MAKE) -C oracle
 
 clean:
-	rm -f hartallo_amd/libhartallo_amd.so tests/emu/libhl_emu.so tests/gpu_unit/libhl_unit.so
+	rm -f hartallo_amd/libhartallo_amd.so tests/emu/libhl_emu.so tests/gpu_unit/libhl_unit.so tests/sanitize/*.so tests/sanitize/*.o tests/sanitize/rowgate_tsan
 	$(MAKE) -C oracle clean

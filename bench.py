@@ -430,7 +430,13 @@ def spawn_ranks(n, argv, script=None):
     touched the GPU and does not afterwards: it only launches and waits.
     Ranks inherit stdout/stderr (rank 0 prints the line).  When one rank
     fails the others are terminated: they would wait forever at the next
-    collective."""
+    collective.  Deadlines: HL_BENCH_TIMEOUT seconds for the whole group
+    (default 1800), and HL_BENCH_GRACE seconds (default 120) for the others
+    once any rank has exited, even with 0 (a peer stuck at a collective or
+    on the GPU would otherwise be waited for forever); stragglers get
+    SIGTERM, then SIGKILL 10 s later, and the status is non-zero.  A failed
+    rendezvous is not retried on another port: a rank that failed may have
+    failed on the GPU, and GPU steps are never retried."""
     import signal
     import socket
 
@@ -444,6 +450,19 @@ def spawn_ranks(n, argv, script=None):
         procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + argv, env=env))
     rc = 0
     live = list(procs)
+    t0 = time.monotonic()
+    deadline = t0 + float(os.environ.get("HL_BENCH_TIMEOUT", "1800"))
+    grace = float(os.environ.get("HL_BENCH_GRACE", "120"))
+    term_at = None  # when the stragglers were sent SIGTERM
+
+    def stop(why):
+        nonlocal term_at
+        if term_at is None:
+            print(f"bench.py: {why}; stopping ranks {[procs.index(q) for q in live]}", file=sys.stderr, flush=True)
+            for q in live:
+                q.send_signal(signal.SIGTERM)
+            term_at = time.monotonic()
+
     try:
         while live:
             for p in list(live):
@@ -453,10 +472,19 @@ def spawn_ranks(n, argv, script=None):
                 live.remove(p)
                 if c and not rc:
                     rc = c if c > 0 else 128 - c
-                    print(f"bench.py: rank {procs.index(p)} exited with status {c}; stopping the other ranks",
-                          file=sys.stderr, flush=True)
-                    for q in live:
-                        q.send_signal(signal.SIGTERM)
+                    stop(f"rank {procs.index(p)} exited with status {c}")
+                elif live and deadline > time.monotonic() + grace:
+                    deadline = time.monotonic() + grace  # the others have `grace` seconds to follow
+            now = time.monotonic()
+            if live and term_at is None and now > deadline:
+                rc = rc or 124
+                stop(f"deadline reached after {now - t0:.0f} s")
+            if live and term_at is not None and now > term_at + 10:
+                for q in live:
+                    q.kill()
+                for q in live:
+                    q.wait()
+                live = []
             time.sleep(0.05)
     except KeyboardInterrupt:
         for p in live:

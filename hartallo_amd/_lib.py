@@ -148,8 +148,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_set_pipeline.restype = i32
     lib.hl_amd_set_rate_control.argtypes = [vp, ctypes.c_int64, i32, i32, i32, i32, i32]
     lib.hl_amd_set_rate_control.restype = i32
-    lib.hl_amd_set_max_ref_frame.argtypes = [vp, i32]
-    lib.hl_amd_set_max_ref_frame.restype = i32
+    if hasattr(lib, "hl_amd_set_max_ref_frame"):  # (absent from builds before round 5 loaded through HL_LIB)
+        lib.hl_amd_set_max_ref_frame.argtypes = [vp, i32]
+        lib.hl_amd_set_max_ref_frame.restype = i32
     lib.hl_amd_last_qp.argtypes = [vp]
     lib.hl_amd_last_qp.restype = i32
     lib.hl_amd_pipeline_occupancy.argtypes = []

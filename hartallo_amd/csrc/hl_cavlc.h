@@ -123,7 +123,7 @@ HD void cavlc_block(B& bw, const T* coeffLevel, int endIdx, int maxNumCoef, int 
             bw.u((uint32_t)((1 - nz[j]) >> 1) & 1u, 1);
             continue;
         }
-        int lc = nz[j] >= 0 ? (nz[j] << 1) - 2 : -(nz[j] << 1) - 1;
+        int lc = nz[j] >= 0 ? nz[j] * 2 - 2 : -(nz[j] * 2) - 1;
         if (j == t1 && t1 < 3 && lc >= 2) lc -= 2;
         int prefix, size;
         uint32_t suffix;

@@ -324,7 +324,7 @@ __device__ __forceinline__ int coop_dequant(int c, int ls, int qP)
 {
     const int q6 = qP / 6;
     const int p = __mul24(c, ls);
-    return qP >= 24 ? p << (q6 - 4) : (p + (1 << (3 - q6))) >> (4 - q6);
+    return qP >= 24 ? p * (1 << (q6 - 4)) : (p + (1 << (3 - q6))) >> (4 - q6);
 }
 
 }  // namespace hl

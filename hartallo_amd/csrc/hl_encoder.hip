@@ -998,7 +998,7 @@ struct hl_amd_encoder_s {
     IntraSpec* d_ispec = nullptr;                // intra helper results, per MB address
     bool helpers = true;                         // P macroblocks of pipelined runs get intra helper tasks
     int32_t helper_kept = 0, helper_rejected = 0, helper_self = 0;  // hl_amd_last_helper_stats
-    bool fam3 = true;                            // ... and 8x8-family helper tasks (HL_AMD_FAM3=0: off)
+    int fam3 = 1;                                // ... and 8x8-family helper tasks (HL_AMD_FAM3: 0 off, 2 runs too)
     int32_t fam3_kept = 0, fam3_rejected = 0;    // hl_amd_last_fam3_stats
     Fam3Out* d_f3 = nullptr;                     // 8x8-family helper results [MB] (only runs of one picture use them)
     PipeFrame *d_pf, *h_pf;
@@ -1144,7 +1144,7 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
         const char* h = getenv("HL_AMD_HELPERS");  // A/B knob (hl_amd_set_intra_helpers)
         e->helpers = !(h && atoi(h) == 0);
         const char* h3 = getenv("HL_AMD_FAM3");  // A/B knob
-        e->fam3 = !(h3 && atoi(h3) == 0);
+        e->fam3 = h3 ? atoi(h3) : 1;  // 0 off, 1 lone pictures, 2 every run of one stream
     }
     e->reach = 2;
     e->window = 64;
@@ -1239,7 +1239,7 @@ static int32_t encode_frame(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t
     F.is_intra = intra;
     F.me_range = std::min(64, std::max(1, e->p.me_range));
     F.early_term = e->p.me_early_term != 0;
-    F.lambda = 0.852 * (double)(1 << ((qp - 12) / 3));  // slice.c:1766
+    F.lambda = rdo_lambda(qp);  // slice.c:1766
     F.src[0] = y;
     F.src[1] = u;
     F.src[2] = v;
@@ -1474,7 +1474,7 @@ static FrameArgs frame_args(hl_amd_encoder_t* e, bool intra, int qp)
     F.is_intra = intra;
     F.me_range = std::min(64, std::max(1, e->p.me_range));
     F.early_term = e->p.me_early_term != 0;
-    F.lambda = 0.852 * (double)(1 << ((qp - 12) / 3));  // slice.c:1766
+    F.lambda = rdo_lambda(qp);  // slice.c:1766
     F.pstride = e->pstride;
     F.plsz = (int32_t)e->plsz;
     F.st = e->d_st;
@@ -1567,7 +1567,7 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
     const int slots = S * m;
     // a lone picture runs the kernel built with the 8x8-family helper tasks
     // (hl_encoder_fam3.hip): most workgroups would idle beside its wavefront
-    const bool fam3 = slots == 1 && e0->helpers && e0->fam3;
+    const bool fam3 = e0->helpers && (slots == 1 ? e0->fam3 != 0 : S == 1 && e0->fam3 == 2);
     for (int si = 0; si < S; ++si) {
         hl_amd_encoder_t* e = es[si];
         if (e->rc && (m != 1 || S != 1)) return HL_AMD_ERROR_INVALID_STATE;
@@ -1654,7 +1654,7 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
                 F.ispec = e->d_ispec;
                 F.hstate = e0->d_hstate + nmb * slot;
                 if (fam3) {
-                    F.f3 = e0->d_f3;  // fam3 runs hold one picture (slot 0)
+                    F.f3 = e0->d_f3;  // per MB address: one stream (a picture's helper ends before the next picture's MB starts)
                     F.hstate3 = e0->d_hstate + (size_t)nmb * (slots + slot);
                 }
             }
@@ -2013,7 +2013,10 @@ extern "C" int32_t hl_amd_encode_batch(hl_amd_encoder_t* e, int32_t n, const uin
 
 extern "C" int32_t hl_amd_set_max_ref_frame(hl_amd_encoder_t* e, int32_t max_ref_frame)
 {
-    if (!e || max_ref_frame < 0 || max_ref_frame > 16) return HL_AMD_ERROR_INVALID_PARAMETER;
+    // any value: the SPS carries min(MaxDpbMbs / PicSizeInMbs, max_ref_frame)
+    // (sps.c:635-636); refused only when that value itself is above 16 (the
+    // enhancement layers are larger pictures: their value is never higher)
+    if (!e || max_ref_frame < 0 || sps_max_num_ref_frames(e->W, e->H, max_ref_frame) > 16) return HL_AMD_ERROR_INVALID_PARAMETER;
     // the reference reads it once, when it builds the first SPS (sps.c:620-636)
     if (e->frame_index != 0 || svc_started(e)) return HL_AMD_ERROR_INVALID_STATE;
     e->max_ref_frame = max_ref_frame;

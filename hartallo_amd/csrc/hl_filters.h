@@ -144,7 +144,7 @@ HD void deblock_line(uint8_t* s, int step, int bS, bool chroma, int indexA, int 
     if (bS < 4) {
         const int tc0 = tc0_of(indexA, bS);
         const int tc = chroma ? tc0 + 1 : tc0 + (ap < beta) + (aq < beta);
-        const int delta = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+        const int delta = clip3(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
         s[-step] = (uint8_t)clip255(p0 + delta);
         s[0] = (uint8_t)clip255(q0 - delta);
         if (!chroma && ap < beta) s[-2 * step] = (uint8_t)(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));

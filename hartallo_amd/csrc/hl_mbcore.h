@@ -690,7 +690,7 @@ HD void grid_set(Shared& S, int x, int y, int w, int h, int mvx, int mvy)
     for (int by = y >> 2; by < (y + h) >> 2; ++by)
         for (int bx = x >> 2; bx < (x + w) >> 2; ++bx) {
             S.mvs[by + 1][bx + 1] = 2;
-            S.mvg[by + 1][bx + 1] = (mvx & 0xFFFF) | (mvy << 16);
+            S.mvg[by + 1][bx + 1] = (mvx & 0xFFFF) | (int)((uint32_t)mvy << 16);
         }
 }
 HD void grid_reset_inside(Shared& S)
@@ -968,7 +968,7 @@ __device__ __forceinline__ void mb_begin(Ctx& c)
                 const int pi = ((y >> lg2(M.part_h)) << (4 - lg2(M.part_w))) + (x >> lg2(M.part_w));
                 const int spi = is8x8(M.e_type) ? (((y & 7) >> lg2(M.sub_h[pi])) << (3 - lg2(M.sub_w[pi]))) + ((x & 7) >> lg2(M.sub_w[pi])) : 0;
                 st = 2;
-                v = (M.mv[pi][spi][0] & 0xFFFF) | (M.mv[pi][spi][1] << 16);
+                v = (M.mv[pi][spi][0] & 0xFFFF) | (int)((uint32_t)M.mv[pi][spi][1] << 16);
             }
         }
         S.mvs[gy][gx] = (int8_t)st;
@@ -1150,7 +1150,7 @@ HD void mb_begin(Ctx& c)
                 const int pi = ((y >> lg2(M.part_h)) << (4 - lg2(M.part_w))) + (x >> lg2(M.part_w));
                 const int spi = is8x8(M.e_type) ? (((y & 7) >> lg2(M.sub_h[pi])) << (3 - lg2(M.sub_w[pi]))) + ((x & 7) >> lg2(M.sub_w[pi])) : 0;
                 st = 2;
-                v = (M.mv[pi][spi][0] & 0xFFFF) | (M.mv[pi][spi][1] << 16);
+                v = (M.mv[pi][spi][0] & 0xFFFF) | (int)((uint32_t)M.mv[pi][spi][1] << 16);
             }
         }
         S.mvs[gy][gx] = (int8_t)st;
@@ -2167,7 +2167,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
                 lo[k] = __popcll(bal & ((1ull << (16 * k)) - 1ull));
                 n[k] = __popcll(bal & (0xFFFFull << (16 * k)));
             }
-            if (en) put_cand(c, g.px, g.py, g.pw, g.ph, __popcll(bal & ((1ull << i) - 1ull)), mx << sh, my << sh, i & 15, true);
+            if (en) put_cand(c, g.px, g.py, g.pw, g.ph, __popcll(bal & ((1ull << i) - 1ull)), mx * (1 << sh), my * (1 << sh), i & 15, true);
         }
 #if defined(HL_STEP_PROF)
         HL_PROF_ADD(c, 19, tgen);  // the pass's candidates generated and stored
@@ -2199,7 +2199,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
                         if (!((fl >> pt) & 1)) continue;
                         const int mx = ccx + (int)((pkx >> (3 * pt)) & 7) - 2, my = ccy + (int)((pky >> (3 * pt)) & 7) - 2;
                         if (mx < l0 || mx > r0 || my < t0 || my > b0) continue;
-                        put_cand(c, g.px, g.py, g.pw, g.ph, tot++, mx << sh, my << sh, pt, true);
+                        put_cand(c, g.px, g.py, g.pw, g.ph, tot++, mx * (1 << sh), my * (1 << sh), pt, true);
                     }
                 }
                 n[j] = tot - lo[j];
@@ -2448,7 +2448,7 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     if (c.tid < g.nblk) {
         const int bx = (g.px >> 2) + (c.tid & (g.nbw - 1)), by = (g.py >> 2) + (c.tid >> g.lbw);
         S.mvs[by + 1][bx + 1] = 2;
-        S.mvg[by + 1][bx + 1] = (b.mv[0] & 0xFFFF) | (b.mv[1] << 16);
+        S.mvg[by + 1][bx + 1] = (b.mv[0] & 0xFFFF) | (int)((uint32_t)b.mv[1] << 16);
     }
 #endif
     HL_SYNC();
@@ -2820,7 +2820,7 @@ HD void reconstruct_chroma(Ctx& c, bool intra_flag)
                 const int f00 = (L[0] + L[2]) + (L[1] + L[3]), f01 = (L[0] + L[2]) - (L[1] + L[3]);
                 const int f10 = (L[0] - L[2]) + (L[1] - L[3]), f11 = (L[0] - L[2]) - (L[1] - L[3]);
                 const int f = b == 0 ? f00 : (b == 1 ? f01 : (b == 2 ? f10 : f11));
-                dcc = ((f * scale) << (qP / 6)) >> 5;
+                dcc = ((f * scale) * (1 << (qP / 6))) >> 5;
             }
             if (dcc || (cac[comp] & (1 << b))) {  // (quad-uniform)
                 int q[4];
@@ -2850,7 +2850,7 @@ HD void reconstruct_chroma(Ctx& c, bool intra_flag)
                 const int f00 = (L[0] + L[2]) + (L[1] + L[3]), f01 = (L[0] + L[2]) - (L[1] + L[3]);
                 const int f10 = (L[0] - L[2]) + (L[1] - L[3]), f11 = (L[0] - L[2]) - (L[1] - L[3]);
                 const int f = b == 0 ? f00 : (b == 1 ? f01 : (b == 2 ? f10 : f11));
-                dcc = ((f * scale) << (qP / 6)) >> 5;
+                dcc = ((f * scale) * (1 << (qP / 6))) >> 5;
             }
             if (dcc || (cac[comp] & (1 << b))) {
                 int list[16], m[16];
@@ -3073,7 +3073,7 @@ HD void i16_heavy(Ctx& c)
             S.ih_dcl[mode][c.k().s] = (int16_t)qd;
             const int f = coop_lin(c.k().had, qd);
             const int scale = level_scale(qp % 6, 0, 0), q6 = qp / 6;
-            S.dcY[mode * 16 + c.k().p] = qp >= 36 ? (f * scale) << (q6 - 6) : (f * scale + (1 << (5 - q6))) >> (6 - q6);
+            S.dcY[mode * 16 + c.k().p] = qp >= 36 ? (f * scale) * (1 << (q6 - 6)) : (f * scale + (1 << (5 - q6))) >> (6 - q6);
             if (lane == 0) {  // block 0's nC neighbours lie outside the MB: the DC rate is fixed
                 const int nC = nc_luma_of(S, 0, [&](int ni) -> int { return S.tc[ni]; });
                 S.ih.dcs[mode][0] = sd.rest + coop_token_len(S.ct, nC, sd.tc, sd.t1);
@@ -3158,7 +3158,7 @@ HD void i16_heavy(Ctx& c)
                 f[i * 4 + 3] = d[i * 4 + 0] - d[i * 4 + 1] + d[i * 4 + 2] - d[i * 4 + 3];
             }
             const int scale = level_scale(F.qp % 6, 0, 0), q6 = F.qp / 6;
-            for (int i = 0; i < 16; ++i) dcY[i] = F.qp >= 36 ? (f[i] * scale) << (q6 - 6) : (f[i] * scale + (1 << (5 - q6))) >> (6 - q6);
+            for (int i = 0; i < 16; ++i) dcY[i] = F.qp >= 36 ? (f[i] * scale) * (1 << (q6 - 6)) : (f[i] * scale + (1 << (5 - q6))) >> (6 - q6);
         }
         int df = 0, dz = 0;
         for (int t = 0; t < 16; ++t) {

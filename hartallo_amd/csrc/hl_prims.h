@@ -125,6 +125,14 @@ static constexpr uint8_t kTc0[52][3] = {
 // tc0 for bS 1..3 (bS 4 uses the strong filter)
 HD int tc0_of(int indexA, int bS) { return kTc0[indexA][bS - 1]; }
 
+// lambda_mode = HL_CODEC_264_RDO_LAMBDA_FACT_ALL * (1 << ((QP - 12) / 3)) as
+// the reference's x86 build computes it (slice.c:1766): the int shift count
+// is negative below QP 10, and x86's SHL uses its low 5 bits -- QP 0-2 give
+// 2^28 / 2^29, QP 3-6 2^30, QP 7-9 (int)(1u << 31) = INT_MIN, a negative
+// lambda.  Written with that masking explicit (a negative shift count is
+// undefined in C++).
+HD double rdo_lambda(int qp) { return 0.852 * (double)(int32_t)(1u << (((qp - 12) / 3) & 31)); }
+
 // coeff_token lengths, Table 9-5: [vlc 0..2][TrailingOnes][TotalCoeff]
 static constexpr uint8_t kTokLen[3][4][17] = {
     {{1, 6, 8, 9, 10, 11, 13, 13, 13, 14, 14, 15, 15, 16, 16, 16, 16},
@@ -254,7 +262,7 @@ HD CavlcStat cavlc_stat(const T* coeffLevel, int maxNumCoef, int endIdx, bool ch
                 bits += 1;
             }
             else {
-                int lc = nz[j] >= 0 ? (nz[j] << 1) - 2 : -(nz[j] << 1) - 1;
+                int lc = nz[j] >= 0 ? nz[j] * 2 - 2 : -(nz[j] * 2) - 1;
                 if (j == t1 && t1 < 3 && lc >= 2) lc -= 2;
                 bits += level_code_len(suffixLength, lc);
                 if (suffixLength == 0) suffixLength = 1;
@@ -296,17 +304,17 @@ HD void fwd4x4(const int* in, int* out)
     for (int i = 0; i < 4; ++i) {
         const int a = in[0 * 4 + i], b = in[1 * 4 + i], c = in[2 * 4 + i], d = in[3 * 4 + i];
         t[0 * 4 + i] = a + b + c + d;
-        t[1 * 4 + i] = (a << 1) + b - c - (d << 1);
+        t[1 * 4 + i] = a * 2 + b - c - d * 2;
         t[2 * 4 + i] = a - b - c + d;
-        t[3 * 4 + i] = a - (b << 1) + (c << 1) - d;
+        t[3 * 4 + i] = a - b * 2 + c * 2 - d;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int a = t[i * 4 + 0], b = t[i * 4 + 1], c = t[i * 4 + 2], d = t[i * 4 + 3];
         out[i * 4 + 0] = a + b + c + d;
-        out[i * 4 + 1] = (a << 1) + b - c - (d << 1);
+        out[i * 4 + 1] = a * 2 + b - c - d * 2;
         out[i * 4 + 2] = a - b - c + d;
-        out[i * 4 + 3] = a - (b << 1) + (c << 1) - d;
+        out[i * 4 + 3] = a - b * 2 + c * 2 - d;
     }
 }
 
@@ -389,7 +397,7 @@ HD void dequant_idct(int qP, const int* c, bool keep_dc, int* r)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int ls = level_scale(qm, i >> 2, i & 3);
-        d[i] = qP >= 24 ? (c[i] * ls) << (q6 - 4) : (c[i] * ls + (1 << (3 - q6))) >> (4 - q6);
+        d[i] = qP >= 24 ? (c[i] * ls) * (1 << (q6 - 4)) : (c[i] * ls + (1 << (3 - q6))) >> (4 - q6);
     }
     if (keep_dc) d[0] = c[0];
     idct4x4(d, r);

@@ -474,7 +474,7 @@ HD void svc_encode_mb(const SvcArgs& A, SvcShared& S, int addr, int tid, int nth
                 const int f00 = (L[0] + L[2]) + (L[1] + L[3]), f01 = (L[0] + L[2]) - (L[1] + L[3]);
                 const int f10 = (L[0] - L[2]) + (L[1] - L[3]), f11 = (L[0] - L[2]) - (L[1] - L[3]);
                 const int f = b == 0 ? f00 : (b == 1 ? f01 : (b == 2 ? f10 : f11));
-                dcc = ((f * scale) << (qP / 6)) >> 5;
+                dcc = ((f * scale) * (1 << (qP / 6))) >> 5;
             }
             if (dcc || (cac[comp] & (1 << b))) {
                 int list[16], m[16];

@@ -165,7 +165,7 @@ void write_block(BitWriter& bw, const T* coeffLevel, int endIdx, int maxNumCoef,
             bw.u1((uint32_t)((1 - nz[j]) >> 1));
             continue;
         }
-        int lc = nz[j] >= 0 ? (nz[j] << 1) - 2 : -(nz[j] << 1) - 1;
+        int lc = nz[j] >= 0 ? nz[j] * 2 - 2 : -(nz[j] * 2) - 1;
         if (j == t1 && t1 < 3 && lc >= 2) lc -= 2;
         const LevelCode& L = level_code(suffixLength, lc);
         if (L.prefix > 0) bw.u(0, L.prefix);

@@ -130,7 +130,7 @@ def hl_codec_encode(codec: hl_codec_t, frame: hl_frame_video_t, result: hl_codec
     if frame.width % 16 or frame.height % 16:
         return HL_ERROR_INVALID_FORMAT  # hl_codec_264.c:437-438
     if codec._enc is None or (codec.width, codec.height) != (frame.width, frame.height):
-        if codec.threads_count != 1:  # threads_count slices per picture (hl_codec_264.c:571): one slice here
+        if codec.threads_count > 1:  # threads_count slices per picture (hl_codec_264.c:571): one slice here; <= 0 is 1 (hl_codec_264.c:1053-1054)
             return HL_ERROR_NOT_IMPLEMENTED
         try:
             codec._enc = Encoder(frame.width, frame.height, codec.qp, codec.me_range, codec.deblock_flag, codec.gop_size,

@@ -139,8 +139,10 @@ int32_t hl_amd_set_rate_control(hl_amd_encoder_t* encoder, int64_t bitrate, int3
  * num_ref_idx_l0_default_active_minus1 (hl_codec_264_pps.c:291), for every
  * (subset) SPS / PPS of the stream.  The reference's P slices override the
  * active references to one (slice.c:289, encode.c:269), so only the headers
- * change.  0..16; call before the first frame (the reference reads it when
- * it builds the first SPS), else HL_AMD_ERROR_INVALID_STATE. */
+ * change.  Any value >= 0 (the reference takes any and writes the clamped
+ * one: 720p with 32 gives 5); HL_AMD_ERROR_INVALID_PARAMETER only when the
+ * clamped value is above 16.  Call before the first frame (the reference
+ * reads it when it builds the first SPS), else HL_AMD_ERROR_INVALID_STATE. */
 int32_t hl_amd_set_max_ref_frame(hl_amd_encoder_t* encoder, int32_t max_ref_frame);
 
 /* SliceQPY of the last encoded picture (the rate-controlled QP), or -1 */

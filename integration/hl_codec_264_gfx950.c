@@ -18,6 +18,7 @@
 #include <hartallo/hl_object.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "hartallo_amd.h" /* include/hartallo_amd.h of the gfx950 library */
 
@@ -74,7 +75,13 @@ static HL_ERROR_T gfx950_open(hl_codec_264_gfx950_t* self, hl_codec_t* base, hl_
     p.deblock = base->deblock_flag;
     p.gop_size = base->gop_size;
     p.me_early_term = base->me_early_term_flag;
-    p.device = 0; /* one process per GPU (HIP_VISIBLE_DEVICES) */
+    /* the HIP device: HL_AMD_DEVICE, read at every open (a process that
+     * drives several GPUs through this API sets it before hl_codec_encode
+     * opens the codec's encoder), else 0 (one process per GPU) */
+    {
+        const char* dv = getenv("HL_AMD_DEVICE");
+        p.device = dv ? atoi(dv) : 0;
+    }
     if ((err = hl_amd_encoder_create(&p, &self->enc))) return (HL_ERROR_T)err; /* HL_ERROR_T values (hl_types.h:101-122) */
     /* SPS max_num_ref_frames / PPS num_ref_idx_l0_default_active_minus1
      * (hl_codec_264_sps.c:620-636, hl_codec_264_pps.c:291) */

@@ -2414,7 +2414,10 @@ int hlo_encode_frame(hlo_enc_t* e, const uint8_t* y, const uint8_t* u, const uin
     }
     if (e->frame_index == 0) n += write_headers(e, out);
     e->qp = e->p.qp;
-    e->lambda_mode = LAMBDA_FACT * (double)(1 << ((e->qp - 12) / 3));
+    /* slice.c:1766 as the reference's x86 build computes it: below QP 10 the
+     * int shift count (QP - 12) / 3 is negative and SHL uses its low 5 bits
+     * (QP 7-9: (int)(1u << 31) = INT_MIN, a negative lambda) */
+    e->lambda_mode = LAMBDA_FACT * (double)(int32_t)(1u << (((e->qp - 12) / 3) & 31));
     e->skip_run = 0;
     memset(e->slice_buf, 0, e->slice_cap);
     bw_init(&bw, e->slice_buf, e->slice_cap);
@@ -2514,7 +2517,7 @@ void hlo_dump_mbs(const hlo_enc_t* e, int32_t* recs)
 /* hl_codec_t.max_ref_frame, before the first frame (only the SPS / PPS read it) */
 int hlo_set_max_ref_frame(hlo_enc_t* e, int max_ref_frame)
 {
-    if (!e || max_ref_frame < 0 || max_ref_frame > 16 || e->frame_index) return -1;
+    if (!e || max_ref_frame < 0 || e->frame_index) return -1; /* any value: the SPS carries min(MaxDpbMbs / PicSizeInMbs, it) (sps.c:635-636) */
     e->max_ref_frame = max_ref_frame;
     return 0;
 }

@@ -311,7 +311,7 @@ extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, co
     F.is_intra = intra;
     F.me_range = e->me_range;
     F.early_term = e->early_term;
-    F.lambda = 0.852 * (double)(1 << ((qp - 12) / 3));
+    F.lambda = rdo_lambda(qp);
     F.src[0] = y;
     F.src[1] = u;
     F.src[2] = v;

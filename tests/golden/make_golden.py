@@ -16,6 +16,7 @@ including make_decoded_golden.py's decoded_md5 fields -- is kept.
 """
 import json
 import os
+import re
 import subprocess
 import sys
 import tempfile
@@ -25,7 +26,8 @@ sys.path.insert(0, os.path.dirname(HERE))
 
 import numpy as np  # noqa: E402
 
-from hl_testlib import GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, GOLDEN_MRF_CONFIGS, GOLDEN_RC_CONFIGS, REF_ENC, golden_input, md5, slice_qps  # noqa: E402
+from hl_testlib import (GOLDEN_CONFIGS, GOLDEN_ET_CONFIGS, GOLDEN_FAIL_CONFIGS, GOLDEN_MRF_CONFIGS, GOLDEN_RC_CONFIGS, REF_ENC,  # noqa: E402
+                        golden_input, md5, slice_qps)
 
 
 def main():
@@ -35,7 +37,7 @@ def main():
     gpath = os.path.join(HERE, "golden.json")
     table = json.load(open(gpath)) if only else {}
     with tempfile.TemporaryDirectory() as td:
-        for cfg in GOLDEN_CONFIGS + GOLDEN_ET_CONFIGS + GOLDEN_RC_CONFIGS + GOLDEN_MRF_CONFIGS:
+        for cfg in GOLDEN_CONFIGS + GOLDEN_ET_CONFIGS + GOLDEN_RC_CONFIGS + GOLDEN_MRF_CONFIGS + GOLDEN_FAIL_CONFIGS:
             name, w, h, n, qp, mer, db, gop, seed = cfg[:9]
             if only and name not in only:
                 continue
@@ -52,10 +54,17 @@ def main():
             inp = os.path.join(td, name + ".yuv")
             clip.tofile(inp)
             pre = os.path.join(td, name)
-            subprocess.run([REF_ENC, str(w), str(h), str(n), str(qp), str(mer), str(db), str(gop), str(et), inp, pre, "rec"],
-                           check=True, stdout=subprocess.DEVNULL, env=env)
+            r = subprocess.run([REF_ENC, str(w), str(h), str(n), str(qp), str(mer), str(db), str(gop), str(et), inp, pre, "rec"],
+                               stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True, env=env)
+            fail = {}
+            if cfg in GOLDEN_FAIL_CONFIGS:  # ref_harness.c: "encode err <code> at frame <f>", exit status 4
+                m = re.search(r"encode err (\d+) at frame (\d+)", r.stderr)
+                assert r.returncode == 4 and m, f"{name}: the reference was expected to fail"
+                fail = {"fail_error": int(m.group(1)), "fail_frame": int(m.group(2))}
+            elif r.returncode:
+                raise subprocess.CalledProcessError(r.returncode, REF_ENC, stderr=r.stderr[-2000:])
             stream = open(pre + ".264", "rb").read()
-            rec = np.fromfile(pre + ".rec.yuv", dtype=np.uint8).reshape(n, -1)
+            rec = np.fromfile(pre + ".rec.yuv", dtype=np.uint8).reshape(-1, w * h * 3 // 2)
             with open(os.path.join(HERE, name + ".264"), "wb") as f:
                 f.write(stream)
             table[name] = {
@@ -64,6 +73,7 @@ def main():
                 **({"rc_bitrate": cfg[9], "rc_basicunit": cfg[10], "rc_qp_min": cfg[11], "rc_qp_max": cfg[12],
                     "fps_num": 1, "fps_den": 15} if cfg in GOLDEN_RC_CONFIGS else {}),
                 **({"max_ref_frame": cfg[9]} if cfg in GOLDEN_MRF_CONFIGS else {}),
+                **fail,
                 "stream_md5": md5(stream), "stream_bytes": len(stream), "slice_qp": slice_qps(stream, qp),
                 "recon_md5": [md5(r) for r in rec],
             }

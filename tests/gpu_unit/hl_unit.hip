@@ -8,6 +8,8 @@
 #include "../../hartallo_amd/csrc/hl_coop.h"
 #include "../../hartallo_amd/csrc/hl_quad.h"
 #include "../../hartallo_amd/csrc/hl_filters.h"
+#include "../../hartallo_amd/csrc/hl_mbcore.h"
+#include "../../hartallo_amd/csrc/hl_cavlc.h"
 
 using namespace hl;
 
@@ -168,4 +170,177 @@ extern "C" int unit_planes(const uint8_t* h_ref, int W, int H, uint8_t* out_gpu,
         for (int y = 0; y < ph; ++y)
             for (int x = 0; x < W + 2 * kPad; ++x) out_host[p * plsz + (size_t)y * pstride + x] = qpel_plane_sample(h_ref, W, H, p, x - kPad, y - kPad);
     return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Op-level parity against the reference's own kernels (tests/test_gpu_ops.py,
+// tests/golden/ops_*.npz made by tests/golden/make_op_golden.py through
+// oracle/_ref/ref_ops)
+// ---------------------------------------------------------------------------
+
+// CAVLC residual blocks from scan-order level lists.
+//   cavlc_block (hl_cavlc.h, the GPU slice writer) -> the bits themselves;
+//   quad_cavlc (hl_quad.h, the candidate evaluation's and Intra16x16's rate)
+//   for kinds 0 / 4 -> rest + the coeff_token length of the nC class (tc >
+//   0; -1 else)
+struct UnitCavlcIn {
+    int32_t kind, nC, level[16];  // kind 0 luma 4x4, 1 Intra16x16 AC, 2 chroma DC, 3 chroma AC, 4 AC as the RDO prices it
+};
+struct UnitCavlcOut {
+    int32_t nbits, quad_bits, tc, pad;
+    uint32_t words[24];
+};
+
+__global__ __launch_bounds__(64) void k_unit_cavlc_block(const UnitCavlcIn* in, int n, UnitCavlcOut* out)
+{
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    const UnitCavlcIn& x = in[i];
+    const int maxn = (x.kind == 0 || x.kind == 4) ? 16 : (x.kind == 2 ? 4 : 15);
+    BitOr bw{out[i].words, 0};
+    cavlc_block(bw, x.level, maxn - 1, maxn, x.nC);
+    out[i].nbits = (int)bw.pos;
+}
+
+__global__ __launch_bounds__(256) void k_unit_cavlc_quad(const UnitCavlcIn* in, int n, UnitCavlcOut* out)
+{
+    __shared__ CoopTables T;
+    __shared__ int lvs[64][16];
+    coop_tables_init(T, threadIdx.x, 256);
+    __syncthreads();
+    const LaneQ Q = make_laneq(threadIdx.x, 28);  // (the scan word does not depend on the QP)
+    const int qg = threadIdx.x >> 2;
+    const int b = blockIdx.x * 64 + qg;
+    if (b >= n) return;  // whole quads
+    const UnitCavlcIn& x = in[b];
+    const int ac = (x.kind == 1 || x.kind == 4) ? 1 : 0;
+    int L[4];
+    for (int c = 0; c < 4; ++c) {  // this lane's coefficient row, raster: the level at its scan index
+        const int li = (int)((Q.zz >> (4 * c)) & 15) - ac;
+        L[c] = li >= 0 ? x.level[li] : 0;
+    }
+    const CoopStat st = quad_cavlc(T, Q, L, ac, lvs[qg]);
+    if (Q.r == 0 && (x.kind == 0 || x.kind == 4)) {  // the RDO's 16-entry lists (rdo.c:1676, 1981)
+        const int cls = x.nC < 2 ? 0 : (x.nC < 4 ? 1 : (x.nC < 8 ? 2 : 3));
+        out[b].quad_bits = st.tc ? st.rest + (int)((T.tok3[st.t1][st.tc] >> (5 * cls)) & 31) : -1;
+        out[b].tc = st.tc;
+    }
+}
+
+extern "C" int unit_cavlc(const UnitCavlcIn* h_in, int n, UnitCavlcOut* h_out)
+{
+    UnitCavlcIn* d_in = nullptr;
+    UnitCavlcOut* d_out = nullptr;
+    if (hipMalloc(&d_in, sizeof(UnitCavlcIn) * (size_t)n) || hipMalloc(&d_out, sizeof(UnitCavlcOut) * (size_t)n)) return -1;
+    if (hipMemcpy(d_in, h_in, sizeof(UnitCavlcIn) * (size_t)n, hipMemcpyHostToDevice) ||
+        hipMemset(d_out, 0, sizeof(UnitCavlcOut) * (size_t)n))
+        return -2;
+    k_unit_cavlc_block<<<(n + 63) / 64, 64>>>(d_in, n, d_out);
+    k_unit_cavlc_quad<<<(n + 63) / 64, 256>>>(d_in, n, d_out);
+    const hipError_t e = hipDeviceSynchronize();
+    (void)hipMemcpy(h_out, d_out, sizeof(UnitCavlcOut) * (size_t)n, hipMemcpyDeviceToHost);
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    return e == hipSuccess ? 0 : -3;
+}
+extern "C" int unit_sizeof_cavlc_out() { return (int)sizeof(UnitCavlcOut); }
+
+// 16x16 luma inter predictions as the macroblock's finalize computes them
+// (hl_mbcore.h inter_pred_mb: the partition origin clamped to [-17, W + 17]
+// like interpol.c, the quarter-pel phase's two samples of the k_planes
+// planes via qpel_entry (kQpelTab), their rounded average); one 4-lane quad
+// per (record, 4x4 block), lane r = row r.
+struct UnitPredIn {
+    int32_t mbx, mby, mvx, mvy;
+};
+__global__ __launch_bounds__(256) void k_unit_lpred(const uint8_t* pl, int W, int H, int pstride, int plsz, const UnitPredIn* in, int n,
+                                                    uint8_t* out)
+{
+    const int q = (blockIdx.x * 256 + threadIdx.x) >> 2, r = threadIdx.x & 3;
+    const int i = q >> 4, t = q & 15;
+    if (i >= n) return;
+    const UnitPredIn x = in[i];
+    const int bx = (t & 3) * 4, by = (t >> 2) * 4;
+    const int X = clip3(-17, W + 17, 16 * x.mbx + (x.mvx >> 2)) + kPad + bx;
+    const int Y = clip3(-17, H + 17, 16 * x.mby + (x.mvy >> 2)) + kPad + by + r;
+    const uint32_t e = qpel_entry(((x.mvy & 3) << 2) | (x.mvx & 3));
+    const int o1 = (int)(e & 3) * plsz + (Y + (int)((e >> 3) & 1)) * pstride + X + (int)((e >> 2) & 1);
+    const int o2 = (e & 16) ? (int)((e >> 5) & 3) * plsz + (Y + (int)((e >> 8) & 1)) * pstride + X + (int)((e >> 7) & 1) : o1;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const auto base = gmem(pl);
+    const uint32_t pr = avg_u8x4(ld_u8x4(base, o1), ld_u8x4(base, o2));
+    *reinterpret_cast<uint32_t*>(out + 256 * (size_t)i + (by + r) * 16 + bx) = pr;
+#endif
+}
+
+extern "C" int unit_lpred(const uint8_t* h_ref, int W, int H, const UnitPredIn* h_in, int n, uint8_t* h_out)
+{
+    const int pstride = (W + 2 * kPad + 63) & ~63, ph = H + 2 * kPad;
+    const size_t plsz = (size_t)pstride * ph;
+    uint8_t *d_ref = nullptr, *d_pl = nullptr, *d_out = nullptr;
+    UnitPredIn* d_in = nullptr;
+    // (+64: the 4-byte loads read whole aligned words past the last plane's end)
+    if (hipMalloc(&d_ref, (size_t)W * H) || hipMalloc(&d_pl, 4 * plsz + 64) || hipMalloc(&d_in, sizeof(UnitPredIn) * (size_t)n) ||
+        hipMalloc(&d_out, 256 * (size_t)n))
+        return 1;
+    for (int i = 0; i < n; ++i)  // the kernel's addressing assumes the records' blocks inside the padded planes
+        if (h_in[i].mbx < 0 || h_in[i].mby < 0 || 16 * h_in[i].mbx >= W || 16 * h_in[i].mby >= H) return 2;
+    if (hipMemcpy(d_ref, h_ref, (size_t)W * H, hipMemcpyHostToDevice) || hipMemset(d_pl, 0, 4 * plsz + 64) ||
+        hipMemcpy(d_in, h_in, sizeof(UnitPredIn) * (size_t)n, hipMemcpyHostToDevice))
+        return 3;
+    const dim3 grid((W + 2 * kPad + kPlTileW - 1) / kPlTileW, (H + 2 * kPad + kPlTileH - 1) / kPlTileH);
+    k_planes<<<grid, 256>>>(d_ref, W, H, d_pl, pstride, (int)plsz);
+    k_unit_lpred<<<(n * 64 + 255) / 256, 256>>>(d_pl, W, H, pstride, (int)plsz, d_in, n, d_out);
+    const hipError_t e = hipDeviceSynchronize();
+    (void)hipMemcpy(h_out, d_out, 256 * (size_t)n, hipMemcpyDeviceToHost);
+    (void)hipFree(d_ref);
+    (void)hipFree(d_pl);
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    return e == hipSuccess ? 0 : 4;
+}
+
+// Deblocking of 8 lines across one edge (p[k][l] = pk of line l) with the
+// product's line filter (hl_filters.h deblock_line, kAlpha / kBeta / kTc0),
+// one lane per line.
+struct UnitDbIn {
+    uint8_t p[4][8], q[4][8];
+    int32_t bS, indexA, chroma;
+};
+struct UnitDbOut {
+    uint8_t p[3][8], q[3][8];
+};
+__global__ __launch_bounds__(64) void k_unit_dblk(const UnitDbIn* in, int n, UnitDbOut* out)
+{
+    const int g = blockIdx.x * 64 + threadIdx.x;
+    const int i = g >> 3, l = g & 7;
+    if (i >= n) return;
+    const UnitDbIn& x = in[i];
+    uint8_t s[8];
+    for (int k = 0; k < 4; ++k) {
+        s[3 - k] = x.p[k][l];
+        s[4 + k] = x.q[k][l];
+    }
+    const int ia = x.indexA;
+    deblock_line(s + 4, 1, x.bS, x.chroma != 0, ia, kAlpha[ia], kBeta[ia]);
+    for (int k = 0; k < 3; ++k) {
+        out[i].p[k][l] = s[3 - k];
+        out[i].q[k][l] = s[4 + k];
+    }
+}
+
+extern "C" int unit_dblk(const UnitDbIn* h_in, int n, UnitDbOut* h_out)
+{
+    UnitDbIn* d_in = nullptr;
+    UnitDbOut* d_out = nullptr;
+    for (int i = 0; i < n; ++i)  // table indices the kernel reads
+        if (h_in[i].indexA < 0 || h_in[i].indexA > 51 || h_in[i].bS < 1 || h_in[i].bS > 4) return -4;
+    if (hipMalloc(&d_in, sizeof(UnitDbIn) * (size_t)n) || hipMalloc(&d_out, sizeof(UnitDbOut) * (size_t)n)) return -1;
+    if (hipMemcpy(d_in, h_in, sizeof(UnitDbIn) * (size_t)n, hipMemcpyHostToDevice)) return -2;
+    k_unit_dblk<<<(n * 8 + 63) / 64, 64>>>(d_in, n, d_out);
+    const hipError_t e = hipDeviceSynchronize();
+    (void)hipMemcpy(h_out, d_out, sizeof(UnitDbOut) * (size_t)n, hipMemcpyDeviceToHost);
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    return e == hipSuccess ? 0 : -3;
 }

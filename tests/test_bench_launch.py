@@ -8,6 +8,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -73,3 +74,28 @@ def test_spawn_ranks_failure_stops_the_others(tmp_path):
                      "if os.environ['RANK'] == '1':\n    sys.exit(3)\n"
                      "time.sleep(600)\n")
     assert bench.spawn_ranks(2, [], script=str(probe)) == 3
+
+
+def test_spawn_ranks_straggler_after_clean_exit(tmp_path, monkeypatch):
+    """Rank 1 exits 0 while rank 0 hangs (a peer stuck at a collective or on
+    the GPU): after the grace period rank 0 is stopped (SIGTERM, then SIGKILL
+    if it ignores it) and the status is non-zero."""
+    probe = tmp_path / "probe.py"
+    probe.write_text("import os, signal, sys, time\n"
+                     "if os.environ['RANK'] == '1':\n    sys.exit(0)\n"
+                     "signal.signal(signal.SIGTERM, signal.SIG_IGN)\n"
+                     "time.sleep(600)\n")
+    monkeypatch.setenv("HL_BENCH_GRACE", "1")
+    t = time.monotonic()
+    assert bench.spawn_ranks(2, [], script=str(probe)) == 124
+    assert time.monotonic() - t < 60
+
+
+def test_spawn_ranks_deadline(tmp_path, monkeypatch):
+    """Every rank hangs: the whole-group deadline stops them."""
+    probe = tmp_path / "probe.py"
+    probe.write_text("import time\ntime.sleep(600)\n")
+    monkeypatch.setenv("HL_BENCH_TIMEOUT", "2")
+    t = time.monotonic()
+    assert bench.spawn_ranks(2, [], script=str(probe)) == 124
+    assert time.monotonic() - t < 60

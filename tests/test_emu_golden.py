@@ -165,3 +165,17 @@ def test_fam3_helpers_match_reference(cfg, mode):
     rejected = enc.lib.emu_helper_fam3(ctypes.c_void_p(enc.h_), 1)
     if any(f % gop for f in range(n)) and w * h >= 64 * 48:
         assert kept + rejected > 0
+
+
+def test_kernel_logic_fails_where_reference_fails():
+    """QP 8 (negative lambda): the first P picture's slice outgrows the
+    reference's slice buffer; the kernel logic and the host writer refuse the
+    same frame (HL_ERROR_TOOSHORT in the product) after the same bytes."""
+    from hl_testlib import _planes, check_reference_failure
+
+    def enc_ok(e, frame):
+        y, u, v = _planes(frame, e.w, e.h)
+        n = e.lib.emu_encode_frame(ctypes.c_void_p(e.h_), y.ctypes.data, u.ctypes.data, v.ctypes.data, e.out.ctypes.data, e.out.size)
+        return e.out[:n].tobytes() if n > 0 else None
+
+    check_reference_failure("fail_qcif_qp8_neg_lambda", lambda c: EmuEncoder(c[1], c[2], c[4], c[5], c[6], c[7]), enc_ok, GOLD)

@@ -131,6 +131,28 @@ def test_gop2_short_frames_vs_oracle(gpu):
     _vs_oracle(320, 240, 5, 26, 8, 1, 2, 21)
 
 
+def test_fails_where_reference_fails(gpu):
+    """QP 8: the reference's lambda is negative (slice.c:1766 with x86's
+    shift-count masking, hl_prims.h rdo_lambda) and its first P picture's
+    slice outgrows the slice buffer: HL_ERROR_TOOSHORT.  The GPU encoder
+    codes the I picture byte for byte and refuses the P picture with the same
+    error, per call and batched."""
+    from hartallo_amd import HlAmdError
+
+    from hl_testlib import check_reference_failure
+
+    g = GOLD["fail_qcif_qp8_neg_lambda"]
+
+    def enc_ok(e, frame):
+        try:
+            return e.encode(frame)
+        except HlAmdError as x:
+            assert x.code == g["fail_error"], f"refused with {x.code}, the reference with {g['fail_error']}"
+            return None
+
+    check_reference_failure("fail_qcif_qp8_neg_lambda", lambda c: GpuEncoder(c[1], c[2], c[4], c[5], c[6], c[7]), enc_ok, GOLD)
+
+
 def test_rejects_bad_format(gpu):
     from hartallo_amd import Encoder, HlAmdError
 

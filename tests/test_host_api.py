@@ -31,8 +31,10 @@ def test_frame_fill_and_format_errors():
     import torch
 
     if not torch.cuda.is_available():  # max_ref_frame is forwarded; without a GPU the encoder refuses loudly
-        c.threads_count, c.max_ref_frame = 1, 4
-        assert hc.hl_codec_encode(c, f, hc.hl_codec_result_create()) not in (hc.HL_ERROR_SUCCESS, hc.HL_ERROR_NOT_IMPLEMENTED)
+        # threads_count <= 0 counts as 1 (hl_codec_264.c:1053-1054), as in the C plugin: not refused as slices
+        for tc in (1, 0, -3):
+            c.threads_count, c.max_ref_frame = tc, 4
+            assert hc.hl_codec_encode(c, f, hc.hl_codec_result_create()) not in (hc.HL_ERROR_SUCCESS, hc.HL_ERROR_NOT_IMPLEMENTED)
 
 
 def test_synth_is_deterministic():

@@ -115,3 +115,22 @@ def test_sse_reference_svc_build_matches_goldens(name, tmp_path):
     subprocess.run([REF_SVC_SSE, str(L), str(w0), str(h0), str(g["frames"]), str(g["qp"]), str(g["me_range"]), str(g["deblock"]),
                     str(g["gop"]), str(g["early_term"]), str(tmp_path / "o")] + ins + ["quiet"], check=True, capture_output=True)
     assert hashlib.md5((tmp_path / "o.264").read_bytes()).hexdigest() == g["stream_md5"]
+
+
+def test_oracle_fails_where_reference_fails():
+    """QP 8: the reference's negative lambda (slice.c:1766, x86 shift-count
+    masking) overflows the first P picture's slice buffer, HL_ERROR_TOOSHORT;
+    the oracle refuses the same frame after the same bytes."""
+    from hl_testlib import check_reference_failure, oracle_lib
+    import ctypes
+
+    def enc_ok(e, frame):
+        from hl_testlib import _planes
+        y, u, v = _planes(frame, e.w, e.h)
+        n = ctypes.c_size_t()
+        rc = e.lib.hlo_encode_frame(ctypes.c_void_p(e.h_), y.ctypes.data, u.ctypes.data, v.ctypes.data, e.out.ctypes.data, e.out.size,
+                                    ctypes.byref(n))
+        return None if rc else e.out[:n.value].tobytes()
+
+    assert GOLD["fail_qcif_qp8_neg_lambda"]["fail_error"] == 15  # HL_ERROR_TOOSHORT
+    check_reference_failure("fail_qcif_qp8_neg_lambda", lambda c: OracleEncoder(c[1], c[2], c[4], c[5], c[6], c[7]), enc_ok, GOLD)
