@@ -175,9 +175,6 @@ __global__ __launch_bounds__(64) void k_deblock_rows(DeblockArgs D, int32_t* row
 #endif
 
 // 1: the task's plane and deblocked-sample stores non-temporal
-#ifndef HL_NT_STORES
-#define HL_NT_STORES 0
-#endif
 // Deblocking and plane blocks of task (x, y) (hl_pipeline.h).
 // The deblocking of one MB in the LDS tile (DbMbTile, hl_filters.h) that
 // aliases the decision's prediction scratch (free once the MB is decided):
@@ -237,17 +234,10 @@ __device__ void plane_block_lds(const uint8_t* ref, int W, uint8_t* pl0, int pst
             j |= (uint32_t)clip255(vj) << (8 * k);
         }
         const size_t o = (size_t)(Y * 16 + r + kPad) * pstride + X * 16 + c0 + kPad;
-#if HL_NT_STORES
-        __builtin_nontemporal_store(f, gmem(reinterpret_cast<uint32_t*>(pl0 + o)));
-        __builtin_nontemporal_store(b, gmem(reinterpret_cast<uint32_t*>(pl0 + plsz + o)));
-        __builtin_nontemporal_store(h, gmem(reinterpret_cast<uint32_t*>(pl0 + 2 * (size_t)plsz + o)));
-        __builtin_nontemporal_store(j, gmem(reinterpret_cast<uint32_t*>(pl0 + 3 * (size_t)plsz + o)));
-#else
         *gmem(reinterpret_cast<uint32_t*>(pl0 + o)) = f;
         *gmem(reinterpret_cast<uint32_t*>(pl0 + plsz + o)) = b;
         *gmem(reinterpret_cast<uint32_t*>(pl0 + 2 * (size_t)plsz + o)) = h;
         *gmem(reinterpret_cast<uint32_t*>(pl0 + 3 * (size_t)plsz + o)) = j;
-#endif
     }
     __syncthreads();  // the scratch is reused by the next block
 }
@@ -285,23 +275,10 @@ __device__ __forceinline__ int udiv_small(int a, int d, float inv)
     q += (q + 1) * d <= a ? 1 : 0;
     return q;
 }
-#ifndef HL_ARGS_OPAQUE
-#define HL_ARGS_OPAQUE 1
-#endif
-#ifndef HL_LOOP_STATE_LDS
-#define HL_LOOP_STATE_LDS 1
-#endif
 // 1: scheduler reciprocals in LDS, task coordinates and the wave's first
 // lane index in SGPRs (k_pipeline): VGPR spills 15 -> 13, but 0.4 % slower
 // (profiles/r05_ab_sched_lds_sgpr_coords_not_kept.log)
-#ifndef HL_SCHED_LDS
-#define HL_SCHED_LDS 0
-#endif
-#if HL_SCHED_LDS
-__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-#else
 __device__ __forceinline__ int uni(int v) { return v; }
-#endif
 struct SchedRecip {
     float mbw, nmb, S, spp;  // 1 / (MBs per row, MBs per picture, streams, pictures per stream)
 };
@@ -366,11 +343,6 @@ __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
 // steps; each later picture adds the lag of task_deps' staircase, about
 // 3 (R+2) steps (P.hop).  The oldest-first order lets the newest pictures'
 // wavefronts start late, and the run ends on their critical path.
-// 1: pop_task acquires as soon as it has observed the task's queue entry,
-// before its claim (0: after the pop)
-#ifndef HL_EARLY_ACQ
-#define HL_EARLY_ACQ 0
-#endif
 #if defined(HL_PROFILE)
 #define HL_POPSTAT(i) (++pst[i])
 #else
@@ -472,11 +444,6 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc, 
         if (i0 >= 0) {
             HL_POPSTAT(0);
             const int f = bfl, qf = bql;
-#if HL_EARLY_ACQ
-            // the entry that made the task ready is observed: acquire now, so
-            // that the L1 invalidate overlaps the claim's round trips
-            if (v > 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
-#endif
             int r = 0;
             if (lane == 0 && atomicCAS(P.head + qf, hh, hh + 1) == hh) {
                 r = v;
@@ -492,9 +459,6 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc, 
             r = __builtin_amdgcn_readfirstlane(r);
             if (r < 0) return -1;
             if (r > 0) {
-#if HL_EARLY_ACQ
-                if (v <= 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
-#endif
                 return f * nmb + r - 1;
             }
             HL_POPSTAT(1);
@@ -522,9 +486,6 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc, 
                 kind = __builtin_amdgcn_readfirstlane(kind);
                 if (r < 0) return -1;
                 if (r > 0) {
-#if HL_EARLY_ACQ
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
-#endif
                     return (1 + kind) * P.nframes * nmb + r - 1;  // intra helpers, then 8x8-family helpers
                 }
                 continue;
@@ -580,14 +541,8 @@ __device__ int claim_next(const PipeArgs& P, int nmb, int& cursor)
 #ifndef HL_PIPE_WAVES_PER_EU
 #define HL_PIPE_WAVES_PER_EU 2
 #endif
-#ifndef HL_EARLY_RELEASE
-#define HL_EARLY_RELEASE 1
-#endif
 // 1: successor-counter decrements relaxed behind the task's release fence,
 // an acquire fence only before a push (0: acq_rel decrements)
-#ifndef HL_CNT_SPLIT
-#define HL_CNT_SPLIT 1
-#endif
 __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(PipeArgs Pk, int mbw, int mbh)
 {
     const PipeArgs& P0 = Pk;  // (the prologue's reads; the loop reads P, below)
@@ -596,7 +551,6 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
     __shared__ int32_t s_task;
     const int nmb = mbw * mbh;
     const bool in_order = blockIdx.x == 0;  // claims tasks in run order (claim_next)
-#if HL_LOOP_STATE_LDS
     // wave 0's loop state per lane in LDS (claim_next's cursor, pop_task's
     // oldest pictures of the previous call): held in VGPRs, the two were
     // spilled in the prologue
@@ -605,36 +559,12 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         s_sched[0][threadIdx.x] = 0;
         s_sched[1][threadIdx.x] = -1;
     }
-#else
-    int cursor = 0;
-    int olc = -1;  // wave 0: pop_task's oldest pictures of the previous call
-#endif
-#if HL_SCHED_LDS
-    // the scheduler's reciprocals in LDS and the wave's first lane index in an
-    // SGPR: loop-invariant VGPRs (the work-item index, the four reciprocals)
-    // were spilled at the loop head and restored inside the macroblock body
-    __shared__ SchedRecip s_rc;
-    if (threadIdx.x == 0) s_rc = SchedRecip{1.0f / (float)mbw, 1.0f / (float)nmb, 1.0f / (float)P0.nstreams, 1.0f / (float)P0.spp};
-    const int wbase = __builtin_amdgcn_readfirstlane(threadIdx.x) & ~63;
-#define HL_RC s_rc
-#define HL_WAVE0 (wbase == 0)
-#define HL_TID (wbase + (int)__lane_id())
-#else
-#if !HL_ARGS_OPAQUE
-    const SchedRecip rc{1.0f / (float)mbw, 1.0f / (float)nmb, 1.0f / (float)P0.nstreams, 1.0f / (float)P0.spp};
-#endif
 #define HL_RC rc
-#if HL_LOOP_STATE_LDS
     // the wave's first lane index in an SGPR (the work-item index VGPR was
     // spilled in the prologue and reloaded per task)
     const int wbase = __builtin_amdgcn_readfirstlane(threadIdx.x) & ~63;
 #define HL_WAVE0 (wbase == 0)
 #define HL_TID (wbase + (int)__lane_id())
-#else
-#define HL_WAVE0 (threadIdx.x < 64)
-#define HL_TID ((int)threadIdx.x)
-#endif
-#endif
 #if defined(HL_PRIO_YOUNG)
     // the second-dispatched half of the workgroup (waves 4-7) loses every VALU
     // arbitration to its SIMD partner at equal priority (MI355X_MICROARCH.md,
@@ -651,7 +581,6 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
     unsigned long long* prof = P0.fr[0].F.prof;
 #endif
     for (;;) {
-#if HL_ARGS_OPAQUE
         // the run's arguments read from the kernel-argument segment in every
         // task (scalar loads through a pointer the compiler cannot follow),
         // not held in registers across the task body (spilled in the prologue)
@@ -659,7 +588,6 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         KArgs* pk = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
         asm volatile("" : "+s"(pk));
         const PipeArgs& P = *(const PipeArgs*)pk;
-#if !HL_SCHED_LDS
         // the scheduler's reciprocals per task, from opaque copies (hoisted,
         // they were held across the body too); udiv_small corrects the
         // approximate reciprocal's quotient
@@ -667,29 +595,21 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         asm volatile("" : "+s"(iw), "+s"(in));
         const SchedRecip rc{__builtin_amdgcn_rcpf((float)iw), __builtin_amdgcn_rcpf((float)in), __builtin_amdgcn_rcpf((float)P.nstreams),
                             __builtin_amdgcn_rcpf((float)P.spp)};
-#endif
-#else
-        const PipeArgs& P = P0;
-#endif
 #if defined(HL_PROFILE)
         const unsigned long long pt0 = __builtin_readcyclecounter();
 #endif
         if (HL_WAVE0) {
-#if HL_LOOP_STATE_LDS
             int ln = __lane_id();
             asm volatile("" : "+v"(ln));  // (its LDS address computed here, not held)
             int cursor = s_sched[0][ln], olc = s_sched[1][ln];
-#endif
             const int t = in_order ? claim_next(P, nmb, cursor) : pop_task(P, nmb, mbw, mbh, olc, HL_RC
 #if defined(HL_PROFILE)
                                                                                            , pst
 #endif
             );
-#if HL_LOOP_STATE_LDS
             s_sched[0][ln] = cursor;
             s_sched[1][ln] = olc;
-#endif
-            if (!HL_EARLY_ACQ || in_order) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);  // (pop_task acquires itself)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
             if (__lane_id() == 0) s_task = t;
         }
@@ -711,9 +631,6 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         // across the whole body (160 spilled VGPRs without this)
         int tid = HL_TID;
         asm volatile("" : "+v"(tid));
-#if HL_SCHED_LDS
-        const SchedRecip rc = s_rc;
-#endif
         // (the task's coordinates are uniform: computed on the VALU (float
         // reciprocals), held in SGPRs across the macroblock body)
         const int f = uni(udiv_small(t, nmb, rc.nmb)), addr = t - f * nmb;
@@ -792,15 +709,11 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
                 const bool hlp = P.helpers && !(fo == fk ? sF.is_intra : ld_relaxed(&P.fr[fo + fb].F.is_intra));
                 fo += fb;
                 const int a = yo * mbw + xo;
-#if HL_CNT_SPLIT
                 // the release half is the fence before release(); the acquire
                 // half (the other dependencies' writes happen before the push)
                 // only where this decrement was the last
                 if (__hip_atomic_fetch_add(P.cnt + fo * nmb + a, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1) continue;
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
-#else
-                if (__hip_atomic_fetch_add(P.cnt + fo * nmb + a, -1, HL_CNT_ORDER, __HIP_MEMORY_SCOPE_AGENT) != 1) continue;
-#endif
                 const int qf = fo * kSubQ + a % kSubQ;
                 const int pos = __hip_atomic_fetch_add(P.tail + qf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const int hp = hlp ? __hip_atomic_fetch_add(P.hq_tail, 1 + P.fam3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
@@ -811,7 +724,6 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
                 }
             }
         };
-#if HL_EARLY_RELEASE
         // This picture's successors need the decision (its reconstruction, MB
         // object, chain record), not this task's deblocking and plane blocks:
         // they are released before those.  The filters then wait for the
@@ -860,7 +772,6 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #endif
         }
         __syncthreads();
-#endif
 #if defined(HL_PROFILE)
         const unsigned long long pt2e = __builtin_readcyclecounter();
 #endif
@@ -897,7 +808,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
                 // writers consume the picture row by row)
                 if (x == mbw - 1 && PF.rows) __hip_atomic_store(PF.rows, y + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
-            release(HL_EARLY_RELEASE ? 1 : 2);
+            release(1);
             // a stream's pictures finish in order: the last MB depends on every
             // other one and on the previous picture's last MB
             if (tid == 0 && addr == nmb - 1) {

@@ -356,19 +356,11 @@ HD void db_mb_store(const DeblockArgs& D, const DbMbTile& t, int X, int Y, int j
     }
     if (comp < 0) {
         const int py = Y * 16 - 4 + tr, px = X * 16 - 4 + tc;
-#if defined(__HIP_DEVICE_COMPILE__) && defined(HL_NT_STORES) && HL_NT_STORES
-        if (py >= 0 && px >= 0) __builtin_nontemporal_store(t.T[tr * kDbL + tc], gmem(D.pic[0]) + (size_t)py * D.W + px);
-#else
         if (py >= 0 && px >= 0) gmem(D.pic[0])[(size_t)py * D.W + px] = t.T[tr * kDbL + tc];
-#endif
     }
     else {
         const int py = Y * 8 - 4 + tr, px = X * 8 - 4 + tc;
-#if defined(__HIP_DEVICE_COMPILE__) && defined(HL_NT_STORES) && HL_NT_STORES
-        if (py >= 0 && px >= 0) __builtin_nontemporal_store(t.C[comp][tr * kDbC + tc], gmem(D.pic[1 + comp]) + (size_t)py * D.Wc + px);
-#else
         if (py >= 0 && px >= 0) gmem(D.pic[1 + comp])[(size_t)py * D.Wc + px] = t.C[comp][tr * kDbC + tc];
-#endif
     }
 }
 

@@ -116,68 +116,22 @@ constexpr int kMaxSeg = 4;
 constexpr int kMaxPass = (9 * 16 + kMbRows - 1) / kMbRows;  // rows per lane for the largest step
 // Candidate evaluation with one 4-lane quad per 4x4 block (hl_quad.h, the
 // default) or one 16-lane row per block (hl_coop.h): blocks a pass can hold.
-#ifndef HL_QUAD_EVAL
-#define HL_QUAD_EVAL 1
-#endif
 // quad rounds per pass: 2 x 128 blocks at 512 lanes; smaller workgroups take
 // enough rounds for the largest non-speculative step (9 16x16 candidates)
 #ifndef HL_QPASS
 #define HL_QPASS 2  // quad rounds a 512-lane pass holds (3: a 16x16 pass holds two steps)
 #endif
 constexpr int kQPass = kMbThreads >= 512 ? HL_QPASS : (9 * 16 + (kMbThreads >> 2) - 1) / (kMbThreads >> 2);
-constexpr int kPassItems = HL_QUAD_EVAL ? kQPass * (kMbThreads >> 2) : kMaxPass * kMbRows;
-constexpr int kSpecMaxBlocks = HL_QUAD_EVAL ? HL_SPEC_MAX_BLOCKS : 8;
+constexpr int kPassItems = kQPass * (kMbThreads >> 2);
+constexpr int kSpecMaxBlocks = HL_SPEC_MAX_BLOCKS;
 
 // One candidate of a step: plane offsets of its quarter-pel prediction
 // (second plane = first when the phase needs no average) and its MV.
-#ifndef HL_LDS_WINDOW
-#define HL_LDS_WINDOW 0
-#endif
-#ifndef HL_ROWS_PERMLANE  // 1: a pass's step minima combined across the two 16-lane rows by v_permlane16_swap
-#define HL_ROWS_PERMLANE 0
-#endif
-#ifndef HL_RESOLVE_SELECTS  // 1: a pass's chain resolution as selects
-#define HL_RESOLVE_SELECTS 0
-#endif
-#ifndef HL_MVP_SELECTS  // 1: the motion vector predictor as selects
-#define HL_MVP_SELECTS 1
-#endif
-#ifndef HL_NC_SELECTS  // 1: the cost phase's neighbour TotalCoeffs and sums as selects (no branches)
-#define HL_NC_SELECTS 1
-#endif
-#ifndef HL_GRID_LANES  // 1: a searched partition's motion-grid cells written lane-parallel (shift indexing)
-#define HL_GRID_LANES 1
-#endif
-#ifndef HL_QOFF_TABLE  // 1: put_cand's sample offsets from a per-phase table built at the MB start
-#define HL_QOFF_TABLE 1
-#endif
-#ifndef HL_TC_MASKS  // 1: per-block masks of the candidates with a nonzero TotalCoeff (LDS OR in the
-#define HL_TC_MASKS 1  // evaluation) instead of scanning the TotalCoeff rows for the last writer
-#endif
-#ifndef HL_DEFER_COMMIT  // 1: a search pass's commit after the next pass's candidate generation
-#define HL_DEFER_COMMIT 0
-#endif
-#ifndef HL_LDS_WINDOW_DMA  // 1: the window filled by LDS-DMA (with HL_LDS_WINDOW=1)
-#define HL_LDS_WINDOW_DMA 0
-#endif
 struct alignas(16) CandSlot {
     int32_t off1, off2;
     int16_t mvx, mvy;
     int32_t pad;
-#if HL_LDS_WINDOW
-    int32_t w1, w2;  // the same two offsets in the LDS search window (Shared::win), or -1 when the partition leaves it
-    int32_t unused[2];
-#endif
 };
-// LDS-staged search window (device, HL_LDS_WINDOW=1; measured, not the
-// default: profiles/r03_ab_lds_window.log): the four quarter-pel planes of the
-// reference over padded columns [xL, xL + 96) and rows [yL, yL + 88), i.e.
-// picture samples 40 to the left / above the MB to 47 (cols 55) beyond its
-// origin -- the MBs up to (x + 2, y + 2), which a pipelined task's reach R = 2
-// guarantees complete.  Loaded once per MB; a candidate whose whole
-// partition (+1 sample for the second plane) lies inside reads its
-// prediction from LDS, otherwise from the planes in HBM/L2.
-constexpr int kWinW = 96, kWinH = 88, kWinPlane = kWinW * kWinH;
 constexpr int kNA = -1;   // not-available sample marker
 
 // The intra fallback of a P macroblock (rdo.c:1161-1167 -> rdo.c:99-299)
@@ -326,7 +280,7 @@ struct Shared {
     // already write the next step's -- a step only reuses the buffer of the
     // step before the previous one, whose readers all passed a barrier since.
     alignas(16) uint8_t be_tcb[2][16][kMaxCand];         // TotalCoeff [parity][block][candidate]
-    uint32_t be_tcm[3][16];  // HL_TC_MASKS: candidates with a nonzero TotalCoeff [pass mod 3][block]
+    uint32_t be_tcm[3][16];  // candidates with a nonzero TotalCoeff [pass mod 3][block]
     alignas(16) int32_t lvs[kMaxWaves * 4][16];          // per-row level scratch of coop_cavlc
     alignas(16) int32_t lvq[kMaxWaves * 16][16];         // per-quad level scratch of quad_cavlc
     CoopTables ct;
@@ -392,9 +346,6 @@ struct Shared {
     // VGPRs for the whole MB (which the compiler spilled to scratch: those
     // scratch stores were most of k_pipeline's HBM writes)
     LaneK lk[16];
-#if HL_LDS_WINDOW
-    alignas(16) uint8_t win[4 * kWinPlane];  // the search window (kWinW x kWinH per plane)
-#endif
 };
 
 // 8x8-family helper tasks (guess_inter): 1 = built in.  Off
@@ -449,7 +400,6 @@ struct Ctx {
     LaneQ Q{};              // per-lane constants of the quad block pipeline (registers: the search loop reads them every pass)
 #endif
     int gx, gy;             // reference planes known complete for MBs (X <= gx, Y <= gy) (pipelined runs)
-    int wux = 0, wuy = 0;   // usable columns / rows of the LDS search window (0: none)
     int spec = 0;           // 1 = chain is still a row-start speculation (uniform)
     int par = 0;            // buffer parity of the last candidate step (Shared::cd, be_tcb)
     int p3 = 0;             // the last candidate step's slot of Shared::be_tcm (pass mod 3)
@@ -620,7 +570,7 @@ HD void mvp(const Shared& S, const PartShape& ps, int pi, int spi, int out[2])
     }
     MvN nb[3];
     nb_motion(S, x + xS, y + yS, ppw, nb);
-#if defined(__HIP_DEVICE_COMPILE__) && HL_MVP_SELECTS
+#if defined(__HIP_DEVICE_COMPILE__)
     {
         // 8.4.1.3 as selects (the values are uniform but live in VGPRs: every
         // branch on them would be an exec-mask branch)
@@ -924,7 +874,7 @@ __device__ __forceinline__ void mb_begin(Ctx& c)
     }
     if (tid < 15 * 16) b2 = kTzLen[tid >> 4][tid & 15];
     if (tid < 3 * 4 * 17) b3 = kTokLen[tid / 68][(tid / 17) % 4][tid % 17];
-    if (HL_RB_TABLE && tid >= 256) b4 = kRbTab.v[(tid - 256) >> 4][tid & 15];
+    if (tid >= 256) b4 = kRbTab.v[(tid - 256) >> 4][tid & 15];
     uint32_t b5 = 0;
     if (tid >= 240 && tid < 240 + 4 * 17) b5 = kTok3Tab.v[(tid - 240) / 17][(tid - 240) % 17];
     // ---- stores
@@ -940,7 +890,7 @@ __device__ __forceinline__ void mb_begin(Ctx& c)
     else if (tid >= 96 && tid < 112) S.cleft[(tid - 96) >> 3][(tid - 96) & 7] = (int16_t)b1;
     if (tid < 15 * 16) S.ct.tz[tid >> 4][tid & 15] = (uint8_t)b2;
     if (tid < 3 * 4 * 17) S.ct.tok[tid / 68][(tid / 17) % 4][tid % 17] = (uint8_t)b3;
-    if (HL_RB_TABLE && tid >= 256) S.ct.rb[(tid - 256) >> 4][tid & 15] = (uint8_t)b4;
+    if (tid >= 256) S.ct.rb[(tid - 256) >> 4][tid & 15] = (uint8_t)b4;
     if (tid >= 240 && tid < 240 + 4 * 17) S.ct.tok3[(tid - 240) / 17][(tid - 240) % 17] = b5;
     if (tid >= kMbThreads - 48) (&S.be_tcm[0][0])[tid - (kMbThreads - 48)] = 0u;  // every slot empty at the MB start
     if (tid >= 448 && tid < 464) {
@@ -1267,7 +1217,7 @@ HD void put_cand(Ctx& c, int xo, int yo, int pw, int pht, int i, int mx, int my,
     const uint32_t e = (uint32_t)(w >> (9 * (ph < 7 ? ph : (ph < 14 ? ph - 7 : ph - 14)))) & 0x1FF;
     const int X = clip3(-17, F.W + 17, c.xL + xo + (mx >> 2)) + kPad, Y = clip3(-17, F.H + 17, c.yL + yo + (my >> 2)) + kPad;
     CandSlot cs;
-#if defined(__HIP_DEVICE_COMPILE__) && HL_QOFF_TABLE
+#if defined(__HIP_DEVICE_COMPILE__)
     // the phase's two sample offsets from the MB start's table (S.qoff)
     const int2 qo = c.S.qoff[ph];
     const int base = Y * F.pstride + X;
@@ -1281,17 +1231,8 @@ HD void put_cand(Ctx& c, int xo, int yo, int pw, int pht, int i, int mx, int my,
     cs.mvx = (int16_t)mx;
     cs.mvy = (int16_t)my;
     cs.pad = pt;  // diamond point index
-#if HL_LDS_WINDOW
-    // window-relative origin of the partition (padded coordinates minus the window's)
-    const int rx = X - c.xL, ry = Y - c.yL;  // (the window starts at padded (xL, yL))
-    const bool in = rx >= 0 && ry >= 0 && rx + pw + 1 <= c.wux && ry + pht + 1 <= c.wuy;
-    cs.w1 = in ? (int)(e & 3) * kWinPlane + (ry + (int)((e >> 3) & 1)) * kWinW + rx + (int)((e >> 2) & 1) : -1;
-    cs.w2 = !in ? -1 : ((e & 16) ? (int)((e >> 5) & 3) * kWinPlane + (ry + (int)((e >> 8) & 1)) * kWinW + rx + (int)((e >> 7) & 1) : cs.w1);
-    cs.unused[0] = cs.unused[1] = 0;
-#else
     (void)pw;
     (void)pht;
-#endif
     if (writer) c.S.wc[c.tid >> 6][i] = cs;
 }
 
@@ -1303,30 +1244,6 @@ HD double mv_cost(const FrameArgs& F, int dist, int bits, int mvx, int mvy, cons
 
 #if defined(HL_STATS) && !defined(__HIP_DEVICE_COMPILE__)
 extern long long g_hl_stats[8];
-#endif
-
-#if defined(__HIP_DEVICE_COMPILE__)
-// bit i set iff byte i of w is non-zero
-__device__ __forceinline__ uint32_t nz_bytes(uint32_t w)
-{
-    const uint32_t t = ((w | ((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu)) >> 7) & 0x01010101u;
-    return (t * 0x01020408u) >> 24;
-}
-// Last candidate (bit set in `allow`) whose TotalCoeff in the block row
-// (32 candidates, two 16-byte words) is non-zero: its TotalCoeff, or -1.
-__device__ __forceinline__ int tcb_last(const uint8_t* row, uint32_t allow)
-{
-    const uint4 a = *reinterpret_cast<const uint4*>(row), b = *reinterpret_cast<const uint4*>(row + 16);
-    const uint32_t m = (nz_bytes(a.x) | (nz_bytes(a.y) << 4) | (nz_bytes(a.z) << 8) | (nz_bytes(a.w) << 12) | (nz_bytes(b.x) << 16) |
-                        (nz_bytes(b.y) << 20) | (nz_bytes(b.z) << 24) | (nz_bytes(b.w) << 28)) &
-                       allow;
-    if (!m) return -1;
-    const int j = 31 - __clz(m);
-    const uint4 q = j < 16 ? a : b;
-    const int jj = j & 15;
-    const uint32_t w = jj < 4 ? q.x : (jj < 8 ? q.y : (jj < 12 ? q.z : q.w));
-    return (int)((w >> ((jj & 3) * 8)) & 0xFF);
-}
 #endif
 
 // Evaluates the candidates S.wc[wave][0..ncand) of partition g in order.
@@ -1350,7 +1267,6 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
     uint8_t(&tcb)[16][kMaxCand] = S.be_tcb[c.par];
     HL_PROF_T(tp0);
 #if defined(__HIP_DEVICE_COMPILE__)
-#if HL_QUAD_EVAL
     // phase 1: one 4-lane quad per (candidate, 4x4 block), lane r = block row
     // r (hl_quad.h); every quad issues its prediction loads for both rounds
     // before computing
@@ -1372,10 +1288,6 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
             }, S.f3lo, S.f3hi);
         int o1[kQPass], o2[kQPass];
         uint32_t sv[kQPass], pr[kQPass];
-#if HL_LDS_WINDOW
-        int l1[kQPass], l2[kQPass];
-        bool inw = true;
-#endif
 #pragma unroll
         for (int j = 0; j < kQPass; ++j) {
             const int item = min(qg + j * nq, n - 1);  // clamped: no divergence, valid addresses
@@ -1385,24 +1297,9 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
             const int o = ((hy << 2) + Q.r) * F.pstride + (hx << 2);
             o1[j] = cs.x + o;
             o2[j] = cs.y + o;
-#if HL_LDS_WINDOW
-            const int2 cw = *reinterpret_cast<const int2*>(&S.wc[wave][ci].w1);
-            const int ow = ((hy << 2) + Q.r) * kWinW + (hx << 2);
-            l1[j] = cw.x + ow;
-            l2[j] = cw.y + ow;
-            inw = inw && (cw.x >= 0 || qg + j * nq >= n);
-#endif
             sv[j] = *reinterpret_cast<const uint32_t*>(&S.src[(g.py + (hy << 2) + Q.r) * 16 + g.px + (hx << 2)]);
         }
         HL_PROF_T(ta0);
-#if HL_LDS_WINDOW
-        if (__ballot(!inw) == 0) {  // every candidate block of the wave inside the LDS window
-#pragma unroll
-            for (int j = 0; j < kQPass; ++j)
-                if (qg + j * nq < n) pr[j] = avg_u8x4(ld_lds_u8x4(S.win, l1[j]), ld_lds_u8x4(S.win, l2[j]));
-        }
-        else
-#endif
         {
 #pragma unroll
             for (int j = 0; j < kQPass; ++j)
@@ -1448,9 +1345,7 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                 if (Q.r == 0) {
                     S.be_w[ci][k] = make_int4(st.tc | (st.t1 << 5) | ((st.sctr + 1) << 8), st.rest | (dist << 16), tok, 0);
                     tcb[k][ci] = (uint8_t)st.tc;
-#if HL_TC_MASKS
                     if (st.tc) atomicOr(&S.be_tcm[c.p3][k], 1u << ci);
-#endif
                     if (g.nblk == 1) {
                         // a single-block partition: both nC neighbours lie outside it, so the
                         // nC (and the candidate's cost) needs no other block (phase 2 skipped)
@@ -1471,112 +1366,14 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         HL_PROF_ADD(c, 13, ta1);
 #endif
     }
-#else
-    // phase 1: one 16-lane row per (candidate, 4x4 block); every row of the
-    // wave issues its prediction loads for all its passes before computing
-    {
-        const int wave = c.tid >> 6, grp = c.tid >> 4, ngrp = c.nthr >> 4;
-        const int n = ncand << g.lnb;
-        const int qbits = 15 + F.qp / 6, f = (1 << qbits) / 6;
-        const int pr = c.k().p >> 2, pc = c.k().p & 3;
-        const auto base = gmem(F.pl[0]);
-        int pa[kMaxPass], pb[kMaxPass], sv[kMaxPass];
-        // single-block partitions: both nC neighbours lie outside the partition,
-        // so nC is fixed for its whole search (read here, beside the loads)
-        const int nc1 = g.nblk == 1 ? nc_luma_of(S, blk_idx(g.px, g.py), [&](int ni) -> int { return S.tc[ni]; }) : 0;
-        if (HL_F3REC(c) && g.nblk == 1 && c.tid == 0)  // fam3_helper: its entry reads (lane 0; phase 2 does not run)
-            nc_luma_iv(S, blk_idx(g.px, g.py), [&](int ni, bool& e) -> int {
-                e = !((S.f3w >> ni) & 1);
-                return S.tc[ni];
-            }, S.f3lo, S.f3hi);
-        // slots and source samples first (one LDS round trip), then all loads
-        int o1[kMaxPass], o2[kMaxPass];
-        HL_PROF_T(ta0);
-#pragma unroll
-        for (int j = 0; j < kMaxPass; ++j) {
-            const int item = min(grp + j * ngrp, n - 1);  // clamped: no divergence, valid addresses
-            const int ci = item >> g.lnb, k = item & (g.nblk - 1);
-            const int hx = k & (g.nbw - 1), hy = k >> g.lbw;
-            const int2 cs = *reinterpret_cast<const int2*>(&S.wc[wave][ci]);
-            const int o = ((hy << 2) + pr) * F.pstride + (hx << 2) + pc;
-            o1[j] = cs.x + o;
-            o2[j] = cs.y + o;
-            sv[j] = S.src[(g.py + (hy << 2) + pr) * 16 + g.px + (hx << 2) + pc];
-        }
-#pragma unroll
-        for (int j = 0; j < kMaxPass; ++j) {
-            if (grp + j * ngrp < n) {
-                pa[j] = base[o1[j]];
-                pb[j] = base[o2[j]];
-            }
-        }
 #if defined(HL_STEP_PROF)
-        sv[0] += pa[0] * 0;  // wait for the loads here (profiling only)
-        HL_PROF_ADD(c, 12, ta0);
-        HL_PROF_T(ta1);
-#endif
-#pragma unroll
-        for (int j = 0; j < kMaxPass; ++j) {
-            const int item = grp + j * ngrp;
-            if (item < n) {
-                const int ci = item >> g.lnb, k = item & (g.nblk - 1);
-                const int pred = (pa[j] + pb[j] + 1) >> 1;
-                const int res = sv[j] - pred;
-                const int q = coop_quant(coop_fwd(c.k(), res), c.k().mf, qbits, f);
-#if defined(HL_STEP_PROF)
-                HL_PROF_ADD(c, 13, ta1);
-                HL_PROF_T(ta2);
-#endif
-                CoopStat st{0, 0, 0, -1};
-                int tok = 0, dist;
-                if (__ballot(q != 0) == 0) {  // every block of the wave quantised to zero
-                    dist = row_sum(iabs(res));
-                }
-                else {
-                    // reconstruction distortion first: independent of the CAVLC
-                    // chain, so the two DPP chains interleave in one basic block
-                    const int r = coop_idct(c.k(), coop_dequant(q, c.k().ls, F.qp));
-                    dist = row_sum(iabs(sv[j] - clip255(pred + r)));
-                    st = coop_cavlc(S.ct, q, c.k().s, S.lvs[grp]);
-                    if (c.k().p == 0 && st.tc)  // coeff_token lengths for the four nC classes
-                        tok = S.ct.tok[0][st.t1][st.tc] | (S.ct.tok[1][st.t1][st.tc] << 5) | (S.ct.tok[2][st.t1][st.tc] << 10) | (6 << 15);
-                }
-#if defined(HL_STEP_PROF)
-                HL_PROF_ADD(c, 14, ta2);
-                HL_PROF_T(ta3);
-#endif
-#if defined(HL_STEP_PROF)
-                HL_PROF_ADD(c, 15, ta3);
-#endif
-                if (c.k().p == 0) {
-                    S.be_w[ci][k] = make_int4(st.tc | (st.t1 << 5) | ((st.sctr + 1) << 8), st.rest | (dist << 16), tok, 0);
-                    tcb[k][ci] = (uint8_t)st.tc;
-                    if (g.nblk == 1) {
-                        // a single-block partition: both nC neighbours lie outside it, so the
-                        // nC (and the candidate's cost) needs no other row (phase 2 skipped)
-                        int bits = 0;
-                        if (st.tc) bits = st.rest + ((tok >> (5 * (nc1 < 2 ? 0 : (nc1 < 4 ? 1 : (nc1 < 8 ? 2 : 3))))) & 31);
-                        const CandSlot cs = S.wc[wave][ci];
-                        R.cost[ci] = mv_cost(F, dist, bits, cs.mvx, cs.mvy, pmv);
-                        R.bits[ci] = bits;
-                        R.dist[ci] = dist;
-                        R.single[ci] = st.tc ? st.sctr : 0;
-                        R.cbp[ci] = st.tc ? 1 << blk_idx(g.px, g.py) : 0;
-                        R.last[ci] = st.tc ? st.sctr : -1;
-                    }
-                }
-            }
-        }
-    }
-#endif
-#if defined(HL_STEP_PROF) && HL_QUAD_EVAL
     HL_PROF_T(tb0);
     HL_SYNC();
     HL_PROF_ADD(c, 14, tb0);
 #else
     HL_SYNC();
 #endif
-#if defined(__HIP_DEVICE_COMPILE__) && HL_QUAD_EVAL && HL_TC_MASKS
+#if defined(__HIP_DEVICE_COMPILE__)
     // the slot the pass after next ORs into: its last readers (the phase 2
     // and commit of the pass before this one) are done, and its first
     // writer runs after the next pass's barrier above
@@ -1613,7 +1410,6 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
         const CandSlot cs = S.wc[wave][ci];
         int bits = 0, dist = 0, cs_sum = 0, last = 0;
         const int tc = w0 & 31;
-#if HL_NC_SELECTS
         if (!HL_FAM3 || !REC) {
             // selects throughout (no exec-mask branches): the neighbours'
             // TotalCoeffs as the nC reads them (live value of the last
@@ -1638,7 +1434,6 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
             (void)f3w;
         }
         else
-#endif
         if (valid) {
             dist = w1 >> 16;
             if (tc) {
@@ -1650,12 +1445,8 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                     nA = aA ? eA : 0;
                 }
                 else if (cbp & (1 << (niA >> 2))) {
-#if HL_TC_MASKS
                     const uint32_t mA = inA ? S.be_tcm[c.p3][kkA] & allow : 0u;
                     const int v = mA ? (int)rA[31 - __clz(mA)] : -1;
-#else
-                    const int v = inA ? tcb_last(rA, allow) : -1;
-#endif
                     nA = v >= 0 ? v : tA;
                     enA = HL_F3REC(c) && v < 0 && !((f3w >> niA) & 1);
                 }
@@ -1664,12 +1455,8 @@ HD void eval_candidates(Ctx& c, const PartGeo& g, int ncand, const int pmv[2])
                     nB = aB ? eB : 0;
                 }
                 else if (cbp & (1 << (niB >> 2))) {
-#if HL_TC_MASKS
                     const uint32_t mB = inB ? S.be_tcm[c.p3][kkB] & allow : 0u;
                     const int v = mB ? (int)rB[31 - __clz(mB)] : -1;
-#else
-                    const int v = inB ? tcb_last(rB, allow) : -1;
-#endif
                     nB = v >= 0 ? v : tB;
                     enB = HL_F3REC(c) && v < 0 && !((f3w >> niB) & 1);
                 }
@@ -1828,12 +1615,8 @@ HD void commit_candidates(Ctx& c, const PartGeo& g, int n, int last_l = -2)
     const uint8_t(&tcb)[16][kMaxCand] = S.be_tcb[c.par];
     if (c.tid < g.nblk) {
         const int k = c.tid;
-#if HL_TC_MASKS
         const uint32_t mk = S.be_tcm[c.p3][k] & (n >= 32 ? ~0u : (1u << n) - 1u);
         const int v = mk ? (int)tcb[k][31 - __clz(mk)] : -1;
-#else
-        const int v = tcb_last(tcb[k], n >= 32 ? ~0u : (1u << n) - 1u);
-#endif
         const int bi = blk_idx(g.px + ((k & (g.nbw - 1)) << 2), g.py + ((k >> g.lbw) << 2));
         if (v >= 0) {
             S.tc[bi] = (int8_t)v;
@@ -2117,14 +1900,6 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
     // point enabled; the half stage starts at the integer MV value read as
     // half-pel (me_ds.c:360)
     auto centre_of = [](int st, int m) { return st == 0 ? m : m >> 2; };
-#if defined(__HIP_DEVICE_COMPILE__) && HL_DEFER_COMMIT
-    // a pass's commit of the live state (commit_candidates) runs after the
-    // next pass's candidates are generated: the generation reads only the
-    // resolved search state, the commit only the pass's results, so the two
-    // dependent chains interleave; the next evaluation reads what the commit
-    // wrote (S.tc, the chain) after both
-    int pend_used = 0, pend_last = -1;
-#endif
     while (stage >= 0) {
         HL_PROF_T(tgap);
         // the chain: step 0 = the current step, then fresh stages from the
@@ -2171,10 +1946,6 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         }
 #if defined(HL_STEP_PROF)
         HL_PROF_ADD(c, 19, tgen);  // the pass's candidates generated and stored
-#endif
-#if HL_DEFER_COMMIT
-        if (pend_used) commit_candidates<REC>(c, g, pend_used, pend_last);  // the previous pass's (see above)
-        pend_used = 0;
 #endif
 #else
         {
@@ -2246,19 +2017,10 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
 #pragma unroll
             for (int j = 0; j < kMaxSeg; ++j) {
                 const unsigned long long b0 = __builtin_bit_cast(unsigned long long, rm[j]);
-#if HL_ROWS_PERMLANE
-                // the two rows' minima exchanged by v_permlane16_swap (lanes
-                // 16-31 <-> 0-15, in registers): every lane holds both, no readlane
-                const auto lo2 = __builtin_amdgcn_permlane16_swap((unsigned)b0, (unsigned)b0, false, false);
-                const auto hi2 = __builtin_amdgcn_permlane16_swap((unsigned)(b0 >> 32), (unsigned)(b0 >> 32), false, false);
-                const double m0 = __builtin_bit_cast(double, (unsigned long long)hi2[0] << 32 | lo2[0]);
-                const double m1 = __builtin_bit_cast(double, (unsigned long long)hi2[1] << 32 | lo2[1]);
-#else
                 const double m0 = __builtin_bit_cast(double, (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(b0 >> 32), 0) << 32 |
                                                                  (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b0, 0));
                 const double m1 = __builtin_bit_cast(double, (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(b0 >> 32), 16) << 32 |
                                                                  (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b0, 16));
-#endif
                 sm[j] = fmin(m0, m1);
                 sb[j] = __ffsll((long long)(__ballot(in[j] && v[j] == sm[j]) & 0xFFFFFFFFull)) - 1;
             }
@@ -2281,68 +2043,6 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         // that cost, and every step before it ends its stage.  The stage's
         // window is the one re-centred when it began (kept by a move).
         int used;
-#if defined(__HIP_DEVICE_COMPILE__) && HL_RESOLVE_SELECTS
-        {
-            // the same resolution as selects: the state is uniform but held in
-            // VGPRs, so each branch on it would be an exec-mask branch
-            auto rl = [](int v, int l) { return __builtin_amdgcn_readlane(v, l); };
-            // the MVP/(0,0) step (stage 3 passes only)
-            const bool s3 = stage == 3;
-            const int bi0 = sb[0] < 0 ? 0 : sb[0];
-            const bool t0 = s3 && sm[0] < b.cost;
-            b.cost = t0 ? sm[0] : b.cost;
-            b.single = t0 ? rl(pv_single, bi0) : b.single;
-            b.dist = t0 ? rl(pv_dist, bi0) : b.dist;
-            b.cbp = t0 ? rl(pv_cbp, bi0) : b.cbp;
-            b.mv[0] = t0 ? rl(pv_mvx, bi0) : b.mv[0];
-            b.mv[1] = t0 ? rl(pv_mvy, bi0) : b.mv[1];
-            const int j0 = s3 ? 1 : 0;
-            const bool cut = s3 && (b.mv[0] != pmv[0] || b.mv[1] != pmv[1]);  // the (0,0) candidate won: the continuations assumed the MVP
-            const int st0 = s3 ? 2 : stage;
-            const int cx3 = centre_of(2, b.mv[0]), cy3 = centre_of(2, b.mv[1]);
-            cx = s3 ? cx3 : cx;
-            cy = s3 ? cy3 : cy;
-            flags = s3 ? 0x1FF : flags;
-            left = s3 ? cx3 - range : left;
-            right = s3 ? cx3 + range : right;
-            top = s3 ? cy3 - range : top;
-            bottom = s3 ? cy3 + range : bottom;
-            unsigned mv_mask = 0;  // steps with a candidate below the best cost
-#pragma unroll
-            for (int j = 0; j < kMaxSeg; ++j) mv_mask |= (j >= j0 && j < nseg && n[j] && sm[j] < b.cost) ? 1u << j : 0u;
-            const bool moved = !cut && mv_mask != 0, none = !cut && mv_mask == 0;
-            // a move at step jm: the steps before it ended their stages (the
-            // stage began at step jm, its window re-centred then, on the best
-            // MV before the move); the stage goes on from the new centre
-            const int jm = mv_mask ? __builtin_ctz(mv_mask) : 0;
-            const int stm = st0 - (jm > j0 ? jm - j0 : 0);
-            const int wx = centre_of(stm, b.mv[0]), wy = centre_of(stm, b.mv[1]);
-            const bool rewin = moved && jm > j0;
-            const int bim = jm == 0 ? sb[0] : (jm == 1 ? sb[1] : (jm == 2 ? sb[2] : sb[3]));
-            const double smm = jm == 0 ? sm[0] : (jm == 1 ? sm[1] : (jm == 2 ? sm[2] : sm[3]));
-            const int bimc = bim < 0 ? 0 : bim;
-            const int mvx = rl(pv_mvx, bimc), mvy = rl(pv_mvy, bimc), pad = rl(pv_pad, bimc);
-            // no step moved: each ended its stage
-            const int stn = st0 - (nseg - j0);
-            const int nx = centre_of(stn < 0 ? 0 : stn, b.mv[0]), ny = centre_of(stn < 0 ? 0 : stn, b.mv[1]);
-            const bool renew = none && stn >= 0;
-            left = rewin ? wx - range : (renew ? nx - range : left);
-            right = rewin ? wx + range : (renew ? nx + range : right);
-            top = rewin ? wy - range : (renew ? ny - range : top);
-            bottom = rewin ? wy + range : (renew ? ny + range : bottom);
-            b.cost = moved ? smm : b.cost;
-            b.single = moved ? rl(pv_single, bimc) : b.single;
-            b.dist = moved ? rl(pv_dist, bimc) : b.dist;
-            b.cbp = moved ? rl(pv_cbp, bimc) : b.cbp;
-            b.mv[0] = moved ? mvx : b.mv[0];
-            b.mv[1] = moved ? mvy : b.mv[1];
-            cx = moved ? mvx >> stm : (renew ? nx : cx);
-            cy = moved ? mvy >> stm : (renew ? ny : cy);
-            flags = moved ? mask_of(stm, pad) : (renew ? 0x1FF : flags);
-            stage = cut ? st0 : (moved ? stm : stn);
-            used = cut ? lo[0] + n[0] : (moved ? lo[jm] + n[jm] : lo[nseg - 1] + n[nseg - 1]);
-        }
-#else
         {
             int j0 = 0;
             bool cut = false;  // the (0,0) candidate won: the continuations assumed the MVP
@@ -2405,25 +2105,16 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
                 used = lo[nseg - 1] + n[nseg - 1];
             }
         }
-#endif
 #if defined(__HIP_DEVICE_COMPILE__)
 #if defined(HL_STEP_PROF)
         HL_PROF_ADD(c, 18, tres);  // the chain resolved
 #endif
-#if HL_DEFER_COMMIT
-        pend_used = used;
-        pend_last = pv_last;
-#else
         if (used) commit_candidates<REC>(c, g, used, pv_last);
-#endif
 #else
         if (used) commit_candidates<REC>(c, g, used);
 #endif
         HL_PROF_ADD(c, 17, tsel);
     }
-#if defined(__HIP_DEVICE_COMPILE__) && HL_DEFER_COMMIT
-    if (pend_used) commit_candidates<REC>(c, g, pend_used, pend_last);
-#endif
     // (no barrier before these stores: after the last pass, waves still read
     // only the pass's candidate results, S.cd / S.wc / S.be_tcb, which lane 0
     // does not write here; the barrier below orders them for the next search)
@@ -2438,11 +2129,11 @@ HD bool search_partition(Ctx& c, const PartDef& pd, int pi, int spi, bool probe)
         S.bmvp[pi][spi][1] = (int16_t)pmv[1];
         S.nb[0].mv[pi][spi][0] = (int16_t)b.mv[0];  // MvL0 feeds the MVP of later partitions
         S.nb[0].mv[pi][spi][1] = (int16_t)b.mv[1];
-#if !(defined(__HIP_DEVICE_COMPILE__) && HL_GRID_LANES)
+#if !defined(__HIP_DEVICE_COMPILE__)
         grid_set(S, g.px, g.py, g.pw, g.ph, b.mv[0], b.mv[1]);
 #endif
     }
-#if defined(__HIP_DEVICE_COMPILE__) && HL_GRID_LANES
+#if defined(__HIP_DEVICE_COMPILE__)
     // the partition's 4x4 blocks in the motion grid, lane k of wave 0 block k
     // (shifts by the partition's log2 width, no division)
     if (c.tid < g.nblk) {
@@ -5057,59 +4748,7 @@ HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, in
 #endif
 #endif
     HL_PROF_T(t0);
-#if defined(__HIP_DEVICE_COMPILE__) && HL_LDS_WINDOW
-    // the LDS search window: loads issued here, stored after mb_begin's load
-    // round (their latency overlaps it); read after guess_inter's barriers
-    constexpr int kWinChunks = 4 * kWinPlane / 16, kWinRounds = (kWinChunks + kMbThreads - 1) / kMbThreads;
-#if HL_LDS_WINDOW_DMA
-    // LDS-DMA form: global_load_lds_dwordx4, no VGPR staging; every wave
-    // writes 1 KiB of the window per instruction (lane-linear), drained by
-    // the compiler's vmcnt(0) at mb_begin's first barrier
-    static_assert(kWinChunks % 64 == 0, "whole waves of 16-byte window chunks");
-    if (!F.is_intra) {
-        const int bx = c.gx >= F.mbw - 1 ? F.W + 2 * kPad : 16 * (c.gx + 1) + kPad;
-        const int by = c.gy >= F.mbh - 1 ? F.H + 2 * kPad : 16 * (c.gy + 1) + kPad;
-        c.wux = min(kWinW, bx - c.xL);
-        c.wuy = min(kWinH, by - c.yL);
-        const auto pl = gmem(F.pl[0]);
-        const int wbase = tid & ~63;
-#pragma unroll
-        for (int k = 0; k < kWinRounds; ++k) {
-            const int i0 = wbase + k * kMbThreads;  // the wave's first chunk (uniform)
-            if (i0 < kWinChunks) {
-                const int i = i0 + (tid & 63);
-                const int p = i / (kWinPlane / 16), rem = i - p * (kWinPlane / 16), r = rem / (kWinW / 16), cc = rem - r * (kWinW / 16);
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void*)(pl + (size_t)p * F.plsz + (size_t)(c.yL + r) * F.pstride + c.xL + cc * 16),
-                    (__attribute__((address_space(3))) void*)(S.win + 16 * i0), 16, 0, 0);
-            }
-        }
-    }
-#else
-    uint4 wv[kWinRounds];
-    if (!F.is_intra) {
-        const int bx = c.gx >= F.mbw - 1 ? F.W + 2 * kPad : 16 * (c.gx + 1) + kPad;
-        const int by = c.gy >= F.mbh - 1 ? F.H + 2 * kPad : 16 * (c.gy + 1) + kPad;
-        c.wux = min(kWinW, bx - c.xL);
-        c.wuy = min(kWinH, by - c.yL);
-        const auto pl = gmem(F.pl[0]);
-#pragma unroll
-        for (int k = 0; k < kWinRounds; ++k) {
-            const int i = min(tid + k * kMbThreads, kWinChunks - 1);
-            const int p = i / (kWinPlane / 16), rem = i - p * (kWinPlane / 16), r = rem / (kWinW / 16), cc = rem - r * (kWinW / 16);
-            wv[k] = *reinterpret_cast<const __attribute__((address_space(1))) uint4*>(pl + (size_t)p * F.plsz + (size_t)(c.yL + r) * F.pstride + c.xL + cc * 16);
-        }
-    }
-#endif
-#endif
     mb_begin(c);
-#if defined(__HIP_DEVICE_COMPILE__) && HL_LDS_WINDOW && !HL_LDS_WINDOW_DMA
-    if (!F.is_intra) {
-#pragma unroll
-        for (int k = 0; k < kWinRounds; ++k)
-            if (tid + k * kMbThreads < kWinChunks) reinterpret_cast<uint4*>(S.win)[tid + k * kMbThreads] = wv[k];
-    }
-#endif
     HL_PROF_ADD(c, 6, t0);
     if (f3out) {
 #if defined(HL_EMU_BUILD) && !defined(__HIP_DEVICE_COMPILE__)

@@ -22,12 +22,6 @@
 namespace hl {
 
 constexpr int kQX1 = 0xB1, kQX2 = 0x4E, kQX3 = 0x1B;  // quad_perm lane ^ 1, lane ^ 2, lane ^ 3
-#ifndef HL_RB_TABLE  // 1: run_before lengths from an LDS table instead of the packed closed form
-#define HL_RB_TABLE 1
-#endif
-#ifndef HL_CAVLC_REGLOOP  // 1: quad_cavlc's level chain over registers (see there)
-#define HL_CAVLC_REGLOOP 1
-#endif
 
 // A DPP read kept as its own v_mov_b32_dpp: the empty asm stops LLVM's DPP
 // combiner from folding it into the subtraction that consumes it.  On the
@@ -235,13 +229,9 @@ __device__ __forceinline__ CoopStat quad_cavlc(const CoopTables& T, const LaneQ&
         const uint32_t lower = nz & ((1u << lis) - 1u);
         const int zl = lis - __popc(lower);
         const int run = lis - 1 - (31 - __clz(lower));  // lis when lower == 0 (__clz(0) = 32)
-#if HL_RB_TABLE
         // run_before length from the LDS table (zerosLeft 0 reads 0)
         const int rbv = T.rb[zl & 15][run & 15];
         rbs += (nzl[c] & (int)(lower != 0)) ? rbv : 0;
-#else
-        rbs += (nzl[c] & (int)(lower != 0) & (int)(zl > 0)) ? quad_rb_len(zl, run) : 0;
-#endif
         const int am = nzl[c] ? aL[c] : 0;
         absum += am;
         amax = max(amax, am);
@@ -279,7 +269,6 @@ __device__ __forceinline__ CoopStat quad_cavlc(const CoopTables& T, const LaneQ&
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         int sl = sl0;
-#if HL_CAVLC_REGLOOP
         // the 16 words in registers at once (four ds_read_b128 in flight), then
         // the chain over them unrolled: no LDS round trip per level
         const int4 w0 = reinterpret_cast<const int4*>(lvs)[0], w1 = reinterpret_cast<const int4*>(lvs)[1];
@@ -294,13 +283,6 @@ __device__ __forceinline__ CoopStat quad_cavlc(const CoopTables& T, const LaneQ&
                 sl = next_sl(sl, v[k] & 0xFFFF);
             }
         }
-#else
-        for (int k = 0; k < tc - t1; ++k) {
-            const int v = lvs[k];
-            bits += level_len(sl, v >> 16);
-            sl = next_sl(sl, v & 0xFFFF);
-        }
-#endif
     }
     st.tc = tc;
     st.t1 = tc ? t1 : 0;

@@ -10,13 +10,31 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "tests"))
-from test_isa import _disassemble  # noqa: E402
+LLVM = "/opt/rocm/lib/llvm/bin"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _disassemble_all(lib, td):
+    """Every code object of the library's .hip_fatbin (one bundle per HIP
+    translation unit: hl_encoder.hip and hl_encoder_fam3.hip)."""
+    fat = os.path.join(td, "fat.bin")
+    subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", lib], check=True, capture_output=True)
+    data = open(fat, "rb").read()
+    starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)]
+    text = []
+    for k, a in enumerate(starts):
+        b = starts[k + 1] if k + 1 < len(starts) else len(data)
+        part, co = os.path.join(td, f"b{k}.bin"), os.path.join(td, f"co{k}.elf")
+        open(part, "wb").write(data[a:b])
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={part}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True, capture_output=True)
+        text.append(subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", co], check=True, capture_output=True, text=True).stdout)
+    return "\n".join(text), len(starts)
 
 
 def digest(lib):
     with tempfile.TemporaryDirectory() as td:
-        text = _disassemble(lib, td)
+        text, nb = _disassemble_all(lib, td)
     lines = []
     for ln in text.splitlines():
         ln = re.sub(r"//.*$", "", ln).strip()
@@ -24,7 +42,7 @@ def digest(lib):
         ln = re.sub(r"<[^>]*\+0x[0-9a-f]+>", "", ln)
         if ln and not ln.startswith("Disassembly") and not ln.endswith("file format elf64-amdgpu"):
             lines.append(ln)
-    return hashlib.sha256("\n".join(lines).encode()).hexdigest()[:16], len(lines)
+    return hashlib.sha256("\n".join(lines).encode()).hexdigest()[:16], len(lines), f"{nb} code objects"
 
 
 if __name__ == "__main__":
