@@ -319,7 +319,6 @@ struct Shared {
     double i4r_dmin[16];       // per block, in z-order accumulation after the wavefront
     int32_t i4r_dist[16], i4r_sct[16], i4r_zero[16];
     int32_t luma_level[16][16];
-    int16_t i4nb[2][16];         // neighbours of the current 4x4 blocks (p[13] layout)
     int32_t dcY[64];             // I16x16: scaled DC per DC-matrix position (per mode)
     int32_t chain_x;             // resolve_chain result
     int32_t hs_x;                // intra helper state seen by the MB (HS_*)
@@ -3120,10 +3119,16 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
         const int blk = sl == 0 ? kWave[d][0] : (sl == 1 ? kWave[d][1] : 255);
         if (blk != 255) {  // (wave-uniform)
             const int xO = blk_x(blk), yO = blk_y(blk);
-            if (lane < 16) {
-                // lane i: neighbour sample i (i4_neighbours, one sample per
-                // lane); lane 13: the DC value (mode 2 of i4_pred_px)
-                const int i = lane;
+            // nC first: its LDS reads overlap the neighbour gather
+            // (nC is the same for all nine modes of a block: they only rewrite it)
+            const int nC = uni(nc_luma_of(S, blk, [&](int ni) -> int { return S.tc[ni]; }));
+            // lane i < 13: neighbour sample i (i4_neighbours, one sample per
+            // lane); lane 13: the DC value (mode 2 of i4_pred_px); every lane
+            // computes (the reads are clamped in range), lanes 0-13 are read
+            // back with ds_bpermute (no LDS store, no wave barrier)
+            int nbv;
+            {
+                const int i = lane & 15;
                 const int X = i < 5 ? -1 : i - 5, Y = i < 5 ? i - 1 : -1;
                 const int x = xO + X, y = yO + Y;
                 const bool na = i >= 13 || (x > 15 && y >= 0) || (X > 3 && (blk == 3 || blk == 11));
@@ -3136,26 +3141,25 @@ HD void guess_i4(Ctx& c, double& best_cost, int& cbp4, int& best_dist)
                 const unsigned al = (unsigned)__ballot(isl && v != kNA) & 0xFFFFu, at = (unsigned)__ballot(ist && v != kNA) & 0xFFFFu;
                 const bool ya = al == 0x1Eu, xa = at == 0x1E0u;
                 const int dc = (xa && ya) ? (sumt + suml + 4) >> 3 : (ya ? (suml + 2) >> 2 : (xa ? (sumt + 2) >> 2 : 128));
-                if (i < 14) S.i4nb[sl][i] = (int16_t)(i == 13 ? dc : v);  // [13]: the DC value
+                nbv = i == 13 ? dc : v;
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // nC is the same for all nine modes of a block: they only rewrite it
-            const int nC = uni(nc_luma_of(S, blk, [&](int ni) -> int { return S.tc[ni]; }));
 #if defined(HL_I4_PROF)
             HL_PROF_ADD(c, 12, ti1);  // neighbours, nC
             HL_PROF_T(ti3);
 #endif
-            const int16_t* nb = S.i4nb[sl];
-            const bool ok = (lane >> 2) < 9 && i4_avail(m, nb);
+            struct {
+                int v;
+                __device__ int operator[](int i) const { return __builtin_amdgcn_readlane(v, i); }  // constant indices (i4_avail)
+            } nbr{nbv};
+            const bool ok = (lane >> 2) < 9 && i4_avail(m, nbr);
             const uint32_t sv4 = *reinterpret_cast<const uint32_t*>(&S.src[(yO + rr) * 16 + xO]);
             int x[4], y[4], q[4], r[4];
             uint32_t pr4 = 0;
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc) {
                 const uint32_t e = te[cc];
-                const int pred = i4_tab_pred(e, nb[e & 15], nb[(e >> 4) & 15], nb[(e >> 8) & 15]);
+                const int pred = i4_tab_pred(e, __shfl(nbv, (int)(e & 15), 64), __shfl(nbv, (int)((e >> 4) & 15), 64),
+                                             __shfl(nbv, (int)((e >> 8) & 15), 64));
                 x[cc] = (int)((sv4 >> (8 * cc)) & 255) - pred;
                 pr4 |= (uint32_t)pred << (8 * cc);
             }

@@ -6,10 +6,18 @@ stdout).
 
 Units and corrections (MI355X_MICROARCH.md): SQ_WAVE_CYCLES / SQ_WAIT_* /
 SQ_ACTIVE_INST_* count quad-cycles (the ratios between them are unit-free);
-FETCH_SIZE / WRITE_SIZE are KiB (TCC_EA0_*REQ x 64 B / 1024) and FETCH_SIZE
-is doubled for gfx950 (128-B requests tallied at 64 B; calibrated for
-16 B/lane streaming reads -- this kernel's byte gathers are uncalibrated, and
-Infinity-Cache hits are counted, not excluded).
+FETCH_SIZE / WRITE_SIZE are KiB.  FETCH_SIZE is TCC_EA0_RDREQ x 64 B and is
+doubled: calibrated in round 6 (tools/fetch_calib.hip,
+profiles/r06_fetch_write_calib.log) for this kernel's own pattern -- a
+4-lane quad gathering 8 bytes per lane from rows of a 2048-byte-stride
+plane -- as for streaming reads, every L2 miss is one 128-byte request
+(TCC_EA0_RDREQ_128B) tallied at 64 B.  WRITE_SIZE is exact: 64-byte
+requests for whole-sector streaming stores, one 32-byte request per 16- or
+4-byte partial store, each counted at its size.  Infinity-Cache hits are
+counted, not excluded.  With the request-size passes (pmc_record.sh) the
+reads are also given as TCC_EA0_RDREQ_128B x 128 + the rest x 64 and the
+writes split into 64-byte / other requests and into IO (host-memory) and
+atomic requests.
 
   python tools/pmc_summary.py --warmup W --steps S DIR [DIR ...]
 """
@@ -73,6 +81,21 @@ def main():
         out.update({"fetch_bytes_per_launch_x2": rd, "write_bytes_per_launch": wr, "traffic_bytes_per_launch": rd + wr,
                     "fetch_bytes_per_mb_x2": round(rd / mbs, 1), "write_bytes_per_mb": round(wr / mbs, 1),
                     "traffic_bytes_per_mb": round((rd + wr) / mbs, 1)})
+    out["fetch_size_factor"] = {"factor": 2.0, "calibrated": "round 6, tools/fetch_calib.hip: streaming 16 B/lane, the search's "
+                                "8-byte quad gathers and 4-byte line reads all issue one 128-B request per L2 miss "
+                                "(TCC_EA0_RDREQ_128B), FETCH_SIZE = requests x 64 B", "log": "profiles/r06_fetch_write_calib.log"}
+    if "TCC_EA0_RDREQ_sum" in c and "TCC_EA0_RDREQ_128B_sum" in c:
+        r128, rall = c["TCC_EA0_RDREQ_128B_sum"], c["TCC_EA0_RDREQ_sum"]
+        out["read_requests_per_mb"] = {"all": round(rall / mbs, 1), "128B": round(r128 / mbs, 1),
+                                       "bytes_per_mb": round((r128 * 128 + (rall - r128) * 64) / mbs, 1)}
+    if "TCC_EA0_WRREQ_sum" in c and "TCC_EA0_WRREQ_64B_sum" in c:
+        w64, wall = c["TCC_EA0_WRREQ_64B_sum"], c["TCC_EA0_WRREQ_sum"]
+        out["write_requests_per_mb"] = {"all": round(wall / mbs, 1), "64B": round(w64 / mbs, 1), "32B_or_less": round((wall - w64) / mbs, 1),
+                                        "bytes_per_mb": round((w64 * 64 + (wall - w64) * 32) / mbs, 1)}
+        for k, n in (("TCC_EA0_WRREQ_WRITE_IO_32B_sum", "io_32B"), ("TCC_EA0_WRREQ_ATOMIC_DRAM_sum", "atomic_dram"),
+                     ("TCC_EA0_WRREQ_WRITE_DRAM_sum", "write_dram")):
+            if k in c:
+                out["write_requests_per_mb"][n] = round(c[k] / mbs, 1)
     print(json.dumps(out, indent=1))
 
 
