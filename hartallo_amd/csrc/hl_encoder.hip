@@ -312,18 +312,18 @@ __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
         for (int q = 0; q < kSubQ; ++q) P.queue[(f * kSubQ + q) * nmb + a] = k == 0 && a == 0 && q == 0 ? 1 : 0;  // every stream's first task
         P.claim[i] = 0;
         P.hstate[i] = HS_FREE;
-        P.hstate3[i] = HS_FREE;
-        P.hq[i] = 0;
-        P.hq[P.nframes * nmb + i] = 0;
+        for (int j = 0; j < 4; ++j) P.hstate3[4 * i + j] = HS_FREE;
+        for (int j = 0; j < 5; ++j) P.hq[j * P.nframes * nmb + i] = 0;
     }
+    if (i < kHelperQ) P.hq[5 * P.nframes * nmb + i] = 0;  // (kHelperQ * hq_cap < 5 nframes nmb + kHelperQ; the grid has >= 256 threads)
     if (i < P.nframes * kSubQ) {
         P.head[i] = 0;
         P.tail[i] = (i / kSubQ) % P.spp == 0 && i % kSubQ == 0 ? 1 : 0;
     }
     if (i < P.nstreams) P.oldest[i] = 0;
-    if (i == 0) {
-        *P.hq_head = 0;
-        *P.hq_tail = 0;
+    if (i < kHelperQ) {
+        P.hq_head[i] = 0;
+        P.hq_tail[i] = 0;
     }
     if (i == 0) {
         for (int k = 0; k < 8; ++k) P.err[k] = 0;  // give-ups, chain walks, helper I4 kept / rejected / taken over, -, 8x8 family kept / rejected
@@ -462,31 +462,45 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc, 
                 return f * nmb + r - 1;
             }
             HL_POPSTAT(1);
-            continue;  // another workgroup took it
+            // another workgroup took it: retry, except beside a lone picture
+            // (the 8x8 family's helpers on), where ~200 idle workgroups race for
+            // each ready macroblock and the losers take a helper task instead
+            if (!P.fam3) continue;
         }
-        if (P.helpers) {  // no macroblock ready: an intra helper task, unless its macroblock took it over
-            const int hh = ld_relaxed(P.hq_head), ht = ld_relaxed(P.hq_tail);
-            if (hh < ht) {
+        if (P.helpers) {  // no macroblock ready: a helper task, unless its macroblock took it over
+            // lane q reads FIFO q; the workgroup's own FIFO first, then the
+            // next non-empty one after it
+            int qh = 0, qt = 0;
+            if (lane < kHelperQ) {
+                qh = ld_relaxed(P.hq_head + lane);
+                qt = ld_relaxed(P.hq_tail + lane);
+            }
+            const unsigned ne = (unsigned)__ballot(lane < kHelperQ && qh < qt);
+            if (ne) {
+                const int own = (int)(blockIdx.x % kHelperQ);
+                const unsigned rot = ((ne >> own) | (ne << (kHelperQ - own))) & ((1u << kHelperQ) - 1u);
+                const int q = (own + __builtin_ctz(rot)) % kHelperQ;
+                const int hh = __builtin_amdgcn_readlane(qh, q);
                 int r = 0;
                 int kind = 0;
-                if (lane == 0 && atomicCAS(P.hq_head, hh, hh + 1) == hh) {
-                    for (unsigned k = 0; (r = ld_relaxed(P.hq + hh)) == 0; ++k)
+                if (lane == 0 && atomicCAS(P.hq_head + q, hh, hh + 1) == hh) {
+                    for (unsigned k = 0; (r = ld_relaxed(P.hq + q * P.hq_cap + hh)) == 0; ++k)
                         if (k > (1u << 26)) {
                             atomicAdd(P.err, 1);
                             r = -1;
                             break;
                         }
                     if (r > 0) {
-                        kind = r >> 30;
-                        r &= (1 << 30) - 1;
-                        if (atomicCAS((kind ? P.hstate3 : P.hstate) + r - 1, HS_FREE, HS_CLAIMED) != HS_FREE) r = 0;
+                        kind = r >> 27;
+                        r &= (1 << 27) - 1;
+                        if (atomicCAS(kind ? P.hstate3 + 4 * (r - 1) + kind - 1 : P.hstate + r - 1, HS_FREE, HS_CLAIMED) != HS_FREE) r = 0;
                     }
                 }
                 r = __builtin_amdgcn_readfirstlane(r);
                 kind = __builtin_amdgcn_readfirstlane(kind);
                 if (r < 0) return -1;
                 if (r > 0) {
-                    return (1 + kind) * P.nframes * nmb + r - 1;  // intra helpers, then 8x8-family helpers
+                    return (1 + kind) * P.nframes * nmb + r - 1;  // intra helpers, then the 8x8 family's partitionings 3..6
                 }
                 continue;
             }
@@ -574,7 +588,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #if defined(HL_PROFILE)
     // per-workgroup totals (profiling build): prof[40..44] = waits for a ready
     // task, decisions, filters, tasks, workgroup lifetime (shader clock)
-    unsigned long long pw_wait = 0, pw_mb = 0, pw_filt = 0, pw_n = 0, pw_hlp = 0, pw_hn = 0;
+    unsigned long long pw_wait = 0, pw_mb = 0, pw_filt = 0, pw_n = 0, pw_hlp = 0, pw_hn = 0, pw_phlp = 0, pw_phn = 0;
     unsigned long long pst[3] = {0, 0, 0};  // pop_task rounds (wave 0)
     unsigned long long ptail[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // after the filters: barrier, release fence, successors' release; early release; its fence, release, spin, acquire
     const unsigned long long pw_t0 = __builtin_readcyclecounter();
@@ -619,10 +633,15 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
 #if defined(HL_PROFILE)
         const unsigned long long pw_start = wall_clock64();  // (the task's timeline, below)
 #endif
-        // helper tasks (hl_mbcore.h): 1 = intra_helper, 2 = fam3_helper
-        const int hk = t >= 2 * P.nframes * nmb ? 2 : (t >= P.nframes * nmb ? 1 : 0);
+        // helper tasks (hl_mbcore.h): 1 = intra_helper, 2..5 = the 8x8 family's
+        // partitioning hk + 1 (guess_inter)
+        int hk = 0;
+        while (t >= P.nframes * nmb) {
+            t -= P.nframes * nmb;
+            ++hk;
+        }
+        hk = uni(hk);
         const bool helper = hk > 0;
-        t -= hk * P.nframes * nmb;
 #if defined(HL_DIAG) && HL_DIAG == 1
         __syncthreads();
 #endif
@@ -663,7 +682,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         // (one call site of encode_mb: the macroblock and its 8x8-family helper
         // share the inlined search)
         if (hk == 1) intra_helper(sF, S, addr, tid, kMbThreads, s_in, PF.F.ispec + addr);
-        else encode_mb(sF, S, addr, tid, kMbThreads, s_in, gx, gy, spec_in, hk == 2 ? PF.F.f3 + addr : nullptr);
+        else encode_mb(sF, S, addr, tid, kMbThreads, s_in, gx, gy, spec_in, hk >= 2 ? PF.F.f3 + addr * 4 + (hk - 2) : nullptr, hk + 1);
         if (helper) {
             // results, every wave's stores drained, barrier, one release, the state
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -671,11 +690,15 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
             if (tid < 64) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, HL_REL_SCOPE);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (tid == 0) st_relaxed((hk == 1 ? P.hstate : P.hstate3) + t, HS_DONE);
+                if (tid == 0) st_relaxed(hk == 1 ? P.hstate + t : P.hstate3 + 4 * t + hk - 2, HS_DONE);
             }
 #if defined(HL_PROFILE)
             pw_hlp += __builtin_readcyclecounter() - pt1;
             ++pw_hn;
+            if (hk >= 2) {  // of which the 8x8 family's partitioning helpers
+                pw_phlp += __builtin_readcyclecounter() - pt1;
+                ++pw_phn;
+            }
 #endif
             continue;
         }
@@ -716,12 +739,18 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
                 const int qf = fo * kSubQ + a % kSubQ;
                 const int pos = __hip_atomic_fetch_add(P.tail + qf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const int hp = hlp ? __hip_atomic_fetch_add(P.hq_tail, 1 + P.fam3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-                __hip_atomic_store(P.queue + qf * nmb + pos, a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                if (hlp) {  // the 8x8-family helper first (the longer one), then the intra helper
-                    if (P.fam3) __hip_atomic_store(P.hq + hp, (1 << 30) | (fo * nmb + a + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(P.hq + hp + P.fam3, fo * nmb + a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                // helper kinds: 0 = intra, 1..4 = the 8x8 family's partitioning kind + 2
+                const int g = fo * nmb + a, nk = hlp ? 1 + 4 * P.fam3 : 0;
+                int hq[5], hp[5];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) {
+                    hq[k] = (5 * g + k) % kHelperQ;
+                    hp[k] = k < nk ? __hip_atomic_fetch_add(P.hq_tail + hq[k], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
                 }
+                __hip_atomic_store(P.queue + qf * nmb + pos, a + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                for (int k = 0; k < 5; ++k)
+                    if (k < nk) __hip_atomic_store(P.hq + hq[k] * P.hq_cap + hp[k], (k << 27) | (g + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             }
         };
         // This picture's successors need the decision (its reconstruction, MB
@@ -837,6 +866,8 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
         atomicAdd(prof + 44, __builtin_readcyclecounter() - pw_t0);
         atomicAdd(prof + 45, pw_hlp);  // intra helper tasks: cycles, count
         atomicAdd(prof + 46, pw_hn);
+        atomicAdd(prof + 58, pw_phlp);
+        atomicAdd(prof + 59, pw_phn);
         for (int i = 0; i < 3; ++i) atomicAdd(prof + 47 + i, pst[i]);  // pops: attempts, lost, empty rounds
         for (int i = 0; i < 8; ++i) atomicAdd(prof + 50 + i, ptail[i]);  // filters' barrier, release fence, successors, early release (fence, release, spin, acquire)
     }
@@ -911,7 +942,7 @@ struct hl_amd_encoder_s {
     int32_t helper_kept = 0, helper_rejected = 0, helper_self = 0;  // hl_amd_last_helper_stats
     int fam3 = 1;                                // ... and 8x8-family helper tasks (HL_AMD_FAM3: 0 off, 2 runs too)
     int32_t fam3_kept = 0, fam3_rejected = 0;    // hl_amd_last_fam3_stats
-    Fam3Out* d_f3 = nullptr;                     // 8x8-family helper results [MB] (only runs of one picture use them)
+    Fam3Out* d_f3 = nullptr;                     // 8x8-family partitioning helper results [MB][4] ([slot][MB][4] with HL_AMD_FAM3=2)
     PipeFrame *d_pf, *h_pf;
     std::vector<std::vector<uint8_t>> bout;  // bitstreams of the last hl_amd_encode_batch
     int nwriters;                            // host slice writer threads of a run
@@ -1340,13 +1371,14 @@ static hipError_t ensure_sched(hl_amd_encoder_t* e, int slots)
     e->h_pf = nullptr;
     e->scap = 0;
     hipError_t r;
-    // (helper states: intra [slot][MB], then 8x8 family; the helper FIFO sits
-    // after the ready queues, two entries per MB)
+    // (helper states: intra [slot][MB], then the 8x8 family's [slot][MB][4];
+    // the helper FIFO sits after the ready queues, five entries per MB)
     if ((r = hipMalloc(&e->d_pf, sizeof(PipeFrame) * slots)) || (r = hipHostMalloc(&e->h_pf, sizeof(PipeFrame) * slots, hipHostMallocDefault)) ||
         (r = hipMalloc(&e->d_cnt, sizeof(int32_t) * 2 * nmb * slots)) || (r = hipMalloc(&e->d_done, sizeof(int32_t) * nmb * slots)) ||
-        (r = hipMalloc(&e->d_queue, sizeof(int32_t) * (kSubQ + 2) * nmb * slots)) ||
-        (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * kSubQ * slots + kMaxStreams + 2))) ||
-        (r = hipMalloc(&e->d_hstate, sizeof(int32_t) * 2 * nmb * slots)) || (r = hipMalloc(&e->d_f3, sizeof(Fam3Out) * nmb)))
+        (r = hipMalloc(&e->d_queue, sizeof(int32_t) * ((kSubQ + 5) * nmb * slots + kHelperQ))) ||
+        (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * kSubQ * slots + kMaxStreams + 2 * kHelperQ))) ||
+        (r = hipMalloc(&e->d_hstate, sizeof(int32_t) * 5 * nmb * slots)) ||
+        (r = hipMalloc(&e->d_f3, sizeof(Fam3Out) * 4 * nmb * (e->fam3 == 2 ? slots : 1))))
         return r;
     if (!e->d_err && (r = hipMalloc(&e->d_err, sizeof(int32_t) * 8))) return r;
     e->scap = slots;
@@ -1565,8 +1597,10 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
                 F.ispec = e->d_ispec;
                 F.hstate = e0->d_hstate + nmb * slot;
                 if (fam3) {
-                    F.f3 = e0->d_f3;  // per MB address: one stream (a picture's helper ends before the next picture's MB starts)
-                    F.hstate3 = e0->d_hstate + (size_t)nmb * (slots + slot);
+                    // per MB address and partitioning; per picture too in runs
+                    // (a helper may still run after its macroblock ended)
+                    F.f3 = e0->d_f3 + (e0->fam3 == 2 ? (size_t)4 * nmb * slot : 0);
+                    F.hstate3 = e0->d_hstate + (size_t)nmb * slots + (size_t)4 * nmb * slot;
                 }
             }
             pf.D.W = e->W;
@@ -1607,8 +1641,9 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
     P.head = e0->d_head;
     P.tail = e0->d_head + kSubQ * slots;
     P.oldest = e0->d_head + 2 * kSubQ * slots;
+    P.hq_cap = (5 * slots * nmb + kHelperQ - 1) / kHelperQ;
     P.hq_head = e0->d_head + 2 * kSubQ * slots + kMaxStreams;
-    P.hq_tail = e0->d_head + 2 * kSubQ * slots + kMaxStreams + 1;
+    P.hq_tail = e0->d_head + 2 * kSubQ * slots + kMaxStreams + kHelperQ;
     P.err = e0->d_err;
     static const bool trace = getenv("HL_AMD_TRACE_WRITERS") != nullptr;
     static unsigned long long* h_clock = nullptr;

@@ -171,11 +171,12 @@ static_assert(sizeof(IntraSpec) % 16 == 0, "IntraSpec in whole 16-byte words");
 // helper task state (FrameArgs::hstate[addr])
 enum : int32_t { HS_FREE = 0, HS_CLAIMED = 1, HS_MAIN = 2, HS_DONE = 3 };
 
-// An 8x8-family helper task's results (fam3_helper, FrameArgs::f3[addr]): the
-// P8x8 partitionings (kParts[3..6], rdo.c:745-760) searched from the MB-start
-// live TotalCoeffs while the macroblock searches 16x16 / 16x8 / 8x16, with the
+// A partitioning helper task's results (FrameArgs::f3[addr * 4 + j - 3]): P8x8
+// partitioning j (kParts[3..6], rdo.c:745-760) searched from the MB-start live
+// TotalCoeffs while the macroblock searches 16x16 / 16x8 / 8x16, with the
 // intervals of the entry values under which every nC class it used holds
-// (f3_verify), and the state the family leaves behind.
+// (f3_verify), and the state the partitioning leaves behind (the per-
+// partitioning arrays hold j's entry only).
 struct Fam3Out {
     double cost[4];               // partitioning j = 3..6: sum of the partitions' best costs (header bits not added)
     int32_t single[4], dist[4];
@@ -227,8 +228,8 @@ struct FrameArgs {
     IntraSpec* ispec;
     int32_t* hstate;
     // 8x8-family helper tasks (the same pictures): this picture's results and states
-    Fam3Out* f3;
-    int32_t* hstate3;
+    Fam3Out* f3;       // [addr * 4 + j - 3]
+    int32_t* hstate3;  // [addr * 4 + j - 3]
 };
 
 struct NbInfo {
@@ -3927,16 +3928,20 @@ HD bool search_family_part(Ctx& c, int j, int fam, double& cost_sum, int& single
 }
 
 // --------------------------------------------------------------------------
-// 8x8-family helper tasks (pipelined runs): while a P macroblock searches
-// 16x16 / 16x8 / 8x16, an idle workgroup searches the P8x8 partitionings
-// (kParts[3..6]) from the MB-start live TotalCoeffs.  The family reads the
-// live TotalCoeffs it starts from only through nC classes, and only until the
-// family itself overwrites a block; fam3_helper records, for every such read,
-// the interval of the entry value (or of the sum of two) that keeps the class
-// (Shared::f3lo / f3hi).  The family never reads rdo.Single_ctr.  So if the
-// macroblock's real entry values lie in every interval, the family's every
-// cost, decision and write is the same, and the macroblock takes them
-// (f3_import); otherwise it searches the family itself.
+// Partitioning helper tasks of the 8x8 family (lone pictures): while a P
+// macroblock searches 16x16 / 16x8 / 8x16, idle workgroups search the P8x8
+// partitionings (kParts[3..6]), one task per partitioning, each from the
+// MB-start live TotalCoeffs.  A partitioning reads the live TotalCoeffs it
+// starts from only through nC classes, and only until it overwrites a block
+// itself; the helper records, for every such read, the interval of the entry
+// value (or of the sum of two) that keeps the class (Shared::f3lo / f3hi).  A
+// partitioning never reads rdo.Single_ctr, nor the motion another one left.
+// So if the macroblock's real entry values for partitioning j -- what j - 1
+// left, imported or searched -- lie in every interval of j's helper, j's every
+// cost, decision and write is the helper's, and the macroblock takes them
+// (f3_import); otherwise it searches j itself.  The four run side by side:
+// the macroblock's 8x8-family latency is that of its longest partitioning
+// (4x4, 16 searches), not of the family's 36 searches in a row.
 // --------------------------------------------------------------------------
 // The macroblock's real entry values (S.f3entry) against the helper's intervals
 template <typename P>
@@ -3954,9 +3959,9 @@ HD bool f3_verify(const Shared& S, P h)
     return ok;
 }
 
-// f3out: run as the macroblock's 8x8-family helper task instead (the family
-// only, recorded for f3_verify, into f3out; see above)
-HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr)
+// f3out: run as the macroblock's helper task of partitioning hj (3..6) instead
+// (that partitioning only, recorded for f3_verify, into f3out; see above)
+HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr, int hj = 3)
 {
     const FrameArgs& F = c.F;
     Shared& S = c.S;
@@ -4002,152 +4007,159 @@ HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr)
         }
         if (c.tid == 0) {
             S.f3w = 0;
-            S.f3b[0] = 0;  // partitionings searched
-            S.f3b[1] = 3;  // the last one
+            S.f3b[0] = 0;  // searched (mode_flags)
         }
         HL_SYNC();
         c.f3rec = 1;
         c.fresh = 0;
     }
     for (int fam = HL_FAM3 && f3out ? 3 : 0; fam < 4 && !best_found; ++fam) {
-        // the 8x8 family's helper (pipelined runs): taken over if no workgroup
-        // claimed it, else polled between partition searches
-        int h3 = HS_MAIN;
-        if (HL_FAM3 && fam == 3 && F.hstate3 && !f3out) {
+        const int jlo = HL_FAM3 && f3out ? hj : fam_first(fam), jhi = HL_FAM3 && f3out ? hj + 1 : fam_first(fam + 1);
+        for (int j = jlo; j < jhi; ++j) {
+            if (!((1 << (j + 1)) & mode_flags)) continue;
+            // partitioning j's helper (8x8 family): taken over if no workgroup
+            // claimed it, else polled between partition searches
+            int h3 = HS_MAIN;
+            const int hx = c.addr * 4 + (j - 3);  // its state and results
+            if (HL_FAM3 && fam == 3 && F.hstate3 && !f3out) {
 #if defined(__HIP_DEVICE_COMPILE__)
-            if (c.tid == 0) S.hs3_x = atomicCAS(F.hstate3 + c.addr, HS_FREE, HS_MAIN);
-            HL_SYNC();
-            h3 = uni(S.hs3_x);
+                if (c.tid == 0) S.hs3_x = atomicCAS(F.hstate3 + hx, HS_FREE, HS_MAIN);
+                HL_SYNC();
+                h3 = uni(S.hs3_x);
 #else
-            h3 = F.hstate3[c.addr] == HS_FREE ? HS_MAIN : F.hstate3[c.addr];
-            if (h3 == HS_MAIN) F.hstate3[c.addr] = HS_MAIN;
+                h3 = F.hstate3[hx] == HS_FREE ? HS_MAIN : F.hstate3[hx];
+                if (h3 == HS_MAIN) F.hstate3[hx] = HS_MAIN;
 #endif
-            if (h3 == HS_FREE) h3 = HS_MAIN;
-            if (h3 != HS_MAIN) {  // the state the family starts from, and the best so far
-                for (int i = c.tid; i < 16; i += c.nthr) S.f3entry[i] = S.tc[i];
-                for (int i = c.tid; i < 32; i += c.nthr) {
-                    (&S.f3best_mv[0][0][0])[i] = (&S.best_mv[0][0][0])[i];
-                    (&S.f3best_mvp[0][0][0])[i] = (&S.best_mvp[0][0][0])[i];
+                if (h3 == HS_FREE) {
+                    h3 = HS_MAIN;
+#if defined(__HIP_DEVICE_COMPILE__) && defined(HL_PROFILE)
+                    if (c.tid == 0 && F.prof) atomicAdd(F.prof + 60, 1ull);  // not claimed in time: taken over
+#endif
                 }
-                if (c.tid == 0) {
-                    S.f3b_cost = best_cost;
-                    S.f3b[0] = best_single;
-                    S.f3b[1] = best_part;
-                    S.f3b[2] = best_fam;
-                    S.f3b[3] = best_dist;
-                    S.f3b[4] = c.chain;
-                    S.f3b[5] = c.fresh;
-                    S.f3b[6] = c.spec;
+                if (h3 != HS_MAIN) {  // the state partitioning j starts from, and the best so far
+                    for (int i = c.tid; i < 16; i += c.nthr) S.f3entry[i] = S.tc[i];
+                    for (int i = c.tid; i < 32; i += c.nthr) {
+                        (&S.f3best_mv[0][0][0])[i] = (&S.best_mv[0][0][0])[i];
+                        (&S.f3best_mvp[0][0][0])[i] = (&S.best_mvp[0][0][0])[i];
+                    }
+                    if (c.tid == 0) {
+                        S.f3b_cost = best_cost;
+                        S.f3b[0] = best_single;
+                        S.f3b[1] = best_part;
+                        S.f3b[2] = best_fam;
+                        S.f3b[3] = best_dist;
+                        S.f3b[4] = c.chain;
+                        S.f3b[5] = c.fresh;
+                        S.f3b[6] = c.spec;
+                    }
+                    HL_SYNC();
+                }
+            }
+            // a claimed helper: has it finished?  (the first check at once, then
+            // between partition searches)
+            auto h3_done = [&]() -> bool {
+                if (h3 != HS_CLAIMED) return h3 == HS_DONE;
+#if defined(__HIP_DEVICE_COMPILE__)
+                if (c.tid == 0) S.hs3_x = ld_relaxed(F.hstate3 + hx);
+                HL_SYNC();
+                if (uni(S.hs3_x) == HS_DONE) h3 = HS_DONE;
+#else
+                if (F.hstate3[hx] == HS_DONE) h3 = HS_DONE;
+#endif
+                return h3 == HS_DONE;
+            };
+            // the helper finished, and its partitioning is proven for this MB's
+            // entry state?  (asked at the partitioning's start and before each
+            // partition search while the helper runs; a helper found unproven is
+            // not asked again)
+            auto f3_ready = [&]() -> bool {
+                if (h3 == HS_MAIN) return false;
+                if (!h3_done()) return false;
+#if defined(__HIP_DEVICE_COMPILE__)
+                if (c.tid < 64) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
                 HL_SYNC();
-            }
-        }
-        // a claimed helper: has it finished?  (the first check at once, then
-        // between partition searches)
-        auto h3_done = [&]() -> bool {
-            if (h3 != HS_CLAIMED) return h3 == HS_DONE;
-#if defined(__HIP_DEVICE_COMPILE__)
-            if (c.tid == 0) S.hs3_x = ld_relaxed(F.hstate3 + c.addr);
-            HL_SYNC();
-            if (uni(S.hs3_x) == HS_DONE) h3 = HS_DONE;
+                const auto hv = gmem(F.f3 + hx);
+                const bool ok = ((uni((int)hv->done_mask) >> (j - 3)) & 1) && f3_verify(S, hv);
 #else
-            if (F.hstate3[c.addr] == HS_DONE) h3 = HS_DONE;
+                const bool ok = ((F.f3[hx].done_mask >> (j - 3)) & 1) && f3_verify(S, F.f3 + hx);
 #endif
-            return h3 == HS_DONE;
-        };
-        // the helper finished, and its family is proven for this MB's entry state?
-        // (asked at the family's start and before each partition search while
-        // the helper runs; a helper found unproven is not asked again)
-        auto f3_ready = [&]() -> bool {
-            if (h3 == HS_MAIN) return false;
-            if (!h3_done()) return false;
+                if (!ok) {
+                    h3 = HS_MAIN;  // (decided once)
 #if defined(__HIP_DEVICE_COMPILE__)
-            if (c.tid < 64) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            HL_SYNC();
-            const bool ok = f3_verify(S, gmem(F.f3 + c.addr));
+                    if (c.tid == 0 && F.perr) atomicAdd(F.perr + 6, 1);
 #else
-            const bool ok = f3_verify(S, F.f3 + c.addr);
+                    if (F.perr) ++F.perr[6];
 #endif
-            if (!ok) {
-                h3 = HS_MAIN;  // (decided once)
-#if defined(__HIP_DEVICE_COMPILE__)
-                if (c.tid == 0 && F.perr) atomicAdd(F.perr + 6, 1);
-#else
-                if (F.perr) ++F.perr[6];
-#endif
-            }
-            return ok;
-        };
-        // the helper's family from the entry state: the best so far, the live
-        // TotalCoeffs, rdo.Single_ctr and the partition state it leaves
-        auto f3_import = [&]() {
-#if defined(__HIP_DEVICE_COMPILE__)
-            const auto h = gmem(F.f3 + c.addr);
-#else
-            const Fam3Out* h = F.f3 + c.addr;
-#endif
-            HL_SYNC();
-            best_cost = uni(S.f3b_cost);
-            best_single = uni(S.f3b[0]);
-            best_part = uni(S.f3b[1]);
-            best_fam = uni(S.f3b[2]);
-            best_dist = uni(S.f3b[3]);
-            for (int i = c.tid; i < 32; i += c.nthr) {
-                (&S.best_mv[0][0][0])[i] = (&S.f3best_mv[0][0][0])[i];
-                (&S.best_mvp[0][0][0])[i] = (&S.f3best_mvp[0][0][0])[i];
-            }
-            const int done = uni((int)h->done_mask), wm = uni((int)h->wmask), last = uni((int)h->e_last);
-#pragma unroll
-            for (int j = 3; j < 7; ++j)
-                if ((done >> (j - 3)) & 1)
-                    take_part(j, 3, uni((double)h->cost[j - 3]), uni((int)h->single[j - 3]), uni((int)h->dist[j - 3]), &h->bmv[j - 3][0][0][0],
-                              &h->bmvp[j - 3][0][0][0]);
-            HL_SYNC();
-            for (int i = c.tid; i < 16; i += c.nthr) S.tc[i] = ((wm >> i) & 1) ? h->tc[i] : S.f3entry[i];
-            for (int i = c.tid; i < 32; i += c.nthr) {
-                (&S.nb[0].mv[0][0][0])[i] = (&h->nbmv[0][0][0])[i];
-                (&S.bmv[0][0][0])[i] = (&h->bmv[last - 3][0][0][0])[i];
-                (&S.bmvp[0][0][0])[i] = (&h->bmvp[last - 3][0][0][0])[i];
-            }
-            for (int i = c.tid; i < 36; i += c.nthr) {
-                (&S.mvg[0][0])[i] = (&h->mvg[0][0])[i];
-                (&S.mvs[0][0])[i] = (&h->mvs[0][0])[i];
-            }
-            if (c.tid == 0) {
-                const PartDef& pd = kParts[last];
-                S.e_type = fam_etype(3);
-                S.nb[0].e_type = fam_etype(3);
-                S.nb[0].part_w = pd.part_w;
-                S.nb[0].part_h = pd.part_h;
-                for (int i = 0; i < 4; ++i) {
-                    S.nb[0].sub_w[i] = pd.sub_w;
-                    S.nb[0].sub_h[i] = pd.sub_h;
                 }
-            }
-            if (uni((int)h->fresh)) chain_write(c, uni((int)h->chain));
-            else {
-                c.chain = uni(S.f3b[4]);
-                c.fresh = uni(S.f3b[5]);
-                c.spec = uni(S.f3b[6]);
-            }
-            HL_SYNC();
+                return ok;
+            };
+            // the helper's partitioning from the entry state: the best so far,
+            // the live TotalCoeffs, rdo.Single_ctr and the partition state it leaves
+            auto f3_import = [&]() {
 #if defined(__HIP_DEVICE_COMPILE__)
-            if (c.tid == 0 && F.perr) atomicAdd(F.perr + 5, 1);
+                const auto h = gmem(F.f3 + hx);
 #else
-            if (F.perr) ++F.perr[5];
+                const Fam3Out* h = F.f3 + hx;
 #endif
-        };
-        bool imported = false;
-        if (HL_FAM3 && h3 != HS_MAIN && f3_ready()) {
-            f3_import();
-            imported = true;
-        }
-        for (int j = fam_first(fam); j < fam_first(fam + 1) && !imported; ++j) {
-            const PartDef& pd = kParts[j];
-            if (!((1 << (j + 1)) & mode_flags)) continue;
+                HL_SYNC();
+                best_cost = uni(S.f3b_cost);
+                best_single = uni(S.f3b[0]);
+                best_part = uni(S.f3b[1]);
+                best_fam = uni(S.f3b[2]);
+                best_dist = uni(S.f3b[3]);
+                for (int i = c.tid; i < 32; i += c.nthr) {
+                    (&S.best_mv[0][0][0])[i] = (&S.f3best_mv[0][0][0])[i];
+                    (&S.best_mvp[0][0][0])[i] = (&S.f3best_mvp[0][0][0])[i];
+                }
+                const int wm = uni((int)h->wmask);
+                take_part(j, 3, uni((double)h->cost[j - 3]), uni((int)h->single[j - 3]), uni((int)h->dist[j - 3]), &h->bmv[j - 3][0][0][0],
+                          &h->bmvp[j - 3][0][0][0]);
+                HL_SYNC();
+                for (int i = c.tid; i < 16; i += c.nthr) S.tc[i] = ((wm >> i) & 1) ? h->tc[i] : S.f3entry[i];
+                for (int i = c.tid; i < 32; i += c.nthr) {
+                    (&S.nb[0].mv[0][0][0])[i] = (&h->nbmv[0][0][0])[i];
+                    (&S.bmv[0][0][0])[i] = (&h->bmv[j - 3][0][0][0])[i];
+                    (&S.bmvp[0][0][0])[i] = (&h->bmvp[j - 3][0][0][0])[i];
+                }
+                for (int i = c.tid; i < 36; i += c.nthr) {
+                    (&S.mvg[0][0])[i] = (&h->mvg[0][0])[i];
+                    (&S.mvs[0][0])[i] = (&h->mvs[0][0])[i];
+                }
+                if (c.tid == 0) {
+                    const PartDef& pd = kParts[j];
+                    S.e_type = fam_etype(3);
+                    S.nb[0].e_type = fam_etype(3);
+                    S.nb[0].part_w = pd.part_w;
+                    S.nb[0].part_h = pd.part_h;
+                    for (int i = 0; i < 4; ++i) {
+                        S.nb[0].sub_w[i] = pd.sub_w;
+                        S.nb[0].sub_h[i] = pd.sub_h;
+                    }
+                }
+                if (uni((int)h->fresh)) chain_write(c, uni((int)h->chain));
+                else {
+                    c.chain = uni(S.f3b[4]);
+                    c.fresh = uni(S.f3b[5]);
+                    c.spec = uni(S.f3b[6]);
+                }
+                probably = false;  // (the probe is 16x16's; partitioning j was the last searched)
+                HL_SYNC();
+#if defined(__HIP_DEVICE_COMPILE__)
+                if (c.tid == 0 && F.perr) atomicAdd(F.perr + 5, 1);
+#else
+                if (F.perr) ++F.perr[5];
+#endif
+            };
+#if defined(__HIP_DEVICE_COMPILE__) && defined(HL_PROFILE)
+            if (HL_FAM3 && h3 == HS_CLAIMED && c.tid == 0 && F.prof) atomicAdd(F.prof + 61, 1ull);  // claimed, still running
+#endif
+            if (HL_FAM3 && h3 != HS_MAIN && f3_ready()) {
+                f3_import();
+                continue;
+            }
             if (F.early_term && j == 0) {
 #if !defined(HL_STEP_PROF) && !defined(HL_I4_PROF) && !defined(HL_NBLK_PROF)
                 HL_PROF_T(tet);
@@ -4164,10 +4176,9 @@ HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr)
             // (the helper runs its own instantiation, with the recording)
             if (HL_FAM3 && f3out) probably = search_family_part<true>(c, j, fam, cost_sum, single_sum, dist_sum, [] { return false; }, aborted);
             else probably = search_family_part<false>(c, j, fam, cost_sum, single_sum, dist_sum, [&] { return HL_FAM3 && h3 == HS_CLAIMED && f3_ready(); }, aborted);
-            if (HL_FAM3 && aborted) {  // the helper's family is ready and proven: taken instead
+            if (HL_FAM3 && aborted) {  // the helper's partitioning is ready and proven: taken instead
                 f3_import();
-                imported = true;
-                break;
+                continue;
             }
             if (HL_FAM3 && f3out) {  // the helper: this partitioning's results
                 HL_SYNC();
@@ -4181,7 +4192,6 @@ HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr)
                     o->single[j - 3] = single_sum;
                     o->dist[j - 3] = dist_sum;
                     S.f3b[0] |= 1 << (j - 3);
-                    S.f3b[1] = j;
                 }
                 for (int i = c.tid; i < 32; i += c.nthr)  // best MVs and MVPs, 16 words each
                     (i < 16 ? reinterpret_cast<int32_t*>(&o->bmv[j - 3][0][0][0]) : reinterpret_cast<int32_t*>(&o->bmvp[j - 3][0][0][0]))[i & 15] =
@@ -4196,7 +4206,6 @@ HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr)
             }
             take_part(j, fam, cost_sum, single_sum, dist_sum, &S.bmv[0][0][0], &S.bmvp[0][0][0]);
         }
-        if (imported) probably = false;  // (the probe is 16x16's)
         pskip = probably;
         if (pskip) {  // _is_zeros_inter16x16_chroma, rdo.c:2140-2215
             HL_SYNC();
@@ -4211,7 +4220,7 @@ HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr)
         }
         best_found = best_found || best_cost == 0.0 || pskip;
     }
-    if (HL_FAM3 && f3out) {  // the helper: the family's end state (the task publishes it with its release)
+    if (HL_FAM3 && f3out) {  // the helper: the partitioning's end state (the task publishes it with its release)
         HL_SYNC();
 #if defined(__HIP_DEVICE_COMPILE__)
         auto o = gmem(f3out);
@@ -4223,7 +4232,7 @@ HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr)
             o->wmask = S.f3w;
             o->chain = c.chain;
             o->fresh = c.fresh;
-            o->e_last = S.f3b[1];
+            o->e_last = hj;
         }
         for (int i = c.tid; i < 16; i += c.nthr) o->tc[i] = S.tc[i];
         for (int i = c.tid; i < 32; i += c.nthr) {
@@ -4237,6 +4246,12 @@ HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr)
         }
         return;
     }
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the helpers of partitionings the macroblock did not reach (a P_Skip or a
+    // zero cost ended the search, or early termination left them out): not
+    // started yet, they are cancelled (a running one writes only its own slot)
+    if (HL_FAM3 && F.hstate3 && c.tid < 4) atomicCAS(F.hstate3 + c.addr * 4 + c.tid, HS_FREE, HS_MAIN);
+#endif
     if (!pskip) {
         HL_PROF_T(ti);
         HL_PROF_T(tj);
@@ -4727,9 +4742,9 @@ HD void intra_helper(
 // One macroblock, start to end.  s_in = rdo.Single_ctr on entry (spec_in = 1
 // while it is a row-start speculation); (gx, gy) = reference region already
 // known complete (pipelined runs; see reach_wait).
-// f3out: the macroblock's 8x8-family helper task instead (guess_inter)
+// f3out: the macroblock's helper task of 8x8-family partitioning hj instead (guess_inter)
 HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, int s_in, int gx = 1 << 20, int gy = 1 << 20,
-               int spec_in = 1, Fam3Out* f3out = nullptr)
+               int spec_in = 1, Fam3Out* f3out = nullptr, int hj = 3)
 {
     Ctx c{F, S, tid, nthr, addr, addr % F.mbw, addr / F.mbw, (addr % F.mbw) * 16, (addr / F.mbw) * 16, s_in, 0, 0};
     c.gx = gx;
@@ -4759,7 +4774,7 @@ HD void encode_mb(const FrameArgs& F, Shared& S, int addr, int tid, int nthr, in
         if (g_emu_bad_guess3)  // tests: a wrong guess of the entry values, so that f3_verify must reject
             for (int i = 0; i < 16; ++i) S.tc[i] = (int8_t)((i * 5 + addr) % 11);
 #endif
-        if (HL_FAM3) guess_inter(c, f3out);
+        if (HL_FAM3) guess_inter(c, f3out, hj);
         return;
     }
     if (F.is_intra) guess_intra(c);

@@ -171,6 +171,8 @@ HD int task_succ(int f, int X, int Y, int mbw, int mbh, int R, int nframes, int 
 // A run holds nstreams independent streams of spp consecutive pictures each:
 // picture k of stream s is slot s * spp + k; task_deps / task_succ apply to
 // the pictures of one stream (k), offset by the stream's first slot.
+constexpr int kHelperQ = 16;  // helper FIFOs (PipeArgs::hq)
+
 struct PipeArgs {
     const PipeFrame* fr;
     int32_t nframes;  // slots: nstreams * spp
@@ -183,16 +185,20 @@ struct PipeArgs {
     int32_t* claim;  // [nframes][nmb] 1 once a workgroup holds the task
     int32_t* done;   // [nframes][nmb] 1 once the task finished (reach_wait polls it)
     int32_t* queue;  // [nframes][kSubQ][nmb] ready tasks, MB address + 1 (0 = slot not yet written)
-    // intra helper tasks (hl_mbcore.h intra_helper): a ready P macroblock also
-    // queues its helper, in one FIFO that workgroups take from only when no
-    // macroblock is ready (ramp and tail of a run, a lone picture)
+    // helper tasks (hl_mbcore.h intra_helper, guess_inter with f3out): a
+    // ready P macroblock also queues its helpers, in kHelperQ FIFOs that
+    // workgroups take from only when no macroblock is ready (ramp and tail of
+    // a run, a lone picture).  Helper kind k of task g = f * nmb + addr goes
+    // to FIFO (5 g + k) % kHelperQ: a bijection of [0, 5 nframes nmb), so no
+    // FIFO holds more than ceil(5 nframes nmb / kHelperQ) entries
     int32_t helpers; // 1 = queue them
-    int32_t* hstate; // [nframes][nmb] helper task states (HS_*)
-    int32_t* hstate3; // [nframes][nmb] 8x8-family helper task states
-    int32_t fam3;    // 1 = queue 8x8-family helpers too
-    int32_t* hq;     // [2 * nframes * nmb] FIFO of helper tasks, kind << 30 | (f * nmb + MB address + 1) (0 = slot not yet written)
-    int32_t* hq_head;
-    int32_t* hq_tail;
+    int32_t* hstate; // [nframes][nmb] intra helper task states (HS_*)
+    int32_t* hstate3; // [nframes][nmb][4] states of the 8x8 family's partitioning helpers (j = 3..6)
+    int32_t fam3;    // 1 = queue the partitioning helpers too
+    int32_t* hq;     // [kHelperQ][hq_cap] helper FIFOs, kind << 27 | (f * nmb + MB address + 1) (0 = slot not yet written)
+    int32_t hq_cap;
+    int32_t* hq_head;  // [kHelperQ]
+    int32_t* hq_tail;  // [kHelperQ]
     int32_t* head;   // [nframes][kSubQ] next queue slot to pop
     int32_t* tail;   // [nframes][kSubQ] next queue slot to push
     int32_t* oldest; // [nstreams] first unfinished picture of each stream

@@ -332,7 +332,7 @@ extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, co
     // intra_helper) runs first, on its own workgroup image, as a pipelined
     // run's helper task would; the macroblock then uses its results
     // (2: the helpers guess the live TotalCoeffs wrongly; emu_set_helper)
-    // (4: every P macroblock's 8x8-family helper, fam3_helper, likewise;
+    // (4: every P macroblock's 8x8-family partitioning helpers likewise;
     // 8: with a wrong guess of the entry values)
     const int helper = e->helper_mode;
 #if !defined(__HIP_DEVICE_COMPILE__)
@@ -350,8 +350,8 @@ extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, co
         F.hstate = e->hstate.data();
     }
     if ((helper & 12) && !intra) {
-        e->f3.resize(e->nmb);
-        e->hstate3.assign(e->nmb, HS_DONE);
+        e->f3.resize(4 * e->nmb);
+        e->hstate3.assign(4 * e->nmb, HS_DONE);
         F.f3 = e->f3.data();
         F.hstate3 = e->hstate3.data();
     }
@@ -376,10 +376,11 @@ extern "C" long emu_encode_frame(void* h, const uint8_t* y, const uint8_t* u, co
             intra_helper(F, *e->S2, a, 0, 1, chain, F.ispec + a);
             ++e->helper_runs;
         }
-        if (F.hstate3) {
-            encode_mb(F, *e->S2, a, 0, 1, chain, 1 << 20, 1 << 20, 1, F.f3 + a);  // as the 8x8-family helper task
-            ++e->helper3_runs;
-        }
+        if (F.hstate3)
+            for (int j = 3; j < 7; ++j) {  // as the helper tasks of the 8x8 family's partitionings
+                encode_mb(F, *e->S2, a, 0, 1, chain, 1 << 20, 1 << 20, 1, F.f3 + 4 * a + j - 3, j);
+                ++e->helper3_runs;
+            }
         encode_mb(F, *e->S, a, 0, 1, chain);
         chain = e->chain[a].s_out;
     }

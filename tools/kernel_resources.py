@@ -15,13 +15,25 @@ KEYS = (".vgpr_count", ".vgpr_spill_count", ".sgpr_count", ".sgpr_spill_count", 
         ".private_segment_fixed_size")
 
 
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
 def resources(lib):
+    """Every code object of the library's .hip_fatbin (one bundle per HIP
+    translation unit: hl_encoder.hip and hl_encoder_fam3.hip)."""
+    notes = ""
     with tempfile.TemporaryDirectory() as td:
-        fat, co = os.path.join(td, "fat.bin"), os.path.join(td, "co.elf")
+        fat = os.path.join(td, "fat.bin")
         subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", lib], check=True, capture_output=True)
-        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
-                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True, capture_output=True)
-        notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True, capture_output=True, text=True).stdout
+        data = open(fat, "rb").read()
+        starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)]
+        for k, a in enumerate(starts):
+            b = starts[k + 1] if k + 1 < len(starts) else len(data)
+            part, co = os.path.join(td, f"b{k}.bin"), os.path.join(td, f"co{k}.elf")
+            open(part, "wb").write(data[a:b])
+            subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={part}",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True, capture_output=True)
+            notes += subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True, capture_output=True, text=True).stdout
     # one YAML list item per kernel: keys before and after .name belong to it
     out, item = {}, {}
     def flush():
