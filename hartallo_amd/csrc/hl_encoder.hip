@@ -312,7 +312,7 @@ __global__ __launch_bounds__(256) void k_pipe_init(PipeArgs P, int mbw, int mbh)
         for (int q = 0; q < kSubQ; ++q) P.queue[(f * kSubQ + q) * nmb + a] = k == 0 && a == 0 && q == 0 ? 1 : 0;  // every stream's first task
         P.claim[i] = 0;
         P.hstate[i] = HS_FREE;
-        for (int j = 0; j < 4; ++j) P.hstate3[4 * i + j] = HS_FREE;
+        for (int j = 0; j < 4; ++j) P.hstate3[4 * i + j] = HS_MAIN;  // (HS_FREE once queued)
         for (int j = 0; j < 5; ++j) P.hq[j * P.nframes * nmb + i] = 0;
     }
     if (i < kHelperQ) P.hq[5 * P.nframes * nmb + i] = 0;  // (kHelperQ * hq_cap < 5 nframes nmb + kHelperQ; the grid has >= 256 threads)
@@ -465,7 +465,8 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc, 
             // another workgroup took it: retry, except beside a lone picture
             // (the 8x8 family's helpers on), where ~200 idle workgroups race for
             // each ready macroblock and the losers take a helper task instead
-            if (!P.fam3) continue;
+            // (in runs, measured: no gain, profiles/r06_ab_partitioning_helpers_in_runs.log)
+            if (!P.fam3 || P.nframes > 1) continue;
         }
         if (P.helpers) {  // no macroblock ready: a helper task, unless its macroblock took it over
             // lane q reads FIFO q; the workgroup's own FIFO first, then the
@@ -730,6 +731,7 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
                 task_succ(fk, x, y, mbw, mbh, P.reach, P.spp, j, fo, xo, yo);
                 if (phase != 2 && (fo == fk) != (phase == 0)) continue;
                 const bool hlp = P.helpers && !(fo == fk ? sF.is_intra : ld_relaxed(&P.fr[fo + fb].F.is_intra));
+                const bool h3 = hlp && P.fam3 && (fo < P.f3_first || fo >= P.spp - P.f3_last);
                 fo += fb;
                 const int a = yo * mbw + xo;
                 // the release half is the fence before release(); the acquire
@@ -740,7 +742,14 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
                 const int qf = fo * kSubQ + a % kSubQ;
                 const int pos = __hip_atomic_fetch_add(P.tail + qf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 // helper kinds: 0 = intra, 1..4 = the 8x8 family's partitioning kind + 2
-                const int g = fo * nmb + a, nk = hlp ? 1 + 4 * P.fam3 : 0;
+                const int g = fo * nmb + a, nk = hlp ? (h3 ? 5 : 1) : 0;
+                if (h3) {  // the partitioning helpers' states, before the macroblock's push (its pop reads them)
+                    int32_t* st = P.hstate3 + 4 * g;
+                    st_relaxed(st, HS_FREE);
+                    st_relaxed(st + 1, HS_FREE);
+                    st_relaxed(st + 2, HS_FREE);
+                    st_relaxed(st + 3, HS_FREE);
+                }
                 int hq[5], hp[5];
 #pragma unroll
                 for (int k = 0; k < 5; ++k) {
@@ -1086,7 +1095,7 @@ extern "C" int32_t hl_amd_encoder_create(const hl_amd_params_t* p, hl_amd_encode
         const char* h = getenv("HL_AMD_HELPERS");  // A/B knob (hl_amd_set_intra_helpers)
         e->helpers = !(h && atoi(h) == 0);
         const char* h3 = getenv("HL_AMD_FAM3");  // A/B knob
-        e->fam3 = h3 ? atoi(h3) : 1;  // 0 off, 1 lone pictures, 2 every run of one stream
+        e->fam3 = h3 ? atoi(h3) : 1;  // 0 off, 1 lone pictures, 2 runs of one stream too (their first / last pictures, HL_AMD_F3_EDGE)
     }
     e->reach = 2;
     e->window = 64;
@@ -1378,7 +1387,7 @@ static hipError_t ensure_sched(hl_amd_encoder_t* e, int slots)
         (r = hipMalloc(&e->d_queue, sizeof(int32_t) * ((kSubQ + 5) * nmb * slots + kHelperQ))) ||
         (r = hipMalloc(&e->d_head, sizeof(int32_t) * (2 * kSubQ * slots + kMaxStreams + 2 * kHelperQ))) ||
         (r = hipMalloc(&e->d_hstate, sizeof(int32_t) * 5 * nmb * slots)) ||
-        (r = hipMalloc(&e->d_f3, sizeof(Fam3Out) * 4 * nmb * (e->fam3 == 2 ? slots : 1))))
+        (r = hipMalloc(&e->d_f3, sizeof(Fam3Out) * 4 * nmb * (e->fam3 >= 2 ? slots : 1))))
         return r;
     if (!e->d_err && (r = hipMalloc(&e->d_err, sizeof(int32_t) * 8))) return r;
     e->scap = slots;
@@ -1510,7 +1519,7 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
     const int slots = S * m;
     // a lone picture runs the kernel built with the 8x8-family helper tasks
     // (hl_encoder_fam3.hip): most workgroups would idle beside its wavefront
-    const bool fam3 = e0->helpers && (slots == 1 ? e0->fam3 != 0 : S == 1 && e0->fam3 == 2);
+    const bool fam3 = e0->helpers && (slots == 1 ? e0->fam3 != 0 : S == 1 && e0->fam3 >= 2);
     for (int si = 0; si < S; ++si) {
         hl_amd_encoder_t* e = es[si];
         if (e->rc && (m != 1 || S != 1)) return HL_AMD_ERROR_INVALID_STATE;
@@ -1599,7 +1608,7 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
                 if (fam3) {
                     // per MB address and partitioning; per picture too in runs
                     // (a helper may still run after its macroblock ended)
-                    F.f3 = e0->d_f3 + (e0->fam3 == 2 ? (size_t)4 * nmb * slot : 0);
+                    F.f3 = e0->d_f3 + (e0->fam3 >= 2 ? (size_t)4 * nmb * slot : 0);
                     F.hstate3 = e0->d_hstate + (size_t)nmb * slots + (size_t)4 * nmb * slot;
                 }
             }
@@ -1637,6 +1646,13 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
     P.hstate3 = e0->d_hstate + (size_t)nmb * slots;
     P.helpers = e0->helpers ? 1 : 0;
     P.fam3 = fam3 ? 1 : 0;
+    {  // the pictures of a run whose macroblocks get partitioning helpers (every picture of a lone one)
+        static const char* fe = getenv("HL_AMD_F3_EDGE");  // A/B knob: "first,last" (default 1,2)
+        int a = 1, b = 2;
+        if (fe) sscanf(fe, "%d,%d", &a, &b);
+        P.f3_first = m == 1 ? 1 : a;
+        P.f3_last = m == 1 ? 1 : b;
+    }
     P.hq = e0->d_queue + kSubQ * nmb * slots;
     P.head = e0->d_head;
     P.tail = e0->d_head + kSubQ * slots;

@@ -326,10 +326,10 @@ struct Shared {
     int32_t hs3_x;               // 8x8-family helper state seen by the MB
     int32_t f3lo[32], f3hi[32];  // fam3_helper: entry-value intervals being recorded (see Fam3Out)
     int32_t f3w;                 // fam3_helper: blocks whose live TotalCoeff the family wrote so far
-    int8_t f3entry[16];          // the MB's live TotalCoeffs entering the family
-    int16_t f3best_mv[4][4][2], f3best_mvp[4][4][2];  // best_mv / best_mvp entering the family
-    double f3b_cost;             // the best so far entering the family, and rdo.Single_ctr (LDS: nothing
-    int32_t f3b[8];              // extra stays live in registers across the family's searches)
+    int8_t f3pad0[16];
+    int16_t f3pad1[64];          // (unused: they keep the later fields' LDS offsets, which the register allocation follows)
+    double f3pad2;
+    int32_t f3b[8];              // the partitioning helper: [0] partitionings searched (mode_flags)
     int32_t homo[4];             // early termination: homogeneity of the four 8x8 source quadrants
     int32_t predc[2][64];
     int32_t cres_dc[2][4], cres_cac[2][4], cres_cdc[2][4], cres_tc[2][4], cres_sctr[2][4];
@@ -3886,15 +3886,12 @@ HD int32_t fam_etype(int f) { return f < 3 ? ET_P16x16 + f : ET_P8x8REF0; }
 
 // One partitioning j of family fam searched (rdo.c:731-760): the partition
 // mode's best cost (header bits not added), its Single_ctr sum and
-// distortion; returns the P_Skip probe's outcome (16x16 only).  abort() is
-// asked before every partition search; when it says so the search stops
-// (aborted = true) and the results are meaningless.
-template <bool REC, typename A>
-HD bool search_family_part(Ctx& c, int j, int fam, double& cost_sum, int& single_sum, int& dist_sum, A abort, bool& aborted)
+// distortion; returns the P_Skip probe's outcome (16x16 only).
+template <bool REC>
+HD bool search_family_part(Ctx& c, int j, int fam, double& cost_sum, int& single_sum, int& dist_sum)
 {
     Shared& S = c.S;
     const PartDef& pd = kParts[j];
-    aborted = false;
     HL_SYNC();
     if (c.tid == 0) {
         S.e_type = fam_etype(fam);
@@ -3911,10 +3908,6 @@ HD bool search_family_part(Ctx& c, int j, int fam, double& cost_sum, int& single
     bool prob = false;
     for (int pi = 0; pi < pd.num_part; ++pi)
         for (int spi = 0; spi < pd.num_sub; ++spi) {
-            if (abort()) {
-                aborted = true;
-                return false;
-            }
             const bool p = search_partition<REC>(c, pd, pi, spi, j == 0 && pi == 0 && spi == 0);
             if (j == 0 && pi == 0 && spi == 0) prob = p;
         }
@@ -3943,16 +3936,16 @@ HD bool search_family_part(Ctx& c, int j, int fam, double& cost_sum, int& single
 // the macroblock's 8x8-family latency is that of its longest partitioning
 // (4x4, 16 searches), not of the family's 36 searches in a row.
 // --------------------------------------------------------------------------
-// The macroblock's real entry values (S.f3entry) against the helper's intervals
+// The macroblock's real entry values e (its live TotalCoeffs) against the helper's intervals
 template <typename P>
-HD bool f3_verify(const Shared& S, P h)
+HD bool f3_verify(const int8_t* e, P h)
 {
     bool ok = true;
     for (int i = 0; i < 16; ++i) {
-        const int v = S.f3entry[i];
+        const int v = e[i];
         ok = ok && v >= h->lo[i] && v <= h->hi[i];
         if (blk_x(i) > 0 && blk_y(i) > 0) {
-            const int sm = S.f3entry[blk_idx(blk_x(i) - 4, blk_y(i))] + S.f3entry[blk_idx(blk_x(i), blk_y(i) - 4)];
+            const int sm = e[blk_idx(blk_x(i) - 4, blk_y(i))] + e[blk_idx(blk_x(i), blk_y(i) - 4)];
             ok = ok && sm >= h->lo[16 + i] && sm <= h->hi[16 + i];
         }
     }
@@ -3974,6 +3967,13 @@ HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr, int hj = 3)
     bool probably = false;
     int mode_flags = 0xFFFF;  // rdo.c:874
     if (c.tid == 0) S.flags = FL_INTER;
+    // were this macroblock's partitioning helpers queued?  (HS_MAIN: no;
+    // read at the start, used at the 8x8 family)
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (HL_FAM3 && F.hstate3 && !f3out && c.tid == 0) S.f3b[1] = ld_relaxed(F.hstate3 + c.addr * 4) != HS_MAIN;
+#else
+    if (HL_FAM3 && F.hstate3 && !f3out && c.tid == 0) S.f3b[1] = F.hstate3[c.addr * 4] != HS_MAIN;
+#endif
     // a partitioning's results against the best so far (rdo.c:1148-1160)
     auto take_part = [&](int j, int fam, double cost_sum, int single_sum, int dist_sum, auto bmv, auto bmvp) {
         const PartDef& pd = kParts[j];
@@ -4018,147 +4018,92 @@ HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr, int hj = 3)
         for (int j = jlo; j < jhi; ++j) {
             if (!((1 << (j + 1)) & mode_flags)) continue;
             // partitioning j's helper (8x8 family): taken over if no workgroup
-            // claimed it, else polled between partition searches
-            int h3 = HS_MAIN;
-            const int hx = c.addr * 4 + (j - 3);  // its state and results
-            if (HL_FAM3 && fam == 3 && F.hstate3 && !f3out) {
+            // claimed it yet, else waited for (it waits on nothing) and taken
+            // if its intervals hold for the real entry state (the live
+            // TotalCoeffs partitioning j - 1 left)
+            if (HL_FAM3 && fam == 3 && F.hstate3 && !f3out && uni(S.f3b[1])) {
+                const int hx = c.addr * 4 + (j - 3);  // its state and results
 #if defined(__HIP_DEVICE_COMPILE__)
-                if (c.tid == 0) S.hs3_x = atomicCAS(F.hstate3 + hx, HS_FREE, HS_MAIN);
-                HL_SYNC();
-                h3 = uni(S.hs3_x);
-#else
-                h3 = F.hstate3[hx] == HS_FREE ? HS_MAIN : F.hstate3[hx];
-                if (h3 == HS_MAIN) F.hstate3[hx] = HS_MAIN;
+                if (c.tid == 0) {
+                    const int st = atomicCAS(F.hstate3 + hx, HS_FREE, HS_MAIN);
+#if defined(HL_PROFILE)
+                    if (F.prof) atomicAdd(F.prof + (st == HS_FREE ? 60 : (st == HS_CLAIMED ? 61 : 62)), 1ull);  // taken over / still running / done
 #endif
-                if (h3 == HS_FREE) {
-                    h3 = HS_MAIN;
-#if defined(__HIP_DEVICE_COMPILE__) && defined(HL_PROFILE)
-                    if (c.tid == 0 && F.prof) atomicAdd(F.prof + 60, 1ull);  // not claimed in time: taken over
-#endif
+                    S.f3b[4 + j - 3] = st == HS_FREE ? HS_MAIN : st;
                 }
-                if (h3 != HS_MAIN) {  // the state partitioning j starts from, and the best so far
-                    for (int i = c.tid; i < 16; i += c.nthr) S.f3entry[i] = S.tc[i];
-                    for (int i = c.tid; i < 32; i += c.nthr) {
-                        (&S.f3best_mv[0][0][0])[i] = (&S.best_mv[0][0][0])[i];
-                        (&S.f3best_mvp[0][0][0])[i] = (&S.best_mvp[0][0][0])[i];
-                    }
-                    if (c.tid == 0) {
-                        S.f3b_cost = best_cost;
-                        S.f3b[0] = best_single;
-                        S.f3b[1] = best_part;
-                        S.f3b[2] = best_fam;
-                        S.f3b[3] = best_dist;
-                        S.f3b[4] = c.chain;
-                        S.f3b[5] = c.fresh;
-                        S.f3b[6] = c.spec;
-                    }
-                    HL_SYNC();
-                }
-            }
-            // a claimed helper: has it finished?  (the first check at once, then
-            // between partition searches)
-            auto h3_done = [&]() -> bool {
-                if (h3 != HS_CLAIMED) return h3 == HS_DONE;
-#if defined(__HIP_DEVICE_COMPILE__)
-                if (c.tid == 0) S.hs3_x = ld_relaxed(F.hstate3 + hx);
-                HL_SYNC();
-                if (uni(S.hs3_x) == HS_DONE) h3 = HS_DONE;
-#else
-                if (F.hstate3[hx] == HS_DONE) h3 = HS_DONE;
-#endif
-                return h3 == HS_DONE;
-            };
-            // the helper finished, and its partitioning is proven for this MB's
-            // entry state?  (asked at the partitioning's start and before each
-            // partition search while the helper runs; a helper found unproven is
-            // not asked again)
-            auto f3_ready = [&]() -> bool {
-                if (h3 == HS_MAIN) return false;
-                if (!h3_done()) return false;
-#if defined(__HIP_DEVICE_COMPILE__)
                 if (c.tid < 64) {
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
                 HL_SYNC();
-                const auto hv = gmem(F.f3 + hx);
-                const bool ok = ((uni((int)hv->done_mask) >> (j - 3)) & 1) && f3_verify(S, hv);
 #else
-                const bool ok = ((F.f3[hx].done_mask >> (j - 3)) & 1) && f3_verify(S, F.f3 + hx);
+                if (c.tid == 0) S.f3b[4 + j - 3] = F.hstate3[hx] == HS_FREE ? HS_MAIN : F.hstate3[hx];
 #endif
-                if (!ok) {
-                    h3 = HS_MAIN;  // (decided once)
+                int h3 = uni(S.f3b[4 + j - 3]);
+#if defined(__HIP_DEVICE_COMPILE__)
+                if (h3 == HS_CLAIMED) {
+                    if (c.tid < 64) {
+                        if (c.tid == 0) {
+                            spin_ge(F.hstate3 + hx, HS_DONE, F.perr);
+                            S.f3b[4 + j - 3] = ld_relaxed(F.hstate3 + hx) == HS_DONE ? HS_DONE : HS_MAIN;  // (a wait that gave up: searched here)
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
+                    HL_SYNC();
+                    h3 = uni(S.f3b[4 + j - 3]);
+                }
+                const auto h = gmem(F.f3 + hx);
+#else
+                const Fam3Out* h = F.f3 + hx;
+#endif
+                if (h3 == HS_DONE) {
+                    if (((uni((int)h->done_mask) >> (j - 3)) & 1) && f3_verify(S.tc, h)) {
+                        // the helper's partitioning from the entry state: its
+                        // results against the best so far, the live TotalCoeffs
+                        // it wrote, rdo.Single_ctr, the partition state it leaves
+                        const int wm = uni((int)h->wmask);
+                        take_part(j, 3, uni((double)h->cost[j - 3]), uni((int)h->single[j - 3]), uni((int)h->dist[j - 3]), &h->bmv[j - 3][0][0][0],
+                                  &h->bmvp[j - 3][0][0][0]);
+                        HL_SYNC();
+                        for (int i = c.tid; i < 16; i += c.nthr)
+                            if ((wm >> i) & 1) S.tc[i] = h->tc[i];
+                        for (int i = c.tid; i < 32; i += c.nthr) {
+                            (&S.nb[0].mv[0][0][0])[i] = (&h->nbmv[0][0][0])[i];
+                            (&S.bmv[0][0][0])[i] = (&h->bmv[j - 3][0][0][0])[i];
+                            (&S.bmvp[0][0][0])[i] = (&h->bmvp[j - 3][0][0][0])[i];
+                        }
+                        for (int i = c.tid; i < 36; i += c.nthr) {
+                            (&S.mvg[0][0])[i] = (&h->mvg[0][0])[i];
+                            (&S.mvs[0][0])[i] = (&h->mvs[0][0])[i];
+                        }
+                        if (c.tid == 0) {
+                            const PartDef& pd = kParts[j];
+                            S.e_type = fam_etype(3);
+                            S.nb[0].e_type = fam_etype(3);
+                            S.nb[0].part_w = pd.part_w;
+                            S.nb[0].part_h = pd.part_h;
+                            for (int i = 0; i < 4; ++i) {
+                                S.nb[0].sub_w[i] = pd.sub_w;
+                                S.nb[0].sub_h[i] = pd.sub_h;
+                            }
+                        }
+                        if (uni((int)h->fresh)) chain_write(c, uni((int)h->chain));
+                        probably = false;  // (the probe is 16x16's; partitioning j was the last searched)
+                        HL_SYNC();
+#if defined(__HIP_DEVICE_COMPILE__)
+                        if (c.tid == 0 && F.perr) atomicAdd(F.perr + 5, 1);
+#else
+                        if (F.perr) ++F.perr[5];
+#endif
+                        continue;
+                    }
 #if defined(__HIP_DEVICE_COMPILE__)
                     if (c.tid == 0 && F.perr) atomicAdd(F.perr + 6, 1);
 #else
                     if (F.perr) ++F.perr[6];
 #endif
                 }
-                return ok;
-            };
-            // the helper's partitioning from the entry state: the best so far,
-            // the live TotalCoeffs, rdo.Single_ctr and the partition state it leaves
-            auto f3_import = [&]() {
-#if defined(__HIP_DEVICE_COMPILE__)
-                const auto h = gmem(F.f3 + hx);
-#else
-                const Fam3Out* h = F.f3 + hx;
-#endif
-                HL_SYNC();
-                best_cost = uni(S.f3b_cost);
-                best_single = uni(S.f3b[0]);
-                best_part = uni(S.f3b[1]);
-                best_fam = uni(S.f3b[2]);
-                best_dist = uni(S.f3b[3]);
-                for (int i = c.tid; i < 32; i += c.nthr) {
-                    (&S.best_mv[0][0][0])[i] = (&S.f3best_mv[0][0][0])[i];
-                    (&S.best_mvp[0][0][0])[i] = (&S.f3best_mvp[0][0][0])[i];
-                }
-                const int wm = uni((int)h->wmask);
-                take_part(j, 3, uni((double)h->cost[j - 3]), uni((int)h->single[j - 3]), uni((int)h->dist[j - 3]), &h->bmv[j - 3][0][0][0],
-                          &h->bmvp[j - 3][0][0][0]);
-                HL_SYNC();
-                for (int i = c.tid; i < 16; i += c.nthr) S.tc[i] = ((wm >> i) & 1) ? h->tc[i] : S.f3entry[i];
-                for (int i = c.tid; i < 32; i += c.nthr) {
-                    (&S.nb[0].mv[0][0][0])[i] = (&h->nbmv[0][0][0])[i];
-                    (&S.bmv[0][0][0])[i] = (&h->bmv[j - 3][0][0][0])[i];
-                    (&S.bmvp[0][0][0])[i] = (&h->bmvp[j - 3][0][0][0])[i];
-                }
-                for (int i = c.tid; i < 36; i += c.nthr) {
-                    (&S.mvg[0][0])[i] = (&h->mvg[0][0])[i];
-                    (&S.mvs[0][0])[i] = (&h->mvs[0][0])[i];
-                }
-                if (c.tid == 0) {
-                    const PartDef& pd = kParts[j];
-                    S.e_type = fam_etype(3);
-                    S.nb[0].e_type = fam_etype(3);
-                    S.nb[0].part_w = pd.part_w;
-                    S.nb[0].part_h = pd.part_h;
-                    for (int i = 0; i < 4; ++i) {
-                        S.nb[0].sub_w[i] = pd.sub_w;
-                        S.nb[0].sub_h[i] = pd.sub_h;
-                    }
-                }
-                if (uni((int)h->fresh)) chain_write(c, uni((int)h->chain));
-                else {
-                    c.chain = uni(S.f3b[4]);
-                    c.fresh = uni(S.f3b[5]);
-                    c.spec = uni(S.f3b[6]);
-                }
-                probably = false;  // (the probe is 16x16's; partitioning j was the last searched)
-                HL_SYNC();
-#if defined(__HIP_DEVICE_COMPILE__)
-                if (c.tid == 0 && F.perr) atomicAdd(F.perr + 5, 1);
-#else
-                if (F.perr) ++F.perr[5];
-#endif
-            };
-#if defined(__HIP_DEVICE_COMPILE__) && defined(HL_PROFILE)
-            if (HL_FAM3 && h3 == HS_CLAIMED && c.tid == 0 && F.prof) atomicAdd(F.prof + 61, 1ull);  // claimed, still running
-#endif
-            if (HL_FAM3 && h3 != HS_MAIN && f3_ready()) {
-                f3_import();
-                continue;
             }
             if (F.early_term && j == 0) {
 #if !defined(HL_STEP_PROF) && !defined(HL_I4_PROF) && !defined(HL_NBLK_PROF)
@@ -4171,15 +4116,10 @@ HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr, int hj = 3)
             }
             double cost_sum = 0.0;
             int single_sum = 0, dist_sum = 0;
-            bool aborted = false;
             // (one call site: every copy of the search is inlined)
             // (the helper runs its own instantiation, with the recording)
-            if (HL_FAM3 && f3out) probably = search_family_part<true>(c, j, fam, cost_sum, single_sum, dist_sum, [] { return false; }, aborted);
-            else probably = search_family_part<false>(c, j, fam, cost_sum, single_sum, dist_sum, [&] { return HL_FAM3 && h3 == HS_CLAIMED && f3_ready(); }, aborted);
-            if (HL_FAM3 && aborted) {  // the helper's partitioning is ready and proven: taken instead
-                f3_import();
-                continue;
-            }
+            if (HL_FAM3 && f3out) probably = search_family_part<true>(c, j, fam, cost_sum, single_sum, dist_sum);
+            else probably = search_family_part<false>(c, j, fam, cost_sum, single_sum, dist_sum);
             if (HL_FAM3 && f3out) {  // the helper: this partitioning's results
                 HL_SYNC();
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -4250,7 +4190,7 @@ HD void guess_inter(Ctx& c, Fam3Out* f3out = nullptr, int hj = 3)
     // the helpers of partitionings the macroblock did not reach (a P_Skip or a
     // zero cost ended the search, or early termination left them out): not
     // started yet, they are cancelled (a running one writes only its own slot)
-    if (HL_FAM3 && F.hstate3 && c.tid < 4) atomicCAS(F.hstate3 + c.addr * 4 + c.tid, HS_FREE, HS_MAIN);
+    if (HL_FAM3 && F.hstate3 && c.tid < 4 && S.f3b[1]) atomicCAS(F.hstate3 + c.addr * 4 + c.tid, HS_FREE, HS_MAIN);
 #endif
     if (!pskip) {
         HL_PROF_T(ti);

@@ -193,8 +193,11 @@ struct PipeArgs {
     // FIFO holds more than ceil(5 nframes nmb / kHelperQ) entries
     int32_t helpers; // 1 = queue them
     int32_t* hstate; // [nframes][nmb] intra helper task states (HS_*)
-    int32_t* hstate3; // [nframes][nmb][4] states of the 8x8 family's partitioning helpers (j = 3..6)
-    int32_t fam3;    // 1 = queue the partitioning helpers too
+    int32_t* hstate3; // [nframes][nmb][4] states of the 8x8 family's partitioning helpers (j = 3..6); HS_MAIN
+                      // unless they were queued
+    int32_t fam3;    // 1 = queue the partitioning helpers too, for pictures k < f3_first or k >= spp - f3_last of each
+                     // stream (the ramp and tail of a run; every picture of a lone one)
+    int32_t f3_first, f3_last;
     int32_t* hq;     // [kHelperQ][hq_cap] helper FIFOs, kind << 27 | (f * nmb + MB address + 1) (0 = slot not yet written)
     int32_t hq_cap;
     int32_t* hq_head;  // [kHelperQ]
