@@ -76,7 +76,8 @@ def main():
             print(f"   helper tasks {hn} ({hn / max(1, n * nmb):.2f} per MB), {hlp / hn / 1e3:.1f} kcycles each")
         if cnt[59]:
             print(f"   of which 8x8-family partitioning helpers {cnt[59]}, {cnt[58] / cnt[59] / 1e3:.1f} kcycles each; "
-                  f"partitionings the MB found unclaimed {cnt[60]}, claimed and still running {cnt[61]}")
+                  f"partitionings the MB found unclaimed {cnt[60]}, still running {cnt[61]} (waited {cnt[63] / max(1, n * nmb) / 1e3:.1f} "
+                  f"kcycles/MB), done {cnt[62]}")
         print(f"   after the filters: barrier {cnt[50] / max(1, tasks) / 1e3:.1f}, release fence {cnt[51] / max(1, tasks) / 1e3:.1f}, "
               f"successors {cnt[52] / max(1, tasks) / 1e3:.1f} kcycles/task; early release block (in the filters) {cnt[53] / max(1, tasks) / 1e3:.1f} "
               f"(fence {cnt[54] / max(1, tasks) / 1e3:.1f}, release {cnt[55] / max(1, tasks) / 1e3:.1f}, spin {cnt[56] / max(1, tasks) / 1e3:.1f}, "
