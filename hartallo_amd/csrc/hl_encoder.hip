@@ -1647,7 +1647,7 @@ static int32_t encode_group(hl_amd_encoder_t* const* es, int S, int m, const uin
     P.helpers = e0->helpers ? 1 : 0;
     P.fam3 = fam3 ? 1 : 0;
     {  // the pictures of a run whose macroblocks get partitioning helpers (every picture of a lone one)
-        static const char* fe = getenv("HL_AMD_F3_EDGE");  // A/B knob: "first,last" (default 1,2)
+        const char* fe = getenv("HL_AMD_F3_EDGE");  // A/B knob: "first,last" (default 1,2)
         int a = 1, b = 2;
         if (fe) sscanf(fe, "%d,%d", &a, &b);
         P.f3_first = m == 1 ? 1 : a;

@@ -115,12 +115,25 @@ def test_bench_stream_per_picture(gpu):
     torch.cuda.synchronize()
     enc = Encoder(w, h, g["qp"], g["me_range"], g["deblock"], g["gop"])
     outs, recons = [], []
-    for p in _ptrs(dev, w, h):
+    for i, p in enumerate(_ptrs(dev, w, h)):
         outs.append(enc.encode_device(*p).annexb())
         _check_clean_runs(enc, 1)  # one persistent launch per picture
         recons.append(np.concatenate(enc.recon()))
+        if i > 0:  # a lone P picture runs its macroblocks' helper tasks
+            hs = enc.last_helper_stats()
+            assert hs["i4_kept"] > 0 and hs["fam3_kept"] > 0, hs
     enc.close()
     _check("bench_1088p_s11", 0, outs, recons)
+
+
+def test_bench_stream_partitioning_helpers_in_runs(gpu, monkeypatch):
+    # the partitioning helpers in a run of one stream (HL_AMD_FAM3=2, read
+    # when the encoder opens), for every picture and for the run's edges only
+    for edge in ("99,99", "1,2"):
+        monkeypatch.setenv("HL_AMD_FAM3", "2")
+        monkeypatch.setenv("HL_AMD_F3_EDGE", edge)
+        outs, recons = _batch("bench_1088p_s11", [3, 8])
+        _check("bench_1088p_s11", 0, outs, recons)
 
 
 def test_config2_720p_pipelined(gpu):
