@@ -32,6 +32,8 @@ EXPORTED_SYMBOLS = (
     "hl_amd_encoder_create",
     "hl_amd_encoder_destroy",
     "hl_amd_encode",
+    "hl_amd_set_lookahead",
+    "hl_amd_flush",
     "hl_amd_encode_device",
     "hl_amd_encode_batch",
     "hl_amd_encode_streams",
@@ -172,7 +174,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hl_amd_last_batch_stats.argtypes = [vp, ctypes.POINTER(i32)]
     lib.hl_amd_last_batch_stats.restype = i32
     for name, args in (("hl_amd_set_intra_helpers", [vp, i32]), ("hl_amd_last_helper_stats", [vp, ctypes.POINTER(i32)]),
-                       ("hl_amd_last_fam3_stats", [vp, ctypes.POINTER(i32)])):
+                       ("hl_amd_last_fam3_stats", [vp, ctypes.POINTER(i32)]), ("hl_amd_set_lookahead", [vp, i32]),
+                       ("hl_amd_flush", [vp, ctypes.POINTER(_Result)])):
         if hasattr(lib, name):  # (absent from builds before round 4 loaded through HL_LIB)
             getattr(lib, name).argtypes = args
             getattr(lib, name).restype = i32
@@ -267,6 +270,24 @@ class Encoder:
         rc = self.lib.hl_amd_encode(self._h, ys[0].ctypes.data, ys[1].ctypes.data, ys[2].ctypes.data, ctypes.byref(r))
         if rc != HL_AMD_SUCCESS:
             raise HlAmdError(rc, "hl_amd_encode")
+        return self._result(r)
+
+    def set_lookahead(self, frames: int) -> None:
+        """Look-ahead for per-frame callers (hl_amd_set_lookahead): encode()
+        queues frames and codes them `frames` at a time; each call returns the
+        next coded result in order (type 0 while the queue fills), flush()
+        the rest."""
+        rc = self.lib.hl_amd_set_lookahead(self._h, frames)
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_set_lookahead")
+
+    def flush(self) -> EncodeResult:
+        """Codes what the look-ahead still queues and returns the next
+        result (type 0 once none is left)."""
+        r = _Result()
+        rc = self.lib.hl_amd_flush(self._h, ctypes.byref(r))
+        if rc != HL_AMD_SUCCESS:
+            raise HlAmdError(rc, "hl_amd_flush")
         return self._result(r)
 
     def encode_device(self, y_ptr: int, u_ptr: int, v_ptr: int, collect: bool = True):

@@ -977,6 +977,19 @@ struct hl_amd_encoder_s {
     int32_t last_qp;                             // SliceQPY of the last encoded picture
     struct SvcState* svc = nullptr;              // spatial SVC layers (hl_amd_add_layer), else null
     int32_t* d_rows = nullptr;                   // k_deblock_rows: per-row progress [mbh], spin failures [mbh]
+    // look-ahead (hl_amd_set_lookahead): host frames queued in device memory
+    // and coded `lookahead` at a time as one hl_amd_encode_batch; results
+    // handed out one per call, in order
+    struct LaOut {
+        int32_t type = 0;
+        std::vector<uint8_t> hdr, data;
+    };
+    int32_t lookahead = 1;
+    uint8_t* d_la = nullptr;                     // [lookahead] frames, Y | U | V each
+    int32_t la_n = 0;                            // frames queued, not yet coded
+    std::vector<LaOut> la_out;                   // coded results not yet handed out, from la_head
+    size_t la_head = 0;
+    LaOut la_cur;                                // the result the last call handed out (valid until the next call)
 };
 
 static void svc_free(hl_amd_encoder_t* e);
@@ -999,6 +1012,7 @@ static void free_all(hl_amd_encoder_t* e)
     (void)hipFree(e->d_spec);
     (void)hipFree(e->d_prof);
     (void)hipFree(e->d_rows);
+    (void)hipFree(e->d_la);
     (void)hipFree(e->d_bpic);
     (void)hipFree(e->d_bpl);
     (void)hipFree(e->d_brec);
@@ -2033,9 +2047,91 @@ extern "C" int32_t hl_amd_encode_device(hl_amd_encoder_t* e, const uint8_t* y, c
     return encode_pictures(e, 1, &y, &u, &v, r);
 }
 
+// Look-ahead: the queued frames as one batch; every result copied out (a
+// batch's result data is valid only until the next call)
+static int32_t la_run(hl_amd_encoder_t* e)
+{
+    const int n = e->la_n;
+    if (!n) return HL_AMD_SUCCESS;
+    e->la_n = 0;
+    const size_t ny = (size_t)e->W * e->H, nc = (size_t)e->Wc * e->Hc;
+    std::vector<const uint8_t*> y(n), u(n), v(n);
+    for (int i = 0; i < n; ++i) {
+        y[i] = e->d_la + (ny + 2 * nc) * i;
+        u[i] = y[i] + ny;
+        v[i] = u[i] + nc;
+    }
+    std::vector<hl_amd_result_t> res(n);
+    const int32_t rc = encode_pictures(e, n, y.data(), u.data(), v.data(), res.data());
+    if (rc) return rc;
+    if (e->la_head == e->la_out.size()) {
+        e->la_out.clear();
+        e->la_head = 0;
+    }
+    for (const hl_amd_result_t& r : res) {
+        hl_amd_encoder_s::LaOut o;
+        o.type = r.type;
+        if (r.type & HL_AMD_RESULT_TYPE_HDR) o.hdr.assign(r.hdr, r.hdr + r.hdr_size);
+        if (r.type & HL_AMD_RESULT_TYPE_DATA) o.data.assign(r.data, r.data + r.data_size);
+        e->la_out.push_back(std::move(o));
+    }
+    return HL_AMD_SUCCESS;
+}
+
+// the next coded result, or TYPE 0 (nothing yet)
+static void la_pop(hl_amd_encoder_t* e, hl_amd_result_t* r)
+{
+    memset(r, 0, sizeof(*r));
+    if (e->la_head == e->la_out.size()) return;
+    e->la_cur = std::move(e->la_out[e->la_head++]);
+    r->type = e->la_cur.type;
+    if (r->type & HL_AMD_RESULT_TYPE_HDR) {
+        r->hdr = e->la_cur.hdr.data();
+        r->hdr_size = e->la_cur.hdr.size();
+    }
+    if (r->type & HL_AMD_RESULT_TYPE_DATA) {
+        r->data = e->la_cur.data.data();
+        r->data_size = e->la_cur.data.size();
+    }
+}
+
+extern "C" int32_t hl_amd_set_lookahead(hl_amd_encoder_t* e, int32_t frames)
+{
+    if (!e || frames < 1 || frames > 128) return HL_AMD_ERROR_INVALID_PARAMETER;
+    if (e->frame_index != 0 || e->la_n || svc_started(e) || e->svc) return HL_AMD_ERROR_INVALID_STATE;  // before the first frame, AVC only
+    (void)hipFree(e->d_la);
+    e->d_la = nullptr;
+    e->lookahead = frames;
+    return HL_AMD_SUCCESS;
+}
+
+extern "C" int32_t hl_amd_flush(hl_amd_encoder_t* e, hl_amd_result_t* r)
+{
+    if (!e || !r) return HL_AMD_ERROR_INVALID_PARAMETER;
+    const int32_t rc = la_run(e);
+    if (rc) return rc;
+    la_pop(e, r);
+    return HL_AMD_SUCCESS;
+}
+
 extern "C" int32_t hl_amd_encode(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t* u, const uint8_t* v, hl_amd_result_t* r)
 {
     if (!e || !y || !u || !v || !r) return HL_AMD_ERROR_INVALID_PARAMETER;
+    if (e->lookahead > 1) {  // queue the frame (copied: the caller may reuse its buffer), code a full queue
+        const size_t ny = (size_t)e->W * e->H, nc = (size_t)e->Wc * e->Hc, fb = ny + 2 * nc;
+        if (!e->d_la) HL_HIP_CHECK(hipMalloc(&e->d_la, fb * e->lookahead));
+        uint8_t* d = e->d_la + fb * e->la_n;
+        HL_HIP_CHECK(hipMemcpyAsync(d, y, ny, hipMemcpyHostToDevice, e->stream));
+        HL_HIP_CHECK(hipMemcpyAsync(d + ny, u, nc, hipMemcpyHostToDevice, e->stream));
+        HL_HIP_CHECK(hipMemcpyAsync(d + ny + nc, v, nc, hipMemcpyHostToDevice, e->stream));
+        HL_HIP_CHECK(hipStreamSynchronize(e->stream));
+        if (++e->la_n == e->lookahead) {
+            const int32_t rc = la_run(e);
+            if (rc) return rc;
+        }
+        la_pop(e, r);
+        return HL_AMD_SUCCESS;
+    }
     HL_HIP_CHECK(hipMemcpyAsync(e->d_in[0], y, (size_t)e->W * e->H, hipMemcpyHostToDevice, e->stream));
     HL_HIP_CHECK(hipMemcpyAsync(e->d_in[1], u, (size_t)e->Wc * e->Hc, hipMemcpyHostToDevice, e->stream));
     HL_HIP_CHECK(hipMemcpyAsync(e->d_in[2], v, (size_t)e->Wc * e->Hc, hipMemcpyHostToDevice, e->stream));

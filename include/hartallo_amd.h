@@ -89,6 +89,20 @@ void hl_amd_encoder_destroy(hl_amd_encoder_t* encoder);
 int32_t hl_amd_encode(hl_amd_encoder_t* encoder, const uint8_t* y, const uint8_t* u, const uint8_t* v,
                       hl_amd_result_t* result);
 
+/* Look-ahead for per-frame callers (no reference interface: hl_codec_encode,
+ * hl_codec.c:152-159, codes one frame per call and has no flush).  With
+ * frames = k > 1, set before the first frame: hl_amd_encode queues each host
+ * frame in device memory and codes every k queued frames as one
+ * hl_amd_encode_batch (a frame-pipelined run); each call hands out the next
+ * coded result in order -- type 0 (nothing) while the first k - 1 frames
+ * queue, so a frame's bytes come k - 1 calls later -- and hl_amd_flush codes
+ * what is still queued and hands out the remaining results, one per call,
+ * type 0 once none is left.  The bytes are those of k separate calls.  An
+ * error is reported by the call that codes the batch.  k = 1: off (the
+ * default).  AVC only (not with layers). */
+int32_t hl_amd_set_lookahead(hl_amd_encoder_t* encoder, int32_t frames);
+int32_t hl_amd_flush(hl_amd_encoder_t* encoder, hl_amd_result_t* result);
+
 /* same, with the planes already resident in device memory (HBM) */
 int32_t hl_amd_encode_device(hl_amd_encoder_t* encoder, const uint8_t* y, const uint8_t* u, const uint8_t* v,
                              hl_amd_result_t* result);

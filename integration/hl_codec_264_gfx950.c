@@ -83,6 +83,15 @@ static HL_ERROR_T gfx950_open(hl_codec_264_gfx950_t* self, hl_codec_t* base, hl_
         p.device = dv ? atoi(dv) : 0;
     }
     if ((err = hl_amd_encoder_create(&p, &self->enc))) return (HL_ERROR_T)err; /* HL_ERROR_T values (hl_types.h:101-122) */
+    /* look-ahead (opt-in, no reference counterpart): HL_AMD_LOOKAHEAD=k codes
+     * every k frames as one pipelined run; each hl_codec_encode then returns
+     * the result of the frame k - 1 calls earlier (NONE while the first ones
+     * queue) and the caller drains the rest with hl_codec_264_gfx950_flush.
+     * AVC only: an SVC encoder (layers added after the open) ignores it. */
+    {
+        const char* la = getenv("HL_AMD_LOOKAHEAD");
+        if (la && atoi(la) > 1 && (err = hl_amd_set_lookahead(self->enc, atoi(la)))) return (HL_ERROR_T)err;
+    }
     /* SPS max_num_ref_frames / PPS num_ref_idx_l0_default_active_minus1
      * (hl_codec_264_sps.c:620-636, hl_codec_264_pps.c:291) */
     if ((err = hl_amd_set_max_ref_frame(self->enc, base->max_ref_frame))) return (HL_ERROR_T)err;
@@ -95,6 +104,22 @@ static HL_ERROR_T gfx950_open(hl_codec_264_gfx950_t* self, hl_codec_t* base, hl_
     self->width = W;
     self->height = H;
     return HL_ERROR_SUCCESS;
+}
+
+/* the encoder's result as hl_codec_264.c returns it */
+static void gfx950_result(hl_codec_t* base, const hl_amd_result_t* r, hl_codec_result_t* result)
+{
+    result->type = HL_CODEC_RESULT_TYPE_NONE;
+    if (r->type & HL_AMD_RESULT_TYPE_HDR) { /* hl_codec_264.c:675-686 */
+        base->hdr_bytes = r->hdr;
+        base->hdr_bytes_count = r->hdr_size;
+        result->type |= HL_CODEC_RESULT_TYPE_HDR;
+    }
+    if (r->type & HL_AMD_RESULT_TYPE_DATA) { /* hl_codec_264.c:1000-1006 */
+        result->type |= HL_CODEC_RESULT_TYPE_DATA;
+        result->data_ptr = r->data; /* owned by the encoder, valid until the next call */
+        result->data_size = r->data_size;
+    }
 }
 
 /* plugin encode(): one planar YUV420 frame in host memory -> headers + one
@@ -149,19 +174,28 @@ static HL_ERROR_T gfx950_encode(hl_codec_t* base, const hl_frame_t* frame, hl_co
         if ((err = hl_amd_encode(self->enc, f->data_ptr[0], f->data_ptr[1], f->data_ptr[2], &r)))
             return (HL_ERROR_T)err;
     }
-    result->type = HL_CODEC_RESULT_TYPE_NONE;
-    if (r.type & HL_AMD_RESULT_TYPE_HDR) { /* hl_codec_264.c:675-686 */
-        base->hdr_bytes = r.hdr;
-        base->hdr_bytes_count = r.hdr_size;
-        result->type |= HL_CODEC_RESULT_TYPE_HDR;
-    }
-    if (r.type & HL_AMD_RESULT_TYPE_DATA) { /* hl_codec_264.c:1000-1006 */
-        result->type |= HL_CODEC_RESULT_TYPE_DATA;
-        result->data_ptr = r.data; /* owned by the encoder, valid until the next call */
-        result->data_size = r.data_size;
-    }
+    gfx950_result(base, &r, result);
     result->width = f->data_width[0];
     result->height = f->data_height[0];
+    return HL_ERROR_SUCCESS;
+}
+
+/* Look-ahead (HL_AMD_LOOKAHEAD, gfx950_open): codes the frames still queued
+ * and returns the next result, one per call, NONE once none is left.  A
+ * caller that opted in calls it after its last hl_codec_encode until NONE;
+ * without look-ahead it returns NONE at once. */
+HL_ERROR_T hl_codec_264_gfx950_flush(hl_codec_t* base, hl_codec_result_t* result)
+{
+    hl_codec_264_gfx950_t* self = (hl_codec_264_gfx950_t*)base;
+    hl_amd_result_t r;
+    int32_t err;
+    if (!self || !result) return HL_ERROR_INVALID_PARAMETER;
+    result->type = HL_CODEC_RESULT_TYPE_NONE;
+    if (!self->enc || self->layers) return HL_ERROR_SUCCESS;
+    if ((err = hl_amd_flush(self->enc, &r))) return (HL_ERROR_T)err;
+    gfx950_result(base, &r, result);
+    result->width = self->width;
+    result->height = self->height;
     return HL_ERROR_SUCCESS;
 }
 

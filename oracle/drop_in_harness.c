@@ -36,6 +36,7 @@
 
 extern const hl_codec_plugin_def_t hl_codec_264_gfx950_plugin_def_s;
 HL_ERROR_T hl_codec_264_gfx950_install(void);
+HL_ERROR_T hl_codec_264_gfx950_flush(hl_codec_t* codec, hl_codec_result_t* result);
 
 static int run_svc(int argc, char** argv);
 static int run_dec(int argc, char** argv);
@@ -101,6 +102,23 @@ int main(int argc, char** argv)
         }
         ++n;
     }
+    /* the plugin's look-ahead (HL_AMD_LOOKAHEAD): the frames it still holds */
+    struct timespec tf0, tf1;
+    clock_gettime(CLOCK_MONOTONIC, &tf0);
+    for (;;) {
+        int e = hl_codec_264_gfx950_flush(c, r);
+        if (e) {
+            fprintf(stderr, "flush err %d\n", e);
+            return 6;
+        }
+        if (!(r->type & (HL_CODEC_RESULT_TYPE_HDR | HL_CODEC_RESULT_TYPE_DATA))) break;
+        if (r->type & HL_CODEC_RESULT_TYPE_HDR) fwrite(c->hdr_bytes, 1, c->hdr_bytes_count, fo);
+        if (r->type & HL_CODEC_RESULT_TYPE_DATA) {
+            fwrite(scp, 1, 3, fo);
+            fwrite(r->data_ptr, 1, r->data_size, fo);
+        }
+    }
+    clock_gettime(CLOCK_MONOTONIC, &tf1);
     fclose(fo);
     fclose(fi);
     hl_object_unref(r);
@@ -108,7 +126,7 @@ int main(int argc, char** argv)
     hl_object_unref(f);
     printf("{\"frames\": %d, \"encode_ms\": [", n);
     for (int i = 0; i < n; ++i) printf("%s%.3f", i ? ", " : "", ms[i]);
-    printf("]}\n");
+    printf("], \"flush_ms\": %.3f}\n", (tf1.tv_sec - tf0.tv_sec) * 1e3 + (tf1.tv_nsec - tf0.tv_nsec) * 1e-6);
     free(ms);
     return 0;
 }

@@ -76,6 +76,33 @@ def test_drop_in_through_hl_codec_encode(gpu, cfg):
     assert got == ref, f"{name}: first differing byte {first_diff(got, ref)}"
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("lookahead", [4, 7])
+@pytest.mark.parametrize("cfg", CASES[:2] + [c for c in CASES if c in GOLDEN_RC_CONFIGS][:1], ids=lambda c: c[0] if isinstance(c, tuple) else None)
+def test_drop_in_lookahead(gpu, cfg, lookahead):
+    # the plugin's opt-in look-ahead (HL_AMD_LOOKAHEAD): hl_codec_encode hands
+    # out each frame's bytes lookahead - 1 calls late and the harness drains
+    # the rest with hl_codec_264_gfx950_flush -- the same stream, including
+    # frame counts that are not multiples of the look-ahead
+    if not os.path.exists(DROP_IN):
+        pytest.fail("oracle/_ref/drop_in_enc missing (built in the build container by make -C oracle ref)")
+    name, w, h, n, qp, mer, db, gop, seed = cfg[:9]
+    et = -1 if GOLD[name].get("early_term", 0) else 0
+    env = dict(os.environ, HL_AMD_LOOKAHEAD=str(lookahead))
+    if cfg in GOLDEN_RC_CONFIGS:
+        env.update(HL_REF_RC_BITRATE=str(cfg[9]), HL_REF_RC_BASICUNIT=str(cfg[10]), HL_REF_RC_QP_MIN=str(cfg[11]),
+                   HL_REF_RC_QP_MAX=str(cfg[12]))
+    with tempfile.TemporaryDirectory() as td:
+        inp, out = os.path.join(td, "in.yuv"), os.path.join(td, "out.264")
+        golden_input(cfg).tofile(inp)
+        r = subprocess.run([DROP_IN, str(w), str(h), str(n), str(qp), str(mer), str(db), str(gop), str(et), inp, out],
+                           capture_output=True, text=True, timeout=240, env=env)
+        assert r.returncode == 0, r.stderr
+        got = open(out, "rb").read()
+    ref = open(os.path.join(GOLDEN, name + ".264"), "rb").read()
+    assert got == ref, f"{name} (look-ahead {lookahead}): first differing byte {first_diff(got, ref)}"
+
+
 SVC_GOLD = json.load(open(os.path.join(GOLDEN, "svc_golden.json")))
 
 

@@ -126,6 +126,35 @@ def test_bench_stream_per_picture(gpu):
     _check("bench_1088p_s11", 0, outs, recons)
 
 
+def test_bench_stream_lookahead(gpu):
+    # host frames through hl_amd_encode with an 8-frame look-ahead: results in
+    # order, lookahead - 1 calls late, the rest from flush(); each equals the
+    # reference's frame; setting it after the first frame is refused
+    g = BENCH["bench_1088p_s11"]
+    w, h, n = g["width"], g["height"], 13
+    clip = _clip("bench_1088p_s11")[:n]
+    enc = Encoder(w, h, g["qp"], g["me_range"], g["deblock"], g["gop"])
+    enc.set_lookahead(8)
+    outs, got = [], 0
+    ny = w * h
+    for i in range(n):
+        f = clip[i].reshape(-1)
+        r = enc.encode(f[:ny], f[ny:ny + ny // 4], f[ny + ny // 4:])
+        assert (r.type != 0) == (i >= 7), (i, r.type)
+        if r.type:
+            outs.append(r.annexb())
+    while True:
+        r = enc.flush()
+        if not r.type:
+            break
+        outs.append(r.annexb())
+    with pytest.raises(Exception):
+        enc.set_lookahead(4)
+    enc.close()
+    assert len(outs) == n
+    _check("bench_1088p_s11", 0, outs, [])
+
+
 def test_bench_stream_partitioning_helpers_in_runs(gpu, monkeypatch):
     # the partitioning helpers in a run of one stream (HL_AMD_FAM3=2, read
     # when the encoder opens), for every picture and for the run's edges only
