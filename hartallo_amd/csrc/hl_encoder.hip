@@ -2623,7 +2623,8 @@ static int32_t svc_join(hl_amd_encoder_t* e, int upto)
 extern "C" int32_t hl_amd_add_layer(hl_amd_encoder_t* e, int32_t width, int32_t height)
 {
     if (!e || width <= 0 || height <= 0) return HL_AMD_ERROR_INVALID_PARAMETER;
-    if (e->frame_index > 0 || (e->svc && e->svc->started)) return HL_AMD_ERROR_INVALID_STATE;
+    if (e->frame_index > 0 || e->la_n || (e->svc && e->svc->started)) return HL_AMD_ERROR_INVALID_STATE;
+    e->lookahead = 1;  // (the look-ahead is AVC only: an encoder with layers ignores it)
     if (!e->svc) e->svc = new SvcState();
     SvcState* s = e->svc;
     if ((int)s->w.size() >= 4) return HL_AMD_ERROR_OUTOFCAPACITY;  // HL_ENCODER_MAX_LAYERS

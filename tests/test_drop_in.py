@@ -107,18 +107,23 @@ SVC_GOLD = json.load(open(os.path.join(GOLDEN, "svc_golden.json")))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", sorted(SVC_GOLD))
+@pytest.mark.parametrize("name", sorted(SVC_GOLD) + ["svc2_qcif_qp28_db+lookahead"])
 def test_drop_in_svc_through_hl_codec_encode(gpu, name):
     """Spatial SVC through the reference's own API with the gfx950 plugin:
     hl_codec_add_layer per layer, then hl_codec_encode per layer per frame
     (oracle/drop_in_harness.c svc mode), every access unit equal to the
-    reference encoder's (tests/golden/svc_golden.json)."""
+    reference encoder's (tests/golden/svc_golden.json).  "+lookahead": with
+    HL_AMD_LOOKAHEAD set, which an encoder with layers ignores."""
     import hashlib
 
     from hartallo_amd import synth
 
     if not os.path.exists(DROP_IN):
         pytest.fail("oracle/_ref/drop_in_enc missing (built in the build container by make -C oracle ref)")
+    env = dict(os.environ)
+    if name.endswith("+lookahead"):
+        name = name[:-len("+lookahead")]
+        env["HL_AMD_LOOKAHEAD"] = "4"
     g = SVC_GOLD[name]
     L, w0, h0, n = g["layers"], g["w0"], g["h0"], g["frames"]
     clips = synth.svc_clips(w0 << (L - 1), h0 << (L - 1), L, n, g["seed"])
@@ -130,7 +135,7 @@ def test_drop_in_svc_through_hl_codec_encode(gpu, name):
             clips[l][:n].tofile(ins[-1])
         pre = os.path.join(td, "out")
         r = subprocess.run([DROP_IN, "svc", str(L), str(w0), str(h0), str(n), str(g["qp"]), str(g["me_range"]), str(g["deblock"]),
-                            str(g["gop"]), str(et), pre] + ins, capture_output=True, text=True, timeout=240)
+                            str(g["gop"]), str(et), pre] + ins, capture_output=True, text=True, timeout=240, env=env)
         assert r.returncode == 0, r.stderr
         got = open(pre + ".264", "rb").read()
         idx = [0] + [int(x) for x in open(pre + ".idx").read().split()]
