@@ -1984,6 +1984,7 @@ extern "C" int32_t hl_amd_encode_batch(hl_amd_encoder_t* e, int32_t n, const uin
     if (!e || n <= 0 || !y || !u || !v || !results) return HL_AMD_ERROR_INVALID_PARAMETER;
     for (int i = 0; i < n; ++i)
         if (!y[i] || !u[i] || !v[i]) return HL_AMD_ERROR_INVALID_PARAMETER;
+    if (e->la_n) return HL_AMD_ERROR_INVALID_STATE;  // frames still queued by the look-ahead come first (hl_amd_flush)
     return encode_pictures(e, n, y, u, v, results);
 }
 
@@ -2044,6 +2045,7 @@ extern "C" int32_t hl_amd_pipeline_occupancy(void)
 extern "C" int32_t hl_amd_encode_device(hl_amd_encoder_t* e, const uint8_t* y, const uint8_t* u, const uint8_t* v, hl_amd_result_t* r)
 {
     if (!e || !y || !u || !v || !r) return HL_AMD_ERROR_INVALID_PARAMETER;
+    if (e->la_n) return HL_AMD_ERROR_INVALID_STATE;  // frames still queued by the look-ahead come first (hl_amd_flush)
     return encode_pictures(e, 1, &y, &u, &v, r);
 }
 

@@ -99,7 +99,9 @@ int32_t hl_amd_encode(hl_amd_encoder_t* encoder, const uint8_t* y, const uint8_t
  * what is still queued and hands out the remaining results, one per call,
  * type 0 once none is left.  The bytes are those of k separate calls.  An
  * error is reported by the call that codes the batch.  k = 1: off (the
- * default).  AVC only (not with layers). */
+ * default).  AVC only (adding a layer turns it off).  While frames are
+ * queued, hl_amd_encode_device and hl_amd_encode_batch are refused
+ * (HL_AMD_ERROR_INVALID_STATE): flush first. */
 int32_t hl_amd_set_lookahead(hl_amd_encoder_t* encoder, int32_t frames);
 int32_t hl_amd_flush(hl_amd_encoder_t* encoder, hl_amd_result_t* result);
 
