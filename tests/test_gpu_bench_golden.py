@@ -153,6 +153,19 @@ def test_bench_stream_lookahead(gpu):
     enc.close()
     assert len(outs) == n
     _check("bench_1088p_s11", 0, outs, [])
+    # while frames are queued, device-frame calls are refused (flush first)
+    enc = Encoder(w, h, g["qp"], g["me_range"], g["deblock"], g["gop"])
+    enc.set_lookahead(4)
+    f = clip[0].reshape(-1)
+    assert enc.encode(f[:ny], f[ny:ny + ny // 4], f[ny + ny // 4:]).type == 0
+    dev = torch.from_numpy(np.ascontiguousarray(clip[:1])).cuda()
+    torch.cuda.synchronize()
+    with pytest.raises(Exception):
+        enc.encode_device(*_ptrs(dev, w, h)[0])
+    r = enc.flush()
+    assert r.annexb() and not enc.flush().type
+    enc.close()
+    _check("bench_1088p_s11", 0, [r.annexb()], [])
 
 
 def test_bench_stream_partitioning_helpers_in_runs(gpu, monkeypatch):
