@@ -419,9 +419,9 @@ __device__ int pop_task(const PipeArgs& P, int nmb, int mbw, int mbh, int& olc, 
             for (int i = 0; i < kScan; ++i) {
                 if (qv[i] > 0) {
                     const int a = qv[i] - 1, y = udiv_small(a, mbw, rc.mbw), x = a - y * mbw;
-                    // preference for the workgroup's sub-queue (column band), in wavefront steps of priority
-                    // (12 with address-interleaved sub-queues; 30 with bands: +0.5 / +0.9 %, profiles/r06_ab_column_bands.log)
-                    const int own = sqs[i] == (int)(blockIdx.x % kSubQ) ? 30 : 0;
+                    // preference for the workgroup's sub-queue, in wavefront steps of priority (one stream's
+                    // column bands 30: +0.5 / +0.9 %, profiles/r06_ab_column_bands.log; several streams 12)
+                    const int own = sqs[i] == (int)(blockIdx.x % kSubQ) ? (S == 1 ? 30 : 12) : 0;
                     const int kk = (((mbw - 1 - x) + 2 * (mbh - 1 - y) - P.hop * js[i] + own + 4096) << 6) | (63 - lane);
                     if (kk > key) {
                         key = kk;
@@ -741,11 +741,13 @@ __global__ __launch_bounds__(kMbThreads, HL_PIPE_WAVES_PER_EU) void k_pipeline(P
                 // only where this decrement was the last
                 if (__hip_atomic_fetch_add(P.cnt + fo * nmb + a, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1) continue;
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, HL_ACQ_SCOPE);
-                // sub-queue = the successor's column band (kSubQ bands of MB
-                // columns): a workgroup prefers its own (blockIdx % kSubQ), so a
-                // band's macroblocks, the plane blocks they write and the
-                // reference planes they search stay on two XCDs' L2s
-                const int qf = fo * kSubQ + xo * kSubQ / mbw;
+                // one stream: sub-queue = the successor's column band (kSubQ
+                // bands of MB columns): a workgroup prefers its own (blockIdx %
+                // kSubQ), so a band's macroblocks, the plane blocks they write and
+                // the reference planes they search stay on two XCDs' L2s.  Several
+                // streams: MB address % kSubQ (the bands' preference bent the
+                // streams' priorities: 8 streams -4.5 %, profiles/r06_ab_column_bands.log)
+                const int qf = fo * kSubQ + (P.nstreams == 1 ? xo * kSubQ / mbw : a % kSubQ);
                 const int pos = __hip_atomic_fetch_add(P.tail + qf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 // helper kinds: 0 = intra, 1..4 = the 8x8 family's partitioning kind + 2
                 const int g = fo * nmb + a, nk = hlp ? (h3 ? 5 : 1) : 0;
