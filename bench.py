@@ -66,19 +66,25 @@ def load_pmc(lib_path, warmup, steps, workgroups, streams_per_gpu):
     why not)."""
     import hashlib
 
+    from hartallo_amd import _lib
+
     if not os.path.exists(PMC_FILE):
         return None, "no counters recorded (tools/pmc_record.sh)"
     if not lib_path or not os.path.exists(lib_path):
         return None, "library not found"
     pmc = json.load(open(PMC_FILE))
     sha = hashlib.sha256(open(lib_path, "rb").read()).hexdigest()
-    if pmc.get("lib_sha256") != sha:
+    # the same library file, or one whose code (device and host sections) is
+    # the same: a relink can reorder the ELF string tables only
+    code = _lib.code_sha256(lib_path) if pmc.get("code_sha256") else None
+    if pmc.get("lib_sha256") != sha and (code is None or pmc.get("code_sha256") != code):
         return None, f"stale: recorded on library {pmc.get('lib_sha256', '?')[:12]}, this one is {sha[:12]} (rerun tools/pmc_record.sh)"
     want = {"warmup": warmup, "steps": steps, "width": W, "height": H, "workgroups": workgroups, "streams_per_gpu": streams_per_gpu}
     diff = {k: (pmc.get(k), v) for k, v in want.items() if pmc.get(k) != v}
     if diff:
         return None, "recorded on another workload: " + ", ".join(f"{k} {a} (here {b})" for k, (a, b) in diff.items())
-    return pmc, f"tools/pmc/pmc_k_pipeline.json, library sha256 {sha[:12]}, recorded {pmc.get('recorded', '?')}"
+    same = "library" if pmc.get("lib_sha256") == sha else "code"
+    return pmc, f"tools/pmc/pmc_k_pipeline.json, {same} sha256 {(sha if same == 'library' else code)[:12]}, recorded {pmc.get('recorded', '?')}"
 
 
 def critical_path_steps(frames, mbw, mbh, reach=2):

@@ -116,6 +116,32 @@ _lib = None
 LOADED_PATH = None  # the library file load_library loaded (bench.py stamps counters with its hash)
 
 
+def code_sha256(path: str) -> str:
+    """SHA-256 of a built library's code: its .hip_fatbin (the gfx950 code
+    objects) and .text (the host code) sections, in that order.  Two links of
+    the same sources can lay out the ELF string tables differently (the whole
+    file's hash then differs while every instruction is the same); counters
+    recorded on one are valid for the other."""
+    import hashlib
+    import struct
+
+    data = open(path, "rb").read()
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize) for i in range(shnum)]
+    stroff = secs[shstrndx][4]
+
+    def name(off):
+        return data[stroff + off:data.index(b"\0", stroff + off)].decode()
+
+    by = {name(sn): (o, sz) for sn, _, _, _, o, sz in secs}
+    h = hashlib.sha256()
+    for sec in (".hip_fatbin", ".text"):
+        o, sz = by[sec]
+        h.update(data[o:o + sz])
+    return h.hexdigest()
+
+
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     """Loads the HIP library.  torch (if installed) is imported first so the
     process ends up with one HIP runtime (torch ships its own

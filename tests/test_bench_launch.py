@@ -99,3 +99,32 @@ def test_spawn_ranks_deadline(tmp_path, monkeypatch):
     t = time.monotonic()
     assert bench.spawn_ranks(2, [], script=str(probe)) == 124
     assert time.monotonic() - t < 60
+
+
+def test_pmc_record_identity(tmp_path, monkeypatch):
+    """bench.load_pmc: the counters are used on the library they were taken
+    on, or on a relink of the same code (only the ELF string tables differ);
+    a library with other code, or another workload, gets none."""
+    from hartallo_amd import _lib
+
+    lib = os.path.join(ROOT, "hartallo_amd", "libhartallo_amd.so")
+    if not os.path.exists(lib):
+        pytest.skip("library not built")
+    code = _lib.code_sha256(lib)
+    rec = {"lib_sha256": "0" * 64, "code_sha256": code, "warmup": 1, "steps": 2, "workgroups": 0, "streams_per_gpu": 1,
+           "width": bench.W, "height": bench.H, "recorded": "x"}
+    f = tmp_path / "pmc.json"
+    f.write_text(json.dumps(rec))
+    monkeypatch.setattr(bench, "PMC_FILE", str(f))
+    pmc, why = bench.load_pmc(lib, 1, 2, 0, 1)
+    assert pmc is not None and "code sha256" in why
+    assert bench.load_pmc(lib, 1, 3, 0, 1)[0] is None  # another workload
+    f.write_text(json.dumps(dict(rec, code_sha256="1" * 64)))
+    pmc, why = bench.load_pmc(lib, 1, 2, 0, 1)
+    assert pmc is None and why.startswith("stale")
+    # a copy with a string-table byte changed keeps the code hash
+    data = bytearray(open(lib, "rb").read())
+    data[-1] ^= 0xFF  # the section header table ends the file; its last field is sh_entsize of the last section
+    other = tmp_path / "relink.so"
+    other.write_bytes(bytes(data))
+    assert _lib.code_sha256(str(other)) == code

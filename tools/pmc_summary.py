@@ -1,8 +1,8 @@
 """Summarises rocprofv3 --pmc passes over bench.py (tools/pmc_record.sh)
 into the counters of the timed k_pipeline launch (the last dispatch of the
 kernel: the warm-up call's launch comes first), per launch and per
-macroblock, stamped with the SHA-256 of the library that ran (JSON on
-stdout).
+macroblock, stamped with the SHA-256 of the library that ran and of its
+code sections (JSON on stdout).
 
 Units and corrections (MI355X_MICROARCH.md): SQ_WAVE_CYCLES / SQ_WAIT_* /
 SQ_ACTIVE_INST_* count quad-cycles (the ratios between them are unit-free);
@@ -28,9 +28,12 @@ import glob
 import hashlib
 import json
 import os
+import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from hartallo_amd import _lib  # noqa: E402  (code_sha256 only: loads no library)
 
 
 def timed_launch(d):
@@ -63,7 +66,7 @@ def main():
         launches.add(n)
     mbs = a.steps * (a.width // 16) * (a.height // 16)  # the timed call: one launch of `steps` pictures
     out = {
-        "kernel": "k_pipeline", "lib_sha256": hashlib.sha256(open(a.lib, "rb").read()).hexdigest(),
+        "kernel": "k_pipeline", "lib_sha256": hashlib.sha256(open(a.lib, "rb").read()).hexdigest(), "code_sha256": _lib.code_sha256(a.lib),
         "recorded": time.strftime("%Y-%m-%d"), "warmup": a.warmup, "steps": a.steps,
         # the workload the counters belong to (bench.py uses them only for this one)
         "width": a.width, "height": a.height, "workgroups": a.workgroups, "streams_per_gpu": a.streams_per_gpu,
