@@ -117,8 +117,9 @@ LOADED_PATH = None  # the library file load_library loaded (bench.py stamps coun
 
 
 def code_sha256(path: str) -> str:
-    """SHA-256 of a built library's code: its .hip_fatbin (the gfx950 code
-    objects) and .text (the host code) sections, in that order.  Two links of
+    """SHA-256 of a built library's code and constants: its .hip_fatbin (the
+    gfx950 code objects), .text (the host code), .rodata and .data sections,
+    in that order (a missing one counts as empty).  Two links of
     the same sources can lay out the ELF string tables differently (the whole
     file's hash then differs while every instruction is the same); counters
     recorded on one are valid for the other."""
@@ -136,8 +137,8 @@ def code_sha256(path: str) -> str:
 
     by = {name(sn): (o, sz) for sn, _, _, _, o, sz in secs}
     h = hashlib.sha256()
-    for sec in (".hip_fatbin", ".text"):
-        o, sz = by[sec]
+    for sec in (".hip_fatbin", ".text", ".rodata", ".data"):
+        o, sz = by.get(sec, (0, 0))
         h.update(data[o:o + sz])
     return h.hexdigest()
 
